@@ -1,0 +1,203 @@
+"""Benchmark: Gibbs iterations/s (all chains, whole node) + ESS/s of log10 rho.
+
+Workload (BASELINE.json configs[1]): the simulated J1713+0747 pulsar (720 TOAs,
+30-bin free spectrum + 16-column timing model, m = 76, fixed white noise),
+``--chains`` independent chains per GPU (default 4096), batched on each MI355X.
+A "step" = one Gibbs sweep of every chain (rho|b then b|rho, with the chain
+rows recorded to HBM as PulsarBlockGibbs.sample records them).
+
+N GPUs: one process per GPU (torch.distributed.run), chains sharded by rank
+(chain_base = rank * chains, disjoint Philox streams), no data-path collective
+-> weak scaling.  Timing: barrier + synchronize on both sides of exactly K
+steps, max over ranks.
+
+Extra fields: "roofline" (fp64 work of the fused sweep kernel per launch over
+its HIP-event-timed duration on the launch stream), "cpu_baseline" (the
+oracle's restatement of the reference loop, numpy/LAPACK SVD, 1 thread, on this
+host), "ess_per_s" (min over bins of the summed ESS/s).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")   # reference-faithful CPU baseline
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFLOPS = 78.6          # MI355X FP64 vector = FP64 matrix, AMD public spec
+HBM_PEAK_GBS = 8000.0
+
+
+def flops_per_chain_sweep(m):
+    """potrf m^3/3 + m^2/2 + m/6 + 3 triangular solves 3 m^2."""
+    return m ** 3 / 3 + m ** 2 / 2 + m / 6 + 3 * m ** 2
+
+
+def executed_flops_per_chain_sweep(nf, nm):
+    """What the kernel executes (NF x NF Schur block + solves + fixed-prior GEMVs)."""
+    return nf ** 3 / 3 + nf ** 2 / 2 + nf / 6 + 2 * nf ** 2 + 2 * nm * nf + nm ** 2
+
+
+def cpu_baseline(seconds=12.0):
+    """Reference loop (oracle restatement, SVD draw), 1 thread, bounded sample."""
+    from oracle import gibbs_oracle as O
+    from pulsar_timing_gibbsspec_amd import synthetic
+    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0)
+    T, N, r = pta.get_basis()[0], pta.get_ndiag({})[0], pta.get_residuals()[0]
+    gwid = np.arange(60)
+    rng = np.random.default_rng(0)
+    x = rng.uniform(-9, -4, 30)
+    b = np.zeros(T.shape[1])
+    n_tm = T.shape[1] - 60
+    it = 0
+    t0 = time.perf_counter()
+    while True:
+        TNT, d = O.tnt(T, N, r)                    # recomputed every sweep (pulsar_gibbs.py:664-665)
+        if it == 0:                                # first draw from xs (pulsar_gibbs.py:661-662)
+            b = O.bdraw_svd(TNT, d, O.phiinv_single(x, n_tm), rng.standard_normal(T.shape[1]))
+        tau = O.tau_half(b, gwid)
+        x = 0.5 * np.log10(O.rho_analytic(tau, rng.random(30), 1e-18, 1e-8))
+        b = O.bdraw_svd(TNT, d, O.phiinv_single(x, n_tm), rng.standard_normal(T.shape[1]))
+        it += 1
+        el = time.perf_counter() - t0
+        if el > seconds:
+            break
+    return dict(value=it / el, unit="iters/s", cores=1, kind="port",
+                sample=f"{it} sweeps of the J1713 single-chain loop (oracle restatement of "
+                       f"pulsar_gibbs.py:656-698, numpy/OpenBLAS SVD, OPENBLAS_NUM_THREADS=1) in {el:.1f} s")
+
+
+def ess_min_bin(x_rec, elapsed, n_chains_total, max_chains=256):
+    """Min over the 30 bins of the whole-job ESS/s of log10 rho.
+
+    IAT per chain on the post-burn-in rows (first 20 % dropped) of up to
+    ``max_chains`` chains; ESS/s = mean ESS per chain x all chains / the time
+    the post-burn-in sweeps took."""
+    from pulsar_timing_gibbsspec_amd.diagnostics import iat
+    xr = x_rec[:, :max_chains]                      # (K, C, n_f)
+    K, C, nf = xr.shape
+    burn = K // 5
+    n = K - burn
+    ess = np.array([np.mean([n / max(iat(xr[burn:, c, k]), 1.0) for c in range(C)]) for k in range(nf)])
+    return float(ess.min() * n_chains_total / (elapsed * n / K))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--chains", type=int, default=4096, help="chains per GPU")
+    ap.add_argument("--sweeps-per-launch", type=int, default=100)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel, FreeSpectrumChains
+
+    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0)
+    T, N, r = pta.get_basis()[0], pta.get_ndiag({})[0], pta.get_residuals()[0]
+    gwid = np.arange(60)
+    ctx = _lib.Context(local, seed=20251015)
+    model = DeviceModel(ctx, [T], [N], [r], [gwid], [np.full(T.shape[1] - 60, 1e-40)])
+    C = args.chains
+    x0 = np.random.default_rng(rank).uniform(-9, -4, (C, 30))
+    run = FreeSpectrumChains(model, 1e-18, 1e-8, C, x0, chain_base=rank * C)
+    K, W, S = args.steps, args.warmup, max(1, args.sweeps_per_launch)
+    m = int(model.m[0])
+    x_rec = torch.empty(K, C, 30, dtype=torch.float64, device=dev)
+    b_rec = torch.empty(K, C, model.ldb, dtype=torch.float64, device=dev)
+
+    # warmup (untimed)
+    done = 0
+    while done < W:
+        n = min(S, W - done)
+        run.run(n, x_rec=x_rec[:n], b_rec=b_rec[:n])
+        done += n
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = ctx.stream
+    evs = []
+    t0 = time.perf_counter()
+    done = 0
+    while done < K:
+        n = min(S, K - done)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        run.run(n, x_rec=x_rec[done:done + n], b_rec=b_rec[done:done + n])
+        e1.record(stream)
+        evs.append((e0, e1, n))
+        done += n
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    info = run.info.cpu().numpy()
+    if info.any():
+        raise RuntimeError(f"{int((info != 0).sum())} chains hit a non-PD Sigma")
+
+    total_chains = C * world
+    value = total_chains * K / el
+    # roofline of the fused sweep kernel (dominant kernel: one launch per S sweeps)
+    kern_ms = np.array([a.elapsed_time(b) for a, b, _ in evs])
+    sweeps = np.array([n for _, _, n in evs])
+    per_sweep_s = float(np.sum(kern_ms) / 1e3 / np.sum(sweeps))
+    alg_flops_launch = flops_per_chain_sweep(m) * C * S
+    launch_s = per_sweep_s * S
+    achieved = alg_flops_launch / launch_s / 1e12
+    exe = executed_flops_per_chain_sweep(model.NF, int(model.nm[0])) * C * S / launch_s / 1e12
+    xh = x_rec.cpu().numpy()
+    ess = ess_min_bin(xh, el, total_chains)
+
+    out = None
+    if rank == 0:
+        out = {
+            "metric": "Gibbs iters/sec (all chains, whole node) + ESS/sec of log10_rho",
+            "value": value, "unit": "chain-iters/s", "n_gpus": world, "steps": K, "warmup": W,
+            "ms_per_step": el / K * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": "configs[1]: J1713+0747 sim (720 TOAs, m=76, 30-bin free spectrum), "
+                                   f"{C} independent chains per GPU", "chains_per_gpu": C,
+                       "global_chains": total_chains, "m": m, "n_f": 30,
+                       "sweeps_per_launch": S, "parallelism": f"chains sharded over {world} GPU(s)"},
+            "ess_per_s": ess,
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "kernel": "k_sweep_freespec", "kernel_avg_ms": launch_s * 1e3,
+                         "alg_flops_per_launch": alg_flops_launch,
+                         "executed_tflops": exe, "executed_frac": exe / FP64_PEAK_TFLOPS},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

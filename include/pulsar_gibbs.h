@@ -1,0 +1,161 @@
+/*
+ * pulsar_gibbs.h — C-ABI of the MI355X free-spectrum Gibbs hot path.
+ *
+ * The reference (astrolamb/pulsar_timing_gibbsspec) is pure Python over
+ * numpy/scipy; it has no native boundary.  These entry points replace the
+ * L2 -> L3 arithmetic of its samplers and are bound by
+ * ctypes from pulsar_timing_gibbsspec_amd/_lib.py.  Each entry cites the
+ * reference code it replaces.
+ *
+ * Conventions
+ *   - every array argument is caller-owned DEVICE memory (fp64 unless noted),
+ *     row-major, with the leading dimensions given;
+ *   - a "system" is one (pulsar p, chain c) pair, sys = p * n_chain + c;
+ *   - calls are asynchronous on the context's stream; a context is not
+ *     thread-safe (one host thread per context);
+ *   - return 0 on success, a negative HIP error code (-hipError_t) on a
+ *     runtime failure, or a positive 1-based index of the offending argument;
+ *     gs_last_error() describes the last failure of the calling thread;
+ *   - per-system `info` (int32, may be NULL): 0 = ok, k > 0 = the k-th leading
+ *     minor of Sigma was not positive definite (maps to the reference's
+ *     LinAlgError branch, pulsar_gibbs.py:511, and to the -inf likelihood at
+ *     pulsar_gibbs.py:603-604).
+ *
+ * Random numbers: device Philox4x32-10, key = the context seed, counter =
+ *   (slot, sweep, global chain id, (pulsar << 8) | event).  Any draw can be
+ *   replaced by injected values (parity mode) by passing a non-NULL array.
+ */
+#ifndef PULSAR_GIBBS_H
+#define PULSAR_GIBBS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1
+
+/* Philox event ids (counter word 3, low 8 bits) */
+enum {
+  GS_EV_B0 = 1,     /* first b draw of a run, from xs   (pulsar_gibbs.py:661-662) */
+  GS_EV_RHO = 2,    /* rho|b uniforms                    (pulsar_gibbs.py:215)     */
+  GS_EV_B = 3,      /* gated b draw                      (pulsar_gibbs.py:697-698) */
+  GS_EV_RED = 4,    /* per-pulsar red grid-CDF uniforms  (pta_gibbs.py:271)        */
+  GS_EV_CURN = 5,   /* common grid-CDF uniforms          (pta_gibbs.py:209)        */
+  GS_EV_GUMBEL = 6, /* Gumbel-max uniforms               (pulsar_gibbs.py:233)     */
+  GS_EV_USER = 16   /* first id free for callers                                    */
+};
+
+typedef struct gs_ctx gs_ctx;
+
+/* Ragged-batch descriptor for gs_tnt (one per pulsar, int64 fields, device). */
+typedef struct {
+  int64_t n_toa;   /* TOAs of this pulsar                                   */
+  int64_t m;       /* basis columns                                          */
+  int64_t T_off;   /* element offset of T (n_toa x m, row-major) in T       */
+  int64_t toa_off; /* element offset into Nvec / r                          */
+  int64_t tnt_off; /* element offset of TNT (m x m) in TNT                  */
+  int64_t d_off;   /* element offset of d (m) in d                          */
+} gs_tnt_desc;
+
+/* Per-pulsar descriptor for gs_prefix (device). */
+typedef struct {
+  int64_t m;       /* basis columns                                         */
+  int64_t n_fixed; /* fixed-prior columns nM (m - NF), 0 < nM <= NMX        */
+  int64_t tnt_off; /* element offset of TNT (m x m) in TNT                  */
+  int64_t d_off;   /* element offset of d (m) in d                          */
+} gs_prefix_desc;
+
+int gs_version(void);
+const char* gs_last_error(void);
+
+int gs_ctx_create(int device, uint64_t seed, void* hip_stream, gs_ctx** out);
+int gs_ctx_destroy(gs_ctx* ctx);
+int gs_ctx_set_stream(gs_ctx* ctx, void* hip_stream);
+int gs_ctx_set_seed(gs_ctx* ctx, uint64_t seed);
+
+/* Doubles per pulsar in a model buffer (see gs_prefix). */
+int64_t gs_model_stride(int NF, int NMX);
+/* Dynamic LDS bytes / waves per workgroup the sweep kernel uses for (NF, NMX). */
+int gs_sweep_lds_bytes(int NF, int NMX);
+
+/*
+ * (a2) TNT = T^T N^-1 T, d = T^T N^-1 r for a ragged batch of pulsars.
+ * Replaces pulsar_gibbs.py:500-502 (also :584-586) and pta_gibbs.py:523-526.
+ * fp64 MFMA (v_mfma_f64_16x16x4f64), split over TOAs.
+ */
+int gs_tnt(gs_ctx* ctx, int n_psr, int m_max, const gs_tnt_desc* desc,
+           const double* T, const double* Nvec, const double* r, double* TNT, double* d);
+
+/*
+ * Fixed-prior prefix of the Cholesky of Sigma = TNT + diag(phiinv), with the
+ * fixed-prior columns (timing model; phiinv constant across sweeps) ordered
+ * first and the NF free-spectrum columns (gwid, pulsar_gibbs.py:90-105) last.
+ * Writes, per pulsar p, at model + p * gs_model_stride(NF, NMX):
+ *   S0 [NF x (NF+1)]  Schur complement TNT_FF - W^T W  (row stride NF+1)
+ *   dF [NF]           d_F - W^T L_M^-1 d_M
+ *   G  [NMX x (NF+1)] L_M^-T W  (row stride NF+1)
+ *   h  [NMX]          L_M^-T L_M^-1 d_M
+ *   R  [NMX x NMX]    L_M^-T  (upper)
+ * fidx: [n_psr x NF] column index of each free-spectrum column (gwid);
+ * midx: [n_psr x NMX] column index of each fixed-prior column;
+ * phiinv_fixed: [n_psr x NMX] their (constant) phiinv (1e-40 for the TM).
+ */
+int gs_prefix(gs_ctx* ctx, int n_psr, int NF, int NMX, const gs_prefix_desc* desc,
+              const double* TNT, const double* d, const int32_t* fidx, const int32_t* midx,
+              const double* phiinv_fixed, double* model, int32_t* info);
+
+/*
+ * (a1, a5) Batched b|rho draw: Sigma = TNT + diag(phiinv) -> Cholesky ->
+ * b = Sigma^-1 d + L^-T z for n_psr x n_chain systems, one wavefront each.
+ * Replaces PulsarBlockGibbs.update_b (pulsar_gibbs.py:489-520) and
+ * PTABlockGibbs.update_b (pta_gibbs.py:512-548).
+ * phiinv_F: [n_sys x NF] phiinv of the free-spectrum columns (fidx order);
+ * nm: [n_psr] fixed-prior column count; z: [n_sys x ldb] injected normals
+ * indexed by ORIGINAL column (NULL: Philox, event `event`, sweep `sweep`);
+ * b: [n_sys x ldb] output in original column order.
+ */
+int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,
+             const double* model, const int32_t* fidx, const int32_t* midx, const int32_t* nm,
+             const double* phiinv_F, const double* z, int64_t sweep, int event,
+             int64_t chain_base, double* b, int32_t* info);
+
+/*
+ * (a3) rho|b analytic draw: tau_k = (b_sin^2 + b_cos^2)/2 over fidx,
+ * truncated inverse-gamma inverse CDF, x = 0.5 log10 rho.
+ * Replaces pulsar_gibbs.py:206-216,236.  u: [n_sys x NF/2] injected U(0,1)
+ * (NULL: Philox event GS_EV_RHO).  x: [n_sys x ldx] output (first NF/2 cols).
+ */
+int gs_rho_analytic(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const int32_t* fidx,
+                    const double* b, const double* u, int64_t sweep, int64_t chain_base,
+                    double rhomin, double rhomax, double* x, int ldx);
+
+/*
+ * (a8) Fused free-spectrum sweep for independent chains (configs 1-3):
+ * n_sweeps iterations of PulsarBlockGibbs.sample's loop body
+ * (pulsar_gibbs.py:656-698): record (x, b) before the update, first b draw
+ * from xs when the global sweep index is 0, analytic rho|b, the all(xnew !=
+ * x_old[-1]) gate, b|rho — with each wavefront's state kept in registers.
+ * x_state [n_sys x NF/2] log10 rho, b_state [n_sys x ldb]: read at entry,
+ * written at exit.  x_rec [n_sweeps x n_sys x NF/2], b_rec [n_sweeps x n_sys x ldb]
+ * (either may be NULL).  z0_inj [n_sys x ldb], z_inj [n_sweeps x n_sys x ldb],
+ * u_inj [n_sweeps x n_sys x NF/2]: injected draws or NULL.  info [n_sys].
+ */
+int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,
+                      const double* model, const int32_t* fidx, const int32_t* midx,
+                      const int32_t* nm, double rhomin, double rhomax, int64_t chain_base,
+                      double* x_state, double* b_state, int64_t it0, int n_sweeps,
+                      double* x_rec, double* b_rec, const double* z0_inj, const double* z_inj,
+                      const double* u_inj, int32_t* info);
+
+/*
+ * Philox4x32-10 test hook: out[i] = the 4 words for counter
+ * (ctr[4*i..4*i+3]) under the context key.  ctr/out: [n x 4] uint32.
+ */
+int gs_philox(gs_ctx* ctx, int64_t n, const uint32_t* ctr, uint32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PULSAR_GIBBS_H */

@@ -1,0 +1,122 @@
+"""ctypes binding of the C-ABI in ``include/pulsar_gibbs.h``.
+
+The library is built in-tree (``libpulsar_gibbs.so`` next to this file, see
+``csrc/Makefile``).  ``torch`` is imported first so that the HIP runtime torch
+bundles (soname ``libamdhip64.so.7``) is the one the library binds to: device
+pointers and stream handles are then shared with torch.
+
+There is no CPU fallback: if the library is missing or no GPU is visible, every
+entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load; see module docstring)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpulsar_gibbs.so")
+
+EV_B0, EV_RHO, EV_B, EV_RED, EV_CURN, EV_GUMBEL, EV_USER = 1, 2, 3, 4, 5, 6, 16
+
+_P = C.c_void_p
+_I = C.c_int
+_I64 = C.c_int64
+_D = C.c_double
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "gs_version": (_I, []),
+    "gs_last_error": (C.c_char_p, []),
+    "gs_ctx_create": (_I, [_I, C.c_uint64, _P, C.POINTER(_P)]),
+    "gs_ctx_destroy": (_I, [_P]),
+    "gs_ctx_set_stream": (_I, [_P, _P]),
+    "gs_ctx_set_seed": (_I, [_P, C.c_uint64]),
+    "gs_model_stride": (_I64, [_I, _I]),
+    "gs_sweep_lds_bytes": (_I, [_I, _I]),
+    "gs_tnt": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "gs_prefix": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "gs_bdraw": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _I, _I64, _P, _P]),
+    "gs_rho_analytic": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I64, _I64, _D, _D, _P, _I]),
+    "gs_sweep_freespec": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _D, _D, _I64, _P, _P,
+                               _I64, _I, _P, _P, _P, _P, _P, _P]),
+    "gs_philox": (_I, [_P, _I64, _P, _P]),
+}
+
+_lib = None
+
+
+class GibbsLibError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the CDLL with typed signatures."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GibbsLibError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc, gfx950). There is no CPU fallback.")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().gs_last_error().decode(errors="replace")
+        raise GibbsLibError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise GibbsLibError("expected a device tensor")
+    if not t.is_contiguous():
+        raise GibbsLibError("expected a contiguous tensor")
+    return C.c_void_p(t.data_ptr())
+
+
+class Context:
+    """A ``gs_ctx``: device, Philox seed and the stream every call runs on."""
+
+    def __init__(self, device=0, seed=0, stream=None):
+        if not torch.cuda.is_available():
+            raise GibbsLibError("no GPU visible: the HIP path has no CPU fallback")
+        self.lib = load()
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self.seed = int(seed)
+        with torch.cuda.device(self.device):
+            s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self.stream = s
+        h = C.c_void_p()
+        check(self.lib.gs_ctx_create(self.device.index or 0, C.c_uint64(self.seed),
+                                     C.c_void_p(s.cuda_stream), C.byref(h)), "gs_ctx_create")
+        self.handle = h
+
+    def set_seed(self, seed):
+        self.seed = int(seed)
+        check(self.lib.gs_ctx_set_seed(self.handle, C.c_uint64(self.seed)), "gs_ctx_set_seed")
+
+    def set_stream(self, stream):
+        self.stream = stream
+        check(self.lib.gs_ctx_set_stream(self.handle, C.c_void_p(stream.cuda_stream)), "gs_ctx_set_stream")
+
+    def close(self):
+        if getattr(self, "handle", None) is not None:
+            self.lib.gs_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

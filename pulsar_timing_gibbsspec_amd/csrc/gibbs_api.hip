@@ -1,0 +1,379 @@
+// C-ABI of the MI355X Gibbs hot path (include/pulsar_gibbs.h), plus the TNT,
+// prefix-factorisation and Philox kernels.
+#include <stdio.h>
+
+#include <string>
+
+#include "gibbs_internal.h"
+
+struct gs_ctx {
+  int device;
+  hipStream_t stream;
+  uint64_t seed;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail_arg(int idx, const char* what) {
+  g_err = std::string("argument ") + std::to_string(idx) + ": " + what;
+  return idx;
+}
+
+int check_hip(hipError_t e, const char* where) {
+  if (e == hipSuccess) return 0;
+  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  return -(int)e;
+}
+
+int after_launch(const char* where) { return check_hip(hipGetLastError(), where); }
+
+gs_key key_of(const gs_ctx* c) {
+  gs_key k;
+  k.k0 = (uint32_t)(c->seed & 0xffffffffu);
+  k.k1 = (uint32_t)(c->seed >> 32);
+  return k;
+}
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ TNT (a2)
+// grid (n_psr, nb*nb), nb = ceil(m_max/16); 4 wavefronts split the TOAs.
+// D[i][j] += sum_t (T[t][I0+i] / N[t]) T[t][J0+j] with v_mfma_f64_16x16x4f64:
+// A lane l holds A[l&15][l>>4], B lane l holds B[l>>4][l&15];
+// C/D lane l reg r holds D[(l>>4) + 4r][l&15].
+__global__ __launch_bounds__(256) void k_tnt(const gs_tnt_desc* desc, int nb, const double* T,
+                                             const double* Nv, const double* r, double* TNT) {
+  __shared__ double red[3][4][64];
+  const gs_tnt_desc D = desc[blockIdx.x];
+  const int bi = blockIdx.y / nb, bj = blockIdx.y % nb;
+  const int m = (int)D.m;
+  if (bi * 16 >= m || bj * 16 >= m) return;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int i = l & 15, k = l >> 4;
+  const int ci = bi * 16 + i, cj = bj * 16 + i;
+  const double* Tp = T + D.T_off;
+  const double* Np = Nv + D.toa_off;
+  const int64_t n = D.n_toa;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t t0 = (int64_t)w * 4; t0 < n; t0 += 16) {
+    const int64_t t = t0 + k;
+    const bool ok = t < n;
+    const double invN = ok ? 1.0 / Np[t] : 0.0;
+    const double a = (ok && ci < m) ? Tp[t * m + ci] * invN : 0.0;
+    const double b = (ok && cj < m) ? Tp[t * m + cj] : 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  if (w > 0) {
+    for (int q = 0; q < 4; ++q) red[w - 1][q][l] = acc[q];
+  }
+  __syncthreads();
+  if (w == 0) {
+    for (int q = 0; q < 4; ++q) {
+      const double v = acc[q] + red[0][q][l] + red[1][q][l] + red[2][q][l];
+      const int row = bi * 16 + (l >> 4) + 4 * q, col = bj * 16 + (l & 15);
+      if (row < m && col < m) TNT[D.tnt_off + (int64_t)row * m + col] = v;
+    }
+  }
+  (void)r;
+}
+
+// d = T^T (r / N): grid (n_psr, ceil(m_max/64)), 4 wavefronts split the TOAs.
+__global__ __launch_bounds__(256) void k_tnr(const gs_tnt_desc* desc, const double* T,
+                                             const double* Nv, const double* r, double* d) {
+  __shared__ double red[4][64];
+  const gs_tnt_desc D = desc[blockIdx.x];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int m = (int)D.m;
+  const int j = blockIdx.y * 64 + l;
+  double s = 0.0;
+  if (j < m) {
+    const double* Tp = T + D.T_off;
+    for (int64_t t = w; t < D.n_toa; t += 4) s = fma(Tp[t * m + j], r[D.toa_off + t] / Nv[D.toa_off + t], s);
+  }
+  red[w][l] = s;
+  __syncthreads();
+  if (w == 0 && j < m) d[D.d_off + j] = red[0][l] + red[1][l] + red[2][l] + red[3][l];
+}
+
+// ------------------------------------------------------------------ prefix
+// One workgroup per pulsar; see include/pulsar_gibbs.h gs_prefix for the outputs.
+__global__ __launch_bounds__(256) void k_prefix(const gs_prefix_desc* desc, int NF, int NMX,
+                                                const double* TNT, const double* d,
+                                                const int32_t* fidx, const int32_t* midx,
+                                                const double* phfix, double* model, int64_t mstride,
+                                                int32_t* info) {
+  extern __shared__ double sm[];
+  const int p = blockIdx.x;
+  const gs_prefix_desc D = desc[p];
+  const int m = (int)D.m, nM = (int)D.n_fixed;
+  const double* A = TNT + D.tnt_off;
+  const double* dv = d + D.d_off;
+  const int32_t* Fi = fidx + (int64_t)p * NF;
+  const int32_t* Mi = midx + (int64_t)p * NMX;
+  double* L = sm;                  // NMX x NMX
+  double* W = L + NMX * NMX;       // NMX x (NF+1): column NF holds e = L^-1 d_M
+  double* Rm = W + NMX * (NF + 1); // NMX x NMX
+  __shared__ int s_fail;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int ldw = NF + 1;
+  if (tid == 0) s_fail = 0;
+  for (int q = tid; q < NMX * NMX; q += nt) {
+    const int i = q / NMX, j = q % NMX;
+    double v = 0.0;
+    if (i < nM && j < nM) {
+      v = A[(int64_t)Mi[i] * m + Mi[j]];
+      if (i == j) v += phfix[(int64_t)p * NMX + i];
+    }
+    L[q] = v;
+  }
+  __syncthreads();
+  // right-looking Cholesky of A_MM in LDS
+  for (int k = 0; k < nM; ++k) {
+    if (tid == 0) {
+      const double piv = L[k * NMX + k];
+      if (!(piv > 0.0) && s_fail == 0) s_fail = k + 1;
+      L[k * NMX + k] = sqrt(piv);
+    }
+    __syncthreads();
+    const double lkk = L[k * NMX + k];
+    for (int i = k + 1 + tid; i < nM; i += nt) L[i * NMX + k] /= lkk;
+    __syncthreads();
+    const int len = nM - k - 1;
+    for (int q = tid; q < len * len; q += nt) {
+      const int i = k + 1 + q / len, j = k + 1 + q % len;
+      if (j <= i) L[i * NMX + j] -= L[i * NMX + k] * L[j * NMX + k];
+    }
+    __syncthreads();
+  }
+  // W = L_M^-1 A_MF (columns 0..NF-1) and e = L_M^-1 d_M (column NF)
+  for (int f = tid; f <= NF; f += nt) {
+    for (int i = 0; i < nM; ++i) {
+      double s = (f < NF) ? A[(int64_t)Mi[i] * m + Fi[f]] : dv[Mi[i]];
+      for (int j = 0; j < i; ++j) s -= L[i * NMX + j] * W[j * ldw + f];
+      W[i * ldw + f] = s / L[i * NMX + i];
+    }
+  }
+  // R = L_M^-T (upper), column by column
+  for (int j = tid; j < NMX; j += nt) {
+    for (int i = NMX - 1; i >= 0; --i) {
+      double s = 0.0;
+      if (i < nM && j < nM) {
+        s = (i == j) ? 1.0 : 0.0;
+        for (int q = i + 1; q < nM; ++q) s -= L[q * NMX + i] * Rm[q * NMX + j];
+        s /= L[i * NMX + i];
+      }
+      Rm[i * NMX + j] = s;
+    }
+  }
+  __syncthreads();
+  double* out = model + (int64_t)p * mstride;
+  double* S0 = out;
+  double* dF = S0 + NF * (NF + 1);
+  double* G = dF + NF;
+  double* h = G + NMX * (NF + 1);
+  double* R = h + NMX;
+  for (int q = tid; q < NF * (NF + 1); q += nt) {
+    const int f = q / (NF + 1), g = q % (NF + 1);
+    double s = 0.0;
+    if (g < NF) {
+      s = A[(int64_t)Fi[f] * m + Fi[g]];
+      for (int i = 0; i < nM; ++i) s -= W[i * ldw + f] * W[i * ldw + g];
+    }
+    S0[q] = s;
+  }
+  for (int f = tid; f < NF; f += nt) {
+    double s = dv[Fi[f]];
+    for (int i = 0; i < nM; ++i) s -= W[i * ldw + f] * W[i * ldw + NF];
+    dF[f] = s;
+  }
+  for (int q = tid; q < NMX * (NF + 1); q += nt) {
+    const int mm = q / (NF + 1), f = q % (NF + 1);
+    double s = 0.0;
+    if (f < NF)
+      for (int j = mm; j < nM; ++j) s += Rm[mm * NMX + j] * W[j * ldw + f];
+    G[q] = s;
+  }
+  for (int mm = tid; mm < NMX; mm += nt) {
+    double s = 0.0;
+    for (int j = mm; j < nM; ++j) s += Rm[mm * NMX + j] * W[j * ldw + NF];
+    h[mm] = s;
+  }
+  for (int q = tid; q < NMX * NMX; q += nt) R[q] = Rm[q];
+  for (int64_t q = (int64_t)NF * (NF + 1) + NF + NMX * (NF + 1) + NMX + NMX * NMX + tid; q < mstride; q += nt)
+    out[q] = 0.0;
+  __syncthreads();
+  if (tid == 0 && info) info[p] = s_fail;
+}
+
+__global__ void k_philox(int64_t n, const uint32_t* ctr, uint32_t* out, gs_key key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  gs_u4 c = {ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3]};
+  const gs_u4 w = philox4x32_10(c, key.k0, key.k1);
+  out[4 * i] = w.x;
+  out[4 * i + 1] = w.y;
+  out[4 * i + 2] = w.z;
+  out[4 * i + 3] = w.w;
+}
+
+bool nf_supported(int NF) { return NF == 20 || NF == 40 || NF == 60; }
+
+}  // namespace
+
+// ====================================================================== C-ABI
+extern "C" {
+
+int gs_version(void) { return GS_ABI_VERSION; }
+
+const char* gs_last_error(void) { return g_err.c_str(); }
+
+int gs_ctx_create(int device, uint64_t seed, void* stream, gs_ctx** out) {
+  if (!out) return fail_arg(4, "out is NULL");
+  int rc = check_hip(hipSetDevice(device), "hipSetDevice");
+  if (rc) return rc;
+  gs_ctx* c = new gs_ctx;
+  c->device = device;
+  c->stream = (hipStream_t)stream;
+  c->seed = seed;
+  *out = c;
+  return 0;
+}
+
+int gs_ctx_destroy(gs_ctx* ctx) {
+  delete ctx;
+  return 0;
+}
+
+int gs_ctx_set_stream(gs_ctx* ctx, void* stream) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  ctx->stream = (hipStream_t)stream;
+  return 0;
+}
+
+int gs_ctx_set_seed(gs_ctx* ctx, uint64_t seed) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  ctx->seed = seed;
+  return 0;
+}
+
+int64_t gs_model_stride(int NF, int NMX) { return model_stride_doubles(NF, NMX); }
+
+int gs_sweep_lds_bytes(int NF, int NMX) { return (int)(model_stride_doubles(NF, NMX) * 8); }
+
+int gs_tnt(gs_ctx* ctx, int n_psr, int m_max, const gs_tnt_desc* desc, const double* T,
+           const double* Nvec, const double* r, double* TNT, double* d) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0) return fail_arg(2, "n_psr < 0");
+  if (m_max <= 0 || m_max > 4096) return fail_arg(3, "m_max out of range");
+  if (!desc) return fail_arg(4, "desc is NULL");
+  if (!T || !Nvec || !r) return fail_arg(5, "T/Nvec/r is NULL");
+  if (n_psr == 0) return 0;
+  const int nb = (m_max + 15) / 16;
+  if (TNT) {
+    hipLaunchKernelGGL(k_tnt, dim3(n_psr, nb * nb), dim3(256), 0, ctx->stream, desc, nb, T, Nvec, r, TNT);
+    int rc = after_launch("k_tnt");
+    if (rc) return rc;
+  }
+  if (d) {
+    hipLaunchKernelGGL(k_tnr, dim3(n_psr, (m_max + 63) / 64), dim3(256), 0, ctx->stream, desc, T, Nvec, r, d);
+    return after_launch("k_tnr");
+  }
+  return 0;
+}
+
+int gs_prefix(gs_ctx* ctx, int n_psr, int NF, int NMX, const gs_prefix_desc* desc,
+              const double* TNT, const double* d, const int32_t* fidx, const int32_t* midx,
+              const double* phiinv_fixed, double* model, int32_t* info) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0) return fail_arg(2, "n_psr < 0");
+  if (NF <= 0 || NF > 64 || (NF & 1)) return fail_arg(3, "NF must be even and <= 64");
+  if (NMX <= 0 || NMX > 64) return fail_arg(4, "NMX must be in 1..64");
+  if (!desc || !TNT || !d || !fidx || !midx || !phiinv_fixed || !model)
+    return fail_arg(5, "NULL array");
+  if (n_psr == 0) return 0;
+  const size_t lds = ((size_t)NMX * NMX * 2 + (size_t)NMX * (NF + 1)) * sizeof(double);
+  int rc = check_hip(hipFuncSetAttribute((const void*)k_prefix, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds), "hipFuncSetAttribute(k_prefix)");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_prefix, dim3(n_psr), dim3(256), lds, ctx->stream, desc, NF, NMX, TNT, d, fidx,
+                     midx, phiinv_fixed, model, model_stride_doubles(NF, NMX), info);
+  return after_launch("k_prefix");
+}
+
+int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, const double* model,
+             const int32_t* fidx, const int32_t* midx, const int32_t* nm, const double* phiinv_F,
+             const double* z, int64_t sweep, int event, int64_t chain_base, double* b,
+             int32_t* info) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
+  if (!nf_supported(NF)) return fail_arg(4, "NF must be one of 20, 40, 60");
+  if (NMX <= 0 || NMX > 64) return fail_arg(5, "NMX must be in 1..64");
+  if (ldb < NF + 1) return fail_arg(6, "ldb too small");
+  if (!model || !fidx || !midx || !nm || !phiinv_F || !b) return fail_arg(7, "NULL array");
+  if (n_psr == 0 || n_chain == 0) return 0;
+  BdrawArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.ldb = ldb; a.event = event;
+  a.mstride = model_stride_doubles(NF, NMX); a.sweep = sweep; a.chain_base = chain_base;
+  a.model = model; a.fidx = fidx; a.midx = midx; a.nm = nm; a.phiinv_F = phiinv_F; a.z = z;
+  a.b = b; a.info = info; a.key = key_of(ctx);
+  if (launch_bdraw(ctx->stream, a)) return fail_arg(4, "unsupported NF");
+  return after_launch("k_bdraw");
+}
+
+int gs_rho_analytic(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const int32_t* fidx,
+                    const double* b, const double* u, int64_t sweep, int64_t chain_base,
+                    double rhomin, double rhomax, double* x, int ldx) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
+  if (NF <= 0 || (NF & 1)) return fail_arg(4, "NF must be even");
+  if (!fidx || !b || !x) return fail_arg(6, "NULL array");
+  if (!(rhomin > 0.0) || !(rhomax > rhomin)) return fail_arg(11, "need 0 < rhomin < rhomax");
+  if (ldx < NF / 2) return fail_arg(14, "ldx too small");
+  RhoArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.ldb = ldb; a.ldx = ldx; a.sweep = sweep;
+  a.chain_base = chain_base; a.rhomin = rhomin; a.rhomax = rhomax; a.fidx = fidx; a.b = b;
+  a.u = u; a.x = x; a.key = key_of(ctx);
+  launch_rho_analytic(ctx->stream, a);
+  return after_launch("k_rho_analytic");
+}
+
+int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,
+                      const double* model, const int32_t* fidx, const int32_t* midx,
+                      const int32_t* nm, double rhomin, double rhomax, int64_t chain_base,
+                      double* x_state, double* b_state, int64_t it0, int n_sweeps, double* x_rec,
+                      double* b_rec, const double* z0_inj, const double* z_inj,
+                      const double* u_inj, int32_t* info) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
+  if (!nf_supported(NF)) return fail_arg(4, "NF must be one of 20, 40, 60");
+  if (NMX <= 0 || NMX > 64) return fail_arg(5, "NMX must be in 1..64");
+  if (ldb < NF + 1) return fail_arg(6, "ldb too small");
+  if (!model || !fidx || !midx || !nm) return fail_arg(7, "NULL model array");
+  if (!(rhomin > 0.0) || !(rhomax > rhomin)) return fail_arg(11, "need 0 < rhomin < rhomax");
+  if (!x_state || !b_state) return fail_arg(14, "NULL state");
+  if (it0 < 0) return fail_arg(16, "it0 < 0");
+  if (n_sweeps < 0) return fail_arg(17, "n_sweeps < 0");
+  if (n_psr == 0 || n_chain == 0 || n_sweeps == 0) return 0;
+  SweepArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.ldb = ldb; a.n_sweeps = n_sweeps;
+  a.mstride = model_stride_doubles(NF, NMX); a.it0 = it0; a.chain_base = chain_base;
+  a.rhomin = rhomin; a.rhomax = rhomax; a.model = model; a.fidx = fidx; a.midx = midx; a.nm = nm;
+  a.x_state = x_state; a.b_state = b_state; a.x_rec = x_rec; a.b_rec = b_rec;
+  a.z0_inj = z0_inj; a.z_inj = z_inj; a.u_inj = u_inj; a.info = info; a.key = key_of(ctx);
+  if (launch_sweep_freespec(ctx->stream, a)) return fail_arg(4, "unsupported NF");
+  return after_launch("k_sweep_freespec");
+}
+
+int gs_philox(gs_ctx* ctx, int64_t n, const uint32_t* ctr, uint32_t* out) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n < 0) return fail_arg(2, "n < 0");
+  if (!ctr || !out) return fail_arg(3, "NULL array");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_philox, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, n, ctr, out,
+                     key_of(ctx));
+  return after_launch("k_philox");
+}
+
+}  // extern "C"

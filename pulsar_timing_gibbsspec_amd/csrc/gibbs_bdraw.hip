@@ -1,0 +1,316 @@
+// b|rho conditional and the fused free-spectrum sweep (gfx950, fp64).
+//
+// Algorithm: Sigma = TNT + diag(phiinv) is factorised with the
+// fixed-prior columns (timing model, phiinv constant) first.  That prefix of
+// the Cholesky does not change between sweeps, so it is done once per model by
+// gs_prefix; each sweep only factorises the NF x NF Schur block
+// S = S0 + diag(phiinv_F) (NF = 2 n_f <= 64), one wavefront per system:
+//
+//   lane i owns row i of the SYMMETRIC trailing matrix in registers a[0..NF-1].
+//   Right-looking step k: pivot broadcast by v_readlane, lanes > k scale their
+//   a[k] into L[i][k], every lane > k applies a[j] -= L[i][k] L[j][k] for
+//   j > k with L[j][k] broadcast from lane j.  Because the update is applied to
+//   the whole symmetric trailing block, lane i ends up holding row i of L
+//   (a[j<i]) AND, unscaled, column i of L (a[j>i] = L[j][i] L[i][i]), so both
+//   triangular solves are lane-local AXPYs on a broadcast scalar: no LDS, no
+//   shuffles, no barriers.
+//
+// Reference: PulsarBlockGibbs.update_b pulsar_gibbs.py:489-520 (SVD draw);
+// the draw law is identical (b ~ N(Sigma^-1 d, Sigma^-1)); with injected normals
+// rotated by the oracle (z' = L^T U S^-1/2 z) the samples coincide.
+#include "gibbs_common.h"
+#include "gibbs_internal.h"
+
+#ifndef GS_SWEEP_MINW
+#define GS_SWEEP_MINW 2
+#endif
+
+#ifndef GS_BCAST_CHUNK
+#define GS_BCAST_CHUNK 8
+#endif
+
+namespace {
+
+// An SGPR copy of a compile-time index the compiler cannot see through: keeps
+// the per-step lane masks (lane == k, lane > k) from being CSE'd across the
+// fully unrolled factorisation and held live (3 x NF 64-bit masks -> SGPR spills).
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
+struct ModelLds {
+  const double* S0;  // NF x (NF+1)
+  const double* dF;  // NF
+  const double* G;   // NMX x (NF+1)
+  const double* h;   // NMX
+  const double* R;   // NMX x NMX
+};
+
+__device__ __forceinline__ ModelLds model_view(const double* base, int NF, int NMX) {
+  ModelLds m;
+  m.S0 = base;
+  m.dF = m.S0 + NF * (NF + 1);
+  m.G = m.dF + NF;
+  m.h = m.G + NMX * (NF + 1);
+  m.R = m.h + NMX;
+  return m;
+}
+
+// One b|rho draw for the wavefront's system.  Inputs per lane: phinv (lane < NF),
+// zF (lane < NF), zM (lane < nM).  Outputs: bF (lane < NF), bM (lane < nM).
+// Returns the 1-based index of the first non-positive pivot (0 = ok), uniform.
+template <int NF>
+__device__ __forceinline__ int bdraw_wave(const ModelLds& M, int NMX, int nM, int lane,
+                                          double phinv, double zF, double zM, double& bF,
+                                          double& bM) {
+  const bool act = lane < NF;
+  const int row = act ? lane : 0;
+  double a[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const double v = act ? M.S0[row * (NF + 1) + j] : 0.0;
+    a[j] = (opaque(j) == lane) ? v + phinv : v;
+  }
+  // ---- right-looking Cholesky, symmetric trailing update
+  double dinv = 0.0;
+#pragma unroll
+  for (int k = 0; k < NF; ++k) {
+    const int kk = opaque(k);
+    const double piv = rdlane(a[k], k);
+    const double rs = rsqrt(piv);
+    dinv = (lane == kk) ? rs : dinv;
+    const double lk = a[k] * rs;
+    const bool below = lane > kk;
+    const double f = below ? lk : 0.0;
+    a[k] = below ? lk : a[k];
+#pragma unroll
+    for (int j = k + 1; j < NF; ++j) {
+      a[j] = fma(-f, rdlane(a[k], j), a[j]);
+      // bound the broadcasts in flight (each holds 2 SGPRs until its FMA)
+      if (((j - k) % GS_BCAST_CHUNK) == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // first non-positive pivot: lane k's dinv = rsqrt(pivot k) is NaN/inf/<=0
+  const unsigned long long badm = __ballot(act && !(dinv > 0.0 && dinv < __builtin_inf()));
+  const int fail = badm ? (__ffsll((long long)badm)) : 0;
+  // ---- forward solve L y = dF (column AXPY)
+  double r = act ? M.dF[row] : 0.0;
+#pragma unroll
+  for (int k = 0; k < NF; ++k) {
+    const int kk = opaque(k);
+    const double yk = rdlane(r * dinv, k);
+    r = (lane == kk) ? yk : ((lane > kk) ? fma(-a[k], yk, r) : r);
+  }
+  // ---- back solve L^T x = y + zF; lane i < k holds L[k][i] L[i][i] in a[k]
+  const double w = r + zF;
+  double acc = 0.0, gacc = 0.0;
+  const bool actm = lane < nM;
+  const int mrow = actm ? lane : 0;
+#pragma unroll
+  for (int k = NF - 1; k >= 0; --k) {
+    const int kk = opaque(k);
+    const double xk = rdlane((w - dinv * acc) * dinv, k);
+    bF = (lane == kk) ? xk : bF;
+    acc = (lane < kk) ? fma(a[k], xk, acc) : acc;
+    gacc = fma(actm ? M.G[mrow * (NF + 1) + k] : 0.0, xk, gacc);
+  }
+  // ---- fixed-prior block: x_M = h + R z_M - G x_F
+  double v = actm ? M.h[mrow] - gacc : 0.0;
+  for (int j = 0; j < nM; ++j) {
+    const double zj = rdlane(zM, j);
+    v = fma(actm ? M.R[mrow * NMX + j] : 0.0, zj, v);
+  }
+  if (actm) bM = v;
+  return fail;
+}
+
+// Copy a pulsar's model block into LDS (whole workgroup).
+__device__ __forceinline__ void stage_model(double* lds, const double* g, int64_t n) {
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) lds[i] = g[i];
+  __syncthreads();
+}
+
+// ------------------------------------------------------------ batched b draw
+template <int NF, int WPB>
+__global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_bdraw(BdrawArgs A) {
+  extern __shared__ double lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nb = (A.n_chain + WPB - 1) / WPB;
+  const int p = blockIdx.x / nb;
+  const int c = (blockIdx.x % nb) * WPB + wave;
+  stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+  if (c >= A.n_chain) return;
+  const ModelLds M = model_view(lds, NF, A.NMX);
+  const int64_t sys = (int64_t)p * A.n_chain + c;
+  const int nM = A.nm[p];
+  const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
+  const int mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
+  const double phinv = lane < NF ? A.phiinv_F[sys * NF + lane] : 0.0;
+  double zF = 0.0, zM = 0.0;
+  if (A.z) {
+    zF = lane < NF ? A.z[sys * A.ldb + fi] : 0.0;
+    zM = lane < nM ? A.z[sys * A.ldb + mi] : 0.0;
+  } else {
+    gs_normal2(gs_counter(lane, A.sweep, A.chain_base + c, p, A.event), A.key, zF, zM);
+  }
+  double bF = 0.0, bM = 0.0;
+  const int fail = bdraw_wave<NF>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM);
+  if (lane < NF) A.b[sys * A.ldb + fi] = bF;
+  if (lane < nM) A.b[sys * A.ldb + mi] = bM;
+  if (A.info && lane == 0) A.info[sys] = fail;
+}
+
+// ------------------------------------------------------------ fused sweep
+template <int NF, int WPB>
+__global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_sweep_freespec(SweepArgs A) {
+  extern __shared__ double lds[];
+  constexpr int NFR = NF / 2;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nb = (A.n_chain + WPB - 1) / WPB;
+  const int p = blockIdx.x / nb;
+  const int c = (blockIdx.x % nb) * WPB + wave;
+  stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+  if (c >= A.n_chain) return;
+  const ModelLds M = model_view(lds, NF, A.NMX);
+  const int64_t sys = (int64_t)p * A.n_chain + c;
+  const int64_t n_sys = (int64_t)A.n_psr * A.n_chain;
+  const long long gchain = A.chain_base + c;
+  const int nM = A.nm[p];
+  const bool act = lane < NF, actm = lane < nM;
+  const int kf = act ? (lane >> 1) : 0;  // frequency of this lane
+  const int fi = act ? A.fidx[p * NF + lane] : 0;
+  const int mi = actm ? A.midx[p * A.NMX + lane] : 0;
+
+  // state: x replicated on the (sin, cos) lane pair, b split over F/M lanes
+  double x = act ? A.x_state[sys * NFR + kf] : 0.0;
+  double bF = act ? A.b_state[sys * A.ldb + fi] : 0.0;
+  double bM = actm ? A.b_state[sys * A.ldb + mi] : 0.0;
+  int fail = 0;
+
+  const double rhomin = A.rhomin, rhomax = A.rhomax;
+  for (int sw = 0; sw < A.n_sweeps; ++sw) {
+    const long long ii = A.it0 + sw;
+    const int64_t rec = (int64_t)sw * n_sys + sys;
+    // record-before-update (pulsar_gibbs.py:658-659)
+    if (A.x_rec && act && !(lane & 1)) A.x_rec[rec * NFR + kf] = x;
+    if (A.b_rec) {
+      if (act) A.b_rec[rec * A.ldb + fi] = bF;
+      if (actm) A.b_rec[rec * A.ldb + mi] = bM;
+    }
+    // pass 0: first b draw from xs at global sweep 0 (pulsar_gibbs.py:661-662);
+    // pass 1: rho|b then the gated b draw.  One bdraw_wave call site.
+    for (int pass = (ii == 0) ? 0 : 1; pass < 2; ++pass) {
+      const double* zinj = A.z0_inj;
+      int ev = GS_EV_B0;
+      int64_t zrow = sys;
+      if (pass == 1) {
+        // rho|b analytic (pulsar_gibbs.py:208-216, 236)
+        const double partner = __shfl_xor(bF, 1);
+        const double be = (lane & 1) ? partner : bF, bo = (lane & 1) ? bF : partner;
+        const double tau = (be * be + bo * bo) / 2;
+        double U;
+        if (A.u_inj) {
+          U = act ? A.u_inj[rec * NFR + kf] : 0.5;
+        } else {
+          double u2;
+          gs_uniform2(gs_counter(kf, ii, gchain, p, GS_EV_RHO), A.key, U, u2);
+        }
+        const double hi = 1 - exp((tau / rhomax) - (tau / rhomin));
+        const double eta = 0.0 + hi * U;
+        const double rho = tau / ((tau / rhomax) - log(1 - eta));
+        const double xnew = act ? 0.5 * log10(rho) : 0.0;
+        // gate: all(xnew != x_old[-1])  (pulsar_gibbs.py:697)
+        const double xlast = rdlane(x, NF - 1);
+        const bool same = act && (xnew == xlast);
+        const bool gate = __ballot(same) == 0ull;
+        x = xnew;
+        if (!gate) break;
+        zinj = A.z_inj;
+        ev = GS_EV_B;
+        zrow = rec;
+      }
+      double zF, zM;
+      if (zinj) {
+        zF = act ? zinj[zrow * A.ldb + fi] : 0.0;
+        zM = actm ? zinj[zrow * A.ldb + mi] : 0.0;
+      } else {
+        gs_normal2(gs_counter(lane, ii, gchain, p, ev), A.key, zF, zM);
+      }
+      const double phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;
+      const int f = bdraw_wave<NF>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM);
+      if (!fail) fail = f;
+    }
+  }
+  if (act && !(lane & 1)) A.x_state[sys * NFR + kf] = x;
+  if (act) A.b_state[sys * A.ldb + fi] = bF;
+  if (actm) A.b_state[sys * A.ldb + mi] = bM;
+  if (A.info && lane == 0) A.info[sys] = fail;
+}
+
+// ------------------------------------------------------------ rho|b analytic
+__global__ void k_rho_analytic(RhoArgs A) {
+  const int64_t n_sys = (int64_t)A.n_psr * A.n_chain;
+  const int NFR = A.NF / 2;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_sys * NFR) return;
+  const int64_t sys = t / NFR;
+  const int k = (int)(t % NFR);
+  const int p = (int)(sys / A.n_chain), c = (int)(sys % A.n_chain);
+  const double bs = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k]];
+  const double bc = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k + 1]];
+  const double tau = (bs * bs + bc * bc) / 2;
+  double U;
+  if (A.u) {
+    U = A.u[sys * NFR + k];
+  } else {
+    double u2;
+    gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, p, GS_EV_RHO), A.key, U, u2);
+  }
+  const double hi = 1 - exp((tau / A.rhomax) - (tau / A.rhomin));
+  const double eta = 0.0 + hi * U;
+  const double rho = tau / ((tau / A.rhomax) - log(1 - eta));
+  A.x[sys * A.ldx + k] = 0.5 * log10(rho);
+}
+
+template <int WPB>
+int dispatch_nf_sweep(int NF, dim3 grid, size_t lds, hipStream_t s, const SweepArgs& a) {
+  switch (NF) {
+    case 20: hipLaunchKernelGGL((k_sweep_freespec<20, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 40: hipLaunchKernelGGL((k_sweep_freespec<40, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 60: hipLaunchKernelGGL((k_sweep_freespec<60, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    default: return 1;
+  }
+}
+
+template <int WPB>
+int dispatch_nf_bdraw(int NF, dim3 grid, size_t lds, hipStream_t s, const BdrawArgs& a) {
+  switch (NF) {
+    case 20: hipLaunchKernelGGL((k_bdraw<20, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 40: hipLaunchKernelGGL((k_bdraw<40, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 60: hipLaunchKernelGGL((k_bdraw<60, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    default: return 1;
+  }
+}
+
+}  // namespace
+
+int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
+  const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
+  dim3 grid((unsigned)(a.n_psr * nb));
+  return dispatch_nf_sweep<GS_SWEEP_WPB>(a.NF, grid, (size_t)a.mstride * sizeof(double), s, a);
+}
+
+int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
+  const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
+  dim3 grid((unsigned)(a.n_psr * nb));
+  return dispatch_nf_bdraw<GS_SWEEP_WPB>(a.NF, grid, (size_t)a.mstride * sizeof(double), s, a);
+}
+
+int launch_rho_analytic(hipStream_t s, const RhoArgs& a) {
+  const int64_t n = (int64_t)a.n_psr * a.n_chain * (a.NF / 2);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_rho_analytic, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+  return 0;
+}

@@ -1,0 +1,76 @@
+// Shared device helpers for the gfx950 Gibbs kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GS_WAVE 64
+
+// ---------------------------------------------------------------- cross-lane
+// Broadcast lane `l` of a double to every lane (two v_readlane_b32 -> SGPRs).
+__device__ __forceinline__ double rdlane(double v, int l) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u & 0xffffffffull), l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct gs_u4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ gs_u4 philox4x32_10(gs_u4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    gs_u4 n;
+    n.x = hi1 ^ c.y ^ k0;
+    n.y = lo1;
+    n.z = hi0 ^ c.w ^ k1;
+    n.w = lo0;
+    c = n;
+  }
+  return c;
+}
+
+// 53-bit uniform in [0,1) from two words (hi first).
+__device__ __forceinline__ double gs_u53(uint32_t hi, uint32_t lo) {
+  return (double)((((unsigned long long)hi << 32) | lo) >> 11) * 0x1.0p-53;
+}
+
+struct gs_key {
+  uint32_t k0, k1;
+};
+
+__device__ __forceinline__ gs_u4 gs_counter(uint32_t slot, long long sweep, long long chain,
+                                            int psr, int event) {
+  gs_u4 c;
+  c.x = slot;
+  c.y = (uint32_t)sweep;
+  c.z = (uint32_t)chain;
+  c.w = ((uint32_t)psr << 8) | (uint32_t)(event & 0xff);
+  return c;
+}
+
+// Two uniforms in [0,1) for one counter.
+__device__ __forceinline__ void gs_uniform2(gs_u4 c, gs_key k, double& u1, double& u2) {
+  const gs_u4 w = philox4x32_10(c, k.k0, k.k1);
+  u1 = gs_u53(w.x, w.y);
+  u2 = gs_u53(w.z, w.w);
+}
+
+// Two independent standard normals (Box-Muller) for one counter.
+__device__ __forceinline__ void gs_normal2(gs_u4 c, gs_key k, double& n1, double& n2) {
+  double u1, u2;
+  gs_uniform2(c, k, u1, u2);
+  const double r = sqrt(-2.0 * log(1.0 - u1));
+  double s, co;
+  sincospi(2.0 * u2, &s, &co);
+  n1 = r * co;
+  n2 = r * s;
+}

@@ -1,0 +1,55 @@
+// Internal launch-argument structs shared by the kernel TUs and the C-ABI TU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pulsar_gibbs.h"
+#include "gibbs_common.h"
+
+// Wavefronts (systems) per workgroup of the b-draw / sweep kernels: the
+// workgroup shares one LDS copy of its pulsar's model block.
+#ifndef GS_SWEEP_WPB
+#define GS_SWEEP_WPB 4
+#endif
+
+inline int64_t model_stride_doubles(int NF, int NMX) {
+  const int64_t s = (int64_t)NF * (NF + 1) + NF + (int64_t)NMX * (NF + 1) + NMX + (int64_t)NMX * NMX;
+  return (s + 1) & ~int64_t(1);  // 16-byte multiple
+}
+
+struct BdrawArgs {
+  int n_psr, n_chain, NF, NMX, ldb, event;
+  int64_t mstride, sweep, chain_base;
+  const double* model;
+  const int32_t *fidx, *midx, *nm;
+  const double *phiinv_F, *z;
+  double* b;
+  int32_t* info;
+  gs_key key;
+};
+
+struct SweepArgs {
+  int n_psr, n_chain, NF, NMX, ldb, n_sweeps;
+  int64_t mstride, it0, chain_base;
+  double rhomin, rhomax;
+  const double* model;
+  const int32_t *fidx, *midx, *nm;
+  double *x_state, *b_state, *x_rec, *b_rec;
+  const double *z0_inj, *z_inj, *u_inj;
+  int32_t* info;
+  gs_key key;
+};
+
+struct RhoArgs {
+  int n_psr, n_chain, NF, ldb, ldx;
+  int64_t sweep, chain_base;
+  double rhomin, rhomax;
+  const int32_t* fidx;
+  const double *b, *u;
+  double* x;
+  gs_key key;
+};
+
+int launch_sweep_freespec(hipStream_t s, const SweepArgs& a);
+int launch_bdraw(hipStream_t s, const BdrawArgs& a);
+int launch_rho_analytic(hipStream_t s, const RhoArgs& a);

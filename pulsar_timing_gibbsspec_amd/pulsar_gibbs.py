@@ -1,0 +1,294 @@
+"""``PulsarBlockGibbs`` — drop-in for the reference's single-pulsar sampler.
+
+Mirrors ``/root/reference/pulsar_gibbs.py:14-710``: same constructor, same
+parameter plumbing (``params``, ``param_names``, ``map_params``,
+``get_*_indices``), same prior-bound parsing, same basis-index (gwid)
+discovery, same ``update_b`` / ``update_gwrho_params`` / ``sample`` surface and
+the same chain files.  The arithmetic runs on the GPU through the C-ABI:
+
+* ``update_b``           -> gs_bdraw  (Cholesky draw; reference SVD draw :489-520)
+* ``update_gwrho_params`` -> gs_rho_analytic (:206-216) — analytic branch
+* ``sample``             -> gs_sweep_freespec, the whole loop body (:656-698) on device
+
+Extensions (keyword-only, reference-equivalent defaults): ``nchains``
+(independent chains, chain 0 is written in the reference layout), ``device``,
+``seed`` (Philox key).  Models with Metropolis blocks (white noise, power-law
+red noise, ECORR) are outside the device hot path and raise
+``NotImplementedError`` from ``sample``.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from . import _lib
+from .engine import DeviceModel, FreeSpectrumChains
+
+
+def _parse_uniform_bounds(param):
+    """'name:Uniform(pmin=a, pmax=b)[n]' -> (a, b)  (pulsar_gibbs.py:84-87)."""
+    s = str(param).split("(")[1].split(")")[0].split(", ")
+    return float(s[0].split("=")[1]), float(s[1].split("=")[1])
+
+
+class PulsarBlockGibbs(object):
+    """Gibbs-based pulsar-timing periodogram analysis on MI355X.
+
+    van Haasteren & Vallisneri (2014), PRD 90, 104012 (arXiv:1407.1838);
+    blocked Gibbs: b | rho, data and rho | b.
+    """
+
+    def __init__(self, pta, hypersample="conditional", ecorrsample="mh", psr=None, *,
+                 nchains=1, device=0, seed=None):
+        self.pta = pta
+        self.pulsar_name = pta.pulsars[0]
+        self.hypersample = hypersample
+        self.ecorrsample = ecorrsample
+        self.nchains = int(nchains)
+
+        signal_names = [pta.signals[sc].__class__.__name__ for sc in pta.signals]
+        if np.any(["EcorrKernelNoise" in sc for sc in signal_names]):
+            raise TypeError("Gibbs outlier analysis must use basis_ecorr, not kernel ecorr")
+
+        self._residuals = self.pta.get_residuals()[0]
+        xs = [p.sample() for p in pta.params]
+        self._b = np.zeros(self.pta.get_basis(xs)[0].shape[1])
+
+        self.TNT = None
+        self.d = None
+
+        # prior bounds of the free-spectrum powers (pulsar_gibbs.py:82-87)
+        ind = None
+        for ct, par in enumerate([p.name for p in self.params]):
+            if "rho" in par and "gw" in par:
+                ind = ct
+        if ind is None:
+            raise UnboundLocalError("no gw free-spectrum ('gw' ... 'rho') parameter in the PTA")
+        lo, hi = _parse_uniform_bounds(self.params[ind].params[0])
+        self.rhomin, self.rhomax = 10 ** (2 * lo), 10 ** (2 * hi)
+
+        # basis indices of the GW (and ECORR) processes (pulsar_gibbs.py:89-109)
+        ct = 0
+        self.b_param_names = []
+        self.gwid = None
+        self.ecid = None
+        for sig in self.pta.signals:
+            Fmat = self.pta.signals[sig].get_basis()
+            if "gw" in self.pta.signals[sig].name:
+                self.gwid = ct + np.arange(0, Fmat.shape[1])
+            if "ecorr" in self.pta.signals[sig].name:
+                self.ecid = ct + np.arange(0, Fmat.shape[1])
+            if Fmat is not None and "red" not in sig:
+                ct += Fmat.shape[1]
+                self.b_param_names += [sig + "_" + str(ii) for ii in range(Fmat.shape[1])]
+        if ct == self.pta.get_basis()[0].shape[1]:
+            print("Basis count is good")
+        else:
+            print("WARNING: Miscounted basis entries. Maybe red noise and GW do not share a design matrix.")
+
+        self.red_sig = None
+        self.gw_sig = None
+        for sig in self.pta.signals:
+            if "red" in self.pta.signals[sig].name:
+                self.red_sig = self.pta.signals[sig]
+            if "gw" in self.pta.signals[sig].name:
+                self.gw_sig = self.pta.signals[sig]
+
+        # ---- device side
+        self.ctx = _lib.Context(device, seed=np.random.SeedSequence(seed).generate_state(1, np.uint64)[0]
+                                if seed is not None else 0)
+        self._ndraw = 0
+        self._device_model = None
+
+    # ------------------------------------------------------------ plumbing
+    @property
+    def params(self):
+        return [p for p in self.pta.params]
+
+    @property
+    def param_names(self):
+        ret = []
+        for p in self.params:
+            if p.size:
+                for ii in range(0, p.size):
+                    ret.append(p.name + "_{}".format(ii))
+            else:
+                ret.append(p.name)
+        return ret
+
+    def map_params(self, xs):
+        ret = {}
+        ct = 0
+        for p in self.params:
+            n = p.size if p.size else 1
+            ret[p.name] = xs[ct: ct + n] if n > 1 else float(xs[ct])
+            ct += n
+        return ret
+
+    def _indices(self, pred):
+        return np.array([ct for ct, par in enumerate(self.param_names) if pred(par)])
+
+    def get_gwrho_param_indices(self):
+        return self._indices(lambda par: "rho" in par)
+
+    def get_red_param_indices(self):
+        return self._indices(lambda par: "log10_A" in par or "gamma" in par)
+
+    def get_efacequad_indices(self):
+        return self._indices(lambda par: "efac" in par or "equad" in par)
+
+    def get_ecorr_indices(self):
+        return self._indices(lambda par: "ecorr" in par)
+
+    def get_lnprior(self, params):
+        params = params if isinstance(params, dict) else self.map_params(params)
+        return np.sum([p.get_logpdf(params=params) for p in self.params])
+
+    # ------------------------------------------------------------ device model
+    def _model(self, xs):
+        """TNT/d + fixed-prior prefix on device; rebuilt when N changes."""
+        params = self.map_params(xs)
+        Nvec = self.pta.get_ndiag(params)[0]
+        if self._device_model is not None and np.array_equal(Nvec, self._model_N):
+            return self._device_model
+        T = self.pta.get_basis(params)[0]
+        phiinv = self.pta.get_phiinv(params, logdet=False)[0]
+        mask = np.ones(T.shape[1], bool)
+        mask[self.gwid] = False
+        self._device_model = DeviceModel(self.ctx, [T], [Nvec], [self._residuals], [self.gwid],
+                                         [phiinv[mask]])
+        self._model_N = Nvec.copy()
+        self._phfix = phiinv[mask].copy()
+        return self._device_model
+
+    def _phiinv_F(self, xs):
+        params = self.map_params(xs)
+        phiinv = self.pta.get_phiinv(params, logdet=False)[0]
+        mask = np.ones(phiinv.size, bool)
+        mask[self.gwid] = False
+        if self._device_model is not None and not np.array_equal(phiinv[mask], self._phfix):
+            raise NotImplementedError("phiinv of the non-free-spectrum columns changed between draws; "
+                                      "only fixed-prior columns are supported outside gwid")
+        return phiinv[self.gwid]
+
+    # ------------------------------------------------------------ conditionals
+    def update_b(self, xs, z=None):
+        """b | rho, data (pulsar_gibbs.py:489-520) on the GPU.
+
+        ``z`` (optional, length m): standard normals in the Cholesky draw's
+        coordinates (parity mode); default: device Philox."""
+        model = self._model(xs)
+        self.TNT, self.d = model.tnt_host(0)
+        dev = self.ctx.device
+        ph = torch.as_tensor(self._phiinv_F(xs)[None, :], dtype=torch.float64, device=dev)
+        zt = None if z is None else torch.as_tensor(np.asarray(z, float)[None, :model.ldb],
+                                                    dtype=torch.float64, device=dev)
+        b, info = model.bdraw(ph, 1, z=zt, sweep=self._ndraw, event=_lib.EV_USER)
+        self._ndraw += 1
+        if int(info[0]) != 0:
+            raise np.linalg.LinAlgError(f"Sigma not positive definite (leading minor {int(info[0])})")
+        return b[0, :model.m[0]].cpu().numpy()
+
+    def update_gwrho_params(self, xs, u=None):
+        """rho | b (pulsar_gibbs.py:199-268); analytic branch on the GPU."""
+        gwind = self.get_gwrho_param_indices()
+        xnew = xs.copy()
+        if self.hypersample != "conditional":
+            print("ERROR: Only conditional draws on rho for now...")
+            return xnew
+        if self.red_sig is not None:
+            raise NotImplementedError("grid + Gumbel rho|b with intrinsic red noise: use the "
+                                      "device grid kernel (not yet exposed here)")
+        dev = self.ctx.device
+        n_f = len(self.gwid) // 2
+        b = torch.as_tensor(self._b[None, :], dtype=torch.float64, device=dev)
+        fidx = torch.as_tensor(np.asarray(self.gwid, np.int32)[None, :], device=dev)
+        ut = None if u is None else torch.as_tensor(np.asarray(u, float)[None, :], dtype=torch.float64,
+                                                    device=dev)
+        x = torch.empty(1, n_f, dtype=torch.float64, device=dev)
+        _lib.check(self.ctx.lib.gs_rho_analytic(self.ctx.handle, 1, 1, 2 * n_f, b.shape[1], _lib.ptr(fidx),
+                                                _lib.ptr(b), _lib.ptr(ut), self._ndraw, 0, self.rhomin,
+                                                self.rhomax, _lib.ptr(x), n_f), "gs_rho_analytic")
+        self._ndraw += 1
+        xnew[gwind] = x[0].cpu().numpy()
+        return xnew
+
+    # ------------------------------------------------------------ loop
+    def _check_device_loop(self, xs):
+        extra = [n for n in self.param_names if "rho" not in n]
+        if extra or self.red_sig is not None or self.hypersample != "conditional":
+            raise NotImplementedError(
+                "the device sweep covers free-spectrum-only models (analytic rho|b); "
+                f"found Metropolis-sampled parameters {extra[:4]}...")
+        gwind = self.get_gwrho_param_indices()
+        if not np.array_equal(gwind, np.arange(len(self.gwid) // 2)):
+            raise NotImplementedError("gw rho parameters must be the whole parameter vector")
+
+    def sample(self, xs, outdir="./", niter=10000, resume=False, save_every=100):
+        """PulsarBlockGibbs.sample (pulsar_gibbs.py:620-710) as persistent device sweeps.
+
+        Chain row ii holds the state BEFORE sweep ii (row 0 = xs, bchain[0] = 0).
+        Files: pars_chain.txt, pars_bchain.txt, chain.npy, bchain.npy (chain 0,
+        rows [:ii+1] written at ii % 100 == 0, ii > 0, as the reference), and with
+        nchains > 1 also chains.npy / bchains.npy (leading chain axis)."""
+        self._check_device_loop(xs)
+        print(f"Creating chain directory: {outdir}")
+        os.makedirs(outdir, exist_ok=True)
+        np.savetxt(f"{outdir}/pars_chain.txt", self.param_names, fmt="%s")
+        np.savetxt(f"{outdir}/pars_bchain.txt", self.b_param_names, fmt="%s")
+
+        model = self._model(xs)
+        nc = self.nchains
+        self.chain = np.zeros((niter, len(xs)))
+        self.bchain = np.zeros((niter, len(self._b)))
+        self.chains = np.zeros((nc, niter, len(xs))) if nc > 1 else None
+        self.bchains = np.zeros((nc, niter, len(self._b))) if nc > 1 else None
+        self.iter = 0
+        start = 0
+        x0 = np.asarray(xs, float)
+        if resume and os.path.exists(f"{outdir}/chain.npy"):
+            print("Resuming from previous run...")
+            c0 = np.load(f"{outdir}/chain.npy")
+            b0 = np.load(f"{outdir}/bchain.npy")
+            start = min(c0.shape[0], b0.shape[0])
+            self.chain[:start] = c0[:start]
+            self.bchain[:start] = b0[:start]
+        runner = FreeSpectrumChains(model, self.rhomin, self.rhomax, nc, x0)
+        if start > 0:
+            runner.x.copy_(torch.as_tensor(self.chain[start - 1][None, :], device=self.ctx.device)
+                           .expand(nc, -1))
+            runner.b[:, :model.m[0]] = torch.as_tensor(self.bchain[start - 1], device=self.ctx.device)
+            runner.it = start - 1
+            # re-run sweep start-1 so row start-1's successor state is regenerated
+            runner.run(1, record=False)
+        runner.it = max(runner.it, start)
+        m = int(model.m[0])
+        ii = start
+        while ii < niter:
+            nxt = min(niter, (ii // save_every + 1) * save_every + 1)
+            n = nxt - ii
+            xr, br = runner.run(n)
+            xh = xr.cpu().numpy()
+            bh = br[:, :, :m].cpu().numpy()
+            self.chain[ii:nxt] = xh[:, 0]
+            self.bchain[ii:nxt] = bh[:, 0]
+            if nc > 1:
+                self.chains[:, ii:nxt] = np.moveaxis(xh, 1, 0)
+                self.bchains[:, ii:nxt] = np.moveaxis(bh, 1, 0)
+            ii = nxt
+            self.iter = ii - 1
+            last = ii - 1
+            if last % save_every == 0 and last > 0:
+                np.save(f"{outdir}/chain.npy", self.chain[:last + 1, :])
+                np.save(f"{outdir}/bchain.npy", self.bchain[:last + 1, :])
+                if nc > 1:
+                    np.save(f"{outdir}/chains.npy", self.chains[:, :last + 1])
+                    np.save(f"{outdir}/bchains.npy", self.bchains[:, :last + 1])
+        info = runner.info.cpu().numpy()
+        if info.any():
+            print(f"WARNING: {int((info != 0).sum())} chains hit a non-positive-definite Sigma")
+        self._b = runner.b[0, :m].cpu().numpy()
+        self._runner = runner
+        return self.chain

@@ -1,0 +1,388 @@
+"""Minimal enterprise-compatible PTA facade + synthetic pulsar-timing arrays.
+
+The Gibbs samplers consume an enterprise ``PTA`` duck-typed (SURVEY.md §8b,
+"PTA contract consumed").  enterprise/tempo2 are not installed here or on the
+GPU box, so this module restates the parts of that contract the sampler
+touches:
+
+* ``Uniform`` parameters whose ``str()`` is ``"name:Uniform(pmin=a, pmax=b)[n]"``
+  -- the reference parses prior bounds out of that string
+  (``pulsar_gibbs.py:84-87``, ``pta_gibbs.py:83-94``);
+* Fourier GP signals (sin at even, cos at odd columns, f_k = k/Tspan), with a
+  free-spectrum PSD ``phi = repeat(10**(2*log10_rho), 2)`` or a power-law PSD;
+  GP signals on the same frequencies share basis columns and their phi add
+  (the reference assumes this: ``pulsar_gibbs.py:101-103``);
+* a timing-model GP with phi = 1e40 (phiinv = 1e-40) on an orthonormalised
+  (``use_svd``) or column-normalised design matrix;
+* white noise ``N = efac^2 sigma^2 + 10**(2 log10_tnequad)``;
+* the PTA getters ``get_residuals/get_basis/get_ndiag/get_phiinv`` (lists,
+  one entry per pulsar), ``params`` sorted by name, ordered ``signals``.
+
+The enterprise behaviours restated here are *[upstream, not vendored]*; the
+reference consumes them only through T, N, phiinv and r, which
+is where parity is pinned.
+"""
+from __future__ import annotations
+
+import os
+from collections import OrderedDict
+
+import numpy as np
+
+FYR = 1.0 / (365.25 * 86400.0)
+DAY = 86400.0
+_DATA = os.path.join(os.path.dirname(__file__), "data", "simulated_array.npz")
+
+
+# --------------------------------------------------------------------------- params
+class Uniform:
+    """Uniform prior parameter (scalar or vector of ``size``)."""
+
+    def __init__(self, name, pmin, pmax, size=None, rng=None):
+        self.name = name
+        self.pmin = pmin
+        self.pmax = pmax
+        self.size = size
+        self._rng = rng if rng is not None else np.random.default_rng(12345)
+
+    @property
+    def params(self):
+        return [self]
+
+    def sample(self):
+        v = self._rng.uniform(self.pmin, self.pmax, size=self.size)
+        return v if self.size else np.float64(v)
+
+    def get_logpdf(self, value=None, params=None):
+        if params is not None:
+            value = params[self.name]
+        v = np.atleast_1d(np.asarray(value, dtype=float))
+        inside = np.all((v >= self.pmin) & (v <= self.pmax))
+        return float(-v.size * np.log(self.pmax - self.pmin)) if inside else -np.inf
+
+    def _fmt(self, v):
+        return repr(int(v)) if float(v).is_integer() else repr(float(v))
+
+    def __repr__(self):
+        s = f"{self.name}:Uniform(pmin={self._fmt(self.pmin)}, pmax={self._fmt(self.pmax)})"
+        return s + (f"[{self.size}]" if self.size else "")
+
+    __str__ = __repr__
+
+
+def _value(params, p):
+    v = params[p.name]
+    return np.asarray(v, dtype=float)
+
+
+# --------------------------------------------------------------------------- signals
+def fourier_basis(toas_s, n_f, Tspan):
+    """sin/cos Fourier design matrix, f_k = k/Tspan, k=1..n_f (sin even, cos odd)."""
+    f = np.arange(1, n_f + 1) / Tspan
+    arg = 2.0 * np.pi * toas_s[:, None] * f[None, :]
+    F = np.empty((toas_s.size, 2 * n_f))
+    F[:, ::2] = np.sin(arg)
+    F[:, 1::2] = np.cos(arg)
+    return F, f
+
+
+def powerlaw_phi(f, Tspan, log10_A, gamma):
+    df = 1.0 / Tspan
+    return (10.0 ** log10_A) ** 2 / 12.0 / np.pi ** 2 * FYR ** (gamma - 3) * f ** (-gamma) * df
+
+
+class FourierGP:
+    """GP on a Fourier basis with a free-spectrum or power-law PSD."""
+
+    def __init__(self, psrname, name, toas_s, Tspan, n_f, psd="spectrum", params=()):
+        self.psrname = psrname
+        self.name = name
+        self.signal_id = f"{psrname}_{name}"
+        self.psd = psd
+        self.Tspan = float(Tspan)
+        self.n_f = n_f
+        self._F, self.freqs = fourier_basis(toas_s, n_f, Tspan)
+        self.basis_key = ("fourier", n_f, round(self.Tspan, 3))
+        self.params = list(params)
+
+    def get_basis(self, params=None):
+        return self._F
+
+    def get_phi(self, params):
+        if self.psd == "spectrum":
+            rho = _value(params, self.params[0])
+            return np.repeat(10.0 ** (2.0 * rho), 2)
+        la = _value(params, self.params[0])
+        ga = _value(params, self.params[1])
+        return np.repeat(powerlaw_phi(self.freqs, self.Tspan, la, ga), 2)
+
+
+class TimingModelGP:
+    """Linear timing model as a GP with an (effectively) improper prior, phi = 1e40."""
+
+    def __init__(self, psrname, M, use_svd=True):
+        self.psrname = psrname
+        self.name = "linear_timing_model"
+        self.signal_id = f"{psrname}_{self.name}"
+        if use_svd:
+            self._M = np.linalg.svd(M, full_matrices=False)[0]
+        else:
+            self._M = M / np.linalg.norm(M, axis=0)
+        self.basis_key = ("tm", psrname)
+        self.params = []
+
+    def get_basis(self, params=None):
+        return self._M
+
+    def get_phi(self, params):
+        return 1e40 * np.ones(self._M.shape[1])
+
+
+class MeasurementNoise:
+    """White noise: N = efac^2 sigma^2 + 10**(2 log10_tnequad), per backend."""
+
+    def __init__(self, psrname, sigma, backends=None, efac=None, equad=None):
+        self.psrname = psrname
+        self.name = "measurement_noise"
+        self.signal_id = f"{psrname}_{self.name}"
+        self.sigma = np.asarray(sigma, dtype=float)
+        self.backends = (np.zeros(self.sigma.size, dtype=np.int64) if backends is None
+                         else np.asarray(backends, dtype=np.int64))
+        self.efac = list(efac or [])     # one Uniform per backend (or empty: efac = 1)
+        self.equad = list(equad or [])
+        self.params = self.efac + self.equad
+        self.basis_key = None
+
+    def get_basis(self, params=None):
+        return None
+
+    def get_phi(self, params):
+        return None
+
+    def backend_values(self, params):
+        nb = int(self.backends.max()) + 1
+        ef = np.ones(nb)
+        eq = np.zeros(nb)
+        for i, p in enumerate(self.efac):
+            ef[i] = float(_value(params, p))
+        for i, p in enumerate(self.equad):
+            eq[i] = 10.0 ** (2.0 * float(_value(params, p)))
+        return ef, eq
+
+    def get_ndiag(self, params):
+        ef, eq = self.backend_values(params)
+        return ef[self.backends] ** 2 * self.sigma ** 2 + eq[self.backends]
+
+
+# --------------------------------------------------------------------------- models
+class PulsarModel:
+    """Signal collection of one pulsar (enterprise SignalCollection analogue)."""
+
+    def __init__(self, psrname, toas_s, residuals, signals):
+        self.psrname = psrname
+        self.toas = toas_s
+        self.residuals = np.asarray(residuals, dtype=float)
+        self.signals = list(signals)
+        # column blocks: GP signals with the same basis_key share columns
+        self._blocks = OrderedDict()
+        for s in self.signals:
+            if s.basis_key is None:
+                continue
+            self._blocks.setdefault(s.basis_key, []).append(s)
+        self._T = np.hstack([b[0].get_basis() for b in self._blocks.values()])
+        self.white = [s for s in self.signals if isinstance(s, MeasurementNoise)]
+
+    def get_basis(self, params=None):
+        return self._T
+
+    def get_phi(self, params):
+        return np.concatenate([np.sum([s.get_phi(params) for s in sigs], axis=0)
+                               for sigs in self._blocks.values()])
+
+    def get_ndiag(self, params):
+        return np.sum([w.get_ndiag(params) for w in self.white], axis=0)
+
+
+class PTA:
+    """enterprise-``PTA``-shaped container over ``PulsarModel`` s."""
+
+    def __init__(self, models):
+        self.models = list(models)
+        self.pulsars = [m.psrname for m in self.models]
+        sig = OrderedDict()
+        for m in self.models:
+            for s in m.signals:
+                sig[s.signal_id] = s
+        self._signal_dict = sig
+        pars = {}
+        for m in self.models:
+            for s in m.signals:
+                for p in s.params:
+                    pars[p.name] = p
+        self._params = [pars[k] for k in sorted(pars)]
+
+    @property
+    def params(self):
+        return list(self._params)
+
+    @property
+    def param_names(self):
+        out = []
+        for p in self._params:
+            out += [f"{p.name}_{i}" for i in range(p.size)] if p.size else [p.name]
+        return out
+
+    @property
+    def signals(self):
+        return self._signal_dict
+
+    def map_params(self, xs):
+        ret, ct = {}, 0
+        for p in self._params:
+            n = p.size if p.size else 1
+            ret[p.name] = xs[ct:ct + n] if n > 1 else float(xs[ct])
+            ct += n
+        return ret
+
+    def _as_dict(self, params):
+        if isinstance(params, dict):
+            return params
+        if params is None:
+            return None
+        flat = np.concatenate([np.atleast_1d(np.asarray(v, dtype=float)) for v in params])
+        return self.map_params(flat)
+
+    def get_residuals(self):
+        return [m.residuals for m in self.models]
+
+    def get_basis(self, params=None):
+        return [m.get_basis() for m in self.models]
+
+    def get_ndiag(self, params=None):
+        params = self._as_dict(params) or {}
+        return [m.get_ndiag(params) for m in self.models]
+
+    def get_phi(self, params):
+        params = self._as_dict(params)
+        return [m.get_phi(params) for m in self.models]
+
+    def get_phiinv(self, params, logdet=False):
+        phis = self.get_phi(params)
+        if logdet:
+            return [(1.0 / p, float(np.sum(np.log(p)))) for p in phis]
+        return [1.0 / p for p in phis]
+
+
+# --------------------------------------------------------------------------- data
+def load_simulated_array():
+    """The 45 simulated pulsars (TOA epochs in MJD, errors in us, n fitted params)."""
+    d = np.load(_DATA, allow_pickle=False)
+    names = [str(n) for n in d["names"]]
+    out = OrderedDict()
+    o = d["offsets"]
+    for i, n in enumerate(names):
+        out[n] = dict(mjd=d["mjd"][o[i]:o[i + 1]], err_us=d["err_us"][o[i]:o[i + 1]],
+                      nfit=int(d["nfit"][i]), pb_days=float(d["pb_days"][i]))
+    return out
+
+
+def synthetic_design_matrix(toas_s, n_cols, pb_days=0.0):
+    """Deterministic stand-in for a tempo2 design matrix (offset, spin, astrometry, binary)."""
+    t = toas_s - toas_s.mean()
+    tn = t / np.max(np.abs(t))
+    wy = 2.0 * np.pi * FYR
+    pb = pb_days * DAY if pb_days > 0 else 0.4 / FYR  # isolated: a slow extra harmonic
+    wb = 2.0 * np.pi / pb
+    cols = [np.ones_like(t), tn, tn ** 2,
+            np.sin(wy * t), np.cos(wy * t), tn * np.sin(wy * t), tn * np.cos(wy * t),
+            np.sin(2 * wy * t), np.cos(2 * wy * t),
+            np.sin(wb * t), np.cos(wb * t), np.sin(2 * wb * t), np.cos(2 * wb * t),
+            tn * np.sin(wb * t), tn * np.cos(wb * t), tn ** 3,
+            np.sin(3 * wb * t), np.cos(3 * wb * t), tn ** 4, np.sin(3 * wy * t)]
+    if n_cols > len(cols):
+        raise ValueError(f"at most {len(cols)} synthetic timing-model columns")
+    return np.stack(cols[:n_cols], axis=1)
+
+
+def _simulate_residuals(rng, F, f, Tspan, M, sigma, log10_A, gamma, red=None):
+    phi = np.repeat(powerlaw_phi(f, Tspan, log10_A, gamma), 2)
+    if red is not None:
+        phi = phi + np.repeat(powerlaw_phi(f, Tspan, red[0], red[1]), 2)
+    a = rng.standard_normal(F.shape[1]) * np.sqrt(phi)
+    c = rng.standard_normal(M.shape[1]) * 1e-8
+    return F @ a + M @ c + sigma * rng.standard_normal(sigma.size)
+
+
+def single_pulsar_pta(psr="J1713+0747", n_f=30, rho_prior=(-9.0, -4.0), log10_A=np.log10(2e-15),
+                      gamma=13.0 / 3.0, seed=0, tm_svd=True, n_toa=None, efac_vary=False,
+                      n_backends=1, tm_cols=None, powerlaw_red=False):
+    """Config 1 model: ``ef + gw free spectrum + tm`` (singlepulsar…ipynb:137-150).
+
+    Signal order (white, gw, TM) gives T = [F | M] and gwid = 0..2 n_f - 1.
+    ``n_toa`` > the data's TOA count synthesises a uniform-cadence pulsar (config 5).
+    """
+    rng = np.random.default_rng(seed)
+    if n_toa is None:
+        d = load_simulated_array()[psr]
+        mjd, err = d["mjd"], d["err_us"] * 1e-6
+        ncol = (d["nfit"] + 1) if tm_cols is None else tm_cols
+        pb = d["pb_days"]
+    else:
+        mjd = np.sort(53000.0 + rng.uniform(0, 15 * 365.25, n_toa))
+        err = 10 ** rng.uniform(np.log10(5e-8), np.log10(5e-6), n_toa)
+        ncol = 16 if tm_cols is None else tm_cols
+        pb = 10 ** rng.uniform(0, 2)
+    toas = mjd * DAY
+    Tspan = toas.max() - toas.min()
+    backends = np.arange(toas.size) % n_backends
+    efp = [Uniform(f"{psr}_b{i}_efac", 0.1, 5.0) for i in range(n_backends)] if efac_vary else []
+    eqp = [Uniform(f"{psr}_b{i}_log10_tnequad", -8.5, -5.0) for i in range(n_backends)] \
+        if efac_vary else []
+    white = MeasurementNoise(psr, err, backends, efp, eqp)
+    rho = Uniform("gw_log10_rho", rho_prior[0], rho_prior[1], size=n_f)
+    gw = FourierGP(psr, "gw", toas, Tspan, n_f, "spectrum", [rho])
+    sigs = [white, gw]
+    if powerlaw_red:
+        la = Uniform("red_log10_A", -20.0, -11.0)
+        ga = Uniform("red_gamma", 0.0, 7.0)
+        sigs.append(FourierGP(psr, "red", toas, Tspan, n_f, "powerlaw", [la, ga]))
+    M = synthetic_design_matrix(toas, ncol, pb)
+    tm = TimingModelGP(psr, M, use_svd=tm_svd)
+    sigs.append(tm)
+    r = _simulate_residuals(rng, gw.get_basis(), gw.freqs, Tspan, tm.get_basis(), err,
+                            log10_A, gamma)
+    return PTA([PulsarModel(psr, toas, r, sigs)])
+
+
+def array_pta(kind="curn_red", n_f=30, n_psr=None, gw_prior=(-9.0, -4.0), red_prior=(-10.0, -4.0),
+              log10_A=np.log10(2e-15), gamma=13.0 / 3.0, seed=0):
+    """Config 3/4 models over the simulated array (model_definition.py:184-234 order: TM, CRN, red, white).
+
+    kind = 'curn'      common 'gw_crn' free spectrum only,
+           'curn_red'  + per-pulsar 'red_noise' free spectrum on the same basis.
+    Common Tspan = the array's span (model_utils.get_tspan).
+    """
+    rng = np.random.default_rng(seed)
+    data = load_simulated_array()
+    names = sorted(data)[: n_psr or len(data)]
+    tmin = min(data[n]["mjd"].min() for n in names) * DAY
+    tmax = max(data[n]["mjd"].max() for n in names) * DAY
+    Tspan = tmax - tmin
+    crn = Uniform("gw_crn_log10_rho", gw_prior[0], gw_prior[1], size=n_f)
+    models = []
+    for n in names:
+        d = data[n]
+        toas = d["mjd"] * DAY
+        err = d["err_us"] * 1e-6
+        M = synthetic_design_matrix(toas, d["nfit"] + 1, d["pb_days"])
+        tm = TimingModelGP(n, M, use_svd=False)
+        gw = FourierGP(n, "gw_crn", toas, Tspan, n_f, "spectrum", [crn])
+        sigs = [tm, gw]
+        if kind == "curn_red":
+            rp = Uniform(f"{n}_red_noise_log10_rho", red_prior[0], red_prior[1], size=n_f)
+            sigs.append(FourierGP(n, "red_noise", toas, Tspan, n_f, "spectrum", [rp]))
+        sigs.append(MeasurementNoise(n, err))
+        r = _simulate_residuals(rng, gw.get_basis(), gw.freqs, Tspan, tm.get_basis(), err,
+                                log10_A, gamma, red=(-14.5, 3.0) if kind == "curn_red" else None)
+        models.append(PulsarModel(n, toas, r, sigs))
+    return PTA(models)
