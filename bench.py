@@ -98,6 +98,7 @@ def main():
     ap.add_argument("--sweeps-per-launch", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--bcast", type=int, default=None, help="GS_OPT_BCAST (0 readlane, 1 LDS)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,6 +117,8 @@ def main():
     T, N, r = pta.get_basis()[0], pta.get_ndiag({})[0], pta.get_residuals()[0]
     gwid = np.arange(60)
     ctx = _lib.Context(local, seed=20251015)
+    if args.bcast is not None:
+        ctx.set_option(_lib.OPT_BCAST, args.bcast)
     model = DeviceModel(ctx, [T], [N], [r], [gwid], [np.full(T.shape[1] - 60, 1e-40)])
     C = args.chains
     x0 = np.random.default_rng(rank).uniform(-9, -4, (C, 30))
@@ -183,7 +186,8 @@ def main():
             "config": {"workload": "configs[1]: J1713+0747 sim (720 TOAs, m=76, 30-bin free spectrum), "
                                    f"{C} independent chains per GPU", "chains_per_gpu": C,
                        "global_chains": total_chains, "m": m, "n_f": 30,
-                       "sweeps_per_launch": S, "parallelism": f"chains sharded over {world} GPU(s)"},
+                       "sweeps_per_launch": S, "bcast": ctx.get_option(_lib.OPT_BCAST),
+                       "parallelism": f"chains sharded over {world} GPU(s)"},
             "ess_per_s": ess,
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,

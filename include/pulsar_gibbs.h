@@ -47,6 +47,11 @@ enum {
   GS_EV_USER = 16   /* first id free for callers                                    */
 };
 
+/* Context options (gs_ctx_set_option) */
+enum {
+  GS_OPT_BCAST = 1 /* factorisation broadcast: 0 = v_readlane -> SGPR (default), 1 = LDS */
+};
+
 typedef struct gs_ctx gs_ctx;
 
 /* Ragged-batch descriptor for gs_tnt (one per pulsar, int64 fields, device). */
@@ -74,10 +79,12 @@ int gs_ctx_create(int device, uint64_t seed, void* hip_stream, gs_ctx** out);
 int gs_ctx_destroy(gs_ctx* ctx);
 int gs_ctx_set_stream(gs_ctx* ctx, void* hip_stream);
 int gs_ctx_set_seed(gs_ctx* ctx, uint64_t seed);
+int gs_ctx_set_option(gs_ctx* ctx, int option, int value);
+int gs_ctx_get_option(gs_ctx* ctx, int option); /* -1 on unknown option / NULL ctx */
 
 /* Doubles per pulsar in a model buffer (see gs_prefix). */
 int64_t gs_model_stride(int NF, int NMX);
-/* Dynamic LDS bytes / waves per workgroup the sweep kernel uses for (NF, NMX). */
+/* Dynamic LDS bytes per workgroup of the b-draw / sweep kernels for (NF, NMX). */
 int gs_sweep_lds_bytes(int NF, int NMX);
 
 /*

@@ -17,6 +17,7 @@ import torch  # noqa: F401  (must precede the CDLL load; see module docstring)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpulsar_gibbs.so")
 
+OPT_BCAST = 1
 EV_B0, EV_RHO, EV_B, EV_RED, EV_CURN, EV_GUMBEL, EV_USER = 1, 2, 3, 4, 5, 6, 16
 
 _P = C.c_void_p
@@ -32,6 +33,8 @@ SIGNATURES = {
     "gs_ctx_destroy": (_I, [_P]),
     "gs_ctx_set_stream": (_I, [_P, _P]),
     "gs_ctx_set_seed": (_I, [_P, C.c_uint64]),
+    "gs_ctx_set_option": (_I, [_P, _I, _I]),
+    "gs_ctx_get_option": (_I, [_P, _I]),
     "gs_model_stride": (_I64, [_I, _I]),
     "gs_sweep_lds_bytes": (_I, [_I, _I]),
     "gs_tnt": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
@@ -105,6 +108,12 @@ class Context:
     def set_seed(self, seed):
         self.seed = int(seed)
         check(self.lib.gs_ctx_set_seed(self.handle, C.c_uint64(self.seed)), "gs_ctx_set_seed")
+
+    def set_option(self, option, value):
+        check(self.lib.gs_ctx_set_option(self.handle, int(option), int(value)), "gs_ctx_set_option")
+
+    def get_option(self, option):
+        return int(self.lib.gs_ctx_get_option(self.handle, int(option)))
 
     def set_stream(self, stream):
         self.stream = stream

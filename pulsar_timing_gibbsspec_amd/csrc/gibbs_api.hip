@@ -10,6 +10,7 @@ struct gs_ctx {
   int device;
   hipStream_t stream;
   uint64_t seed;
+  int bcast;  // GS_OPT_BCAST: 0 = v_readlane, 1 = LDS broadcast
 };
 
 namespace {
@@ -237,6 +238,7 @@ int gs_ctx_create(int device, uint64_t seed, void* stream, gs_ctx** out) {
   c->device = device;
   c->stream = (hipStream_t)stream;
   c->seed = seed;
+  c->bcast = 0;
   *out = c;
   return 0;
 }
@@ -258,9 +260,28 @@ int gs_ctx_set_seed(gs_ctx* ctx, uint64_t seed) {
   return 0;
 }
 
+int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  switch (option) {
+    case GS_OPT_BCAST:
+      if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_BCAST must be 0 or 1");
+      ctx->bcast = value;
+      return 0;
+    default:
+      return fail_arg(2, "unknown option");
+  }
+}
+
+int gs_ctx_get_option(gs_ctx* ctx, int option) {
+  if (!ctx) return -1;
+  return option == GS_OPT_BCAST ? ctx->bcast : -1;
+}
+
 int64_t gs_model_stride(int NF, int NMX) { return model_stride_doubles(NF, NMX); }
 
-int gs_sweep_lds_bytes(int NF, int NMX) { return (int)(model_stride_doubles(NF, NMX) * 8); }
+int gs_sweep_lds_bytes(int NF, int NMX) {
+  return (int)((model_stride_doubles(NF, NMX) + 64 * GS_SWEEP_WPB) * 8);
+}
 
 int gs_tnt(gs_ctx* ctx, int n_psr, int m_max, const gs_tnt_desc* desc, const double* T,
            const double* Nvec, const double* r, double* TNT, double* d) {
@@ -317,7 +338,7 @@ int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, cons
   a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.ldb = ldb; a.event = event;
   a.mstride = model_stride_doubles(NF, NMX); a.sweep = sweep; a.chain_base = chain_base;
   a.model = model; a.fidx = fidx; a.midx = midx; a.nm = nm; a.phiinv_F = phiinv_F; a.z = z;
-  a.b = b; a.info = info; a.key = key_of(ctx);
+  a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = ctx->bcast;
   if (launch_bdraw(ctx->stream, a)) return fail_arg(4, "unsupported NF");
   return after_launch("k_bdraw");
 }
@@ -362,6 +383,7 @@ int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.rhomin = rhomin; a.rhomax = rhomax; a.model = model; a.fidx = fidx; a.midx = midx; a.nm = nm;
   a.x_state = x_state; a.b_state = b_state; a.x_rec = x_rec; a.b_rec = b_rec;
   a.z0_inj = z0_inj; a.z_inj = z_inj; a.u_inj = u_inj; a.info = info; a.key = key_of(ctx);
+  a.bcast = ctx->bcast;
   if (launch_sweep_freespec(ctx->stream, a)) return fail_arg(4, "unsupported NF");
   return after_launch("k_sweep_freespec");
 }

@@ -25,6 +25,9 @@
 #define GS_SWEEP_MINW 2
 #endif
 
+#define GS_BCAST_READLANE 0
+#define GS_BCAST_LDS 1
+
 #ifndef GS_BCAST_CHUNK
 #define GS_BCAST_CHUNK 8
 #endif
@@ -60,10 +63,10 @@ __device__ __forceinline__ ModelLds model_view(const double* base, int NF, int N
 // One b|rho draw for the wavefront's system.  Inputs per lane: phinv (lane < NF),
 // zF (lane < NF), zM (lane < nM).  Outputs: bF (lane < NF), bM (lane < nM).
 // Returns the 1-based index of the first non-positive pivot (0 = ok), uniform.
-template <int NF>
+template <int NF, int BC>
 __device__ __forceinline__ int bdraw_wave(const ModelLds& M, int NMX, int nM, int lane,
                                           double phinv, double zF, double zM, double& bF,
-                                          double& bM) {
+                                          double& bM, double* __restrict__ scr) {
   const bool act = lane < NF;
   const int row = act ? lane : 0;
   double a[NF];
@@ -84,11 +87,26 @@ __device__ __forceinline__ int bdraw_wave(const ModelLds& M, int NMX, int nM, in
     const bool below = lane > kk;
     const double f = below ? lk : 0.0;
     a[k] = below ? lk : a[k];
+    if constexpr (BC == GS_BCAST_READLANE) {
 #pragma unroll
-    for (int j = k + 1; j < NF; ++j) {
-      a[j] = fma(-f, rdlane(a[k], j), a[j]);
-      // bound the broadcasts in flight (each holds 2 SGPRs until its FMA)
-      if (((j - k) % GS_BCAST_CHUNK) == 0) __builtin_amdgcn_sched_barrier(0);
+      for (int j = k + 1; j < NF; ++j) {
+        a[j] = fma(-f, rdlane(a[k], j), a[j]);
+        // bound the broadcasts in flight (each holds 2 SGPRs until its FMA)
+        if (((j - k) % GS_BCAST_CHUNK) == 0) __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+      // column k through the wave's LDS slot: one ds_write_b64 per lane, then
+      // same-address (broadcast) ds_read_b128 pairs; DS ops of a wave are in order.
+      scr[lane] = f;
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = (k + 1) & ~1; j < NF; j += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(scr + j);
+        if (j > k) a[j] = fma(-f, v.x, a[j]);
+        a[j + 1] = fma(-f, v.y, a[j + 1]);
+        if ((((j - k) >> 1) % (GS_BCAST_CHUNK / 2)) == 0) __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_wave_barrier();
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -133,7 +151,7 @@ __device__ __forceinline__ void stage_model(double* lds, const double* g, int64_
 }
 
 // ------------------------------------------------------------ batched b draw
-template <int NF, int WPB>
+template <int NF, int WPB, int BC>
 __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_bdraw(BdrawArgs A) {
   extern __shared__ double lds[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -156,14 +174,15 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_bdraw(BdrawArgs A) 
     gs_normal2(gs_counter(lane, A.sweep, A.chain_base + c, p, A.event), A.key, zF, zM);
   }
   double bF = 0.0, bM = 0.0;
-  const int fail = bdraw_wave<NF>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM);
+  double* scr = lds + A.mstride + wave * 64;
+  const int fail = bdraw_wave<NF, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
   if (lane < NF) A.b[sys * A.ldb + fi] = bF;
   if (lane < nM) A.b[sys * A.ldb + mi] = bM;
   if (A.info && lane == 0) A.info[sys] = fail;
 }
 
 // ------------------------------------------------------------ fused sweep
-template <int NF, int WPB>
+template <int NF, int WPB, int BC>
 __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_sweep_freespec(SweepArgs A) {
   extern __shared__ double lds[];
   constexpr int NFR = NF / 2;
@@ -182,6 +201,7 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_sweep_freespec(Swee
   const int kf = act ? (lane >> 1) : 0;  // frequency of this lane
   const int fi = act ? A.fidx[p * NF + lane] : 0;
   const int mi = actm ? A.midx[p * A.NMX + lane] : 0;
+  double* scr = lds + A.mstride + wave * 64;
 
   // state: x replicated on the (sin, cos) lane pair, b split over F/M lanes
   double x = act ? A.x_state[sys * NFR + kf] : 0.0;
@@ -239,7 +259,7 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_sweep_freespec(Swee
         gs_normal2(gs_counter(lane, ii, gchain, p, ev), A.key, zF, zM);
       }
       const double phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;
-      const int f = bdraw_wave<NF>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM);
+      const int f = bdraw_wave<NF, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
       if (!fail) fail = f;
     }
   }
@@ -274,24 +294,25 @@ __global__ void k_rho_analytic(RhoArgs A) {
   A.x[sys * A.ldx + k] = 0.5 * log10(rho);
 }
 
-template <int WPB>
-int dispatch_nf_sweep(int NF, dim3 grid, size_t lds, hipStream_t s, const SweepArgs& a) {
-  switch (NF) {
-    case 20: hipLaunchKernelGGL((k_sweep_freespec<20, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    case 40: hipLaunchKernelGGL((k_sweep_freespec<40, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    case 60: hipLaunchKernelGGL((k_sweep_freespec<60, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    default: return 1;
+#define GS_NF_CASES(KERNEL, ARGS)                                                            \
+  switch (NF * 2 + bc) {                                                                     \
+    case 40: hipLaunchKernelGGL((KERNEL<20, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 41: hipLaunchKernelGGL((KERNEL<20, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 80: hipLaunchKernelGGL((KERNEL<40, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 81: hipLaunchKernelGGL((KERNEL<40, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 120: hipLaunchKernelGGL((KERNEL<60, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 121: hipLaunchKernelGGL((KERNEL<60, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    default: return 1;                                                                       \
   }
+
+template <int WPB>
+int dispatch_nf_sweep(int NF, int bc, dim3 grid, size_t lds, hipStream_t s, const SweepArgs& a) {
+  GS_NF_CASES(k_sweep_freespec, a)
 }
 
 template <int WPB>
-int dispatch_nf_bdraw(int NF, dim3 grid, size_t lds, hipStream_t s, const BdrawArgs& a) {
-  switch (NF) {
-    case 20: hipLaunchKernelGGL((k_bdraw<20, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    case 40: hipLaunchKernelGGL((k_bdraw<40, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    case 60: hipLaunchKernelGGL((k_bdraw<60, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    default: return 1;
-  }
+int dispatch_nf_bdraw(int NF, int bc, dim3 grid, size_t lds, hipStream_t s, const BdrawArgs& a) {
+  GS_NF_CASES(k_bdraw, a)
 }
 
 }  // namespace
@@ -299,13 +320,15 @@ int dispatch_nf_bdraw(int NF, dim3 grid, size_t lds, hipStream_t s, const BdrawA
 int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
-  return dispatch_nf_sweep<GS_SWEEP_WPB>(a.NF, grid, (size_t)a.mstride * sizeof(double), s, a);
+  const size_t lds = ((size_t)a.mstride + 64 * GS_SWEEP_WPB) * sizeof(double);
+  return dispatch_nf_sweep<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
 
 int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
-  return dispatch_nf_bdraw<GS_SWEEP_WPB>(a.NF, grid, (size_t)a.mstride * sizeof(double), s, a);
+  const size_t lds = ((size_t)a.mstride + 64 * GS_SWEEP_WPB) * sizeof(double);
+  return dispatch_nf_bdraw<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
 
 int launch_rho_analytic(hipStream_t s, const RhoArgs& a) {

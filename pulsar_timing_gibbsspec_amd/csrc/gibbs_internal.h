@@ -18,7 +18,7 @@ inline int64_t model_stride_doubles(int NF, int NMX) {
 }
 
 struct BdrawArgs {
-  int n_psr, n_chain, NF, NMX, ldb, event;
+  int n_psr, n_chain, NF, NMX, ldb, event, bcast;
   int64_t mstride, sweep, chain_base;
   const double* model;
   const int32_t *fidx, *midx, *nm;
@@ -29,7 +29,7 @@ struct BdrawArgs {
 };
 
 struct SweepArgs {
-  int n_psr, n_chain, NF, NMX, ldb, n_sweeps;
+  int n_psr, n_chain, NF, NMX, ldb, n_sweeps, bcast;
   int64_t mstride, it0, chain_base;
   double rhomin, rhomax;
   const double* model;
