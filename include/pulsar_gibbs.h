@@ -121,12 +121,13 @@ int gs_prefix(gs_ctx* ctx, int n_psr, int NF, int NMX, const gs_prefix_desc* des
  * phiinv_F: [n_sys x NF] phiinv of the free-spectrum columns (fidx order);
  * nm: [n_psr] fixed-prior column count; z: [n_sys x ldb] injected normals
  * indexed by ORIGINAL column (NULL: Philox, event `event`, sweep `sweep`);
- * b: [n_sys x ldb] output in original column order.
+ * chain_mask: [n_chain] or NULL; systems of chains with mask 0 keep b (the
+ * b-update gate, pta_gibbs.py:703).  b: [n_sys x ldb] output in original column order.
  */
 int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,
              const double* model, const int32_t* fidx, const int32_t* midx, const int32_t* nm,
              const double* phiinv_F, const double* z, int64_t sweep, int event,
-             int64_t chain_base, double* b, int32_t* info);
+             int64_t chain_base, const int32_t* chain_mask, double* b, int32_t* info);
 
 /*
  * (a3) rho|b analytic draw: tau_k = (b_sin^2 + b_cos^2)/2 over fidx,
@@ -155,6 +156,61 @@ int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
                       double* x_state, double* b_state, int64_t it0, int n_sweeps,
                       double* x_rec, double* b_rec, const double* z0_inj, const double* z_inj,
                       const double* u_inj, int32_t* info);
+
+/*
+ * tau[p][k][c] = b_sin^2 + b_cos^2 over fidx (pta_gibbs.py:194-195, 259-260), or
+ * half of it when half != 0 (pulsar_gibbs.py:208-209).  tau: [n_psr x NF/2 x n_chain].
+ */
+int gs_tau(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const int32_t* fidx, const double* b,
+           int half, double* tau);
+
+/*
+ * Grid conditionals.  grid3 = [rho_g | log rho_g | 0.5 log10 rho_g] (3 x ngrid, host numpy,
+ * rho_g = 10**linspace(log10 rhomin, log10 rhomax, ngrid)).  Draws write
+ * x[c * ldx + xcol[...]] = 0.5 log10 rho_g[idx] and, if idx_out != NULL, the index.
+ * One lane per (chain, frequency) row walks the grid serially: numpy's order of
+ * operations (sequential product over pulsars, sequential cumsum, cdf / max,
+ * searchsorted(side='left') - 1 with -1 -> last point) is reproduced exactly.
+ *
+ * (a6) common free spectrum, product over pulsars (pta_gibbs.py:181-214):
+ *   tau, irn [n_psr x n_f x n_chain] (irn NULL = no intrinsic red noise),
+ *   u [n_chain x n_f] or NULL (Philox GS_EV_CURN); xcol [n_f].
+ */
+int gs_rho_curn(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, const double* irn,
+                int ngrid, const double* grid3, const double* u, int64_t sweep, int64_t chain_base,
+                double* x, int ldx, const int32_t* xcol, int32_t* idx_out);
+/*
+ * (a7) per-pulsar red free spectrum conditioned on phi_gw (pta_gibbs.py:252-276):
+ *   tau [n_psr x n_f x n_chain], gw [n_f x n_chain] = phi_gw of the sin columns,
+ *   u [n_chain x n_psr x n_f] or NULL (Philox GS_EV_RED); xcol [n_psr x n_f].
+ */
+int gs_rho_red(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, const double* gw,
+               int ngrid, const double* grid3, const double* u, int64_t sweep, int64_t chain_base,
+               double* x, int ldx, const int32_t* xcol, int32_t* idx_out);
+/*
+ * (a4) single pulsar with intrinsic red noise: grid + Gumbel-max (pulsar_gibbs.py:218-234).
+ *   tau (half convention), irn [n_f x n_chain]; u [n_chain x n_f x ngrid] U(0,1) behind the
+ *   Gumbels (G = -log(-log1p(-u))) or NULL (Philox GS_EV_GUMBEL); xcol [n_f].
+ */
+int gs_rho_gumbel(gs_ctx* ctx, int n_chain, int n_f, const double* tau, const double* irn, int ngrid,
+                  const double* grid3, const double* u, int64_t sweep, int64_t chain_base, double* x,
+                  int ldx, const int32_t* xcol, int32_t* idx_out);
+
+/* out[j][c] = 10**(2 x[c * ldx + cols[j]]): free-spectrum phi (sin column) from log10 rho. */
+int gs_phi_from_x(gs_ctx* ctx, int n_chain, int ncol, const double* x, int ldx, const int32_t* cols,
+                  double* out);
+
+/*
+ * PTA sweep plumbing (PTABlockGibbs.sample, pta_gibbs.py:664-704):
+ * gs_pta_record: x_rec[c] = x[c] (may be NULL), xlast[c] = x[c][n_param-1];
+ * gs_pta_gate_phiinv: gate[c] = all(x[c] != xlast[c]) (xlast NULL: gate = 1) and
+ *   phiinv_F[(p * n_chain + c) x 2 n_f] = 1 / (10**(2 x_gw) + 10**(2 x_red,p)) repeated
+ *   over (sin, cos); gw_col [n_f], red_col [n_psr x n_f] or NULL.
+ */
+int gs_pta_record(gs_ctx* ctx, int n_chain, int n_param, const double* x, double* x_rec, double* xlast);
+int gs_pta_gate_phiinv(gs_ctx* ctx, int n_psr, int n_chain, int n_f, int n_param, const double* x,
+                       const double* xlast, const int32_t* gw_col, const int32_t* red_col,
+                       double* phiinv_F, int32_t* gate);
 
 /*
  * Philox4x32-10 test hook: out[i] = the 4 words for counter

@@ -7,3 +7,4 @@ kernels reached through the C-ABI in ``include/pulsar_gibbs.h``.
 __version__ = "0.1.0"
 
 from .pulsar_gibbs import PulsarBlockGibbs  # noqa: F401,E402
+from .pta_gibbs import PTABlockGibbs  # noqa: F401,E402

@@ -39,11 +39,18 @@ SIGNATURES = {
     "gs_sweep_lds_bytes": (_I, [_I, _I]),
     "gs_tnt": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
     "gs_prefix": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "gs_bdraw": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _I, _I64, _P, _P]),
+    "gs_bdraw": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _I, _I64, _P, _P, _P]),
     "gs_rho_analytic": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I64, _I64, _D, _D, _P, _I]),
     "gs_sweep_freespec": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _D, _D, _I64, _P, _P,
                                _I64, _I, _P, _P, _P, _P, _P, _P]),
     "gs_philox": (_I, [_P, _I64, _P, _P]),
+    "gs_tau": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _P]),
+    "gs_rho_curn": (_I, [_P, _I, _I, _I, _P, _P, _I, _P, _P, _I64, _I64, _P, _I, _P, _P]),
+    "gs_rho_red": (_I, [_P, _I, _I, _I, _P, _P, _I, _P, _P, _I64, _I64, _P, _I, _P, _P]),
+    "gs_rho_gumbel": (_I, [_P, _I, _I, _P, _P, _I, _P, _P, _I64, _I64, _P, _I, _P, _P]),
+    "gs_phi_from_x": (_I, [_P, _I, _I, _P, _I, _P, _P]),
+    "gs_pta_record": (_I, [_P, _I, _I, _P, _P, _P]),
+    "gs_pta_gate_phiinv": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
 }
 
 _lib = None

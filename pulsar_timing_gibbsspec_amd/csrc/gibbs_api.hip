@@ -325,8 +325,8 @@ int gs_prefix(gs_ctx* ctx, int n_psr, int NF, int NMX, const gs_prefix_desc* des
 
 int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, const double* model,
              const int32_t* fidx, const int32_t* midx, const int32_t* nm, const double* phiinv_F,
-             const double* z, int64_t sweep, int event, int64_t chain_base, double* b,
-             int32_t* info) {
+             const double* z, int64_t sweep, int event, int64_t chain_base, const int32_t* chain_mask,
+             double* b, int32_t* info) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
   if (!nf_supported(NF)) return fail_arg(4, "NF must be one of 20, 40, 60");
@@ -337,7 +337,8 @@ int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, cons
   BdrawArgs a;
   a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.ldb = ldb; a.event = event;
   a.mstride = model_stride_doubles(NF, NMX); a.sweep = sweep; a.chain_base = chain_base;
-  a.model = model; a.fidx = fidx; a.midx = midx; a.nm = nm; a.phiinv_F = phiinv_F; a.z = z;
+  a.model = model; a.fidx = fidx; a.midx = midx; a.nm = nm; a.chain_mask = chain_mask;
+  a.phiinv_F = phiinv_F; a.z = z;
   a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = ctx->bcast;
   if (launch_bdraw(ctx->stream, a)) return fail_arg(4, "unsupported NF");
   return after_launch("k_bdraw");
@@ -386,6 +387,99 @@ int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.bcast = ctx->bcast;
   if (launch_sweep_freespec(ctx->stream, a)) return fail_arg(4, "unsupported NF");
   return after_launch("k_sweep_freespec");
+}
+
+int gs_tau(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const int32_t* fidx, const double* b,
+           int half, double* tau) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
+  if (NF <= 0 || (NF & 1)) return fail_arg(4, "NF must be even");
+  if (!fidx || !b || !tau) return fail_arg(6, "NULL array");
+  TauArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.ldb = ldb; a.half = half; a.fidx = fidx; a.b = b;
+  a.tau = tau;
+  launch_tau(ctx->stream, a);
+  return after_launch("k_tau");
+}
+
+static int grid_common(gs_ctx* ctx, GridArgs& a, int n_psr, int n_chain, int n_f, const double* tau,
+                       const double* irn, int ngrid, const double* grid3, const double* u, int64_t sweep,
+                       int64_t chain_base, double* x, int ldx, const int32_t* xcol, int32_t* idx_out) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0 || n_f < 0) return fail_arg(2, "negative batch");
+  if (!tau) return fail_arg(5, "tau is NULL");
+  if (ngrid <= 0) return fail_arg(7, "ngrid <= 0");
+  if (!grid3) return fail_arg(8, "grid3 is NULL");
+  if (!x || !xcol) return fail_arg(12, "x/xcol is NULL");
+  a.n_psr = n_psr; a.n_chain = n_chain; a.n_f = n_f; a.ngrid = ngrid; a.ldx = ldx; a.sweep = sweep;
+  a.chain_base = chain_base; a.tau = tau; a.irn = irn; a.grid3 = grid3; a.u = u; a.xcol = xcol; a.x = x;
+  a.idx_out = idx_out; a.key = key_of(ctx);
+  return 0;
+}
+
+int gs_rho_curn(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, const double* irn,
+                int ngrid, const double* grid3, const double* u, int64_t sweep, int64_t chain_base,
+                double* x, int ldx, const int32_t* xcol, int32_t* idx_out) {
+  GridArgs a;
+  int rc = grid_common(ctx, a, n_psr, n_chain, n_f, tau, irn, ngrid, grid3, u, sweep, chain_base, x, ldx,
+                       xcol, idx_out);
+  if (rc) return rc;
+  launch_rho_curn(ctx->stream, a);
+  return after_launch("k_rho_curn");
+}
+
+int gs_rho_red(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, const double* gw,
+               int ngrid, const double* grid3, const double* u, int64_t sweep, int64_t chain_base,
+               double* x, int ldx, const int32_t* xcol, int32_t* idx_out) {
+  if (!gw) return fail_arg(6, "gw is NULL");
+  GridArgs a;
+  int rc = grid_common(ctx, a, n_psr, n_chain, n_f, tau, gw, ngrid, grid3, u, sweep, chain_base, x, ldx,
+                       xcol, idx_out);
+  if (rc) return rc;
+  launch_rho_red(ctx->stream, a);
+  return after_launch("k_rho_red");
+}
+
+int gs_rho_gumbel(gs_ctx* ctx, int n_chain, int n_f, const double* tau, const double* irn, int ngrid,
+                  const double* grid3, const double* u, int64_t sweep, int64_t chain_base, double* x,
+                  int ldx, const int32_t* xcol, int32_t* idx_out) {
+  if (!irn) return fail_arg(5, "irn is NULL");
+  GridArgs a;
+  int rc = grid_common(ctx, a, 1, n_chain, n_f, tau, irn, ngrid, grid3, u, sweep, chain_base, x, ldx, xcol,
+                       idx_out);
+  if (rc) return rc;
+  launch_rho_gumbel(ctx->stream, a);
+  return after_launch("k_rho_gumbel");
+}
+
+int gs_phi_from_x(gs_ctx* ctx, int n_chain, int ncol, const double* x, int ldx, const int32_t* cols,
+                  double* out) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_chain < 0 || ncol < 0) return fail_arg(2, "negative size");
+  if (!x || !cols || !out) return fail_arg(4, "NULL array");
+  launch_phi_from_x(ctx->stream, n_chain, ncol, x, ldx, cols, out);
+  return after_launch("k_phi_from_x");
+}
+
+int gs_pta_record(gs_ctx* ctx, int n_chain, int n_param, const double* x, double* x_rec, double* xlast) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_chain < 0 || n_param <= 0) return fail_arg(2, "bad size");
+  if (!x || !xlast) return fail_arg(4, "NULL array");
+  launch_pta_record(ctx->stream, n_chain, n_param, x, x_rec, xlast);
+  return after_launch("k_pta_record");
+}
+
+int gs_pta_gate_phiinv(gs_ctx* ctx, int n_psr, int n_chain, int n_f, int n_param, const double* x,
+                       const double* xlast, const int32_t* gw_col, const int32_t* red_col,
+                       double* phiinv_F, int32_t* gate) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0 || n_f <= 0 || n_param <= 0) return fail_arg(2, "bad size");
+  if (!x || !gw_col || !phiinv_F || !gate) return fail_arg(6, "NULL array");
+  PtaGateArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.n_f = n_f; a.n_param = n_param; a.x = x; a.xlast = xlast;
+  a.gw_col = gw_col; a.red_col = red_col; a.phiinv_F = phiinv_F; a.gate = gate;
+  launch_pta_gate_phiinv(ctx->stream, a);
+  return after_launch("k_pta_gate_phiinv");
 }
 
 int gs_philox(gs_ctx* ctx, int64_t n, const uint32_t* ctr, uint32_t* out) {

@@ -160,6 +160,7 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_bdraw(BdrawArgs A) 
   const int c = (blockIdx.x % nb) * WPB + wave;
   stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
   if (c >= A.n_chain) return;
+  if (A.chain_mask && A.chain_mask[c] == 0) return;  // gate closed: keep b
   const ModelLds M = model_view(lds, NF, A.NMX);
   const int64_t sys = (int64_t)p * A.n_chain + c;
   const int nM = A.nm[p];

@@ -1,0 +1,256 @@
+// rho|b grid conditionals (gfx950, fp64): a4 Gumbel-max, a6 common (CURN)
+// product-of-pdfs CDF, a7 per-pulsar red CDF, plus the tau reduction.
+//
+// Mapping: one LANE per (system, frequency) row; the lane walks the 1000-point
+// grid serially.  This reproduces numpy's operation order exactly — the
+// product over pulsars is sequential in pulsar order (np.prod), the CDF is a
+// sequential np.cumsum, normalised by its max (the last element) with a true
+// division, and the draw is searchsorted(cdf, u, 'left') - 1 with -1 wrapping
+// to the top grid point (pta_gibbs.py:205-212) — so grid indices match the
+// reference bit for bit on identical inputs.  Two passes over the grid: the
+// first finds the max, the second the crossing (the pdf is recomputed, not
+// stored: 8 KB/row would cost more HBM than the recompute costs VALU).
+// Rows are laid out [frequency][chain] so lanes of a wave read consecutive
+// chains (coalesced).  The grid rho_g = 10**linspace(...), log rho_g and
+// 0.5*log10 rho_g are computed on the host with numpy and passed in
+// (grid3 = [rho | log rho | 0.5 log10 rho]), bit-identical to the reference's.
+#include "gibbs_common.h"
+#include "gibbs_internal.h"
+
+namespace {
+
+constexpr double LN10 = 2.302585092994045684;  // np.log(10)
+
+// numpy npy_logaddexp
+__device__ __forceinline__ double np_logaddexp(double x, double y) {
+  if (x == y) return x + 0.693147180559945309417232121458176568;  // x + log(2)
+  const double t = x - y;
+  if (t > 0) return x + log1p(exp(-t));
+  if (t <= 0) return y + log1p(exp(t));
+  return t;  // NaN
+}
+
+// ------------------------------------------------------------ tau
+// tau[p][k][c] = (b_sin^2 + b_cos^2) * scale  (scale 1: pta_gibbs.py:194-195; 0.5: pulsar_gibbs.py:209)
+__global__ void k_tau(TauArgs A) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int NFR = A.NF / 2;
+  const int64_t n = (int64_t)A.n_psr * NFR * A.n_chain;
+  if (t >= n) return;
+  const int c = (int)(t % A.n_chain);
+  const int k = (int)((t / A.n_chain) % NFR);
+  const int p = (int)(t / ((int64_t)A.n_chain * NFR));
+  const int64_t sys = (int64_t)p * A.n_chain + c;
+  const double bs = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k]];
+  const double bc = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k + 1]];
+  const double s2 = bs * bs, c2 = bc * bc;
+  A.tau[t] = A.half ? (s2 + c2) / 2 : s2 + c2;
+}
+
+// ------------------------------------------------------------ a6: common CDF
+// rows r = k * n_chain + c; tau/irn [n_psr][n_f][n_chain]; irn may be NULL (zeros).
+__global__ void k_rho_curn(GridArgs A) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nrow = (int64_t)A.n_f * A.n_chain;
+  if (r >= nrow) return;
+  const int c = (int)(r % A.n_chain), k = (int)(r / A.n_chain);
+  const int P = A.n_psr;
+  const int64_t pstride = nrow;
+  double u;
+  if (A.u) {
+    u = A.u[(int64_t)c * A.n_f + k];
+  } else {
+    double u2;
+    gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, 0, GS_EV_CURN), A.key, u, u2);
+  }
+  double total = 0.0;
+  for (int pass = 0; pass < 2; ++pass) {
+    double cum = 0.0;
+    int cnt = 0;
+    for (int g = 0; g < A.ngrid; ++g) {
+      const double rg = A.grid3[g];
+      double prod = 1.0;
+      for (int p = 0; p < P; ++p) {
+        const double tau = A.tau[p * pstride + r];
+        const double irn = A.irn ? A.irn[p * pstride + r] : 0.0;
+        const double ratio = tau / (irn + rg);
+        prod *= ratio * exp(-ratio / 2) * LN10;
+      }
+      cum += prod;
+      if (pass == 1) cnt += (cum / total < u) ? 1 : 0;
+    }
+    if (pass == 0) total = cum;
+    else {
+      int idx = cnt - 1;
+      if (idx < 0) idx += A.ngrid;
+      if (A.idx_out) A.idx_out[r] = idx;
+      A.x[(int64_t)c * A.ldx + A.xcol[k]] = A.grid3[2 * A.ngrid + idx];
+    }
+  }
+}
+
+// ------------------------------------------------------------ a7: red CDF
+// rows r = (p * n_f + k) * n_chain + c; gw [n_f][n_chain] = phi_gw (sin column).
+__global__ void k_rho_red(GridArgs A) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nrow = (int64_t)A.n_psr * A.n_f * A.n_chain;
+  if (r >= nrow) return;
+  const int c = (int)(r % A.n_chain);
+  const int k = (int)((r / A.n_chain) % A.n_f);
+  const int p = (int)(r / ((int64_t)A.n_chain * A.n_f));
+  double u;
+  if (A.u) {
+    u = A.u[((int64_t)c * A.n_psr + p) * A.n_f + k];
+  } else {
+    double u2;
+    gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, p, GS_EV_RED), A.key, u, u2);
+  }
+  const double tau = A.tau[r];
+  const double gw = A.irn[(int64_t)k * A.n_chain + c];
+  double total = 0.0;
+  for (int pass = 0; pass < 2; ++pass) {
+    double cum = 0.0;
+    int cnt = 0;
+    for (int g = 0; g < A.ngrid; ++g) {
+      const double ratio = tau / (gw + A.grid3[g]);
+      cum += ratio * exp(-ratio / 2) * LN10;
+      if (pass == 1) cnt += (cum / total < u) ? 1 : 0;
+    }
+    if (pass == 0) total = cum;
+    else {
+      int idx = cnt - 1;
+      if (idx < 0) idx += A.ngrid;
+      if (A.idx_out) A.idx_out[r] = idx;
+      A.x[(int64_t)c * A.ldx + A.xcol[p * A.n_f + k]] = A.grid3[2 * A.ngrid + idx];
+    }
+  }
+}
+
+// ------------------------------------------------------------ a4: Gumbel-max
+// rows r = k * n_chain + c (one pulsar, systems = chains); tau half-convention.
+// logpdf = log tau - logaddexp(log irn, log rho) - exp(...); argmax(logpdf + G),
+// G = -log(-log1p(-U))  (numpy legacy gumbel), first maximum on ties.
+__global__ void k_rho_gumbel(GridArgs A) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nrow = (int64_t)A.n_f * A.n_chain;
+  if (r >= nrow) return;
+  const int c = (int)(r % A.n_chain), k = (int)(r / A.n_chain);
+  const double ltau = log(A.tau[r]);
+  const double lirn = log(A.irn[r]);
+  double best = -__builtin_inf();
+  int bi = 0;
+  for (int g = 0; g < A.ngrid; ++g) {
+    double u;
+    if (A.u) {
+      u = A.u[((int64_t)c * A.n_f + k) * A.ngrid + g];
+    } else {
+      double u2;
+      gs_uniform2(gs_counter((uint32_t)(k * 1024 + g), A.sweep, A.chain_base + c, 0, GS_EV_GUMBEL), A.key,
+                  u, u2);
+    }
+    const double lr = ltau - np_logaddexp(lirn, A.grid3[A.ngrid + g]);
+    const double lp = lr - exp(lr);
+    const double gum = 0.0 - 1.0 * log(-log1p(-u));
+    const double v = lp + gum;
+    if (v > best) {
+      best = v;
+      bi = g;
+    }
+  }
+  if (A.idx_out) A.idx_out[r] = bi;
+  A.x[(int64_t)c * A.ldx + A.xcol[k]] = A.grid3[2 * A.ngrid + bi];
+}
+
+// ------------------------------------------------------------ phi from x
+// out[j][c] = 10**(2 x[c][cols[j]])  (enterprise free_spectrum phi, sin column)
+__global__ void k_phi_from_x(int n_chain, int ncol, const double* x, int ldx, const int32_t* cols,
+                             double* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)n_chain * ncol) return;
+  const int c = (int)(t % n_chain), j = (int)(t / n_chain);
+  out[t] = pow(10.0, 2.0 * x[(int64_t)c * ldx + cols[j]]);
+}
+
+// ------------------------------------------------------------ PTA record / gate / phiinv
+// record: x_rec[c][:] = x[c][:], xlast[c] = x[c][n_param-1]  (pta_gibbs.py:666)
+__global__ void k_pta_record(int n_chain, int n_param, const double* x, double* x_rec, double* xlast) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)n_chain * n_param) return;
+  if (x_rec) x_rec[t] = x[t];
+  if ((t % n_param) == n_param - 1) xlast[t / n_param] = x[t];
+}
+
+// gate[c] = all_j x[c][j] != xlast[c]  (pta_gibbs.py:703); one wavefront per chain.
+// phiinv_F[p*n_chain + c][2k + {0,1}] = 1 / (10**(2 x_gw[k]) + 10**(2 x_red[p][k]))
+__global__ void k_pta_gate_phiinv(PtaGateArgs A) {
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x;
+  const double* xc = A.x + (int64_t)c * A.n_param;
+  const double xl = A.xlast ? A.xlast[c] : __builtin_nan("");
+  bool same = false;
+  for (int j = lane; j < A.n_param; j += 64) same |= (xc[j] == xl);
+  const bool gate = __ballot(same) == 0ull;
+  if (lane == 0) A.gate[c] = A.xlast ? (gate ? 1 : 0) : 1;
+  for (int t = lane; t < A.n_psr * A.n_f; t += 64) {
+    const int p = t / A.n_f, k = t % A.n_f;
+    double phi = pow(10.0, 2.0 * xc[A.gw_col[k]]);
+    if (A.red_col) phi = phi + pow(10.0, 2.0 * xc[A.red_col[p * A.n_f + k]]);
+    const double pinv = 1.0 / phi;
+    double* o = A.phiinv_F + ((int64_t)p * A.n_chain + c) * (2 * A.n_f);
+    o[2 * k] = pinv;
+    o[2 * k + 1] = pinv;
+  }
+}
+
+inline dim3 grid1(int64_t n, int bs) { return dim3((unsigned)((n + bs - 1) / bs)); }
+
+}  // namespace
+
+int launch_tau(hipStream_t s, const TauArgs& a) {
+  const int64_t n = (int64_t)a.n_psr * (a.NF / 2) * a.n_chain;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_tau, grid1(n, 256), dim3(256), 0, s, a);
+  return 0;
+}
+
+int launch_rho_curn(hipStream_t s, const GridArgs& a) {
+  const int64_t n = (int64_t)a.n_f * a.n_chain;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_rho_curn, grid1(n, 64), dim3(64), 0, s, a);
+  return 0;
+}
+
+int launch_rho_red(hipStream_t s, const GridArgs& a) {
+  const int64_t n = (int64_t)a.n_psr * a.n_f * a.n_chain;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_rho_red, grid1(n, 64), dim3(64), 0, s, a);
+  return 0;
+}
+
+int launch_rho_gumbel(hipStream_t s, const GridArgs& a) {
+  const int64_t n = (int64_t)a.n_f * a.n_chain;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_rho_gumbel, grid1(n, 64), dim3(64), 0, s, a);
+  return 0;
+}
+
+int launch_phi_from_x(hipStream_t s, int n_chain, int ncol, const double* x, int ldx, const int32_t* cols,
+                      double* out) {
+  const int64_t n = (int64_t)n_chain * ncol;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_phi_from_x, grid1(n, 256), dim3(256), 0, s, n_chain, ncol, x, ldx, cols, out);
+  return 0;
+}
+
+int launch_pta_record(hipStream_t s, int n_chain, int n_param, const double* x, double* x_rec, double* xlast) {
+  const int64_t n = (int64_t)n_chain * n_param;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_pta_record, grid1(n, 256), dim3(256), 0, s, n_chain, n_param, x, x_rec, xlast);
+  return 0;
+}
+
+int launch_pta_gate_phiinv(hipStream_t s, const PtaGateArgs& a) {
+  if (a.n_chain == 0) return 0;
+  hipLaunchKernelGGL(k_pta_gate_phiinv, dim3(a.n_chain), dim3(64), 0, s, a);
+  return 0;
+}

@@ -21,7 +21,7 @@ struct BdrawArgs {
   int n_psr, n_chain, NF, NMX, ldb, event, bcast;
   int64_t mstride, sweep, chain_base;
   const double* model;
-  const int32_t *fidx, *midx, *nm;
+  const int32_t *fidx, *midx, *nm, *chain_mask;
   const double *phiinv_F, *z;
   double* b;
   int32_t* info;
@@ -53,3 +53,37 @@ struct RhoArgs {
 int launch_sweep_freespec(hipStream_t s, const SweepArgs& a);
 int launch_bdraw(hipStream_t s, const BdrawArgs& a);
 int launch_rho_analytic(hipStream_t s, const RhoArgs& a);
+
+struct TauArgs {
+  int n_psr, n_chain, NF, ldb, half;
+  const int32_t* fidx;
+  const double* b;
+  double* tau;
+};
+
+struct GridArgs {
+  int n_psr, n_chain, n_f, ngrid, ldx;
+  int64_t sweep, chain_base;
+  const double *tau, *irn, *grid3, *u;
+  const int32_t* xcol;
+  double* x;
+  int32_t* idx_out;
+  gs_key key;
+};
+
+struct PtaGateArgs {
+  int n_psr, n_chain, n_f, n_param;
+  const double *x, *xlast;
+  const int32_t *gw_col, *red_col;
+  double* phiinv_F;
+  int32_t* gate;
+};
+
+int launch_tau(hipStream_t s, const TauArgs& a);
+int launch_rho_curn(hipStream_t s, const GridArgs& a);
+int launch_rho_red(hipStream_t s, const GridArgs& a);
+int launch_rho_gumbel(hipStream_t s, const GridArgs& a);
+int launch_phi_from_x(hipStream_t s, int n_chain, int ncol, const double* x, int ldx, const int32_t* cols,
+                      double* out);
+int launch_pta_record(hipStream_t s, int n_chain, int n_param, const double* x, double* x_rec, double* xlast);
+int launch_pta_gate_phiinv(hipStream_t s, const PtaGateArgs& a);

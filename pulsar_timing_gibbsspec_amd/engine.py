@@ -106,7 +106,7 @@ class DeviceModel:
 
     # ------------------------------------------------------------------ b | rho
     def bdraw(self, phiinv_F, n_chain, z=None, sweep=0, event=_lib.EV_B, chain_base=0, out=None,
-              info=None):
+              info=None, chain_mask=None):
         """Batched b|rho: phiinv_F (P*n_chain, NF) device tensor -> b (P*n_chain, ldb)."""
         dev = self.ctx.device
         n_sys = self.P * n_chain
@@ -114,7 +114,8 @@ class DeviceModel:
         inf = info if info is not None else torch.zeros(n_sys, dtype=torch.int32, device=dev)
         check(self.ctx.lib.gs_bdraw(self.ctx.handle, self.P, n_chain, self.NF, self.NMX, self.ldb,
                                     ptr(self.model), ptr(self.fidx), ptr(self.midx), ptr(self.nm_dev),
-                                    ptr(phiinv_F), ptr(z), sweep, event, chain_base, ptr(b), ptr(inf)),
+                                    ptr(phiinv_F), ptr(z), sweep, event, chain_base, ptr(chain_mask),
+                                    ptr(b), ptr(inf)),
               "gs_bdraw")
         return b, inf
 
@@ -161,3 +162,89 @@ class FreeSpectrumChains:
             ptr(u_inj), ptr(self.info)), "gs_sweep_freespec")
         self.it += int(n_sweeps)
         return x_rec, b_rec
+
+
+def grid3(rhomin, rhomax, n=1000, device="cuda"):
+    """[rho_g | log rho_g | 0.5 log10 rho_g], rho_g = 10**linspace(log10 rhomin, log10 rhomax, n)
+    — numpy on the host, so the device sees the reference's exact grid
+    (pulsar_gibbs.py:228, pta_gibbs.py:189-190, 254-255)."""
+    g = 10 ** np.linspace(np.log10(rhomin), np.log10(rhomax), n)
+    return _t(np.concatenate([g, np.log(g), 0.5 * np.log10(g)]), torch.float64, device)
+
+
+class PTAChains:
+    """n_chain chains of the common free-spectrum model (CURN) over all pulsars of a
+    DeviceModel, optionally with per-pulsar red free spectra sampled conditionally
+    (PTABlockGibbs.sample, pta_gibbs.py:664-704).
+
+    Per sweep (one host-side launch sequence, all chains at once):
+      record x (row ii) -> [ii == 0: b|rho from x0] -> tau -> [red grid-CDF]
+      -> common grid-CDF -> gate + phiinv -> gated b|rho.
+    State (HBM): x (n_chain, n_param) in the PTA's parameter order, b (P*n_chain, ldb).
+    """
+
+    def __init__(self, model: DeviceModel, n_param, gw_col, red_col, gw_bounds, red_bounds, n_chain, x0,
+                 chain_base=0, ngrid=1000):
+        self.model, self.ctx = model, model.ctx
+        dev = self.ctx.device
+        P, C = model.P, int(n_chain)
+        self.P, self.C, self.n_param = P, C, int(n_param)
+        self.n_f = model.NF // 2
+        self.chain_base = int(chain_base)
+        self.ngrid = ngrid
+        self.gw_col = _t(np.asarray(gw_col, np.int32), torch.int32, dev)
+        self.red = red_col is not None
+        self.red_col = _t(np.asarray(red_col, np.int32).ravel(), torch.int32, dev) if self.red else None
+        self.grid_gw = grid3(*gw_bounds, n=ngrid, device=dev)
+        self.grid_red = grid3(*red_bounds, n=ngrid, device=dev) if self.red else None
+        self.x = _t(np.broadcast_to(np.asarray(x0, float), (C, self.n_param)), torch.float64, dev)
+        self.b = torch.zeros(P * C, model.ldb, dtype=torch.float64, device=dev)
+        self.tau = torch.empty(P, self.n_f, C, dtype=torch.float64, device=dev)
+        self.gwphi = torch.empty(self.n_f, C, dtype=torch.float64, device=dev)
+        self.irn = torch.empty(P, self.n_f, C, dtype=torch.float64, device=dev) if self.red else None
+        self.phiinv_F = torch.empty(P * C, model.NF, dtype=torch.float64, device=dev)
+        self.gate = torch.ones(C, dtype=torch.int32, device=dev)
+        self.xlast = torch.empty(C, dtype=torch.float64, device=dev)
+        self.info = torch.zeros(P * C, dtype=torch.int32, device=dev)
+        self.it = 0
+
+    def _bdraw(self, z, event, mask):
+        m = self.model
+        check(self.ctx.lib.gs_bdraw(self.ctx.handle, m.P, self.C, m.NF, m.NMX, m.ldb, ptr(m.model),
+                                    ptr(m.fidx), ptr(m.midx), ptr(m.nm_dev), ptr(self.phiinv_F), ptr(z),
+                                    self.it, event, self.chain_base, ptr(mask), ptr(self.b), ptr(self.info)),
+              "gs_bdraw")
+
+    def _gate_phiinv(self, with_gate):
+        check(self.ctx.lib.gs_pta_gate_phiinv(
+            self.ctx.handle, self.P, self.C, self.n_f, self.n_param, ptr(self.x),
+            ptr(self.xlast) if with_gate else None, ptr(self.gw_col), ptr(self.red_col),
+            ptr(self.phiinv_F), ptr(self.gate)), "gs_pta_gate_phiinv")
+
+    def sweep(self, x_rec=None, z0=None, z=None, u_red=None, u_curn=None):
+        """One PTABlockGibbs sweep for every chain; x_rec: (n_chain, n_param) row or None.
+        z0/z: (P*n_chain, ldb) injected normals (original column order); u_red
+        (n_chain, P, n_f) and u_curn (n_chain, n_f): injected uniforms."""
+        lib, h, m = self.ctx.lib, self.ctx.handle, self.model
+        ii = self.it
+        check(lib.gs_pta_record(h, self.C, self.n_param, ptr(self.x), ptr(x_rec), ptr(self.xlast)),
+              "gs_pta_record")
+        if ii == 0:                                            # pta_gibbs.py:669-670
+            self._gate_phiinv(with_gate=False)
+            self._bdraw(z0, _lib.EV_B0, None)
+        check(lib.gs_tau(h, self.P, self.C, m.NF, m.ldb, ptr(m.fidx), ptr(self.b), 0, ptr(self.tau)),
+              "gs_tau")
+        if self.red:                                           # pta_gibbs.py:252-276
+            check(lib.gs_phi_from_x(h, self.C, self.n_f, ptr(self.x), self.n_param, ptr(self.gw_col),
+                                    ptr(self.gwphi)), "gs_phi_from_x")
+            check(lib.gs_rho_red(h, self.P, self.C, self.n_f, ptr(self.tau), ptr(self.gwphi), self.ngrid,
+                                 ptr(self.grid_red), ptr(u_red), ii, self.chain_base, ptr(self.x),
+                                 self.n_param, ptr(self.red_col), None), "gs_rho_red")
+            check(lib.gs_phi_from_x(h, self.C, self.P * self.n_f, ptr(self.x), self.n_param,
+                                    ptr(self.red_col), ptr(self.irn)), "gs_phi_from_x")
+        check(lib.gs_rho_curn(h, self.P, self.C, self.n_f, ptr(self.tau), ptr(self.irn), self.ngrid,
+                              ptr(self.grid_gw), ptr(u_curn), ii, self.chain_base, ptr(self.x),
+                              self.n_param, ptr(self.gw_col), None), "gs_rho_curn")   # pta_gibbs.py:181-214
+        self._gate_phiinv(with_gate=True)                      # pta_gibbs.py:703
+        self._bdraw(z, _lib.EV_B, self.gate)                   # pta_gibbs.py:704
+        self.it += 1

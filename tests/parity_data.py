@@ -43,3 +43,89 @@ def normwise_rel(a, b, axis=-1):
     num = np.max(np.abs(a - b), axis=axis)
     den = np.maximum(np.max(np.abs(b), axis=axis), 1e-300)
     return float(np.max(num / den))
+
+
+def pta_blocks(g):
+    m, off = g["m"], g["off"]
+    TNT = [g["TNT"][int(np.sum(m[:p] ** 2)): int(np.sum(m[:p + 1] ** 2))].reshape(m[p], m[p])
+           for p in range(m.size)]
+    d = [g["d"][off[p]:off[p + 1]] for p in range(m.size)]
+    return TNT, d
+
+
+def pta_replay(g, kind, rotate=False):
+    """Re-drive PTABlockGibbs's loop (pta_gibbs.py:664-704) with the oracle on the
+    fixture's draws.  Returns chain, b history, final b, #normals and #uniforms
+    consumed, and per-sweep records for device replay: the rotated normals of each
+    draw (if rotate), uniforms, and the grid-draw inputs/outputs."""
+    TNT, d = pta_blocks(g)
+    P = len(TNT)
+    m = g["m"]
+    gwid = g["gwid"]
+    rind, hind = g["rind"], g["hind"]
+    n_f = len(rind)
+    x = g["x0"].copy()
+    b = [np.zeros(mm) for mm in m]
+    zpos, upos = [0], [0]
+    z, U = g["z"], g["U"]
+    ldb = int(m.max())
+    rec = []
+    orders = [O.chol_order(m[p], gwid[p]) for p in range(P)]
+
+    def phiinv(x):
+        out = []
+        gw = 10 ** (2 * x[rind])
+        for p in range(P):
+            phi_f = gw.copy()
+            if kind == "curn_red":
+                phi_f = phi_f + 10 ** (2 * x[hind[p * n_f:(p + 1) * n_f]])
+            ph = np.full(m[p], 1e-40)
+            ph[gwid[p]] = 1.0 / np.repeat(phi_f, 2)
+            out.append(ph)
+        return out
+
+    def draw(x):
+        ph = phiinv(x)
+        out = []
+        zc = np.zeros((P, ldb))
+        for p in range(P):
+            zz = z[zpos[0]:zpos[0] + m[p]]
+            zpos[0] += m[p]
+            out.append(O.bdraw_svd(TNT[p], d[p], ph[p], zz))
+            if rotate:
+                zc[p, :m[p]] = O.rotate_normals(TNT[p], ph[p], zz, orders[p])
+        return out, zc
+
+    def take_u(n):
+        u = U[upos[0]:upos[0] + n]
+        upos[0] += n
+        return u
+
+    chain, bhist = [], []
+    for ii in range(g["chain"].shape[0]):
+        r = {}
+        chain.append(x.copy())
+        bhist.append(np.concatenate(b))
+        if ii == 0:
+            b, r["z0"] = draw(g["x0"])
+        if kind == "curn_red":
+            taus = np.stack([O.tau_full(b[p], gwid[p]) for p in range(P)])
+            gwphi = 10 ** (2 * x[rind])
+            uu = take_u(P * n_f).reshape(P, n_f)
+            rr, ridx = O.rho_grid_cdf_red(taus, gwphi, uu, float(g["rhomin_red"]), float(g["rhomax_red"]))
+            x = x.copy()
+            x[hind] = 0.5 * np.log10(rr.ravel())
+            r.update(tau_red=taus, gwphi=gwphi, u_red=uu, idx_red=ridx, x_red=x.copy())
+        taus = np.stack([O.tau_full(b[p], gwid[p]) for p in range(P)])
+        irn = (np.stack([10 ** (2 * x[hind[p * n_f:(p + 1) * n_f]]) for p in range(P)])
+               if kind == "curn_red" else np.zeros_like(taus))
+        uc = take_u(n_f)
+        rr, cidx = O.rho_grid_cdf_curn(taus, irn, uc, float(g["rhomin_gw"]), float(g["rhomax_gw"]))
+        x = x.copy()
+        x[rind] = 0.5 * np.log10(rr)
+        r.update(tau=taus, irn=irn, u_curn=uc, idx_curn=cidx, x_curn=x.copy())
+        r["gate"] = bool(np.all(x != chain[ii][-1]))
+        if r["gate"]:
+            b, r["z"] = draw(x)
+        rec.append(r)
+    return np.stack(chain), np.stack(bhist), np.concatenate(b), zpos[0], upos[0], rec

@@ -1,0 +1,132 @@
+"""Grid conditionals (a4, a6, a7) and the PTA CURN engine vs the reference's
+golden vectors (needs an MI355X).
+
+Grid draws are integer outcomes: indices and the written log10 rho must match
+the reference EXACTLY on identical inputs (the kernels reproduce numpy's
+operation order).  The PTA sweep fed the reference's rotated normals must
+reproduce its chain (grid values, exact) and b (1e-9 norm-wise)."""
+import numpy as np
+import pytest
+
+from oracle import gibbs_oracle as O
+from tests.conftest import golden
+from tests.parity_data import normwise_rel, pta_replay
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from pulsar_timing_gibbsspec_amd import _lib
+    return _lib.Context(0, seed=99)
+
+
+def dev(a, dtype=torch.float64):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).cuda()
+
+
+def test_gumbel_kernel_exact(ctx):
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import grid3
+    g = golden("gumbel_j1713.npz")
+    nc = g["b"].shape[0]
+    tau = np.stack([O.tau_half(g["b"][c], g["gwid"]) for c in range(nc)])     # (nc, n_f)
+    n_f = tau.shape[1]
+    x = torch.zeros(nc, n_f, dtype=torch.float64, device="cuda")
+    idx = torch.zeros(n_f * nc, dtype=torch.int32, device="cuda")
+    G = grid3(float(g["rhomin"]), float(g["rhomax"]))
+    _lib.check(ctx.lib.gs_rho_gumbel(ctx.handle, nc, n_f, _lib.ptr(dev(tau.T)), _lib.ptr(dev(g["irn"].T)),
+                                     1000, _lib.ptr(G), _lib.ptr(dev(g["gumbel_u"])), 0, 0, _lib.ptr(x), n_f,
+                                     _lib.ptr(dev(np.arange(n_f, dtype=np.int32), torch.int32)),
+                                     _lib.ptr(idx)), "gs_rho_gumbel")
+    want = np.stack([g["xnew"][c][g["gwind"]] for c in range(nc)])
+    assert np.array_equal(x.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("kind", ["curn", "curn_red"])
+def test_grid_cdf_kernels_exact(ctx, kind):
+    """a6 (and a7) on every sweep's recorded inputs: indices bit-exact."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import grid3
+    g = golden(f"pta_{kind}.npz")
+    *_, rec = pta_replay(g, kind)
+    P, n_f = rec[0]["tau"].shape
+    Gg = grid3(float(g["rhomin_gw"]), float(g["rhomax_gw"]))
+    Gr = grid3(float(g["rhomin_red"]), float(g["rhomax_red"]))
+    n_param = g["x0"].size
+    for ii, r in enumerate(rec):
+        if kind == "curn_red":
+            x = dev(g["chain"][ii][None])
+            idx = torch.zeros(P * n_f, dtype=torch.int32, device="cuda")
+            _lib.check(ctx.lib.gs_rho_red(ctx.handle, P, 1, n_f, _lib.ptr(dev(r["tau_red"][:, :, None])),
+                                          _lib.ptr(dev(r["gwphi"][:, None])), 1000, _lib.ptr(Gr),
+                                          _lib.ptr(dev(r["u_red"][None])), 0, 0, _lib.ptr(x), n_param,
+                                          _lib.ptr(dev(g["hind"].astype(np.int32), torch.int32)),
+                                          _lib.ptr(idx)), "gs_rho_red")
+            assert np.array_equal(idx.cpu().numpy(), r["idx_red"].ravel()), ii
+            assert np.array_equal(x.cpu().numpy()[0], r["x_red"]), ii
+        x = dev((r["x_red"] if kind == "curn_red" else g["chain"][ii])[None])
+        idx = torch.zeros(n_f, dtype=torch.int32, device="cuda")
+        irn = dev(r["irn"][:, :, None]) if kind == "curn_red" else None
+        _lib.check(ctx.lib.gs_rho_curn(ctx.handle, P, 1, n_f, _lib.ptr(dev(r["tau"][:, :, None])),
+                                       _lib.ptr(irn), 1000, _lib.ptr(Gg), _lib.ptr(dev(r["u_curn"][None])),
+                                       0, 0, _lib.ptr(x), n_param,
+                                       _lib.ptr(dev(g["rind"].astype(np.int32), torch.int32)),
+                                       _lib.ptr(idx)), "gs_rho_curn")
+        assert np.array_equal(idx.cpu().numpy(), r["idx_curn"]), ii
+        assert np.array_equal(x.cpu().numpy()[0], r["x_curn"]), ii
+
+
+@pytest.mark.parametrize("kind", ["curn", "curn_red"])
+def test_pta_engine_matches_reference_chain(ctx, kind):
+    """PTAChains (45 pulsars) fed the reference's rotated normals and uniforms."""
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
+    from pulsar_timing_gibbsspec_amd import synthetic
+    g = golden(f"pta_{kind}.npz")
+    chain, bhist, bfin, _, _, rec = pta_replay(g, kind, rotate=True)
+    pta = synthetic.array_pta(kind=kind, seed=0)
+    T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
+    gwid = [np.asarray(x) for x in g["gwid"]]
+    fixed = [np.full(T[p].shape[1] - 60, 1e-40) for p in range(len(T))]
+    model = DeviceModel(ctx, T, N, R, gwid, fixed)
+    for p in (0, 17, 44):                                  # same TNT/d as the fixture's
+        a, b = model.tnt_host(p)
+        m = a.shape[0]
+        o = int(np.sum(g["m"][:p] ** 2))
+        assert normwise_rel(a, g["TNT"][o:o + m * m].reshape(m, m)) < 1e-12
+    hind = g["hind"]
+    red_col = hind.reshape(len(T), -1) if kind == "curn_red" else None
+    eng = PTAChains(model, g["x0"].size, g["rind"], red_col, (float(g["rhomin_gw"]), float(g["rhomax_gw"])),
+                    (float(g["rhomin_red"]), float(g["rhomax_red"])), 1, g["x0"])
+    xr = torch.zeros(len(rec), 1, g["x0"].size, dtype=torch.float64, device="cuda")
+    for ii, r in enumerate(rec):
+        eng.sweep(x_rec=xr[ii], z0=dev(r["z0"]) if ii == 0 else None,
+                  z=dev(r["z"]) if r["gate"] else None,
+                  u_red=dev(r["u_red"][None]) if kind == "curn_red" else None,
+                  u_curn=dev(r["u_curn"][None]))
+        assert bool(eng.gate.cpu()[0]) == r["gate"], ii
+    assert np.array_equal(xr.cpu().numpy()[:, 0], g["chain"])
+    b = eng.b.cpu().numpy()
+    bd = np.concatenate([b[p, :g["m"][p]] for p in range(len(T))])
+    assert normwise_rel(bd, g["b_final"]) < 1e-9
+    assert not eng.info.cpu().numpy().any()
+
+
+def test_pta_block_gibbs_surface(tmp_path):
+    from pulsar_timing_gibbsspec_amd import PTABlockGibbs, synthetic
+    pta = synthetic.array_pta(kind="curn_red", n_psr=6, seed=3)
+    gb = PTABlockGibbs(pta, hypersample="conditional", redsample="conditional", nchains=8, seed=1)
+    x0 = np.concatenate([p.sample().flatten() for p in gb.params])
+    chain = gb.sample(x0, outdir=str(tmp_path), niter=120)
+    assert chain.shape == (120, 6 * 30 + 30)
+    saved = np.loadtxt(tmp_path / "chain.txt")
+    assert saved.shape == (101, 210)
+    assert np.array_equal(saved, chain[:101])
+    assert np.load(tmp_path / "chains.npy").shape == (8, 101, 210)
+    gw = chain[1:, gb.get_rho_param_indices()]
+    assert np.all(gw >= -9.0) and np.all(gw <= -4.0)
+    red = chain[1:, gb.get_hyper_param_indices()]
+    assert np.all(red >= -10.0) and np.all(red <= -4.0)
+    b = gb.update_b(chain[-1])
+    assert len(b) == 6 and all(np.all(np.isfinite(bb)) for bb in b)

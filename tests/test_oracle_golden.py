@@ -9,7 +9,7 @@ import pytest
 
 from oracle import gibbs_oracle as O
 from tests.conftest import golden
-from tests.parity_data import normwise_rel, single_replay
+from tests.parity_data import normwise_rel, pta_replay, single_replay
 
 
 def test_tnt_and_svd_sweep_bitwise(single):
@@ -89,81 +89,10 @@ def test_grid_gumbel_exact():
         assert np.array_equal(0.5 * np.log10(rho), g["xnew"][c][gwind])
 
 
-def _pta_blocks(g):
-    m, off = g["m"], g["off"]
-    TNT = [g["TNT"][int(np.sum(m[:p] ** 2)): int(np.sum(m[:p + 1] ** 2))].reshape(m[p], m[p])
-           for p in range(m.size)]
-    d = [g["d"][off[p]:off[p + 1]] for p in range(m.size)]
-    return TNT, d
-
-
-def pta_replay(g, kind):
-    """Re-drive PTABlockGibbs's loop (pta_gibbs.py:664-704) with the oracle."""
-    TNT, d = _pta_blocks(g)
-    P = len(TNT)
-    m, off = g["m"], g["off"]
-    gwid = g["gwid"]
-    rind, hind = g["rind"], g["hind"]
-    x = g["x0"].copy()
-    b = [np.zeros(mm) for mm in m]
-    zpos = [0]
-    upos = [0]
-    z, U = g["z"], g["U"]
-
-    def phiinv(x):
-        out = []
-        gw = 10 ** (2 * x[rind])
-        for p in range(P):
-            phi_f = gw.copy()
-            if kind == "curn_red":
-                phi_f = phi_f + 10 ** (2 * x[hind[p * 30:(p + 1) * 30]])
-            ph = np.full(m[p], 1e-40)
-            ph[gwid[p]] = 1.0 / np.repeat(phi_f, 2)
-            out.append(ph)
-        return out
-
-    def draw(x):
-        ph = phiinv(x)
-        out = []
-        for p in range(P):
-            zz = z[zpos[0]:zpos[0] + m[p]]
-            zpos[0] += m[p]
-            out.append(O.bdraw_svd(TNT[p], d[p], ph[p], zz))
-        return out
-
-    def take_u(n):
-        u = U[upos[0]:upos[0] + n]
-        upos[0] += n
-        return u
-
-    chain, bhist = [], []
-    for ii in range(g["chain"].shape[0]):
-        chain.append(x.copy())
-        bhist.append(np.concatenate(b))
-        if ii == 0:
-            b = draw(g["x0"])
-        if kind == "curn_red":
-            taus = np.stack([O.tau_full(b[p], gwid[p]) for p in range(P)])
-            gwphi = 10 ** (2 * x[rind])
-            uu = take_u(P * 30).reshape(P, 30)
-            rr, _ = O.rho_grid_cdf_red(taus, gwphi, uu, float(g["rhomin_red"]), float(g["rhomax_red"]))
-            x = x.copy()
-            x[hind] = 0.5 * np.log10(rr.ravel())
-        taus = np.stack([O.tau_full(b[p], gwid[p]) for p in range(P)])
-        irn = (np.stack([10 ** (2 * x[hind[p * 30:(p + 1) * 30]]) for p in range(P)])
-               if kind == "curn_red" else np.zeros_like(taus))
-        rr, _ = O.rho_grid_cdf_curn(taus, irn, take_u(30), float(g["rhomin_gw"]), float(g["rhomax_gw"]))
-        x = x.copy()
-        x[rind] = 0.5 * np.log10(rr)
-        if np.all(x != chain[ii][-1]):
-            b = draw(x)
-    return np.stack(chain), np.stack(bhist), np.concatenate(b), zpos[0], upos[0]
-
-
 @pytest.mark.parametrize("kind", ["curn", "curn_red"])
 def test_pta_loop_bitwise(kind):
     g = golden(f"pta_{kind}.npz")
-    ch, bh, bf, nz, nu = pta_replay(g, kind)
+    ch, bh, bf, nz, nu, _ = pta_replay(g, kind)
     assert nz == g["z"].size and nu == g["U"].size
     assert np.array_equal(ch, g["chain"])
     assert np.array_equal(bh, g["bhist"])
@@ -217,7 +146,7 @@ def test_pta_sample_loop_order():
                 off=np.concatenate([[0], np.cumsum(m)]), gwid=gwid, rind=rind, hind=hind,
                 x0=g["x0"], z=g["z"], U=g["U"], chain=g["chain"],
                 rhomin_gw=1e-18, rhomax_gw=1e-8, rhomin_red=1e-20, rhomax_red=1e-8)
-    ch, _, _, nz, nu = pta_replay(fake, "curn_red")
+    ch, _, _, nz, nu, _ = pta_replay(fake, "curn_red")
     assert np.array_equal(ch, g["chain"])
     assert int(g["saved_rows"]) == 101
 
