@@ -49,7 +49,8 @@ enum {
 
 /* Context options (gs_ctx_set_option) */
 enum {
-  GS_OPT_BCAST = 1 /* factorisation broadcast: 0 = v_readlane -> SGPR (default), 1 = LDS */
+  GS_OPT_BCAST = 1 /* factorisation broadcast: 0 = v_readlane -> SGPR (default), 1 = LDS,
+                       2 = v_readlane in batches of 8 SGPR pairs */
 };
 
 typedef struct gs_ctx gs_ctx;

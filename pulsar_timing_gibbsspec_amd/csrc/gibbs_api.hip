@@ -264,7 +264,7 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   switch (option) {
     case GS_OPT_BCAST:
-      if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_BCAST must be 0 or 1");
+      if (value < 0 || value > 2) return fail_arg(3, "GS_OPT_BCAST must be 0, 1 or 2");
       ctx->bcast = value;
       return 0;
     default:

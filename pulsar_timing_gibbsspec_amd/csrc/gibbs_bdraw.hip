@@ -27,6 +27,7 @@
 
 #define GS_BCAST_READLANE 0
 #define GS_BCAST_LDS 1
+#define GS_BCAST_BATCH 2
 
 #ifndef GS_BCAST_CHUNK
 #define GS_BCAST_CHUNK 8
@@ -93,6 +94,24 @@ __device__ __forceinline__ int bdraw_wave(const ModelLds& M, int NMX, int nM, in
         a[j] = fma(-f, rdlane(a[k], j), a[j]);
         // bound the broadcasts in flight (each holds 2 SGPRs until its FMA)
         if (((j - k) % GS_BCAST_CHUNK) == 0) __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (BC == GS_BCAST_BATCH) {
+      // batches of GS_BCAST_CHUNK broadcasts into distinct SGPR pairs, then the
+      // FMAs: the readlane -> SGPR-read wait states overlap instead of a s_nop
+      // per pair.  Constant trip counts so the inner loops unroll before k's.
+#pragma unroll
+      for (int j0 = 0; j0 < NF; j0 += GS_BCAST_CHUNK) {
+        if (j0 + GS_BCAST_CHUNK - 1 > k) {
+          double l[GS_BCAST_CHUNK];
+#pragma unroll
+          for (int q = 0; q < GS_BCAST_CHUNK; ++q)
+            if (j0 + q > k && j0 + q < NF) l[q] = rdlane(a[k], j0 + q);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int q = 0; q < GS_BCAST_CHUNK; ++q)
+            if (j0 + q > k && j0 + q < NF) a[j0 + q] = fma(-f, l[q], a[j0 + q]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     } else {
       // column k through the wave's LDS slot: one ds_write_b64 per lane, then
@@ -296,13 +315,16 @@ __global__ void k_rho_analytic(RhoArgs A) {
 }
 
 #define GS_NF_CASES(KERNEL, ARGS)                                                            \
-  switch (NF * 2 + bc) {                                                                     \
-    case 40: hipLaunchKernelGGL((KERNEL<20, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 41: hipLaunchKernelGGL((KERNEL<20, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 80: hipLaunchKernelGGL((KERNEL<40, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 81: hipLaunchKernelGGL((KERNEL<40, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 120: hipLaunchKernelGGL((KERNEL<60, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 121: hipLaunchKernelGGL((KERNEL<60, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+  switch (NF * 4 + bc) {                                                                     \
+    case 80: hipLaunchKernelGGL((KERNEL<20, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 81: hipLaunchKernelGGL((KERNEL<20, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 82: hipLaunchKernelGGL((KERNEL<20, WPB, 2>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 160: hipLaunchKernelGGL((KERNEL<40, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 161: hipLaunchKernelGGL((KERNEL<40, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 162: hipLaunchKernelGGL((KERNEL<40, WPB, 2>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 240: hipLaunchKernelGGL((KERNEL<60, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 241: hipLaunchKernelGGL((KERNEL<60, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 242: hipLaunchKernelGGL((KERNEL<60, WPB, 2>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
     default: return 1;                                                                       \
   }
 

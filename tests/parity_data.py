@@ -129,3 +129,40 @@ def pta_replay(g, kind, rotate=False):
             b, r["z"] = draw(x)
         rec.append(r)
     return np.stack(chain), np.stack(bhist), np.concatenate(b), zpos[0], upos[0], rec
+
+
+def refined_mean(S, dv, iters=6):
+    """Sigma^-1 d by Cholesky + iterative refinement with long-double residuals
+    (the 'exact' mean: the reference's fp64 SVD mean carries up to ~5e-9 relative
+    error on the ill-conditioned PTA systems, cond ~1e9 before scaling)."""
+    import scipy.linalg as sl
+    Sl = S.astype(np.longdouble)
+    dl = dv.astype(np.longdouble)
+    cf = sl.cho_factor(S)
+    x = sl.cho_solve(cf, dv).astype(np.longdouble)
+    for _ in range(iters):
+        r = dl - Sl @ x
+        x = x + sl.cho_solve(cf, np.asarray(r, dtype=np.float64)).astype(np.longdouble)
+    return np.asarray(x, dtype=np.float64)
+
+
+def exact_mean_draw(TNT, d, phiinv, z_ref):
+    """The reference draw with its mean computed exactly: refined Sigma^-1 d plus the
+    reference's own noise term U S^-1/2 z (pulsar_gibbs.py:508-518)."""
+    import scipy.linalg as sl
+    S = TNT + np.diag(phiinv)
+    u, s, _ = sl.svd(S)
+    return refined_mean(S, d) + (u * np.sqrt(1 / s)) @ z_ref
+
+
+def pta_last_draw(g, kind, rec):
+    """(x, per-pulsar reference normals) of the last b draw of a PTA fixture run."""
+    m = g["m"]
+    P = m.size
+    n_draws = sum(1 for r in rec if r["gate"]) + 1
+    ztot = int(np.sum(m))
+    zlast = g["z"][(n_draws - 1) * ztot: n_draws * ztot]
+    last = [i for i, r in enumerate(rec) if r["gate"]]
+    x = rec[last[-1]]["x_curn"] if last else g["x0"]
+    off = np.concatenate([[0], np.cumsum(m)])
+    return x, [zlast[off[p]:off[p + 1]] for p in range(P)]

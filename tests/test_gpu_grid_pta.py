@@ -10,7 +10,7 @@ import pytest
 
 from oracle import gibbs_oracle as O
 from tests.conftest import golden
-from tests.parity_data import normwise_rel, pta_replay
+from tests.parity_data import exact_mean_draw, normwise_rel, pta_blocks, pta_last_draw, pta_replay
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -26,6 +26,23 @@ def dev(a, dtype=torch.float64):
     return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).cuda()
 
 
+class Keep:
+    """Device copies that stay alive until the test ends.  `_lib.ptr(dev(a))` inline
+    would free the temporary as soon as ptr() returns and torch's caching allocator
+    would hand the same block to the next argument (aliased inputs)."""
+
+    def __init__(self):
+        self.held = []
+
+    def __call__(self, a, dtype=torch.float64):
+        from pulsar_timing_gibbsspec_amd import _lib
+        if a is None:
+            return None
+        t = dev(a, dtype)
+        self.held.append(t)
+        return _lib.ptr(t)
+
+
 def test_gumbel_kernel_exact(ctx):
     from pulsar_timing_gibbsspec_amd import _lib
     from pulsar_timing_gibbsspec_amd.engine import grid3
@@ -36,10 +53,11 @@ def test_gumbel_kernel_exact(ctx):
     x = torch.zeros(nc, n_f, dtype=torch.float64, device="cuda")
     idx = torch.zeros(n_f * nc, dtype=torch.int32, device="cuda")
     G = grid3(float(g["rhomin"]), float(g["rhomax"]))
-    _lib.check(ctx.lib.gs_rho_gumbel(ctx.handle, nc, n_f, _lib.ptr(dev(tau.T)), _lib.ptr(dev(g["irn"].T)),
-                                     1000, _lib.ptr(G), _lib.ptr(dev(g["gumbel_u"])), 0, 0, _lib.ptr(x), n_f,
-                                     _lib.ptr(dev(np.arange(n_f, dtype=np.int32), torch.int32)),
-                                     _lib.ptr(idx)), "gs_rho_gumbel")
+    K = Keep()
+    _lib.check(ctx.lib.gs_rho_gumbel(ctx.handle, nc, n_f, K(tau.T), K(g["irn"].T), 1000, _lib.ptr(G),
+                                     K(g["gumbel_u"]), 0, 0, _lib.ptr(x), n_f,
+                                     K(np.arange(n_f, dtype=np.int32), torch.int32), _lib.ptr(idx)),
+               "gs_rho_gumbel")
     want = np.stack([g["xnew"][c][g["gwind"]] for c in range(nc)])
     assert np.array_equal(x.cpu().numpy(), want)
 
@@ -55,26 +73,39 @@ def test_grid_cdf_kernels_exact(ctx, kind):
     Gg = grid3(float(g["rhomin_gw"]), float(g["rhomax_gw"]))
     Gr = grid3(float(g["rhomin_red"]), float(g["rhomax_red"]))
     n_param = g["x0"].size
+    K = Keep()
     for ii, r in enumerate(rec):
         if kind == "curn_red":
             x = dev(g["chain"][ii][None])
             idx = torch.zeros(P * n_f, dtype=torch.int32, device="cuda")
-            _lib.check(ctx.lib.gs_rho_red(ctx.handle, P, 1, n_f, _lib.ptr(dev(r["tau_red"][:, :, None])),
-                                          _lib.ptr(dev(r["gwphi"][:, None])), 1000, _lib.ptr(Gr),
-                                          _lib.ptr(dev(r["u_red"][None])), 0, 0, _lib.ptr(x), n_param,
-                                          _lib.ptr(dev(g["hind"].astype(np.int32), torch.int32)),
+            _lib.check(ctx.lib.gs_rho_red(ctx.handle, P, 1, n_f, K(r["tau_red"][:, :, None]),
+                                          K(r["gwphi"][:, None]), 1000, _lib.ptr(Gr), K(r["u_red"][None]),
+                                          0, 0, _lib.ptr(x), n_param, K(g["hind"].astype(np.int32), torch.int32),
                                           _lib.ptr(idx)), "gs_rho_red")
-            assert np.array_equal(idx.cpu().numpy(), r["idx_red"].ravel()), ii
+            got = idx.cpu().numpy()
+            # the oracle keeps searchsorted-1 = -1; the device stores the wrapped index
+            bad = np.nonzero(got != r["idx_red"].ravel() % 1000)[0]
+            if bad.size:
+                info = []
+                rho = O.rho_grid(float(g["rhomin_red"]), float(g["rhomax_red"]))
+                for q in bad[:5]:
+                    p_, k_ = divmod(int(q), n_f)
+                    ratio = r["tau_red"][p_, k_] / (r["gwphi"][k_] + rho)
+                    cdf = np.cumsum(ratio * np.exp(-ratio / 2) * np.log(10))
+                    cdf /= cdf.max()
+                    u = r["u_red"][p_, k_]
+                    info.append((p_, k_, int(got[q]), int(r["idx_red"].ravel()[q]), u,
+                                 cdf[max(0, got[q] - 1):got[q] + 2].tolist(), r["tau_red"][p_, k_]))
+                pytest.fail(f"sweep {ii}: {bad.size}/{got.size} red indices differ: {info}")
             assert np.array_equal(x.cpu().numpy()[0], r["x_red"]), ii
         x = dev((r["x_red"] if kind == "curn_red" else g["chain"][ii])[None])
         idx = torch.zeros(n_f, dtype=torch.int32, device="cuda")
-        irn = dev(r["irn"][:, :, None]) if kind == "curn_red" else None
-        _lib.check(ctx.lib.gs_rho_curn(ctx.handle, P, 1, n_f, _lib.ptr(dev(r["tau"][:, :, None])),
-                                       _lib.ptr(irn), 1000, _lib.ptr(Gg), _lib.ptr(dev(r["u_curn"][None])),
-                                       0, 0, _lib.ptr(x), n_param,
-                                       _lib.ptr(dev(g["rind"].astype(np.int32), torch.int32)),
-                                       _lib.ptr(idx)), "gs_rho_curn")
-        assert np.array_equal(idx.cpu().numpy(), r["idx_curn"]), ii
+        irn = r["irn"][:, :, None] if kind == "curn_red" else None
+        _lib.check(ctx.lib.gs_rho_curn(ctx.handle, P, 1, n_f, K(r["tau"][:, :, None]), K(irn), 1000,
+                                       _lib.ptr(Gg), K(r["u_curn"][None]), 0, 0, _lib.ptr(x), n_param,
+                                       K(g["rind"].astype(np.int32), torch.int32), _lib.ptr(idx)),
+                   "gs_rho_curn")
+        assert np.array_equal(idx.cpu().numpy(), r["idx_curn"] % 1000), ii
         assert np.array_equal(x.cpu().numpy()[0], r["x_curn"]), ii
 
 
@@ -108,8 +139,25 @@ def test_pta_engine_matches_reference_chain(ctx, kind):
         assert bool(eng.gate.cpu()[0]) == r["gate"], ii
     assert np.array_equal(xr.cpu().numpy()[:, 0], g["chain"])
     b = eng.b.cpu().numpy()
-    bd = np.concatenate([b[p, :g["m"][p]] for p in range(len(T))])
-    assert normwise_rel(bd, g["b_final"]) < 1e-9
+    # final b per pulsar vs the reference draw with an exact mean (1e-9); the
+    # reference's own fp64 SVD mean is off by up to ~3e-8 on these systems
+    # (tests/test_oracle_golden.py::test_reference_svd_mean_error), so the raw
+    # comparison is bounded by that error + 1e-9.
+    TNTs, ds = pta_blocks(g)
+    x, zl = pta_last_draw(g, kind, rec)
+    off = np.concatenate([[0], np.cumsum(g["m"])])
+    n_f = len(g["rind"])
+    for p in range(len(T)):
+        phi_f = 10 ** (2 * x[g["rind"]])
+        if kind == "curn_red":
+            phi_f = phi_f + 10 ** (2 * x[g["hind"][p * n_f:(p + 1) * n_f]])
+        ph = np.full(g["m"][p], 1e-40)
+        ph[gwid[p]] = 1.0 / np.repeat(phi_f, 2)
+        bx = exact_mean_draw(TNTs[p], ds[p], ph, zl[p])
+        bp = b[p, :g["m"][p]]
+        assert normwise_rel(bp, bx) < 1e-9, p
+        bref = g["b_final"][off[p]:off[p + 1]]
+        assert normwise_rel(bp, bref) <= normwise_rel(bref, bx) + 1e-9, p
     assert not eng.info.cpu().numpy().any()
 
 
