@@ -89,6 +89,89 @@ def ess_min_bin(x_rec, elapsed, n_chains_total, max_chains=256):
     return float(ess.min() * n_chains_total / (elapsed * n / K))
 
 
+def pta_cpu_baseline(kind, seconds=10.0):
+    """The oracle's restatement of PTABlockGibbs.sample (pta_gibbs.py:664-704), SVD draws,
+    1 thread, bounded sample of the same 45-pulsar model."""
+    from oracle import gibbs_oracle as O
+    from pulsar_timing_gibbsspec_amd import synthetic
+    pta = synthetic.array_pta(kind=kind, seed=0)
+    T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
+    P = len(T)
+    TNT = [O.tnt(T[p], N[p], R[p]) for p in range(P)]
+    names = pta.param_names
+    rind = np.array([i for i, n in enumerate(names) if "rho" in n and "gw" in n])
+    hind = np.array([i for i, n in enumerate(names) if "red" in n and "rho" in n])
+    rng = np.random.default_rng(0)
+    x = rng.uniform(-9, -4, len(names))
+    m = [t.shape[1] for t in T]
+    gw = [np.arange(mm - 60, mm) for mm in m]
+
+    def draw(x):
+        out = []
+        for p in range(P):
+            phi = 10 ** (2 * x[rind]) + (10 ** (2 * x[hind[p * 30:(p + 1) * 30]]) if kind == "curn_red" else 0)
+            ph = np.full(m[p], 1e-40)
+            ph[gw[p]] = 1 / np.repeat(phi, 2)
+            out.append(O.bdraw_svd(TNT[p][0], TNT[p][1], ph, rng.standard_normal(m[p])))
+        return out
+    b = draw(x)
+    it, t0 = 0, time.perf_counter()
+    while True:
+        taus = np.stack([O.tau_full(b[p], gw[p]) for p in range(P)])
+        if kind == "curn_red":
+            rr, _ = O.rho_grid_cdf_red(taus, 10 ** (2 * x[rind]), rng.random((P, 30)), 1e-20, 1e-8)
+            x[hind] = 0.5 * np.log10(rr.ravel())
+        irn = (np.stack([10 ** (2 * x[hind[p * 30:(p + 1) * 30]]) for p in range(P)])
+               if kind == "curn_red" else np.zeros_like(taus))
+        rr, _ = O.rho_grid_cdf_curn(taus, irn, rng.random(30), 1e-18, 1e-8)
+        x[rind] = 0.5 * np.log10(rr)
+        b = draw(x)
+        it += 1
+        el = time.perf_counter() - t0
+        if el > seconds:
+            break
+    return dict(value=it / el, unit="iters/s", cores=1, kind="port",
+                sample=f"{it} sweeps of the 45-pulsar {kind} loop (oracle restatement of "
+                       f"pta_gibbs.py:664-704, numpy SVD, 1 thread) in {el:.1f} s")
+
+
+def bench_pta(kind, C, K, W, rank, world, dev, ctx):
+    """Configs 4a/4b: PTAChains over the 45 simulated pulsars, C chains per GPU (chain-sharded)."""
+    from pulsar_timing_gibbsspec_amd import synthetic
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
+    pta = synthetic.array_pta(kind=kind, seed=0)
+    T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
+    names = pta.param_names
+    rind = [i for i, n in enumerate(names) if "rho" in n and "gw" in n]
+    hind = np.array([i for i, n in enumerate(names) if "red" in n and "rho" in n])
+    gwid = [np.arange(t.shape[1] - 60, t.shape[1]) for t in T]
+    model = DeviceModel(ctx, T, N, R, gwid, [np.full(t.shape[1] - 60, 1e-40) for t in T])
+    x0 = np.random.default_rng(rank).uniform(-9, -4, (C, len(names)))
+    eng = PTAChains(model, len(names), rind, hind.reshape(len(T), -1) if kind == "curn_red" else None,
+                    (1e-18, 1e-8), (1e-20, 1e-8), C, x0, chain_base=rank * C)
+    rec = torch.empty(K, C, len(names), dtype=torch.float64, device=dev)
+    for _ in range(W):
+        eng.sweep(x_rec=rec[0])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(K):
+        eng.sweep(x_rec=rec[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if eng.info.cpu().numpy().any():
+        raise RuntimeError("non-PD Sigma in the PTA bench")
+    return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+                chains_per_gpu=C, n_psr=len(T), n_param=len(names))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -98,7 +181,11 @@ def main():
     ap.add_argument("--sweeps-per-launch", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--bcast", type=int, default=None, help="GS_OPT_BCAST (0 readlane, 1 LDS)")
+    ap.add_argument("--bcast", type=int, default=None, help="GS_OPT_BCAST (0 readlane, 1 LDS, 2 batched)")
+    ap.add_argument("--pta", default="curn_red", help="secondary PTA config measured in the same run: "
+                    "curn | curn_red | none")
+    ap.add_argument("--pta-chains", type=int, default=256)
+    ap.add_argument("--pta-steps", type=int, default=20)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -197,6 +284,15 @@ def main():
         }
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if args.pta != "none":
+        sec = bench_pta(args.pta, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx)
+        if rank == 0:
+            sec["config"] = f"configs[3]: 45-pulsar CURN{' + per-pulsar red' if args.pta == 'curn_red' else ''} " \
+                            "free spectrum, chain-sharded"
+            if not args.no_cpu_baseline:
+                sec["cpu_baseline"] = pta_cpu_baseline(args.pta, args.cpu_seconds)
+            out["secondary"] = {args.pta: sec}
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

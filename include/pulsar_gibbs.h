@@ -22,7 +22,7 @@
  *     pulsar_gibbs.py:603-604).
  *
  * Random numbers: device Philox4x32-10, key = the context seed, counter =
- *   (slot, sweep, global chain id, (pulsar << 8) | event).  Any draw can be
+ *   (slot, sweep, global chain id, (global pulsar << 8) | event).  Any draw can be
  *   replaced by injected values (parity mode) by passing a non-NULL array.
  */
 #ifndef PULSAR_GIBBS_H
@@ -49,8 +49,10 @@ enum {
 
 /* Context options (gs_ctx_set_option) */
 enum {
-  GS_OPT_BCAST = 1 /* factorisation broadcast: 0 = v_readlane -> SGPR (default), 1 = LDS,
-                       2 = v_readlane in batches of 8 SGPR pairs */
+  GS_OPT_BCAST = 1,   /* factorisation broadcast: 0 = v_readlane -> SGPR, 1 = LDS,
+                         2 = v_readlane in batches of 8 SGPR pairs (default) */
+  GS_OPT_PSR_BASE = 2 /* global index of this context's pulsar 0 (Philox counters of a
+                         pulsar-sharded run); default 0 */
 };
 
 typedef struct gs_ctx gs_ctx;

@@ -18,6 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL load; see module docstring)
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpulsar_gibbs.so")
 
 OPT_BCAST = 1
+OPT_PSR_BASE = 2
 EV_B0, EV_RHO, EV_B, EV_RED, EV_CURN, EV_GUMBEL, EV_USER = 1, 2, 3, 4, 5, 6, 16
 
 _P = C.c_void_p

@@ -10,7 +10,8 @@ struct gs_ctx {
   int device;
   hipStream_t stream;
   uint64_t seed;
-  int bcast;  // GS_OPT_BCAST: 0 = v_readlane, 1 = LDS broadcast
+  int bcast;     // GS_OPT_BCAST
+  int psr_base;  // GS_OPT_PSR_BASE: global index of this shard's pulsar 0 (RNG counters)
 };
 
 namespace {
@@ -238,7 +239,8 @@ int gs_ctx_create(int device, uint64_t seed, void* stream, gs_ctx** out) {
   c->device = device;
   c->stream = (hipStream_t)stream;
   c->seed = seed;
-  c->bcast = 0;
+  c->bcast = 2;
+  c->psr_base = 0;
   *out = c;
   return 0;
 }
@@ -267,6 +269,10 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
       if (value < 0 || value > 2) return fail_arg(3, "GS_OPT_BCAST must be 0, 1 or 2");
       ctx->bcast = value;
       return 0;
+    case GS_OPT_PSR_BASE:
+      if (value < 0 || value > (1 << 23)) return fail_arg(3, "GS_OPT_PSR_BASE out of range");
+      ctx->psr_base = value;
+      return 0;
     default:
       return fail_arg(2, "unknown option");
   }
@@ -274,7 +280,9 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
 
 int gs_ctx_get_option(gs_ctx* ctx, int option) {
   if (!ctx) return -1;
-  return option == GS_OPT_BCAST ? ctx->bcast : -1;
+  if (option == GS_OPT_BCAST) return ctx->bcast;
+  if (option == GS_OPT_PSR_BASE) return ctx->psr_base;
+  return -1;
 }
 
 int64_t gs_model_stride(int NF, int NMX) { return model_stride_doubles(NF, NMX); }
@@ -339,7 +347,7 @@ int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, cons
   a.mstride = model_stride_doubles(NF, NMX); a.sweep = sweep; a.chain_base = chain_base;
   a.model = model; a.fidx = fidx; a.midx = midx; a.nm = nm; a.chain_mask = chain_mask;
   a.phiinv_F = phiinv_F; a.z = z;
-  a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = ctx->bcast;
+  a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = ctx->bcast; a.psr_base = ctx->psr_base;
   if (launch_bdraw(ctx->stream, a)) return fail_arg(4, "unsupported NF");
   return after_launch("k_bdraw");
 }
@@ -356,7 +364,7 @@ int gs_rho_analytic(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const 
   RhoArgs a;
   a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.ldb = ldb; a.ldx = ldx; a.sweep = sweep;
   a.chain_base = chain_base; a.rhomin = rhomin; a.rhomax = rhomax; a.fidx = fidx; a.b = b;
-  a.u = u; a.x = x; a.key = key_of(ctx);
+  a.u = u; a.x = x; a.key = key_of(ctx); a.psr_base = ctx->psr_base;
   launch_rho_analytic(ctx->stream, a);
   return after_launch("k_rho_analytic");
 }
@@ -384,7 +392,7 @@ int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.rhomin = rhomin; a.rhomax = rhomax; a.model = model; a.fidx = fidx; a.midx = midx; a.nm = nm;
   a.x_state = x_state; a.b_state = b_state; a.x_rec = x_rec; a.b_rec = b_rec;
   a.z0_inj = z0_inj; a.z_inj = z_inj; a.u_inj = u_inj; a.info = info; a.key = key_of(ctx);
-  a.bcast = ctx->bcast;
+  a.bcast = ctx->bcast; a.psr_base = ctx->psr_base;
   if (launch_sweep_freespec(ctx->stream, a)) return fail_arg(4, "unsupported NF");
   return after_launch("k_sweep_freespec");
 }
@@ -413,7 +421,7 @@ static int grid_common(gs_ctx* ctx, GridArgs& a, int n_psr, int n_chain, int n_f
   if (!x || !xcol) return fail_arg(12, "x/xcol is NULL");
   a.n_psr = n_psr; a.n_chain = n_chain; a.n_f = n_f; a.ngrid = ngrid; a.ldx = ldx; a.sweep = sweep;
   a.chain_base = chain_base; a.tau = tau; a.irn = irn; a.grid3 = grid3; a.u = u; a.xcol = xcol; a.x = x;
-  a.idx_out = idx_out; a.key = key_of(ctx);
+  a.idx_out = idx_out; a.key = key_of(ctx); a.psr_base = ctx->psr_base;
   return 0;
 }
 

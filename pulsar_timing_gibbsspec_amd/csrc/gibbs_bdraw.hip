@@ -191,7 +191,7 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_bdraw(BdrawArgs A) 
     zF = lane < NF ? A.z[sys * A.ldb + fi] : 0.0;
     zM = lane < nM ? A.z[sys * A.ldb + mi] : 0.0;
   } else {
-    gs_normal2(gs_counter(lane, A.sweep, A.chain_base + c, p, A.event), A.key, zF, zM);
+    gs_normal2(gs_counter(lane, A.sweep, A.chain_base + c, p + A.psr_base, A.event), A.key, zF, zM);
   }
   double bF = 0.0, bM = 0.0;
   double* scr = lds + A.mstride + wave * 64;
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_sweep_freespec(Swee
           U = act ? A.u_inj[rec * NFR + kf] : 0.5;
         } else {
           double u2;
-          gs_uniform2(gs_counter(kf, ii, gchain, p, GS_EV_RHO), A.key, U, u2);
+          gs_uniform2(gs_counter(kf, ii, gchain, p + A.psr_base, GS_EV_RHO), A.key, U, u2);
         }
         const double hi = 1 - exp((tau / rhomax) - (tau / rhomin));
         const double eta = 0.0 + hi * U;
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_sweep_freespec(Swee
         zF = act ? zinj[zrow * A.ldb + fi] : 0.0;
         zM = actm ? zinj[zrow * A.ldb + mi] : 0.0;
       } else {
-        gs_normal2(gs_counter(lane, ii, gchain, p, ev), A.key, zF, zM);
+        gs_normal2(gs_counter(lane, ii, gchain, p + A.psr_base, ev), A.key, zF, zM);
       }
       const double phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;
       const int f = bdraw_wave<NF, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
@@ -306,7 +306,7 @@ __global__ void k_rho_analytic(RhoArgs A) {
     U = A.u[sys * NFR + k];
   } else {
     double u2;
-    gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, p, GS_EV_RHO), A.key, U, u2);
+    gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, p + A.psr_base, GS_EV_RHO), A.key, U, u2);
   }
   const double hi = 1 - exp((tau / A.rhomax) - (tau / A.rhomin));
   const double eta = 0.0 + hi * U;

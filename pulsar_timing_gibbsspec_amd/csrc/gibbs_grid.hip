@@ -1,15 +1,13 @@
 // rho|b grid conditionals (gfx950, fp64): a4 Gumbel-max, a6 common (CURN)
 // product-of-pdfs CDF, a7 per-pulsar red CDF, plus the tau reduction.
 //
-// Mapping: one LANE per (system, frequency) row; the lane walks the 1000-point
-// grid serially.  This reproduces numpy's operation order exactly — the
-// product over pulsars is sequential in pulsar order (np.prod), the CDF is a
-// sequential np.cumsum, normalised by its max (the last element) with a true
-// division, and the draw is searchsorted(cdf, u, 'left') - 1 with -1 wrapping
-// to the top grid point (pta_gibbs.py:205-212) — so grid indices match the
-// reference bit for bit on identical inputs.  Two passes over the grid: the
-// first finds the max, the second the crossing (the pdf is recomputed, not
-// stored: 8 KB/row would cost more HBM than the recompute costs VALU).
+// All kernels reproduce numpy's operation order exactly — the product over
+// pulsars is sequential in pulsar order (np.prod), the CDF is a sequential
+// np.cumsum, normalised by its max (the last element) with a true division,
+// and the draw is searchsorted(cdf, u, 'left') - 1 with -1 wrapping to the top
+// grid point (pta_gibbs.py:205-212) — so grid indices match the reference bit
+// for bit on identical inputs.  Mappings: a6 one wavefront per row (45 x 1000
+// pdf terms per row); a7/a4 one lane per row (1000 terms per row).
 // Rows are laid out [frequency][chain] so lanes of a wave read consecutive
 // chains (coalesced).  The grid rho_g = 10**linspace(...), log rho_g and
 // 0.5*log10 rho_g are computed on the host with numpy and passed in
@@ -48,14 +46,60 @@ __global__ void k_tau(TauArgs A) {
 }
 
 // ------------------------------------------------------------ a6: common CDF
-// rows r = k * n_chain + c; tau/irn [n_psr][n_f][n_chain]; irn may be NULL (zeros).
-__global__ void k_rho_curn(GridArgs A) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// One WAVEFRONT per row r = k * n_chain + c (GS_CURN_WPB rows per workgroup);
+// tau/irn [n_psr][n_f][n_chain]; irn may be NULL (zeros).
+//  1. lanes split the grid: pdf[g] = prod_p ratio*exp(-ratio/2)*ln10, the product
+//     sequential in pulsar order (np.prod), into LDS;
+//  2. lane 0 runs the sequential cumsum in place (np.cumsum, bit-exact order);
+//  3. all lanes count cdf[g] / total < u (searchsorted 'left') with a ballot.
+#ifndef GS_CURN_WPB
+#define GS_CURN_WPB 4
+#endif
+__global__ __launch_bounds__(64 * GS_CURN_WPB) void k_rho_curn(GridArgs A) {
+  extern __shared__ double sh[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * GS_CURN_WPB + wave;
   const int64_t nrow = (int64_t)A.n_f * A.n_chain;
-  if (r >= nrow) return;
+  if (r >= nrow) return;  // whole wavefront exits together (no block barrier below)
+  double* pdf = sh + (int64_t)wave * A.ngrid;
   const int c = (int)(r % A.n_chain), k = (int)(r / A.n_chain);
   const int P = A.n_psr;
   const int64_t pstride = nrow;
+  for (int g = lane; g < A.ngrid; g += 64) {
+    const double rg = A.grid3[g];
+    double prod = 1.0;
+    for (int p = 0; p < P; ++p) {
+      const double tau = A.tau[p * pstride + r];
+      const double irn = A.irn ? A.irn[p * pstride + r] : 0.0;
+      const double ratio = tau / (irn + rg);
+      prod *= ratio * exp(-ratio / 2) * LN10;
+    }
+    pdf[g] = prod;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane == 0) {
+    double cum = 0.0;
+    int g = 0;
+    for (; g + 8 <= A.ngrid; g += 8) {
+      double v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = pdf[g + q];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        cum += v[q];
+        pdf[g + q] = cum;
+      }
+    }
+    for (; g < A.ngrid; ++g) {
+      cum += pdf[g];
+      pdf[g] = cum;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   double u;
   if (A.u) {
     u = A.u[(int64_t)c * A.n_f + k];
@@ -63,34 +107,27 @@ __global__ void k_rho_curn(GridArgs A) {
     double u2;
     gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, 0, GS_EV_CURN), A.key, u, u2);
   }
-  double total = 0.0;
-  for (int pass = 0; pass < 2; ++pass) {
-    double cum = 0.0;
-    int cnt = 0;
-    for (int g = 0; g < A.ngrid; ++g) {
-      const double rg = A.grid3[g];
-      double prod = 1.0;
-      for (int p = 0; p < P; ++p) {
-        const double tau = A.tau[p * pstride + r];
-        const double irn = A.irn ? A.irn[p * pstride + r] : 0.0;
-        const double ratio = tau / (irn + rg);
-        prod *= ratio * exp(-ratio / 2) * LN10;
-      }
-      cum += prod;
-      if (pass == 1) cnt += (cum / total < u) ? 1 : 0;
-    }
-    if (pass == 0) total = cum;
-    else {
-      int idx = cnt - 1;
-      if (idx < 0) idx += A.ngrid;
-      if (A.idx_out) A.idx_out[r] = idx;
-      A.x[(int64_t)c * A.ldx + A.xcol[k]] = A.grid3[2 * A.ngrid + idx];
-    }
+  const double total = pdf[A.ngrid - 1];
+  int cnt = 0;
+  for (int g0 = 0; g0 < A.ngrid; g0 += 64) {
+    const int g = g0 + lane;
+    const bool lt = g < A.ngrid && (pdf[g] / total < u);
+    cnt += __popcll(__ballot(lt));
+  }
+  if (lane == 0) {
+    int idx = cnt - 1;
+    if (idx < 0) idx += A.ngrid;
+    if (A.idx_out) A.idx_out[r] = idx;
+    A.x[(int64_t)c * A.ldx + A.xcol[k]] = A.grid3[2 * A.ngrid + idx];
   }
 }
 
 // ------------------------------------------------------------ a7: red CDF
-// rows r = (p * n_f + k) * n_chain + c; gw [n_f][n_chain] = phi_gw (sin column).
+// rows r = (p * n_f + k) * n_chain + c, one LANE per row; gw [n_f][n_chain] = phi_gw.
+// One pass over the grid keeps the (sequential, exact) running sum at 16 chunk
+// ends; the crossing chunk is then recomputed from its exact entry value, so the
+// cumsum seen at every compared position is bit-identical to np.cumsum.
+#define GS_RED_NCH 16
 __global__ void k_rho_red(GridArgs A) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nrow = (int64_t)A.n_psr * A.n_f * A.n_chain;
@@ -103,27 +140,50 @@ __global__ void k_rho_red(GridArgs A) {
     u = A.u[((int64_t)c * A.n_psr + p) * A.n_f + k];
   } else {
     double u2;
-    gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, p, GS_EV_RED), A.key, u, u2);
+    gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, p + A.psr_base, GS_EV_RED), A.key, u, u2);
   }
   const double tau = A.tau[r];
   const double gw = A.irn[(int64_t)k * A.n_chain + c];
-  double total = 0.0;
-  for (int pass = 0; pass < 2; ++pass) {
-    double cum = 0.0;
-    int cnt = 0;
-    for (int g = 0; g < A.ngrid; ++g) {
+  const int ch = (A.ngrid + GS_RED_NCH - 1) / GS_RED_NCH;
+  double ck[GS_RED_NCH];
+  double cum = 0.0;
+#pragma unroll
+  for (int j = 0; j < GS_RED_NCH; ++j) {
+    const int g1 = min(A.ngrid, (j + 1) * ch);
+    for (int g = j * ch; g < g1; ++g) {
       const double ratio = tau / (gw + A.grid3[g]);
       cum += ratio * exp(-ratio / 2) * LN10;
-      if (pass == 1) cnt += (cum / total < u) ? 1 : 0;
     }
-    if (pass == 0) total = cum;
-    else {
-      int idx = cnt - 1;
-      if (idx < 0) idx += A.ngrid;
-      if (A.idx_out) A.idx_out[r] = idx;
-      A.x[(int64_t)c * A.ldx + A.xcol[p * A.n_f + k]] = A.grid3[2 * A.ngrid + idx];
+    ck[j] = cum;
+  }
+  const double total = cum;
+  // first chunk whose end crosses u; everything before it counts
+  int jx = GS_RED_NCH;
+  double entry = 0.0;
+#pragma unroll
+  for (int j = GS_RED_NCH - 1; j >= 0; --j) {
+    if (!(ck[j] / total < u)) {
+      jx = j;
+      entry = j > 0 ? ck[j - 1] : 0.0;
     }
   }
+  int cnt;
+  if (jx == GS_RED_NCH) {
+    cnt = A.ngrid;  // u above every cdf value
+  } else {
+    cnt = jx * ch;
+    double cc = entry;
+    const int g1 = min(A.ngrid, (jx + 1) * ch);
+    for (int g = jx * ch; g < g1; ++g) {
+      const double ratio = tau / (gw + A.grid3[g]);
+      cc += ratio * exp(-ratio / 2) * LN10;
+      cnt += (cc / total < u) ? 1 : 0;
+    }
+  }
+  int idx = cnt - 1;
+  if (idx < 0) idx += A.ngrid;
+  if (A.idx_out) A.idx_out[r] = idx;
+  A.x[(int64_t)c * A.ldx + A.xcol[p * A.n_f + k]] = A.grid3[2 * A.ngrid + idx];
 }
 
 // ------------------------------------------------------------ a4: Gumbel-max
@@ -216,7 +276,8 @@ int launch_tau(hipStream_t s, const TauArgs& a) {
 int launch_rho_curn(hipStream_t s, const GridArgs& a) {
   const int64_t n = (int64_t)a.n_f * a.n_chain;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(k_rho_curn, grid1(n, 64), dim3(64), 0, s, a);
+  const size_t lds = (size_t)GS_CURN_WPB * a.ngrid * sizeof(double);
+  hipLaunchKernelGGL(k_rho_curn, grid1(n, GS_CURN_WPB), dim3(64 * GS_CURN_WPB), lds, s, a);
   return 0;
 }
 

@@ -18,7 +18,7 @@ inline int64_t model_stride_doubles(int NF, int NMX) {
 }
 
 struct BdrawArgs {
-  int n_psr, n_chain, NF, NMX, ldb, event, bcast;
+  int n_psr, n_chain, NF, NMX, ldb, event, bcast, psr_base;
   int64_t mstride, sweep, chain_base;
   const double* model;
   const int32_t *fidx, *midx, *nm, *chain_mask;
@@ -29,7 +29,7 @@ struct BdrawArgs {
 };
 
 struct SweepArgs {
-  int n_psr, n_chain, NF, NMX, ldb, n_sweeps, bcast;
+  int n_psr, n_chain, NF, NMX, ldb, n_sweeps, bcast, psr_base;
   int64_t mstride, it0, chain_base;
   double rhomin, rhomax;
   const double* model;
@@ -41,7 +41,7 @@ struct SweepArgs {
 };
 
 struct RhoArgs {
-  int n_psr, n_chain, NF, ldb, ldx;
+  int n_psr, n_chain, NF, ldb, ldx, psr_base;
   int64_t sweep, chain_base;
   double rhomin, rhomax;
   const int32_t* fidx;
@@ -62,7 +62,7 @@ struct TauArgs {
 };
 
 struct GridArgs {
-  int n_psr, n_chain, n_f, ngrid, ldx;
+  int n_psr, n_chain, n_f, ngrid, ldx, psr_base;
   int64_t sweep, chain_base;
   const double *tau, *irn, *grid3, *u;
   const int32_t* xcol;

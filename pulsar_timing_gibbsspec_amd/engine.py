@@ -173,39 +173,63 @@ def grid3(rhomin, rhomax, n=1000, device="cuda"):
 
 
 class PTAChains:
-    """n_chain chains of the common free-spectrum model (CURN) over all pulsars of a
-    DeviceModel, optionally with per-pulsar red free spectra sampled conditionally
+    """n_chain chains of the common free-spectrum model (CURN) over the pulsars of a
+    DeviceModel, optionally with per-pulsar red free spectra drawn conditionally
     (PTABlockGibbs.sample, pta_gibbs.py:664-704).
 
     Per sweep (one host-side launch sequence, all chains at once):
       record x (row ii) -> [ii == 0: b|rho from x0] -> tau -> [red grid-CDF]
-      -> common grid-CDF -> gate + phiinv -> gated b|rho.
-    State (HBM): x (n_chain, n_param) in the PTA's parameter order, b (P*n_chain, ldb).
+      -> [exchange] -> common grid-CDF -> gate + phiinv -> gated b|rho.
+    State (HBM): x (n_chain, n_param) in the PTA's parameter order (every rank
+    holds the full vector), b (P_local*n_chain, ldb).
+
+    Pulsar sharding: the DeviceModel holds this rank's contiguous pulsar block
+    [psr_lo, psr_lo + P_local) of P_global; ``gather`` (distributed.PulsarAllGather)
+    exchanges the [tau | x_red] slabs so the common draw sees every pulsar in global
+    order.  ``sweep_begin`` / ``sweep_end`` expose the two halves around the exchange.
     """
 
     def __init__(self, model: DeviceModel, n_param, gw_col, red_col, gw_bounds, red_bounds, n_chain, x0,
-                 chain_base=0, ngrid=1000):
+                 chain_base=0, ngrid=1000, P_global=None, psr_lo=0, gather=None):
         self.model, self.ctx = model, model.ctx
         dev = self.ctx.device
         P, C = model.P, int(n_chain)
         self.P, self.C, self.n_param = P, C, int(n_param)
+        self.PG = int(P_global) if P_global is not None else P
+        self.psr_lo = int(psr_lo)
+        self.sharded = self.PG != P
+        self.gather = gather
+        if self.sharded and gather is None:
+            raise ValueError("a pulsar-sharded PTAChains needs a gather")
         self.n_f = model.NF // 2
         self.chain_base = int(chain_base)
         self.ngrid = ngrid
+        self.ctx.set_option(_lib.OPT_PSR_BASE, self.psr_lo)
         self.gw_col = _t(np.asarray(gw_col, np.int32), torch.int32, dev)
         self.red = red_col is not None
-        self.red_col = _t(np.asarray(red_col, np.int32).ravel(), torch.int32, dev) if self.red else None
+        if self.red:
+            rg = np.asarray(red_col, np.int32).reshape(self.PG, self.n_f)
+            self.red_col_g = _t(rg.ravel(), torch.int32, dev)
+            self.red_col = _t(rg[self.psr_lo:self.psr_lo + P].ravel(), torch.int32, dev)
+            self.red_col_l64 = torch.as_tensor(rg[self.psr_lo:self.psr_lo + P].ravel(), dtype=torch.long,
+                                               device=dev)
+            self.red_col_g64 = torch.as_tensor(rg.ravel(), dtype=torch.long, device=dev)
+        else:
+            self.red_col = self.red_col_g = None
         self.grid_gw = grid3(*gw_bounds, n=ngrid, device=dev)
         self.grid_red = grid3(*red_bounds, n=ngrid, device=dev) if self.red else None
         self.x = _t(np.broadcast_to(np.asarray(x0, float), (C, self.n_param)), torch.float64, dev)
         self.b = torch.zeros(P * C, model.ldb, dtype=torch.float64, device=dev)
         self.tau = torch.empty(P, self.n_f, C, dtype=torch.float64, device=dev)
+        self.tau_g = torch.empty(self.PG, self.n_f, C, dtype=torch.float64, device=dev) if self.sharded \
+            else self.tau
         self.gwphi = torch.empty(self.n_f, C, dtype=torch.float64, device=dev)
-        self.irn = torch.empty(P, self.n_f, C, dtype=torch.float64, device=dev) if self.red else None
+        self.irn = torch.empty(self.PG, self.n_f, C, dtype=torch.float64, device=dev) if self.red else None
         self.phiinv_F = torch.empty(P * C, model.NF, dtype=torch.float64, device=dev)
         self.gate = torch.ones(C, dtype=torch.int32, device=dev)
         self.xlast = torch.empty(C, dtype=torch.float64, device=dev)
         self.info = torch.zeros(P * C, dtype=torch.int32, device=dev)
+        self.slab_shape = ((2 if self.red else 1), self.n_f, C)
         self.it = 0
 
     def _bdraw(self, z, event, mask):
@@ -221,10 +245,9 @@ class PTAChains:
             ptr(self.xlast) if with_gate else None, ptr(self.gw_col), ptr(self.red_col),
             ptr(self.phiinv_F), ptr(self.gate)), "gs_pta_gate_phiinv")
 
-    def sweep(self, x_rec=None, z0=None, z=None, u_red=None, u_curn=None):
-        """One PTABlockGibbs sweep for every chain; x_rec: (n_chain, n_param) row or None.
-        z0/z: (P*n_chain, ldb) injected normals (original column order); u_red
-        (n_chain, P, n_f) and u_curn (n_chain, n_f): injected uniforms."""
+    def sweep_begin(self, x_rec=None, z0=None, u_red=None):
+        """Record, [first draw], tau and the local red draws.  Returns the local
+        exchange slab [P_local, 1 or 2, n_f, C] (None when not sharded)."""
         lib, h, m = self.ctx.lib, self.ctx.handle, self.model
         ii = self.it
         check(lib.gs_pta_record(h, self.C, self.n_param, ptr(self.x), ptr(x_rec), ptr(self.xlast)),
@@ -240,11 +263,36 @@ class PTAChains:
             check(lib.gs_rho_red(h, self.P, self.C, self.n_f, ptr(self.tau), ptr(self.gwphi), self.ngrid,
                                  ptr(self.grid_red), ptr(u_red), ii, self.chain_base, ptr(self.x),
                                  self.n_param, ptr(self.red_col), None), "gs_rho_red")
-            check(lib.gs_phi_from_x(h, self.C, self.P * self.n_f, ptr(self.x), self.n_param,
-                                    ptr(self.red_col), ptr(self.irn)), "gs_phi_from_x")
-        check(lib.gs_rho_curn(h, self.P, self.C, self.n_f, ptr(self.tau), ptr(self.irn), self.ngrid,
+        if not self.sharded:
+            return None
+        parts = [self.tau.unsqueeze(1)]
+        if self.red:
+            xr = self.x.index_select(1, self.red_col_l64).T.reshape(self.P, 1, self.n_f, self.C)
+            parts.append(xr)
+        return torch.cat(parts, dim=1)
+
+    def sweep_end(self, slab_g=None, z=None, u_curn=None):
+        """Common draw on the global inputs, gate, gated b|rho."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        ii = self.it
+        if self.sharded:
+            self.tau_g.copy_(slab_g[:, 0])
+            if self.red:
+                xr = slab_g[:, 1].reshape(self.PG * self.n_f, self.C).T
+                self.x.index_copy_(1, self.red_col_g64, xr.contiguous())
+        if self.red:
+            check(lib.gs_phi_from_x(h, self.C, self.PG * self.n_f, ptr(self.x), self.n_param,
+                                    ptr(self.red_col_g), ptr(self.irn)), "gs_phi_from_x")
+        check(lib.gs_rho_curn(h, self.PG, self.C, self.n_f, ptr(self.tau_g), ptr(self.irn), self.ngrid,
                               ptr(self.grid_gw), ptr(u_curn), ii, self.chain_base, ptr(self.x),
                               self.n_param, ptr(self.gw_col), None), "gs_rho_curn")   # pta_gibbs.py:181-214
         self._gate_phiinv(with_gate=True)                      # pta_gibbs.py:703
         self._bdraw(z, _lib.EV_B, self.gate)                   # pta_gibbs.py:704
         self.it += 1
+
+    def sweep(self, x_rec=None, z0=None, z=None, u_red=None, u_curn=None):
+        """One PTABlockGibbs sweep for every chain; x_rec: (n_chain, n_param) row or None.
+        z0/z: (P*n_chain, ldb) injected normals (original column order); u_red
+        (n_chain, P, n_f) and u_curn (n_chain, n_f): injected uniforms."""
+        slab = self.sweep_begin(x_rec=x_rec, z0=z0, u_red=u_red)
+        self.sweep_end(self.gather(slab) if self.sharded else None, z=z, u_curn=u_curn)

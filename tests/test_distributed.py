@@ -1,0 +1,91 @@
+"""Multi-process plumbing on CPU (gloo, world_size 2): the sharding helpers and
+the per-sweep exchange used by the pulsar-sharded CURN path."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pulsar_timing_gibbsspec_amd import distributed as D
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, fn, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, fn(rank, world)))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_world(fn, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+def _gather_case(rank, world):
+    P, n_f, C = 7, 5, 3
+    full = torch.arange(P * 2 * n_f * C, dtype=torch.float64).reshape(P, 2, n_f, C)
+    assign = [np.arange(*D.shard_range(P, r, world)) for r in range(world)]
+    g = D.PulsarAllGather(assign, (2, n_f, C))
+    local = full[assign[rank]]
+    out = g(local)
+    return bool(torch.equal(out, full)), g.pmax, D.max_over_ranks(float(rank + 1))
+
+
+def _gather_lpt_case(rank, world):
+    w = np.array([5.0, 1, 1, 4, 2, 3, 3])
+    assign = D.balance_pulsars(w, world)
+    full = torch.randn(len(w), 1, 4, 2, generator=torch.Generator().manual_seed(0), dtype=torch.float64)
+    g = D.PulsarAllGather(assign, (1, 4, 2))
+    return bool(torch.equal(g(full[assign[rank]]), full))
+
+
+def test_shard_range_covers_everything():
+    for n in (0, 1, 7, 45, 4096):
+        for w in (1, 2, 3, 8):
+            blocks = [D.shard_range(n, r, w) for r in range(w)]
+            assert blocks[0][0] == 0 and blocks[-1][1] == n
+            assert all(blocks[i][1] == blocks[i + 1][0] for i in range(w - 1))
+            sizes = [b - a for a, b in blocks]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_balance_pulsars_by_cost():
+    m = np.array([70, 77, 68, 72, 75, 69, 74, 71])
+    a = D.balance_pulsars(m ** 3, 3)
+    assert sorted(np.concatenate(a).tolist()) == list(range(8))
+    loads = [np.sum(m[x] ** 3) for x in a]
+    assert max(loads) / min(loads) < 1.5
+
+
+@pytest.mark.timeout(300)
+def test_pulsar_allgather_gloo_world2():
+    out = run_world(_gather_case, 2)
+    assert all(v[0] for v in out.values())
+    assert out[0][1] == 4 and out[0][2] == 2.0 and out[1][2] == 2.0
+
+
+@pytest.mark.timeout(300)
+def test_pulsar_allgather_uneven_lpt_gloo_world2():
+    out = run_world(_gather_lpt_case, 2)
+    assert all(out.values())

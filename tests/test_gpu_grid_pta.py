@@ -178,3 +178,51 @@ def test_pta_block_gibbs_surface(tmp_path):
     assert np.all(red >= -10.0) and np.all(red <= -4.0)
     b = gb.update_b(chain[-1])
     assert len(b) == 6 and all(np.all(np.isfinite(bb)) for bb in b)
+
+
+@pytest.mark.parametrize("kind", ["curn", "curn_red"])
+def test_pulsar_sharded_engine_bit_identical(kind):
+    """Two pulsar shards (own context, own DeviceModel) exchanging [tau | x_red] slabs
+    reproduce the unsharded engine's chains bit for bit under device Philox
+    (global chain and pulsar ids in the counters)."""
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd.distributed import shard_range
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
+    pta = synthetic.array_pta(kind=kind, n_psr=9, seed=2)
+    T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
+    names = pta.param_names
+    rind = [i for i, n in enumerate(names) if "rho" in n and "gw" in n]
+    hind = np.array([i for i, n in enumerate(names) if "red" in n and "rho" in n])
+    red_col = hind.reshape(len(T), -1) if kind == "curn_red" else None
+    gwid = [np.arange(t.shape[1] - 60, t.shape[1]) for t in T]
+    fixed = [np.full(t.shape[1] - 60, 1e-40) for t in T]
+    C, S = 16, 6
+    x0 = np.random.default_rng(0).uniform(-9, -4, (C, len(names)))
+    bounds = ((1e-18, 1e-8), (1e-20, 1e-8))
+
+    ref_ctx = _lib.Context(0, seed=77)
+    ref = PTAChains(DeviceModel(ref_ctx, T, N, R, gwid, fixed), len(names), rind, red_col, *bounds, C, x0)
+    xr_ref = torch.zeros(S, C, len(names), dtype=torch.float64, device="cuda")
+    for i in range(S):
+        ref.sweep(x_rec=xr_ref[i])
+
+    shards = []
+    for r in range(2):
+        lo, hi = shard_range(len(T), r, 2)
+        ctx = _lib.Context(0, seed=77)
+        mdl = DeviceModel(ctx, T[lo:hi], N[lo:hi], R[lo:hi], gwid[lo:hi], fixed[lo:hi])
+        shards.append(PTAChains(mdl, len(names), rind, red_col, *bounds, C, x0, P_global=len(T), psr_lo=lo,
+                                gather=lambda s: s))
+    xr = [torch.zeros(S, C, len(names), dtype=torch.float64, device="cuda") for _ in range(2)]
+    for i in range(S):
+        slabs = [sh.sweep_begin(x_rec=xr[j][i]) for j, sh in enumerate(shards)]
+        glob = torch.cat(slabs, dim=0)            # the all-gather, in global pulsar order
+        for sh in shards:
+            sh.sweep_end(glob)
+    assert torch.equal(xr[0], xr_ref) and torch.equal(xr[1], xr_ref)
+    bref = ref.b.view(len(T), C, -1)
+    for r, sh in enumerate(shards):
+        lo, hi = shard_range(len(T), r, 2)
+        bs = sh.b.view(hi - lo, C, -1)
+        w = bs.shape[2]
+        assert torch.equal(bs, bref[lo:hi, :, :w]) and not bref[lo:hi, :, w:].any()
