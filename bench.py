@@ -45,6 +45,19 @@ def executed_flops_per_chain_sweep(nf, nm):
     return nf ** 3 / 3 + nf ** 2 / 2 + nf / 6 + 2 * nf ** 2 + 2 * nm * nf + nm ** 2
 
 
+def pmc_traffic(S, C):
+    """HBM bytes per launch of k_sweep_freespec from the committed PMC profile
+    (tools/gpu_profile.sh -> tools/pmc_traffic.py), valid for the same launch shape."""
+    f = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(f))
+    except (OSError, ValueError):
+        return None
+    if d.get("sweeps_per_launch") != S or d.get("chains") != C or "bytes_per_launch" not in d:
+        return None
+    return d["bytes_per_launch"]
+
+
 def cpu_baseline(seconds=12.0):
     """Reference loop (oracle restatement, SVD draw), 1 thread, bounded sample."""
     from oracle import gibbs_oracle as O
@@ -277,7 +290,8 @@ def main():
                        "parallelism": f"chains sharded over {world} GPU(s)"},
             "ess_per_s": ess,
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
+                         "traffic": pmc_traffic(S, C),
                          "kernel": "k_sweep_freespec", "kernel_avg_ms": launch_s * 1e3,
                          "alg_flops_per_launch": alg_flops_launch,
                          "executed_tflops": exe, "executed_frac": exe / FP64_PEAK_TFLOPS},

@@ -314,3 +314,34 @@ def iat(x, c=5.0):
         if M >= c * tau[M]:
             return float(tau[M])
     return float(tau[-1])
+
+
+# ============================================================== white-noise MH (a10)
+MH_SIZES = [0.1, 0.5, 1.0, 3.0, 10.0]
+MH_PROBS = [0.1, 0.15, 0.5, 0.15, 0.1]
+
+
+def ndiag_white(sigma, backends, ef, eq_log10):
+    """N = efac^2 sigma^2 + 10**(2 log10_tnequad) per backend (the facade's get_ndiag;
+    the per-backend power is a Python-float pow there, kept so here bit-for-bit)."""
+    eq = np.array([10.0 ** (2.0 * float(v)) for v in eq_log10])
+    return np.asarray(ef, float)[backends] ** 2 * sigma ** 2 + eq[backends]
+
+
+def white_mh(x, wind, steps, lnlike, lnprior):
+    """Steady-state white-noise Metropolis block (pulsar_gibbs.py:373-404).
+    steps: iterable of (scale, par, z, u) = the values of np.random.choice(sizes, p=probs),
+    np.random.choice(wind), np.random.randn(1), np.random.rand() for each step.
+    The jump is q[par] += z * (0.05 * len(wind)) * scale (:383); accept if
+    (lnlike1 + lnprior1) - (lnlike0 + lnprior0) > log(u) (:398)."""
+    xnew = np.asarray(x, float).copy()
+    l0, p0 = lnlike(xnew), lnprior(xnew)
+    for scale, par, z, u in steps:
+        q = xnew.copy()
+        sigmas = 0.05 * len(wind)
+        q[int(par)] += z * sigmas * scale
+        l1, p1 = lnlike(q), lnprior(q)
+        diff = (l1 + p1) - (l0 + p0)
+        if diff > np.log(u):
+            xnew, l0, p0 = q, l1, p1
+    return xnew

@@ -71,9 +71,19 @@ class Capture:
 
     def __enter__(self):
         R = np.random
-        self._orig = dict(randn=R.randn, uniform=R.uniform, gumbel=R.gumbel)
+        self._orig = dict(randn=R.randn, uniform=R.uniform, gumbel=R.gumbel, choice=R.choice, rand=R.rand)
         rs = R.random_sample
         cap = self
+
+        def choice(a, size=None, replace=True, p=None):
+            v = self._orig["choice"](a, size=size, replace=replace, p=p)
+            cap.log.append(("choice", np.array(v, dtype=float)))
+            return v
+
+        def rand(*shape):
+            v = self._orig["rand"](*shape)
+            cap.log.append(("rand", np.array(v, dtype=float)))
+            return v
 
         def randn(*shape):
             z = self._orig["randn"](*shape)
@@ -94,12 +104,14 @@ class Capture:
             return loc - scale * np.log(-np.log1p(-u))   # numpy legacy gumbel
 
         R.randn, R.uniform, R.gumbel = randn, uniform, gumbel
+        R.choice, R.rand = choice, rand
         return self
 
     def __exit__(self, *a):
         R = np.random
         R.randn, R.uniform, R.gumbel = (self._orig["randn"], self._orig["uniform"],
                                         self._orig["gumbel"])
+        R.choice, R.rand = self._orig["choice"], self._orig["rand"]
 
     def take(self, kind):
         return [a for k, a in self.log if k == kind]
@@ -265,6 +277,51 @@ def likelihoods(ref, out):
     print("likelihoods:", out)
 
 
+def white_mh(ref, out, nsweep=6, acl=40):
+    """White-noise Metropolis block (pulsar_gibbs.py:332-406, steady-state branch)
+    inside the sample loop order (:656-698), driven with the reference's own methods.
+    The warm-up branch (iters=1000) needs `acor` (absent here), so aclength_white is
+    set directly; every MH draw (choice of scale, choice of parameter, randn jump,
+    rand acceptance) is captured."""
+    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0, efac_vary=True, n_backends=3)
+    np.random.seed(13)
+    g = _quiet(ref.PulsarBlockGibbs, pta)
+    x0 = np.concatenate([p.sample().flatten() for p in g.params])
+    names = list(g.param_names)
+    wind = g.get_efacequad_indices()
+    g.aclength_white = acl
+    chain, bhist, white_in, white_out = [], [], [], []
+    xnew = x0.copy()
+    with Capture() as cap:
+        np.random.seed(14)
+        for ii in range(nsweep):
+            chain.append(xnew.copy())
+            bhist.append(g._b.copy())
+            if ii == 0:
+                g._b = g.update_b(x0)
+            g.TNT = g.d = None
+            white_in.append(xnew.copy())
+            xnew = g.update_white_params(xnew, iters=None)
+            white_out.append(xnew.copy())
+            xnew = g.update_gwrho_params(xnew)
+            if np.all(xnew != chain[ii][-1]):
+                g._b = g.update_b(xnew)
+    log = cap.log
+    kinds = np.array([k for k, _ in log])
+    vals = [v for _, v in log]
+    sig = pta.models[0].white[0]
+    np.savez_compressed(out, x0=x0, chain=np.stack(chain), bhist=np.stack(bhist), b_final=g._b,
+                        white_in=np.stack(white_in), white_out=np.stack(white_out),
+                        kinds=kinds, vals=np.concatenate([np.atleast_1d(v).ravel() for v in vals]),
+                        lens=np.array([np.atleast_1d(v).size for v in vals]),
+                        T=pta.get_basis()[0], r=pta.get_residuals()[0], sigma=sig.sigma,
+                        backends=sig.backends, wind=wind, aclength=acl, gwid=np.asarray(g.gwid),
+                        rhomin=g.rhomin, rhomax=g.rhomax, param_names=np.array(names),
+                        pmin=np.array([p.pmin for p in g.params for _ in range(p.size or 1)]),
+                        pmax=np.array([p.pmax for p in g.params for _ in range(p.size or 1)]))
+    print("white:", out, len(log))
+
+
 def main(root):
     mods = load_reference(root)
     PB = mods["pulsar_gibbs"]
@@ -275,6 +332,7 @@ def main(root):
     pta_run(PT, os.path.join(HERE, "pta_curn.npz"), "curn", niter=12)
     pta_run(PT, os.path.join(HERE, "pta_curn_red.npz"), "curn_red", niter=12)
     pta_sample_check(PT, os.path.join(HERE, "pta_sample_small.npz"))
+    white_mh(PB, os.path.join(HERE, "white_mh_j1713.npz"))
     if "--long" in sys.argv:
         single_pulsar_long(PB, os.path.join(HERE, "long_j1713.npz"))
 

@@ -199,3 +199,72 @@ def test_reference_svd_mean_error():
         assert normwise_rel(g["b_final"][off:off + g["m"][p]], bx) < 1e-7
     assert worst_svd > 1e-9          # the reference itself misses 1e-9 here
     assert worst_chol < 1e-10
+
+
+def white_setup(g):
+    """Facade PTA of the white-noise fixture + the reference's likelihood/prior."""
+    from pulsar_timing_gibbsspec_amd import synthetic
+    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0, efac_vary=True, n_backends=3)
+    names = list(g["param_names"])
+    ef_i = [names.index(f"J1713+0747_b{i}_efac") for i in range(3)]
+    eq_i = [names.index(f"J1713+0747_b{i}_log10_tnequad") for i in range(3)]
+
+    def N_of(x):
+        return O.ndiag_white(g["sigma"], g["backends"], x[ef_i], x[eq_i])
+
+    def lnprior(x):
+        params = pta.map_params(x)
+        return np.sum([p.get_logpdf(params=params) for p in pta.params])
+    return pta, N_of, lnprior
+
+
+def split_draws(g):
+    """Re-group the captured draw log into per-sweep records."""
+    kinds, vals, lens = g["kinds"], g["vals"], g["lens"]
+    off = np.concatenate([[0], np.cumsum(lens)])
+    items = [(kinds[i], vals[off[i]:off[i + 1]]) for i in range(kinds.size)]
+    return items
+
+
+def test_white_mh_loop_bitwise():
+    """Loop with the white MH block (pulsar_gibbs.py:656-698, steady state) replayed by
+    the oracle on the reference's draws: chain and b bit-for-bit."""
+    g = golden("white_mh_j1713.npz")
+    pta, N_of, lnprior = white_setup(g)
+    T, r = g["T"], g["r"]
+    wind = g["wind"]
+    acl = int(g["aclength"])
+    gwid = g["gwid"]
+    gwind = np.array([i for i, n in enumerate(g["param_names"]) if "rho" in n])
+    items = iter(split_draws(g))
+    x = g["x0"].copy()
+    b = np.zeros(T.shape[1])
+
+    def draw_b(x):
+        k, z = next(items)
+        assert k == "randn"
+        N = N_of(x)
+        TNT, d = O.tnt(T, N, r)
+        ph = 1.0 / pta.get_phi(pta.map_params(x))[0]
+        return O.bdraw_svd(TNT, d, ph, z)
+
+    for ii in range(g["chain"].shape[0]):
+        assert np.array_equal(x, g["chain"][ii]), ii
+        assert np.array_equal(b, g["bhist"][ii]), (ii, np.abs(b - g["bhist"][ii]).max())
+        if ii == 0:
+            b = draw_b(g["x0"])
+        steps = []
+        for _ in range(acl):
+            (k1, s), (k2, p), (k3, z), (k4, u) = next(items), next(items), next(items), next(items)
+            assert (k1, k2, k3, k4) == ("choice", "choice", "randn", "rand")
+            steps.append((s[0], p[0], z[0], u[0]))
+        xw = O.white_mh(x, wind, steps, lambda q: O.lnlike_white(r, T, b, N_of(q)), lnprior)
+        assert np.array_equal(xw, g["white_out"][ii])
+        k, U = next(items)
+        tau = O.tau_half(b, gwid)
+        xn = xw.copy()
+        xn[gwind] = 0.5 * np.log10(O.rho_analytic(tau, U, float(g["rhomin"]), float(g["rhomax"])))
+        if np.all(xn != x[-1]):
+            b = draw_b(xn)
+        x = xn
+    assert np.array_equal(b, g["b_final"])
