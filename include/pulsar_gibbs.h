@@ -44,6 +44,7 @@ enum {
   GS_EV_RED = 4,    /* per-pulsar red grid-CDF uniforms  (pta_gibbs.py:271)        */
   GS_EV_CURN = 5,   /* common grid-CDF uniforms          (pta_gibbs.py:209)        */
   GS_EV_GUMBEL = 6, /* Gumbel-max uniforms               (pulsar_gibbs.py:233)     */
+  GS_EV_WHITE = 7,  /* white-noise MH draws              (pulsar_gibbs.py:377-398) */
   GS_EV_USER = 16   /* first id free for callers                                    */
 };
 
@@ -214,6 +215,86 @@ int gs_pta_record(gs_ctx* ctx, int n_chain, int n_param, const double* x, double
 int gs_pta_gate_phiinv(gs_ctx* ctx, int n_psr, int n_chain, int n_f, int n_param, const double* x,
                        const double* xlast, const int32_t* gw_col, const int32_t* red_col,
                        double* phiinv_F, int32_t* gate);
+
+/* ------------------------------------------------------------------------
+ * (a10) White-noise Metropolis block and the per-chain TNT it forces
+ * (PulsarBlockGibbs.update_white_params pulsar_gibbs.py:332-406,
+ * get_lnlikelihood_white :523-546, TNT recompute :500-502 / :664-665).
+ *
+ * N_i = efac_k^2 (sigma_i^2 + 10^(2 log10_t2equad_k)) + 10^(2 log10_tnequad_k) for the
+ * backend k of TOA i (absent parameters: efac 1, equads 0).  TOAs of a pulsar are
+ * stored grouped by backend (the likelihood is a sum, so the order is free);
+ * y / sigma2 / r / bk rows use the pulsar's toa_off.  Per-chain arrays of TOAs
+ * (y) are chain-major with leading dimension ldy (>= total TOAs).
+ */
+#define GS_WHITE_MAX_BK 15 /* backends per pulsar  */
+#define GS_WHITE_MAX_W 32  /* white parameters per pulsar */
+enum { GS_WHITE_EFAC = 0, GS_WHITE_TNEQUAD = 1, GS_WHITE_T2EQUAD = 2 };
+
+typedef struct {
+  int64_t n_toa;   /* TOAs of this pulsar                                          */
+  int64_t toa_off; /* element offset into sigma2 / bk / r and each chain's y row    */
+  int64_t w_off;   /* offset of this pulsar's parameters in the wcol/wkind/... tables */
+  int32_t n_bk;    /* backends (<= GS_WHITE_MAX_BK)                                */
+  int32_t n_w;     /* white parameters (<= GS_WHITE_MAX_W)                         */
+  int32_t bk_off[GS_WHITE_MAX_BK + 1]; /* first TOA of each backend group; [n_bk] = n_toa */
+} gs_white_desc;
+
+/*
+ * y = r - T b per (pulsar, chain) (pulsar_gibbs.py:534-535).  tdesc: the gs_tnt_desc
+ * array with T_off indexing Tt, the COLUMN-major (m x n_toa) copy of T.
+ * y: [n_chain x ldy], system (p, c) at y + c * ldy + toa_off.  n_toa_max: largest n_toa.
+ */
+int gs_white_resid(gs_ctx* ctx, int n_psr, int n_chain, int64_t n_toa_max, int ldb,
+                   const gs_tnt_desc* tdesc, const double* Tt, const double* r, const double* b,
+                   int64_t ldy, double* y);
+
+/*
+ * n_steps single-parameter Metropolis steps per (pulsar, chain) on the pulsar's
+ * white parameters (pulsar_gibbs.py:373-404): scale from {0.1,0.5,1,3,10} w.p.
+ * {.1,.15,.5,.15,.1}, one parameter uniformly, jump z * (0.05 n_w) * scale, Uniform
+ * prior [wmin, wmax] (inclusive), accept if dlnL > log U.  One wavefront per system;
+ * a step only re-sums the TOAs of the backend it touches.
+ * wcol/wkind/wbk [sum n_w] int32: x column, GS_WHITE_* kind, backend; wmin/wmax [sum n_w].
+ * x: [n_chain x ldx] read and updated in place.  nsteps_chain [n_chain] (NULL: n_steps).
+ * inj [n_steps x n_sys x 4] (scale value, parameter index within the pulsar's list,
+ * normal, uniform) or NULL (Philox GS_EV_WHITE, sweep `sweep`).
+ * q_rec [n_steps x n_sys x GS_WHITE_MAX_W] proposals q[wind] (short_chain, :390) or NULL;
+ * n_acc [n_sys] accepted steps or NULL.
+ */
+int gs_white_mh(gs_ctx* ctx, int n_psr, int n_chain, const gs_white_desc* wdesc,
+                const int32_t* wcol, const int32_t* wkind, const int32_t* wbk, const double* wmin,
+                const double* wmax, const double* sigma2, const double* y, int64_t ldy, double* x,
+                int ldx, int n_steps, const int32_t* nsteps_chain, int64_t sweep, int64_t chain_base,
+                const double* inj, double* q_rec, int32_t* n_acc);
+
+/*
+ * Per-chain TNT = T^T N_c^-1 T and d = T^T N_c^-1 r with N_c from the chain's white
+ * parameters in x (pulsar_gibbs.py:495-502).  T row-major as in gs_tnt (tdesc T_off);
+ * system (p, c) writes TNT + tdesc[p].tnt_off + c * tnt_cstride (m x m, full) and
+ * d + tdesc[p].d_off + c * d_cstride.  bk [total TOAs] int32 backend of each TOA.
+ */
+int gs_white_tnt(gs_ctx* ctx, int n_psr, int n_chain, int m_max, const gs_tnt_desc* tdesc,
+                 const gs_white_desc* wdesc, const int32_t* wcol, const int32_t* wkind,
+                 const int32_t* wbk, const double* T, const double* sigma2, const int32_t* bk,
+                 const double* r, const double* x, int ldx, int64_t tnt_cstride, int64_t d_cstride,
+                 double* TNT, double* d);
+
+/*
+ * gs_prefix for per-chain systems: system (p, c) reads TNT + desc[p].tnt_off +
+ * c * tnt_cstride, d + desc[p].d_off + c * d_cstride and writes its model block at
+ * model + (p * n_chain + c) * gs_model_stride(NF, NMX).
+ */
+int gs_prefix_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const gs_prefix_desc* desc,
+                  int64_t tnt_cstride, int64_t d_cstride, const double* TNT, const double* d,
+                  const int32_t* fidx, const int32_t* midx, const double* phiinv_fixed,
+                  double* model, int32_t* info);
+
+/* gs_bdraw with one model block per system (model + sys * gs_model_stride). */
+int gs_bdraw_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,
+                 const double* model, const int32_t* fidx, const int32_t* midx, const int32_t* nm,
+                 const double* phiinv_F, const double* z, int64_t sweep, int event,
+                 int64_t chain_base, const int32_t* chain_mask, double* b, int32_t* info);
 
 /*
  * Philox4x32-10 test hook: out[i] = the 4 words for counter

@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpulsar_g
 
 OPT_BCAST = 1
 OPT_PSR_BASE = 2
-EV_B0, EV_RHO, EV_B, EV_RED, EV_CURN, EV_GUMBEL, EV_USER = 1, 2, 3, 4, 5, 6, 16
+EV_B0, EV_RHO, EV_B, EV_RED, EV_CURN, EV_GUMBEL, EV_WHITE, EV_USER = 1, 2, 3, 4, 5, 6, 7, 16
 
 _P = C.c_void_p
 _I = C.c_int
@@ -52,6 +52,12 @@ SIGNATURES = {
     "gs_phi_from_x": (_I, [_P, _I, _I, _P, _I, _P, _P]),
     "gs_pta_record": (_I, [_P, _I, _I, _P, _P, _P]),
     "gs_pta_gate_phiinv": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "gs_prefix_sys": (_I, [_P, _I, _I, _I, _I, _P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P]),
+    "gs_bdraw_sys": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _I, _I64, _P, _P, _P]),
+    "gs_white_resid": (_I, [_P, _I, _I, _I64, _I, _P, _P, _P, _P, _I64, _P]),
+    "gs_white_mh": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _I, _I, _P, _I64, _I64,
+                         _P, _P, _P]),
+    "gs_white_tnt": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I64, _I64, _P, _P]),
 }
 
 _lib = None

@@ -101,17 +101,21 @@ __global__ __launch_bounds__(256) void k_tnr(const gs_tnt_desc* desc, const doub
 
 // ------------------------------------------------------------------ prefix
 // One workgroup per pulsar; see include/pulsar_gibbs.h gs_prefix for the outputs.
+// Per-chain systems (white-noise runs): block sys = p * n_chain + c reads its TNT/d at
+// the pulsar's offsets + c * (tnt_cstride, d_cstride) and writes model block sys.
 __global__ __launch_bounds__(256) void k_prefix(const gs_prefix_desc* desc, int NF, int NMX,
                                                 const double* TNT, const double* d,
                                                 const int32_t* fidx, const int32_t* midx,
                                                 const double* phfix, double* model, int64_t mstride,
-                                                int32_t* info) {
+                                                int32_t* info, int n_chain, int64_t tnt_cstride,
+                                                int64_t d_cstride) {
   extern __shared__ double sm[];
-  const int p = blockIdx.x;
+  const int sys = blockIdx.x;
+  const int p = sys / n_chain, c = sys % n_chain;
   const gs_prefix_desc D = desc[p];
   const int m = (int)D.m, nM = (int)D.n_fixed;
-  const double* A = TNT + D.tnt_off;
-  const double* dv = d + D.d_off;
+  const double* A = TNT + D.tnt_off + (int64_t)c * tnt_cstride;
+  const double* dv = d + D.d_off + (int64_t)c * d_cstride;
   const int32_t* Fi = fidx + (int64_t)p * NF;
   const int32_t* Mi = midx + (int64_t)p * NMX;
   double* L = sm;                  // NMX x NMX
@@ -170,7 +174,7 @@ __global__ __launch_bounds__(256) void k_prefix(const gs_prefix_desc* desc, int 
     }
   }
   __syncthreads();
-  double* out = model + (int64_t)p * mstride;
+  double* out = model + (int64_t)sys * mstride;
   double* S0 = out;
   double* dF = S0 + NF * (NF + 1);
   double* G = dF + NF;
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(256) void k_prefix(const gs_prefix_desc* desc, int 
   for (int64_t q = (int64_t)NF * (NF + 1) + NF + NMX * (NF + 1) + NMX + NMX * NMX + tid; q < mstride; q += nt)
     out[q] = 0.0;
   __syncthreads();
-  if (tid == 0 && info) info[p] = s_fail;
+  if (tid == 0 && info) info[sys] = s_fail;
 }
 
 __global__ void k_philox(int64_t n, const uint32_t* ctr, uint32_t* out, gs_key key) {
@@ -312,6 +316,30 @@ int gs_tnt(gs_ctx* ctx, int n_psr, int m_max, const gs_tnt_desc* desc, const dou
   return 0;
 }
 
+int gs_prefix_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const gs_prefix_desc* desc,
+                  int64_t tnt_cstride, int64_t d_cstride, const double* TNT, const double* d,
+                  const int32_t* fidx, const int32_t* midx, const double* phiinv_fixed,
+                  double* model, int32_t* info) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0) return fail_arg(2, "n_psr < 0");
+  if (n_chain < 0) return fail_arg(3, "n_chain < 0");
+  if (NF <= 0 || NF > 64 || (NF & 1)) return fail_arg(4, "NF must be even and <= 64");
+  if (NMX <= 0 || NMX > 64) return fail_arg(5, "NMX must be in 1..64");
+  if (!desc) return fail_arg(6, "desc is NULL");
+  if (tnt_cstride < 0) return fail_arg(7, "tnt_cstride < 0");
+  if (d_cstride < 0) return fail_arg(8, "d_cstride < 0");
+  if (!TNT || !d || !fidx || !midx || !phiinv_fixed || !model) return fail_arg(9, "NULL array");
+  if (n_psr == 0 || n_chain == 0) return 0;
+  const size_t lds = ((size_t)NMX * NMX * 2 + (size_t)NMX * (NF + 1)) * sizeof(double);
+  int rc = check_hip(hipFuncSetAttribute((const void*)k_prefix, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds), "hipFuncSetAttribute(k_prefix)");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_prefix, dim3(n_psr * n_chain), dim3(256), lds, ctx->stream, desc, NF, NMX, TNT, d,
+                     fidx, midx, phiinv_fixed, model, model_stride_doubles(NF, NMX), info, n_chain,
+                     tnt_cstride, d_cstride);
+  return after_launch("k_prefix");
+}
+
 int gs_prefix(gs_ctx* ctx, int n_psr, int NF, int NMX, const gs_prefix_desc* desc,
               const double* TNT, const double* d, const int32_t* fidx, const int32_t* midx,
               const double* phiinv_fixed, double* model, int32_t* info) {
@@ -321,20 +349,13 @@ int gs_prefix(gs_ctx* ctx, int n_psr, int NF, int NMX, const gs_prefix_desc* des
   if (NMX <= 0 || NMX > 64) return fail_arg(4, "NMX must be in 1..64");
   if (!desc || !TNT || !d || !fidx || !midx || !phiinv_fixed || !model)
     return fail_arg(5, "NULL array");
-  if (n_psr == 0) return 0;
-  const size_t lds = ((size_t)NMX * NMX * 2 + (size_t)NMX * (NF + 1)) * sizeof(double);
-  int rc = check_hip(hipFuncSetAttribute((const void*)k_prefix, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)lds), "hipFuncSetAttribute(k_prefix)");
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_prefix, dim3(n_psr), dim3(256), lds, ctx->stream, desc, NF, NMX, TNT, d, fidx,
-                     midx, phiinv_fixed, model, model_stride_doubles(NF, NMX), info);
-  return after_launch("k_prefix");
+  return gs_prefix_sys(ctx, n_psr, 1, NF, NMX, desc, 0, 0, TNT, d, fidx, midx, phiinv_fixed, model, info);
 }
 
-int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, const double* model,
-             const int32_t* fidx, const int32_t* midx, const int32_t* nm, const double* phiinv_F,
-             const double* z, int64_t sweep, int event, int64_t chain_base, const int32_t* chain_mask,
-             double* b, int32_t* info) {
+static int bdraw_impl(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, const double* model,
+                      const int32_t* fidx, const int32_t* midx, const int32_t* nm, const double* phiinv_F,
+                      const double* z, int64_t sweep, int event, int64_t chain_base,
+                      const int32_t* chain_mask, double* b, int32_t* info, int per_sys) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
   if (!nf_supported(NF)) return fail_arg(4, "NF must be one of 20, 40, 60");
@@ -348,8 +369,45 @@ int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, cons
   a.model = model; a.fidx = fidx; a.midx = midx; a.nm = nm; a.chain_mask = chain_mask;
   a.phiinv_F = phiinv_F; a.z = z;
   a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = ctx->bcast; a.psr_base = ctx->psr_base;
+  a.model_per_sys = per_sys;
   if (launch_bdraw(ctx->stream, a)) return fail_arg(4, "unsupported NF");
   return after_launch("k_bdraw");
+}
+
+int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, const double* model,
+             const int32_t* fidx, const int32_t* midx, const int32_t* nm, const double* phiinv_F,
+             const double* z, int64_t sweep, int event, int64_t chain_base, const int32_t* chain_mask,
+             double* b, int32_t* info) {
+  return bdraw_impl(ctx, n_psr, n_chain, NF, NMX, ldb, model, fidx, midx, nm, phiinv_F, z, sweep, event,
+                    chain_base, chain_mask, b, info, 0);
+}
+
+int gs_bdraw_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, const double* model,
+                 const int32_t* fidx, const int32_t* midx, const int32_t* nm, const double* phiinv_F,
+                 const double* z, int64_t sweep, int event, int64_t chain_base, const int32_t* chain_mask,
+                 double* b, int32_t* info) {
+  return bdraw_impl(ctx, n_psr, n_chain, NF, NMX, ldb, model, fidx, midx, nm, phiinv_F, z, sweep, event,
+                    chain_base, chain_mask, b, info, 1);
+}
+
+// ------------------------------------------------------------------ white noise (a10)
+int gs_white_resid(gs_ctx* ctx, int n_psr, int n_chain, int64_t n_toa_max, int ldb,
+                   const gs_tnt_desc* tdesc, const double* Tt, const double* r, const double* b,
+                   int64_t ldy, double* y) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
+  if (n_toa_max < 0) return fail_arg(4, "n_toa_max < 0");
+  if (ldb <= 0) return fail_arg(5, "ldb <= 0");
+  if (!tdesc) return fail_arg(6, "tdesc is NULL");
+  if (!Tt || !r || !b || !y) return fail_arg(7, "NULL array");
+  if (ldy <= 0) return fail_arg(10, "ldy <= 0");
+  if (n_psr == 0 || n_chain == 0 || n_toa_max == 0) return 0;
+  const int64_t nmax = n_toa_max;
+  WhiteResidArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.ldb = ldb; a.ldy = ldy; a.n_toa_max = nmax;
+  a.tdesc = tdesc; a.Tt = Tt; a.r = r; a.b = b; a.y = y;
+  launch_white_resid(ctx->stream, a);
+  return after_launch("k_white_resid");
 }
 
 int gs_rho_analytic(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const int32_t* fidx,
@@ -500,4 +558,53 @@ int gs_philox(gs_ctx* ctx, int64_t n, const uint32_t* ctr, uint32_t* out) {
   return after_launch("k_philox");
 }
 
+
+int gs_white_mh(gs_ctx* ctx, int n_psr, int n_chain, const gs_white_desc* wdesc, const int32_t* wcol,
+                const int32_t* wkind, const int32_t* wbk, const double* wmin, const double* wmax,
+                const double* sigma2, const double* y, int64_t ldy, double* x, int ldx, int n_steps,
+                const int32_t* nsteps_chain, int64_t sweep, int64_t chain_base, const double* inj,
+                double* q_rec, int32_t* n_acc) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
+  if (!wdesc) return fail_arg(4, "wdesc is NULL");
+  if (!wcol || !wkind || !wbk || !wmin || !wmax) return fail_arg(5, "NULL parameter table");
+  if (!sigma2 || !y) return fail_arg(10, "NULL sigma2 / y");
+  if (ldy <= 0) return fail_arg(12, "ldy <= 0");
+  if (!x || ldx <= 0) return fail_arg(13, "x / ldx");
+  if (n_steps < 0) return fail_arg(15, "n_steps < 0");
+  if (n_psr == 0 || n_chain == 0) return 0;
+  WhiteMhArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.ldx = ldx; a.n_steps = n_steps; a.psr_base = ctx->psr_base;
+  a.ldy = ldy; a.sweep = sweep; a.chain_base = chain_base;
+  a.wdesc = wdesc; a.wcol = wcol; a.wkind = wkind; a.wbk = wbk; a.nsteps_chain = nsteps_chain;
+  a.wmin = wmin; a.wmax = wmax; a.sigma2 = sigma2; a.y = y; a.inj = inj;
+  a.x = x; a.q_rec = q_rec; a.n_acc = n_acc; a.key = key_of(ctx);
+  launch_white_mh(ctx->stream, a);
+  return after_launch("k_white_mh");
+}
+
+int gs_white_tnt(gs_ctx* ctx, int n_psr, int n_chain, int m_max, const gs_tnt_desc* tdesc,
+                 const gs_white_desc* wdesc, const int32_t* wcol, const int32_t* wkind,
+                 const int32_t* wbk, const double* T, const double* sigma2, const int32_t* bk,
+                 const double* r, const double* x, int ldx, int64_t tnt_cstride, int64_t d_cstride,
+                 double* TNT, double* d) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
+  if (m_max <= 0 || m_max > 4096) return fail_arg(4, "m_max out of range");
+  if (!tdesc) return fail_arg(5, "tdesc is NULL");
+  if (!wdesc) return fail_arg(6, "wdesc is NULL");
+  if (!wcol || !wkind || !wbk) return fail_arg(7, "NULL parameter table");
+  if (!T || !sigma2 || !bk || !r) return fail_arg(10, "NULL T / sigma2 / bk / r");
+  if (!x || ldx <= 0) return fail_arg(14, "x / ldx");
+  if (tnt_cstride < 0 || d_cstride < 0) return fail_arg(16, "negative chain stride");
+  if (!TNT || !d) return fail_arg(18, "NULL TNT / d");
+  if (n_psr == 0 || n_chain == 0) return 0;
+  WhiteTntArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.m_max = m_max; a.ldx = ldx;
+  a.tnt_cstride = tnt_cstride; a.d_cstride = d_cstride; a.tdesc = tdesc; a.wdesc = wdesc;
+  a.wcol = wcol; a.wkind = wkind; a.wbk = wbk; a.bk = bk; a.T = T; a.sigma2 = sigma2; a.r = r; a.x = x;
+  a.TNT = TNT; a.d = d;
+  launch_white_tnt(ctx->stream, a);
+  return after_launch("k_white_tnt");
+}
 }  // extern "C"

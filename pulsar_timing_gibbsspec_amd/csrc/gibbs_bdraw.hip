@@ -177,11 +177,14 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_bdraw(BdrawArgs A) 
   const int nb = (A.n_chain + WPB - 1) / WPB;
   const int p = blockIdx.x / nb;
   const int c = (blockIdx.x % nb) * WPB + wave;
-  stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+  // shared pulsar model: staged once per workgroup; per-system models (white-noise
+  // runs, TNT differs per chain) are read from global memory (L2) directly
+  if (!A.model_per_sys) stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
   if (c >= A.n_chain) return;
   if (A.chain_mask && A.chain_mask[c] == 0) return;  // gate closed: keep b
-  const ModelLds M = model_view(lds, NF, A.NMX);
   const int64_t sys = (int64_t)p * A.n_chain + c;
+  const ModelLds M = A.model_per_sys ? model_view(A.model + sys * A.mstride, NF, A.NMX)
+                                     : model_view(lds, NF, A.NMX);
   const int nM = A.nm[p];
   const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
   const int mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_bdraw(BdrawArgs A) 
     gs_normal2(gs_counter(lane, A.sweep, A.chain_base + c, p + A.psr_base, A.event), A.key, zF, zM);
   }
   double bF = 0.0, bM = 0.0;
-  double* scr = lds + A.mstride + wave * 64;
+  double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * 64;
   const int fail = bdraw_wave<NF, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
   if (lane < NF) A.b[sys * A.ldb + fi] = bF;
   if (lane < nM) A.b[sys * A.ldb + mi] = bM;
@@ -350,7 +353,7 @@ int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
 int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
-  const size_t lds = ((size_t)a.mstride + 64 * GS_SWEEP_WPB) * sizeof(double);
+  const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) + 64 * GS_SWEEP_WPB) * sizeof(double);
   return dispatch_nf_bdraw<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
 

@@ -19,6 +19,7 @@ inline int64_t model_stride_doubles(int NF, int NMX) {
 
 struct BdrawArgs {
   int n_psr, n_chain, NF, NMX, ldb, event, bcast, psr_base;
+  int model_per_sys;  // 1: model block per (pulsar, chain) system, read from global
   int64_t mstride, sweep, chain_base;
   const double* model;
   const int32_t *fidx, *midx, *nm, *chain_mask;
@@ -87,3 +88,36 @@ int launch_phi_from_x(hipStream_t s, int n_chain, int ncol, const double* x, int
                       double* out);
 int launch_pta_record(hipStream_t s, int n_chain, int n_param, const double* x, double* x_rec, double* xlast);
 int launch_pta_gate_phiinv(hipStream_t s, const PtaGateArgs& a);
+
+struct WhiteMhArgs {
+  int n_psr, n_chain, ldx, n_steps, psr_base;
+  int64_t ldy, sweep, chain_base;
+  const gs_white_desc* wdesc;
+  const int32_t *wcol, *wkind, *wbk, *nsteps_chain;
+  const double *wmin, *wmax, *sigma2, *y, *inj;
+  double *x, *q_rec;
+  int32_t* n_acc;
+  gs_key key;
+};
+
+struct WhiteResidArgs {
+  int n_psr, n_chain, ldb;
+  int64_t ldy, n_toa_max;
+  const gs_tnt_desc* tdesc;
+  const double *Tt, *r, *b;
+  double* y;
+};
+
+struct WhiteTntArgs {
+  int n_psr, n_chain, m_max, ldx;
+  int64_t tnt_cstride, d_cstride;
+  const gs_tnt_desc* tdesc;
+  const gs_white_desc* wdesc;
+  const int32_t *wcol, *wkind, *wbk, *bk;
+  const double *T, *sigma2, *r, *x;
+  double *TNT, *d;
+};
+
+int launch_white_mh(hipStream_t s, const WhiteMhArgs& a);
+int launch_white_resid(hipStream_t s, const WhiteResidArgs& a);
+int launch_white_tnt(hipStream_t s, const WhiteTntArgs& a);

@@ -1,0 +1,318 @@
+// (a10) White-noise Metropolis block and the per-chain TNT it forces (gfx950, fp64).
+//
+// Reference: PulsarBlockGibbs.update_white_params pulsar_gibbs.py:332-406 (steady
+// state :373-404), get_lnlikelihood_white :523-546, get_lnprior :613-617, and the
+// per-sweep TNT recompute :500-502 / :664-665.
+//
+// The white likelihood is a sum over TOAs; grouping a pulsar's TOAs by backend
+// makes it a sum of per-backend terms S_k, and a single-parameter proposal only
+// changes one backend's term.  Each MH step therefore re-sums only that backend's
+// TOAs (n_toa / n_bk of the reference's full recompute, which also redoes T b every
+// step although b is fixed) and the acceptance uses dlnL = -(S_k' - S_k) / 2.
+#include "gibbs_common.h"
+#include "gibbs_internal.h"
+
+namespace {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Effect of one white parameter value on its backend's (efac^2, t2equad^2, tnequad^2).
+__device__ __forceinline__ void apply_white(int kind, double v, double& ef2, double& t2, double& tn) {
+  if (kind == GS_WHITE_EFAC) {
+    ef2 = v * v;
+  } else if (kind == GS_WHITE_TNEQUAD) {
+    tn = pow(10.0, 2.0 * v);
+  } else {
+    t2 = pow(10.0, 2.0 * v);
+  }
+}
+
+// sum over TOAs [lo, hi) of log N + y^2 / N, N = ef2 (sigma^2 + t2) + tn (whole wave).
+__device__ __forceinline__ double backend_sum(const double* __restrict__ s2, const double* __restrict__ y,
+                                              int lo, int hi, double ef2, double t2, double tn, int lane) {
+  double s = 0.0;
+  for (int i = lo + lane; i < hi; i += GS_WAVE) {
+    const double N = ef2 * (s2[i] + t2) + tn;
+    const double yy = y[i];
+    s += log(N) + yy * yy / N;
+  }
+  return wave_sum(s);
+}
+
+// scale = np.random.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]) (pulsar_gibbs.py:377-381):
+// numpy's choice draws u and takes searchsorted(cdf, u, side='right').
+__device__ __forceinline__ double scale_choice(double u) {
+  if (u < 0.1) return 0.1;
+  if (u < 0.25) return 0.5;
+  if (u < 0.75) return 1.0;
+  if (u < 0.9) return 3.0;
+  return 10.0;
+}
+
+constexpr int MH_WPB = 4;
+
+// grid (ceil(n_chain / MH_WPB), n_psr); one wavefront per (pulsar, chain) system.
+__global__ __launch_bounds__(64 * MH_WPB) void k_white_mh(WhiteMhArgs A) {
+  __shared__ double sb[MH_WPB][4][GS_WHITE_MAX_BK + 1];  // ef2, t2, tn, S per backend
+  __shared__ double sx[MH_WPB][GS_WHITE_MAX_W];         // current white parameter values
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int p = blockIdx.y;
+  const int c = blockIdx.x * MH_WPB + wave;
+  if (c >= A.n_chain) return;  // no workgroup barriers below
+  const gs_white_desc* D = A.wdesc + p;  // bk_off is indexed at run time: keep it in memory
+  const int64_t n_sys = (int64_t)A.n_psr * A.n_chain;
+  const int64_t sys = (int64_t)p * A.n_chain + c;
+  const long long gchain = A.chain_base + c;
+  const int nbk = D->n_bk, nw = D->n_w;
+  double* ef2 = sb[wave][0];
+  double* t2 = sb[wave][1];
+  double* tn = sb[wave][2];
+  double* S = sb[wave][3];
+  double* xs = sx[wave];
+  const int64_t woff = D->w_off;
+  const double* s2 = A.sigma2 + D->toa_off;
+  const double* y = A.y + c * A.ldy + D->toa_off;
+  double* x = A.x + (int64_t)c * A.ldx;
+  const int32_t* wcol = A.wcol + woff;
+  const int32_t* wkind = A.wkind + woff;
+  const int32_t* wbk = A.wbk + woff;
+  const int32_t* bko = D->bk_off;
+
+  if (lane < nbk) {
+    ef2[lane] = 1.0;
+    t2[lane] = 0.0;
+    tn[lane] = 0.0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < nw) {
+    const double v = x[wcol[lane]];
+    xs[lane] = v;
+    const int k = wbk[lane];
+    double e = 1.0, t = 0.0, q = 0.0;
+    apply_white(wkind[lane], v, e, t, q);
+    if (wkind[lane] == GS_WHITE_EFAC) ef2[k] = e;
+    else if (wkind[lane] == GS_WHITE_TNEQUAD) tn[k] = q;
+    else t2[k] = t;
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int k = 0; k < nbk; ++k) {
+    const double s = backend_sum(s2, y, bko[k], bko[k + 1], ef2[k], t2[k], tn[k], lane);
+    if (lane == 0) S[k] = s;
+  }
+  __builtin_amdgcn_wave_barrier();
+
+  const int steps = A.nsteps_chain ? A.nsteps_chain[c] : A.n_steps;
+  const double sig = 0.05 * nw;  // sigmas = 0.05 * len(wind)  (:376)
+  int nacc = 0;
+  for (int st = 0; st < steps; ++st) {
+    double sc, z, u;
+    int w;
+    if (A.inj) {
+      const double* q = A.inj + ((int64_t)st * n_sys + sys) * 4;
+      sc = q[0];
+      w = (int)q[1];
+      z = q[2];
+      u = q[3];
+    } else {
+      double u1, u2, v1, v2, u4;
+      const int ps = p + A.psr_base;
+      gs_uniform2(gs_counter(3u * st, A.sweep, gchain, ps, GS_EV_WHITE), A.key, u1, u2);
+      gs_uniform2(gs_counter(3u * st + 1, A.sweep, gchain, ps, GS_EV_WHITE), A.key, v1, v2);
+      gs_uniform2(gs_counter(3u * st + 2, A.sweep, gchain, ps, GS_EV_WHITE), A.key, u, u4);
+      sc = scale_choice(u1);
+      w = min((int)(u2 * nw), nw - 1);
+      z = sqrt(-2.0 * log(1.0 - v1)) * cospi(2.0 * v2);
+    }
+    // q[par] += randn * sigmas * scale  (:383)
+    const double xo = xs[w];
+    const double xq = xo + (z * sig) * sc;
+    if (A.q_rec && lane < nw)
+      A.q_rec[((int64_t)st * n_sys + sys) * GS_WHITE_MAX_W + lane] = (lane == w) ? xq : xs[lane];
+    // Uniform prior: -inf outside [pmin, pmax] -> diff = -inf, rejected (:613-617, :398)
+    if (xq >= A.wmin[woff + w] && xq <= A.wmax[woff + w]) {
+      const int k = wbk[w];
+      double e = ef2[k], t = t2[k], q = tn[k];
+      apply_white(wkind[w], xq, e, t, q);
+      const double sn = backend_sum(s2, y, bko[k], bko[k + 1], e, t, q, lane);
+      const double diff = (-0.5 * sn) - (-0.5 * S[k]);
+      if (diff > log(u)) {
+        ++nacc;
+        if (lane == 0) {
+          ef2[k] = e;
+          t2[k] = t;
+          tn[k] = q;
+          S[k] = sn;
+          xs[w] = xq;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (lane < nw) x[wcol[lane]] = xs[lane];
+  if (A.n_acc && lane == 0) A.n_acc[sys] = nacc;
+}
+
+// y = r - T b: grid (ceil(n_toa_max / 256), n_psr, ceil(n_chain / RES_CT)); one thread
+// per TOA, RES_CT chains per thread; T column-major so each load is coalesced and
+// b is wave-uniform (scalar loads).
+constexpr int RES_CT = 8;
+
+__global__ __launch_bounds__(256) void k_white_resid(WhiteResidArgs A) {
+  const gs_tnt_desc D = A.tdesc[blockIdx.y];
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= D.n_toa) return;
+  const int p = blockIdx.y;
+  const int c0 = blockIdx.z * RES_CT;
+  const int m = (int)D.m;
+  const int64_t n = D.n_toa;
+  const double* Tt = A.Tt + D.T_off;
+  const double* bb[RES_CT];
+#pragma unroll
+  for (int q = 0; q < RES_CT; ++q)
+    bb[q] = A.b + ((int64_t)p * A.n_chain + min(c0 + q, A.n_chain - 1)) * A.ldb;
+  double acc[RES_CT];
+#pragma unroll
+  for (int q = 0; q < RES_CT; ++q) acc[q] = 0.0;
+  for (int j = 0; j < m; ++j) {
+    const double t = Tt[(int64_t)j * n + i];
+#pragma unroll
+    for (int q = 0; q < RES_CT; ++q) acc[q] = fma(t, bb[q][j], acc[q]);
+  }
+  const double r = A.r[D.toa_off + i];
+#pragma unroll
+  for (int q = 0; q < RES_CT; ++q)
+    if (c0 + q < A.n_chain) A.y[(int64_t)(c0 + q) * A.ldy + D.toa_off + i] = r - acc[q];
+}
+
+// Per-backend noise values of system (p, c) into LDS (whole workgroup).
+__device__ __forceinline__ void stage_white(const WhiteTntArgs& A, const gs_white_desc& W, int c,
+                                            double* ef2, double* t2, double* tn) {
+  const int tid = threadIdx.x;
+  if (tid < W.n_bk) {
+    ef2[tid] = 1.0;
+    t2[tid] = 0.0;
+    tn[tid] = 0.0;
+  }
+  __syncthreads();
+  if (tid < W.n_w) {
+    const int64_t o = W.w_off + tid;
+    const int k = A.wbk[o], kind = A.wkind[o];
+    double e = 1.0, t = 0.0, q = 0.0;
+    apply_white(kind, A.x[(int64_t)c * A.ldx + A.wcol[o]], e, t, q);
+    if (kind == GS_WHITE_EFAC) ef2[k] = e;
+    else if (kind == GS_WHITE_TNEQUAD) tn[k] = q;
+    else t2[k] = t;
+  }
+  __syncthreads();
+}
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// TNT_c: grid (n_sys, nb (nb + 1) / 2) lower 16 x 16 tile pairs, mirrored on store;
+// 4 wavefronts split the TOAs, v_mfma_f64_16x16x4f64 (layout as k_tnt).
+__global__ __launch_bounds__(256) void k_white_tnt(WhiteTntArgs A) {
+  __shared__ double red[3][4][64];
+  __shared__ double sb[3][GS_WHITE_MAX_BK + 1];
+  const int64_t sys = blockIdx.x;
+  const int p = (int)(sys / A.n_chain), c = (int)(sys % A.n_chain);
+  const int q = blockIdx.y;
+  int bi = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+  while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
+  while (bi * (bi + 1) / 2 > q) --bi;
+  const int bj = q - bi * (bi + 1) / 2;
+  const gs_tnt_desc D = A.tdesc[p];
+  const gs_white_desc W = A.wdesc[p];
+  const int m = (int)D.m;
+  if (bi * 16 >= m) return;
+  stage_white(A, W, c, sb[0], sb[1], sb[2]);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int i = l & 15, k = l >> 4;
+  const int ci = bi * 16 + i, cj = bj * 16 + i;
+  const double* Tp = A.T + D.T_off;
+  const double* s2 = A.sigma2 + D.toa_off;
+  const int32_t* bk = A.bk + D.toa_off;
+  const int64_t n = D.n_toa;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t t0 = (int64_t)w * 4; t0 < n; t0 += 16) {
+    const int64_t t = t0 + k;
+    const bool ok = t < n;
+    double invN = 0.0;
+    if (ok) {
+      const int kb = bk[t];
+      invN = 1.0 / (sb[0][kb] * (s2[t] + sb[1][kb]) + sb[2][kb]);
+    }
+    const double a = (ok && ci < m) ? Tp[t * m + ci] * invN : 0.0;
+    const double b = (ok && cj < m) ? Tp[t * m + cj] : 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  if (w > 0)
+    for (int r = 0; r < 4; ++r) red[w - 1][r][l] = acc[r];
+  __syncthreads();
+  if (w == 0) {
+    double* out = A.TNT + D.tnt_off + (int64_t)c * A.tnt_cstride;
+    for (int r = 0; r < 4; ++r) {
+      const double v = acc[r] + red[0][r][l] + red[1][r][l] + red[2][r][l];
+      const int row = bi * 16 + (l >> 4) + 4 * r, col = bj * 16 + (l & 15);
+      if (row < m && col < m) {
+        out[(int64_t)row * m + col] = v;
+        out[(int64_t)col * m + row] = v;
+      }
+    }
+  }
+}
+
+// d_c = T^T (r / N_c): grid (n_sys, ceil(m_max / 64)).
+__global__ __launch_bounds__(256) void k_white_tnr(WhiteTntArgs A) {
+  __shared__ double red[4][64];
+  __shared__ double sb[3][GS_WHITE_MAX_BK + 1];
+  const int64_t sys = blockIdx.x;
+  const int p = (int)(sys / A.n_chain), c = (int)(sys % A.n_chain);
+  const gs_tnt_desc D = A.tdesc[p];
+  const gs_white_desc W = A.wdesc[p];
+  stage_white(A, W, c, sb[0], sb[1], sb[2]);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int m = (int)D.m;
+  const int j = blockIdx.y * 64 + l;
+  double s = 0.0;
+  if (j < m) {
+    const double* Tp = A.T + D.T_off;
+    const double* s2 = A.sigma2 + D.toa_off;
+    const int32_t* bk = A.bk + D.toa_off;
+    const double* r = A.r + D.toa_off;
+    for (int64_t t = w; t < D.n_toa; t += 4) {
+      const int kb = bk[t];
+      const double N = sb[0][kb] * (s2[t] + sb[1][kb]) + sb[2][kb];
+      s = fma(Tp[t * m + j], r[t] / N, s);
+    }
+  }
+  red[w][l] = s;
+  __syncthreads();
+  if (w == 0 && j < m) A.d[D.d_off + (int64_t)c * A.d_cstride + j] = red[0][l] + red[1][l] + red[2][l] + red[3][l];
+}
+
+}  // namespace
+
+int launch_white_mh(hipStream_t s, const WhiteMhArgs& a) {
+  dim3 grid((unsigned)((a.n_chain + MH_WPB - 1) / MH_WPB), (unsigned)a.n_psr);
+  hipLaunchKernelGGL(k_white_mh, grid, dim3(64 * MH_WPB), 0, s, a);
+  return 0;
+}
+
+int launch_white_resid(hipStream_t s, const WhiteResidArgs& a) {
+  dim3 grid((unsigned)((a.n_toa_max + 255) / 256), (unsigned)a.n_psr,
+            (unsigned)((a.n_chain + RES_CT - 1) / RES_CT));
+  hipLaunchKernelGGL(k_white_resid, grid, dim3(256), 0, s, a);
+  return 0;
+}
+
+int launch_white_tnt(hipStream_t s, const WhiteTntArgs& a) {
+  const int nb = (a.m_max + 15) / 16;
+  const int64_t n_sys = (int64_t)a.n_psr * a.n_chain;
+  hipLaunchKernelGGL(k_white_tnt, dim3((unsigned)n_sys, (unsigned)(nb * (nb + 1) / 2)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_white_tnr, dim3((unsigned)n_sys, (unsigned)((a.m_max + 63) / 64)), dim3(256), 0, s, a);
+  return 0;
+}

@@ -10,10 +10,15 @@ the same chain files.  The arithmetic runs on the GPU through the C-ABI:
 * ``update_gwrho_params`` -> gs_rho_analytic (:206-216) — analytic branch
 * ``sample``             -> gs_sweep_freespec, the whole loop body (:656-698) on device
 
+* ``update_white_params`` -> gs_white_resid + gs_white_mh (:332-406), and with
+  white noise sampled ``sample`` runs the per-sweep sequence of
+  white.WhiteFreeSpectrumChains (per-chain TNT via gs_white_tnt, gs_prefix_sys,
+  gs_bdraw_sys)
+
 Extensions (keyword-only, reference-equivalent defaults): ``nchains``
 (independent chains, chain 0 is written in the reference layout), ``device``,
-``seed`` (Philox key).  Models with Metropolis blocks (white noise, power-law
-red noise, ECORR) are outside the device hot path and raise
+``seed`` (Philox key).  Models with other Metropolis blocks (power-law red
+noise via PTMCMC, ECORR) are outside the device hot path and raise
 ``NotImplementedError`` from ``sample``.
 """
 from __future__ import annotations
@@ -24,7 +29,9 @@ import numpy as np
 import torch
 
 from . import _lib
+from .diagnostics import white_aclength
 from .engine import DeviceModel, FreeSpectrumChains
+from .white import MAX_W, WhiteFreeSpectrumChains, WhiteNoiseModel, white_kind
 
 
 def _parse_uniform_bounds(param):
@@ -173,6 +180,99 @@ class PulsarBlockGibbs(object):
                                       "only fixed-prior columns are supported outside gwid")
         return phiinv[self.gwid]
 
+    # ------------------------------------------------------------ white noise
+    def _white_structure(self, xs):
+        """Per-TOA sigma^2, backend groups and the white parameter table, discovered
+        through the PTA contract alone (get_ndiag): sigma^2 = N at efac = 1 and
+        negligible equads; the TOAs a parameter acts on = where N moves when it moves.
+        Verified against get_ndiag at xs before use."""
+        wind = self.get_efacequad_indices()
+        names = self.param_names
+        x0 = np.asarray(xs, float).copy()
+        base = x0.copy()
+        kinds = [white_kind(names[j]) for j in wind]
+        for j, k in zip(wind, kinds):
+            base[j] = 1.0 if k == 0 else -40.0
+        N0 = self.pta.get_ndiag(self.map_params(base))[0]
+        masks = []
+        for j, k in zip(wind, kinds):
+            xp = base.copy()
+            xp[j] = 2.0 if k == 0 else -5.0
+            masks.append(self.pta.get_ndiag(self.map_params(xp))[0] != N0)
+        groups = []
+        bk = np.full(N0.size, -1, np.int64)
+        wl = []
+        bounds = {}
+        for p in self.params:
+            lo, hi = _parse_uniform_bounds(p)
+            for n in ([p.name] if not p.size else [f"{p.name}_{i}" for i in range(p.size)]):
+                bounds[n] = (lo, hi)
+        for j, k, mk in zip(wind, kinds, masks):
+            key = mk.tobytes()
+            if key not in groups:
+                if (bk[mk] != -1).any():
+                    raise NotImplementedError("white-noise selections overlap")
+                groups.append(key)
+                bk[mk] = len(groups) - 1
+            wl.append((int(j), k, groups.index(key), *bounds[names[j]]))
+        if (bk == -1).any():
+            bk[bk == -1] = len(groups)
+        if len(wl) > MAX_W:
+            raise NotImplementedError(f"more than {MAX_W} white parameters")
+        # verify the device formula N = efac^2 (sigma^2 + t2equad^2) + tnequad^2 at xs
+        nb = int(bk.max()) + 1
+        ef, t2, tn = np.ones(nb), np.zeros(nb), np.zeros(nb)
+        for (j, k, g, _, _) in wl:
+            if k == 0:
+                ef[g] = x0[j] ** 2
+            elif k == 1:
+                tn[g] = 10.0 ** (2.0 * x0[j])
+            else:
+                t2[g] = 10.0 ** (2.0 * x0[j])
+        N = ef[bk] * (N0 + t2[bk]) + tn[bk]
+        Nref = self.pta.get_ndiag(self.map_params(x0))[0]
+        if np.max(np.abs(N - Nref) / Nref) > 1e-12:
+            raise NotImplementedError("white-noise model is not efac/equad per backend")
+        return N0, bk, wl
+
+    def _white_model(self, xs, n_chain):
+        params = self.map_params(xs)
+        sigma2, bk, wl = self._white_structure(xs)
+        T = self.pta.get_basis(params)[0]
+        phiinv = self.pta.get_phiinv(params, logdet=False)[0]
+        mask = np.ones(T.shape[1], bool)
+        mask[self.gwid] = False
+        self._phfix = phiinv[mask].copy()
+        return WhiteNoiseModel(self.ctx, [T], [self._residuals], [np.sqrt(sigma2)], [bk], [self.gwid],
+                               [phiinv[mask]], [wl], n_chain)
+
+    def update_white_params(self, xs, iters=None, inj=None):
+        """White-noise Metropolis block (pulsar_gibbs.py:332-406) on the GPU: with
+        ``iters`` the warm-up (sets aclength_white from acor of the proposal chain,
+        cov_white, sigma_white, svd_white), else ``aclength_white`` steady-state steps.
+        ``inj`` (steps, 4): injected (scale, parameter index within wind, normal, uniform)."""
+        dev = self.ctx.device
+        if getattr(self, "_wm1", None) is None:
+            self._wm1 = self._white_model(xs, 1)
+        wm = self._wm1
+        wind = self.get_efacequad_indices()
+        x = torch.as_tensor(np.asarray(xs, float)[None, :], device=dev).contiguous()
+        b = torch.zeros(1, wm.ldb, dtype=torch.float64, device=dev)
+        b[0, :self._b.size] = torch.as_tensor(self._b, device=dev)
+        wm.resid(b)
+        n = int(iters) if iters is not None else int(self.aclength_white)
+        q_rec = torch.empty(n, 1, MAX_W, dtype=torch.float64, device=dev) if iters is not None else None
+        it = None if inj is None else torch.as_tensor(np.asarray(inj, float).reshape(n, 1, 4), device=dev)
+        wm.mh(x, x.shape[1], n, self._ndraw, inj=it, q_rec=q_rec)
+        self._ndraw += 1
+        if iters is not None:
+            short_chain = q_rec[:, 0, :wind.size].cpu().numpy()
+            self.cov_white = np.cov(short_chain[100:, :], rowvar=False)
+            self.sigma_white = np.diag(np.atleast_2d(self.cov_white)) ** 0.5
+            self.svd_white = np.linalg.svd(np.atleast_2d(self.cov_white))
+            self.aclength_white = white_aclength(short_chain)
+        return x[0].cpu().numpy()
+
     # ------------------------------------------------------------ conditionals
     def update_b(self, xs, z=None):
         """b | rho, data (pulsar_gibbs.py:489-520) on the GPU.
@@ -216,14 +316,19 @@ class PulsarBlockGibbs(object):
         return xnew
 
     # ------------------------------------------------------------ loop
+    def _white_loop(self):
+        names = self.param_names
+        extra = [n for n in names if "rho" not in n]
+        return bool(extra) and all(("efac" in n or "equad" in n) for n in extra)
+
     def _check_device_loop(self, xs):
-        extra = [n for n in self.param_names if "rho" not in n]
+        extra = [n for n in self.param_names if "rho" not in n and not self._white_loop()]
         if extra or self.red_sig is not None or self.hypersample != "conditional":
             raise NotImplementedError(
                 "the device sweep covers free-spectrum-only models (analytic rho|b); "
                 f"found Metropolis-sampled parameters {extra[:4]}...")
         gwind = self.get_gwrho_param_indices()
-        if not np.array_equal(gwind, np.arange(len(self.gwid) // 2)):
+        if not self._white_loop() and not np.array_equal(gwind, np.arange(len(self.gwid) // 2)):
             raise NotImplementedError("gw rho parameters must be the whole parameter vector")
 
     def sample(self, xs, outdir="./", niter=10000, resume=False, save_every=100):
@@ -239,6 +344,8 @@ class PulsarBlockGibbs(object):
         np.savetxt(f"{outdir}/pars_chain.txt", self.param_names, fmt="%s")
         np.savetxt(f"{outdir}/pars_bchain.txt", self.b_param_names, fmt="%s")
 
+        if self._white_loop():
+            return self._sample_white(xs, outdir, niter, resume, save_every)
         model = self._model(xs)
         nc = self.nchains
         self.chain = np.zeros((niter, len(xs)))
@@ -286,6 +393,76 @@ class PulsarBlockGibbs(object):
                 if nc > 1:
                     np.save(f"{outdir}/chains.npy", self.chains[:, :last + 1])
                     np.save(f"{outdir}/bchains.npy", self.bchains[:, :last + 1])
+        info = runner.info.cpu().numpy()
+        if info.any():
+            print(f"WARNING: {int((info != 0).sum())} chains hit a non-positive-definite Sigma")
+        self._b = runner.b[0, :m].cpu().numpy()
+        self._runner = runner
+        return self.chain
+
+    def _sample_white(self, xs, outdir, niter, resume, save_every):
+        """sample() with the white-noise MH block (pulsar_gibbs.py:656-698): one device
+        launch sequence per sweep for all chains (white.WhiteFreeSpectrumChains)."""
+        nc = self.nchains
+        dev = self.ctx.device
+        wm = self._white_model(xs, nc)
+        m = int(wm.m[0])
+        n_param = len(xs)
+        self.chain = np.zeros((niter, n_param))
+        self.bchain = np.zeros((niter, len(self._b)))
+        self.chains = np.zeros((nc, niter, n_param)) if nc > 1 else None
+        self.bchains = np.zeros((nc, niter, len(self._b))) if nc > 1 else None
+        start = 0
+        x0 = np.asarray(xs, float)
+        acl = getattr(self, "aclength_white", None)
+        if resume and os.path.exists(f"{outdir}/chain.npy"):
+            print("Resuming from previous run...")
+            c0 = np.load(f"{outdir}/chain.npy")
+            b0 = np.load(f"{outdir}/bchain.npy")
+            start = min(c0.shape[0], b0.shape[0])
+            self.chain[:start] = c0[:start]
+            self.bchain[:start] = b0[:start]
+        runner = WhiteFreeSpectrumChains(wm, n_param, self.get_gwrho_param_indices(), self.rhomin,
+                                         self.rhomax, x0, aclength=acl)
+        if start > 0:
+            runner.x.copy_(torch.as_tensor(self.chain[start - 1][None, :], device=dev).expand(nc, -1))
+            runner.b[:, :m] = torch.as_tensor(self.bchain[start - 1], device=dev)
+            runner.it = start
+            if runner.aclength is None:
+                raise NotImplementedError("resume of a white-noise run needs aclength_white")
+        blk = max(1, save_every)
+        xr = torch.empty(blk + 1, nc, n_param, dtype=torch.float64, device=dev)
+        br = torch.empty(blk + 1, nc, wm.ldb, dtype=torch.float64, device=dev)
+        ii = start
+        while ii < niter:
+            nxt = min(niter, (ii // blk + 1) * blk + 1)
+            n = nxt - ii
+            for k in range(n):
+                runner.sweep(x_rec=xr[k], b_rec=br[k])
+            xh = xr[:n].cpu().numpy()
+            bh = br[:n, :, :m].cpu().numpy()
+            self.chain[ii:nxt] = xh[:, 0]
+            self.bchain[ii:nxt] = bh[:, 0]
+            if nc > 1:
+                self.chains[:, ii:nxt] = np.moveaxis(xh, 1, 0)
+                self.bchains[:, ii:nxt] = np.moveaxis(bh, 1, 0)
+            ii = nxt
+            self.iter = ii - 1
+            last = ii - 1
+            if last % save_every == 0 and last > 0:
+                np.save(f"{outdir}/chain.npy", self.chain[:last + 1, :])
+                np.save(f"{outdir}/bchain.npy", self.bchain[:last + 1, :])
+                if nc > 1:
+                    np.save(f"{outdir}/chains.npy", self.chains[:, :last + 1])
+                    np.save(f"{outdir}/bchains.npy", self.bchains[:, :last + 1])
+        if runner.short_chain is not None:
+            sc = runner.short_chain
+            self.cov_white = np.cov(sc[100:, :], rowvar=False)
+            self.sigma_white = np.diag(np.atleast_2d(self.cov_white)) ** 0.5
+            self.svd_white = np.linalg.svd(np.atleast_2d(self.cov_white))
+        acl = np.atleast_1d(runner.aclength)
+        self.aclength_white = int(acl[0])
+        self.aclength_white_chains = acl
         info = runner.info.cpu().numpy()
         if info.any():
             print(f"WARNING: {int((info != 0).sum())} chains hit a non-positive-definite Sigma")

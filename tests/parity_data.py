@@ -166,3 +166,81 @@ def pta_last_draw(g, kind, rec):
     x = rec[last[-1]]["x_curn"] if last else g["x0"]
     off = np.concatenate([[0], np.cumsum(m)])
     return x, [zlast[off[p]:off[p + 1]] for p in range(P)]
+
+
+def white_params(g):
+    """[(x column, kind, backend, pmin, pmax)] of the white-noise fixture's wind, in wind order."""
+    import re
+    from pulsar_timing_gibbsspec_amd.white import white_kind
+    names = list(g["param_names"])
+    out = []
+    for j in g["wind"]:
+        n = names[int(j)]
+        k = int(re.search(r"_b(\d+)_", n).group(1))
+        out.append((int(j), white_kind(n), k, float(g["pmin"][j]), float(g["pmax"][j])))
+    return out
+
+
+def white_replay(g):
+    """Re-drive the white-noise fixture's loop (pulsar_gibbs.py:656-698) with the oracle and
+    return the injection arrays of every draw for the device path: rotated normals of each
+    b draw (device column order, Sigma at that draw), MH steps (scale, local parameter
+    index, normal, uniform) per sweep, rho uniforms, and the expected trajectory."""
+    from pulsar_timing_gibbsspec_amd import synthetic
+    names = list(g["param_names"])
+    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0, efac_vary=True, n_backends=3)
+    ef_i = [names.index(f"J1713+0747_b{i}_efac") for i in range(3)]
+    eq_i = [names.index(f"J1713+0747_b{i}_log10_tnequad") for i in range(3)]
+    T, r = g["T"], g["r"]
+    m = T.shape[1]
+    gwid = np.asarray(g["gwid"])
+    order = O.chol_order(m, gwid)
+    wind = list(np.asarray(g["wind"]))
+    acl = int(g["aclength"])
+    gwind = np.array([i for i, n in enumerate(names) if "rho" in n])
+    kinds, vals, lens = g["kinds"], g["vals"], g["lens"]
+    off = np.concatenate([[0], np.cumsum(lens)])
+    items = iter([(kinds[i], vals[off[i]:off[i + 1]]) for i in range(kinds.size)])
+
+    def N_of(x):
+        return O.ndiag_white(g["sigma"], g["backends"], x[ef_i], x[eq_i])
+
+    def lnprior(x):
+        params = pta.map_params(x)
+        return np.sum([p.get_logpdf(params=params) for p in pta.params])
+
+    def draw_b(x):
+        k, z = next(items)
+        TNT, d = O.tnt(T, N_of(x), r)
+        ph = 1.0 / pta.get_phi(pta.map_params(x))[0]
+        return O.bdraw_svd(TNT, d, ph, z), O.rotate_normals(TNT, ph, z, order)
+
+    niter = g["chain"].shape[0]
+    x = g["x0"].copy()
+    b = np.zeros(m)
+    z0 = None
+    zs = np.zeros((niter, m))
+    mh = np.zeros((niter, acl, 4))
+    us = np.zeros((niter, gwid.size // 2))
+    gates = np.zeros(niter, bool)
+    for ii in range(niter):
+        if ii == 0:
+            b, z0 = draw_b(g["x0"])
+            b_first = b.copy()
+        steps = []
+        for s in range(acl):
+            (_, sc), (_, p), (_, z), (_, u) = next(items), next(items), next(items), next(items)
+            steps.append((sc[0], p[0], z[0], u[0]))
+            mh[ii, s] = (sc[0], wind.index(int(p[0])), z[0], u[0])
+        xw = O.white_mh(x, wind, steps, lambda q: O.lnlike_white(r, T, b, N_of(q)), lnprior)
+        _, U = next(items)
+        us[ii] = U
+        xn = xw.copy()
+        xn[gwind] = 0.5 * np.log10(O.rho_analytic(O.tau_half(b, gwid), U, float(g["rhomin"]),
+                                                  float(g["rhomax"])))
+        gates[ii] = bool(np.all(xn != x[-1]))
+        if gates[ii]:
+            b, zs[ii] = draw_b(xn)
+        x = xn
+    return dict(z0=z0, z=zs, mh=mh, u=us, gates=gates, gwind=gwind, x_final=x, b_final=b,
+                b_first=b_first)

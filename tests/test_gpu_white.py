@@ -1,0 +1,161 @@
+"""(a10) White-noise MH block + per-chain TNT on the GPU, through the C-ABI, against the
+reference's own run (tests/golden/white_mh_j1713.npz: PulsarBlockGibbs.update_white_params
+steady state inside the sample loop, pulsar_gibbs.py:656-698, with every draw captured).
+
+Injected draws: the reference's MH choices/normals/uniforms verbatim, rho uniforms, and
+its b-draw normals rotated into the Cholesky basis (tests/parity_data.py).  The MH
+accept/reject decisions must coincide (so the white parameters are bit-identical);
+rho and b are compared at 1e-9 relative (north_star tolerance; the device TNT sums
+the TOAs grouped by backend, so it differs from numpy's at the 1e-16 level)."""
+import numpy as np
+import pytest
+
+from tests.conftest import golden, gpu_available
+from tests.parity_data import normwise_rel, white_params, white_replay
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    from pulsar_timing_gibbsspec_amd import _lib
+    return _lib.Context(0, seed=5)
+
+
+def _model(ctx, g, n_chain):
+    from pulsar_timing_gibbsspec_amd.white import WhiteNoiseModel
+    T = g["T"]
+    gwid = np.asarray(g["gwid"])
+    m = T.shape[1]
+    n_fixed = m - gwid.size
+    return WhiteNoiseModel(ctx, [T], [g["r"]], [g["sigma"]], [g["backends"]], [gwid],
+                           [np.full(n_fixed, 1e-40)], [white_params(g)], n_chain)
+
+
+def test_white_tnt_and_resid(ctx):
+    """gs_white_tnt == T^T N(x)^-1 T per chain; gs_white_resid == r - T b."""
+    import torch
+    from tests.parity_data import O
+    g = golden("white_mh_j1713.npz")
+    C = 3
+    wm = _model(ctx, g, C)
+    n_param = g["x0"].size
+    rng = np.random.default_rng(1)
+    x = np.tile(g["x0"], (C, 1))
+    wind = np.asarray(g["wind"])
+    x[:, wind] = rng.uniform(g["pmin"][wind], g["pmax"][wind], (C, wind.size))
+    xd = torch.as_tensor(x, device=ctx.device)
+    wm.refresh(xd, n_param)
+    names = list(g["param_names"])
+    for c in range(C):
+        ef = x[c, [names.index(f"J1713+0747_b{i}_efac") for i in range(3)]]
+        eq = x[c, [names.index(f"J1713+0747_b{i}_log10_tnequad") for i in range(3)]]
+        N = O.ndiag_white(g["sigma"], g["backends"], ef, eq)
+        TNT, d = O.tnt(g["T"], N, g["r"])
+        TNTd, dd = wm.tnt_host(0, c)
+        assert np.max(np.abs(TNTd - TNT)) <= 1e-12 * np.max(np.abs(TNT))
+        assert normwise_rel(dd, d) < 1e-12
+    assert int(wm.pinfo.abs().sum()) == 0
+    b = rng.standard_normal((C, wm.ldb)) * 1e-7
+    wm.resid(torch.as_tensor(b, device=ctx.device))
+    y = wm.y.cpu().numpy()
+    perm = wm.perm[0]
+    for c in range(C):
+        ref = (g["r"] - g["T"] @ b[c, :g["T"].shape[1]])[perm]
+        assert np.max(np.abs(y[c] - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
+def test_white_loop_matches_reference(ctx):
+    import torch
+    from pulsar_timing_gibbsspec_amd.white import WhiteFreeSpectrumChains
+    g = golden("white_mh_j1713.npz")
+    rp = white_replay(g)
+    wm = _model(ctx, g, 1)
+    n_param = g["x0"].size
+    dev = ctx.device
+    ch = WhiteFreeSpectrumChains(wm, n_param, rp["gwind"], float(g["rhomin"]), float(g["rhomax"]), g["x0"],
+                                 aclength=int(g["aclength"]))
+    niter = g["chain"].shape[0]
+    m = g["T"].shape[1]
+    xrec = torch.empty(niter, 1, n_param, dtype=torch.float64, device=dev)
+    brec = torch.empty(niter, 1, wm.ldb, dtype=torch.float64, device=dev)
+
+    def dz(z):
+        out = np.zeros((1, wm.ldb))
+        out[0, :m] = z
+        return torch.as_tensor(out, device=dev)
+    for ii in range(niter):
+        ch.sweep(x_rec=xrec[ii], b_rec=brec[ii], z0=dz(rp["z0"]) if ii == 0 else None, z=dz(rp["z"][ii]),
+                 u=torch.as_tensor(rp["u"][ii][None], device=dev),
+                 mh_inj=torch.as_tensor(np.ascontiguousarray(rp["mh"][ii][:, None, :]), device=dev))
+    x = xrec[:, 0].cpu().numpy()
+    wind = np.asarray(g["wind"])
+    # white parameters: identical MH decisions -> identical values
+    assert np.array_equal(x[:, wind], g["chain"][:, wind])
+    assert np.array_equal(ch.x[0, wind].cpu().numpy(), rp["x_final"][wind])
+    gw = rp["gwind"]
+    assert np.max(np.abs(x[:, gw] - g["chain"][:, gw])) < 1e-9
+    assert normwise_rel(brec[1:, 0, :m].cpu().numpy(), g["bhist"][1:]) < 1e-9
+    assert normwise_rel(ch.b[0, :m].cpu().numpy(), g["b_final"]) < 1e-9
+    assert int(ch.info.abs().sum()) == 0
+
+
+def test_white_philox_chains_run(ctx):
+    """Device-RNG run with the warm-up: aclength from the proposal chain (acor
+    restatement), white parameters stay inside the prior, chains decorrelate."""
+    import torch
+    from pulsar_timing_gibbsspec_amd.white import WhiteFreeSpectrumChains
+    g = golden("white_mh_j1713.npz")
+    C = 64
+    wm = _model(ctx, g, C)
+    n_param = g["x0"].size
+    gw = np.array([i for i, n in enumerate(g["param_names"]) if "rho" in n])
+    ch = WhiteFreeSpectrumChains(wm, n_param, gw, float(g["rhomin"]), float(g["rhomax"]), g["x0"])
+    n = 30
+    xrec = torch.empty(n, C, n_param, dtype=torch.float64, device=ctx.device)
+    for ii in range(n):
+        ch.sweep(x_rec=xrec[ii])
+    x = xrec.cpu().numpy()
+    wind = np.asarray(g["wind"])
+    assert np.all(x[:, :, wind] >= g["pmin"][wind]) and np.all(x[:, :, wind] <= g["pmax"][wind])
+    acl = np.atleast_1d(ch.aclength)
+    assert acl.size == C and acl.min() >= 1
+    assert np.all(np.isfinite(x))
+    assert int(ch.info.abs().sum()) == 0
+    # chains moved and differ from each other
+    assert np.std(x[-1, :, wind[0]]) > 0
+
+
+def test_pulsar_block_gibbs_white_surface(ctx, tmp_path):
+    """PulsarBlockGibbs on a white-noise model: update_white_params replays the
+    reference's first MH block exactly; sample() runs warm-up + steady state."""
+    from oracle import gibbs_oracle as O
+    from pulsar_timing_gibbsspec_amd import PulsarBlockGibbs, synthetic
+    from tests.parity_data import white_replay
+    g = golden("white_mh_j1713.npz")
+    rp = white_replay(g)
+    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0, efac_vary=True, n_backends=3)
+    gb = PulsarBlockGibbs(pta, seed=3)
+    assert list(gb.param_names) == list(g["param_names"])
+    wind = list(np.asarray(g["wind"]))
+    # b after the first draw of the reference run; first MH block from chain[0]
+    gb._b = rp["b_first"].copy()
+    gb.aclength_white = int(g["aclength"])
+    xw = gb.update_white_params(g["x0"].copy(), inj=rp["mh"][0])
+    names = list(g["param_names"])
+    ef_i = [names.index(f"J1713+0747_b{i}_efac") for i in range(3)]
+    eq_i = [names.index(f"J1713+0747_b{i}_log10_tnequad") for i in range(3)]
+    steps = [(s[0], wind[int(s[1])], s[2], s[3]) for s in rp["mh"][0]]
+    xo = O.white_mh(g["x0"], wind, steps,
+                    lambda q: O.lnlike_white(g["r"], g["T"], rp["b_first"],
+                                             O.ndiag_white(g["sigma"], g["backends"], q[ef_i], q[eq_i])),
+                    lambda q: np.sum([p.get_logpdf(params=pta.map_params(q)) for p in pta.params]))
+    assert np.array_equal(xw, xo)
+    assert np.array_equal(xw[wind], g["white_out"][0][wind])
+    gb2 = PulsarBlockGibbs(pta, seed=4, nchains=4)
+    ch = gb2.sample(g["x0"].copy(), outdir=str(tmp_path), niter=12)
+    assert ch.shape == (12, len(names))
+    assert gb2.aclength_white >= 1 and gb2.chains.shape == (4, 12, len(names))
+    assert np.all(np.isfinite(gb2.bchains))
