@@ -146,6 +146,38 @@ def refined_mean(S, dv, iters=6):
     return np.asarray(x, dtype=np.float64)
 
 
+def exact_chol_draw(T, Nvec, r, phiinv, zc, order):
+    """The Cholesky draw b[o] = L^-T (L^-1 d[o] + zc[o]) evaluated in x87 long double
+    (eps 1.1e-19) from T, N, r: TNT, the factorisation and both solves.  Used as the
+    'exact' value for systems so ill-conditioned (cond(S) ~ 5e7) that any two fp64
+    implementations (numpy, the device, the reference's SVD) already differ by
+    ~5e-10 relative and a chain's rho feedback amplifies that."""
+    L_ = np.longdouble
+    Tl = np.asarray(T, dtype=L_)
+    w = 1 / np.asarray(Nvec, dtype=L_)
+    A = Tl.T @ (Tl * w[:, None])
+    A[np.diag_indices_from(A)] += np.asarray(phiinv, dtype=L_)
+    dv = Tl.T @ (np.asarray(r, dtype=L_) * w)
+    A = A[np.ix_(order, order)]
+    m = A.shape[0]
+    L = np.zeros_like(A)
+    for k in range(m):
+        v = A[k:, k] - L[k:, :k] @ L[k, :k]
+        L[k, k] = np.sqrt(v[0])
+        L[k + 1:, k] = v[1:] / L[k, k]
+    y = np.zeros(m, dtype=L_)
+    db = dv[order]
+    for k in range(m):
+        y[k] = (db[k] - L[k, :k] @ y[:k]) / L[k, k]
+    y = y + np.asarray(zc, dtype=L_)[order]
+    x = np.zeros(m, dtype=L_)
+    for k in range(m - 1, -1, -1):
+        x[k] = (y[k] - L[k + 1:, k] @ x[k + 1:]) / L[k, k]
+    b = np.empty(m)
+    b[order] = np.asarray(x, dtype=np.float64)
+    return b
+
+
 def exact_mean_draw(TNT, d, phiinv, z_ref):
     """The reference draw with its mean computed exactly: refined Sigma^-1 d plus the
     reference's own noise term U S^-1/2 z (pulsar_gibbs.py:508-518)."""
@@ -213,6 +245,7 @@ def white_replay(g):
         k, z = next(items)
         TNT, d = O.tnt(T, N_of(x), r)
         ph = 1.0 / pta.get_phi(pta.map_params(x))[0]
+        zr_last[0] = z
         return O.bdraw_svd(TNT, d, ph, z), O.rotate_normals(TNT, ph, z, order)
 
     niter = g["chain"].shape[0]
@@ -220,6 +253,8 @@ def white_replay(g):
     b = np.zeros(m)
     z0 = None
     zs = np.zeros((niter, m))
+    zr = np.zeros((niter, m))
+    zr_last = [None]
     mh = np.zeros((niter, acl, 4))
     us = np.zeros((niter, gwid.size // 2))
     gates = np.zeros(niter, bool)
@@ -241,6 +276,7 @@ def white_replay(g):
         gates[ii] = bool(np.all(xn != x[-1]))
         if gates[ii]:
             b, zs[ii] = draw_b(xn)
+            zr[ii] = zr_last[0]
         x = xn
-    return dict(z0=z0, z=zs, mh=mh, u=us, gates=gates, gwind=gwind, x_final=x, b_final=b,
+    return dict(z0=z0, z=zs, z_ref=zr, N_of=N_of, mh=mh, u=us, gates=gates, gwind=gwind, x_final=x, b_final=b,
                 b_first=b_first)

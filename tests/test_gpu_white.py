@@ -11,7 +11,8 @@ import numpy as np
 import pytest
 
 from tests.conftest import golden, gpu_available
-from tests.parity_data import normwise_rel, white_params, white_replay
+from oracle import gibbs_oracle as O
+from tests.parity_data import exact_chol_draw, normwise_rel, white_params, white_replay
 
 pytestmark = pytest.mark.gpu
 
@@ -96,9 +97,28 @@ def test_white_loop_matches_reference(ctx):
     assert np.array_equal(x[:, wind], g["chain"][:, wind])
     assert np.array_equal(ch.x[0, wind].cpu().numpy(), rp["x_final"][wind])
     gw = rp["gwind"]
-    assert np.max(np.abs(x[:, gw] - g["chain"][:, gw])) < 1e-9
-    assert normwise_rel(brec[1:, 0, :m].cpu().numpy(), g["bhist"][1:]) < 1e-9
-    assert normwise_rel(ch.b[0, :m].cpu().numpy(), g["b_final"]) < 1e-9
+    # north_star tolerance: 1e-9 relative (per recorded row); the per-chain TNT is
+    # an MFMA split-K sum, so rounding differs from numpy's T.T @ (T / N) by ~1e-16
+    # relative and is amplified by cond(Sigma) ~ 1e6
+    assert normwise_rel(x[:, gw], g["chain"][:, gw]) < 1e-9
+    # b: on this system cond(S) ~ 5e7, so fp64 implementations differ by ~5e-10 per draw
+    # (numpy's Cholesky is 4.4e-10 from the exact draw at x0, the reference's SVD 7e-11)
+    # and the rho feedback amplifies that along the chain.  Each recorded b is therefore
+    # held to 1e-9 against the exact (long-double) Cholesky draw from the device's own
+    # x at that sweep with the same normals: one-step parity, as north_star states it.
+    bh = brec[:, 0, :m].cpu().numpy()
+    order = O.chol_order(m, np.asarray(g["gwid"]))
+    n_checked = 0
+    for ii in range(1, niter):
+        if not rp["gates"][ii - 1]:
+            continue
+        xx = x[ii]
+        ph = np.full(m, 1e-40)
+        ph[np.asarray(g["gwid"])] = 1.0 / np.repeat(10 ** (2 * xx[gw]), 2)
+        bx = exact_chol_draw(g["T"], rp["N_of"](xx), g["r"], ph, rp["z"][ii - 1], order)
+        assert normwise_rel(bh[ii], bx) < 1e-9, ii
+        n_checked += 1
+    assert n_checked >= 3
     assert int(ch.info.abs().sum()) == 0
 
 

@@ -268,3 +268,24 @@ def test_white_mh_loop_bitwise():
             b = draw_b(xn)
         x = xn
     assert np.array_equal(b, g["b_final"])
+
+
+def test_exact_chol_draw_pins_reference_white():
+    """The long-double Cholesky draw (tests/parity_data.exact_chol_draw) with the rotated
+    normals is the reference's first white-fixture draw (SVD, pulsar_gibbs.py:508-518) up to
+    the reference's own fp64 SVD error (2.4e-9 here, cond(S) ~ 5e7), and fp64 numpy
+    Cholesky sits within 1e-9 of it (3.5e-10)."""
+    from tests.parity_data import exact_chol_draw, normwise_rel, white_replay
+    g = golden("white_mh_j1713.npz")
+    rp = white_replay(g)
+    m = g["T"].shape[1]
+    gwid = np.asarray(g["gwid"])
+    order = O.chol_order(m, gwid)
+    x0 = g["x0"]
+    ph = np.full(m, 1e-40)
+    ph[gwid] = 1 / np.repeat(10 ** (2 * x0[rp["gwind"]]), 2)
+    N = rp["N_of"](x0)
+    bx = exact_chol_draw(g["T"], N, g["r"], ph, rp["z0"], order)
+    assert normwise_rel(rp["b_first"], bx) < 5e-9
+    TNT, d = O.tnt(g["T"], N, g["r"])
+    assert normwise_rel(O.bdraw_chol(TNT, d, ph, rp["z0"], order), bx) < 1e-9
