@@ -50,8 +50,9 @@ enum {
 
 /* Context options (gs_ctx_set_option) */
 enum {
-  GS_OPT_BCAST = 1,   /* factorisation broadcast: 0 = v_readlane -> SGPR, 1 = LDS,
-                         2 = v_readlane in batches of 8 SGPR pairs (default) */
+  GS_OPT_BCAST = 1,   /* b-draw factorisation variant: 0 = lane-row, v_readlane -> SGPR;
+                         1 = lane-row, LDS broadcast; 2 = lane-row, v_readlane in batches
+                         of 8 SGPR pairs; 3 = 16x16 fp64 MFMA tiles (default) */
   GS_OPT_PSR_BASE = 2 /* global index of this context's pulsar 0 (Philox counters of a
                          pulsar-sharded run); default 0 */
 };

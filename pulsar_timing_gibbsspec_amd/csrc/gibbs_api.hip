@@ -243,7 +243,7 @@ int gs_ctx_create(int device, uint64_t seed, void* stream, gs_ctx** out) {
   c->device = device;
   c->stream = (hipStream_t)stream;
   c->seed = seed;
-  c->bcast = 2;
+  c->bcast = 3;
   c->psr_base = 0;
   *out = c;
   return 0;
@@ -270,7 +270,7 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   switch (option) {
     case GS_OPT_BCAST:
-      if (value < 0 || value > 2) return fail_arg(3, "GS_OPT_BCAST must be 0, 1 or 2");
+      if (value < 0 || value > 3) return fail_arg(3, "GS_OPT_BCAST must be 0, 1, 2 or 3");
       ctx->bcast = value;
       return 0;
     case GS_OPT_PSR_BASE:
@@ -292,7 +292,7 @@ int gs_ctx_get_option(gs_ctx* ctx, int option) {
 int64_t gs_model_stride(int NF, int NMX) { return model_stride_doubles(NF, NMX); }
 
 int gs_sweep_lds_bytes(int NF, int NMX) {
-  return (int)((model_stride_doubles(NF, NMX) + 64 * GS_SWEEP_WPB) * 8);
+  return (int)((model_stride_doubles(NF, NMX) + GS_TILE_SCR * GS_SWEEP_WPB) * 8);
 }
 
 int gs_tnt(gs_ctx* ctx, int n_psr, int m_max, const gs_tnt_desc* desc, const double* T,

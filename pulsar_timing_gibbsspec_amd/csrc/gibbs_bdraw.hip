@@ -20,6 +20,7 @@
 // rotated by the oracle (z' = L^T U S^-1/2 z) the samples coincide.
 #include "gibbs_common.h"
 #include "gibbs_internal.h"
+#include "gibbs_tile.h"
 
 #ifndef GS_SWEEP_MINW
 #define GS_SWEEP_MINW 2
@@ -28,6 +29,14 @@
 #define GS_BCAST_READLANE 0
 #define GS_BCAST_LDS 1
 #define GS_BCAST_BATCH 2
+#define GS_BCAST_TILE 3
+
+// min workgroups per CU (launch bounds): the tile variant fits 3 x 4 waves of
+// <= 168 VGPRs and 3 x 52.5 KB of LDS per CU
+#define GS_MINW(bc) ((bc) == GS_BCAST_TILE ? 3 : GS_SWEEP_MINW)
+
+// per-wave LDS scratch (doubles) of each factorisation variant
+#define GS_SCR_DOUBLES(bc) ((bc) == GS_BCAST_TILE ? GS_TILE_SCR : 64)
 
 #ifndef GS_BCAST_CHUNK
 #define GS_BCAST_CHUNK 8
@@ -163,6 +172,16 @@ __device__ __forceinline__ int bdraw_wave(const ModelLds& M, int NMX, int nM, in
   return fail;
 }
 
+// One b|rho draw with the variant BC (tile MFMA or lane-row broadcast).
+template <int NF, int BC>
+__device__ __forceinline__ int bdraw_sys(const ModelLds& M, int NMX, int nM, int lane, double phinv,
+                                         double zF, double zM, double& bF, double& bM, double* scr) {
+  if constexpr (BC == GS_BCAST_TILE)
+    return bdraw_tile<NF>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
+  else
+    return bdraw_wave<NF, BC>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
+}
+
 // Copy a pulsar's model block into LDS (whole workgroup).
 __device__ __forceinline__ void stage_model(double* lds, const double* g, int64_t n) {
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) lds[i] = g[i];
@@ -171,7 +190,7 @@ __device__ __forceinline__ void stage_model(double* lds, const double* g, int64_
 
 // ------------------------------------------------------------ batched b draw
 template <int NF, int WPB, int BC>
-__global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_bdraw(BdrawArgs A) {
+__global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
   extern __shared__ double lds[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nb = (A.n_chain + WPB - 1) / WPB;
@@ -197,8 +216,8 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_bdraw(BdrawArgs A) 
     gs_normal2(gs_counter(lane, A.sweep, A.chain_base + c, p + A.psr_base, A.event), A.key, zF, zM);
   }
   double bF = 0.0, bM = 0.0;
-  double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * 64;
-  const int fail = bdraw_wave<NF, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
+  double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * GS_SCR_DOUBLES(BC);
+  const int fail = bdraw_sys<NF, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
   if (lane < NF) A.b[sys * A.ldb + fi] = bF;
   if (lane < nM) A.b[sys * A.ldb + mi] = bM;
   if (A.info && lane == 0) A.info[sys] = fail;
@@ -206,7 +225,7 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_bdraw(BdrawArgs A) 
 
 // ------------------------------------------------------------ fused sweep
 template <int NF, int WPB, int BC>
-__global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_sweep_freespec(SweepArgs A) {
+__global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepArgs A) {
   extern __shared__ double lds[];
   constexpr int NFR = NF / 2;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -224,7 +243,7 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_sweep_freespec(Swee
   const int kf = act ? (lane >> 1) : 0;  // frequency of this lane
   const int fi = act ? A.fidx[p * NF + lane] : 0;
   const int mi = actm ? A.midx[p * A.NMX + lane] : 0;
-  double* scr = lds + A.mstride + wave * 64;
+  double* scr = lds + A.mstride + wave * GS_SCR_DOUBLES(BC);
 
   // state: x replicated on the (sin, cos) lane pair, b split over F/M lanes
   double x = act ? A.x_state[sys * NFR + kf] : 0.0;
@@ -233,6 +252,7 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_sweep_freespec(Swee
   int fail = 0;
 
   const double rhomin = A.rhomin, rhomax = A.rhomax;
+#pragma unroll 1
   for (int sw = 0; sw < A.n_sweeps; ++sw) {
     const long long ii = A.it0 + sw;
     const int64_t rec = (int64_t)sw * n_sys + sys;
@@ -244,6 +264,7 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_sweep_freespec(Swee
     }
     // pass 0: first b draw from xs at global sweep 0 (pulsar_gibbs.py:661-662);
     // pass 1: rho|b then the gated b draw.  One bdraw_wave call site.
+#pragma unroll 1
     for (int pass = (ii == 0) ? 0 : 1; pass < 2; ++pass) {
       const double* zinj = A.z0_inj;
       int ev = GS_EV_B0;
@@ -282,7 +303,7 @@ __global__ __launch_bounds__(64 * WPB, GS_SWEEP_MINW) void k_sweep_freespec(Swee
         gs_normal2(gs_counter(lane, ii, gchain, p + A.psr_base, ev), A.key, zF, zM);
       }
       const double phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;
-      const int f = bdraw_wave<NF, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
+      const int f = bdraw_sys<NF, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
       if (!fail) fail = f;
     }
   }
@@ -322,12 +343,15 @@ __global__ void k_rho_analytic(RhoArgs A) {
     case 80: hipLaunchKernelGGL((KERNEL<20, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
     case 81: hipLaunchKernelGGL((KERNEL<20, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
     case 82: hipLaunchKernelGGL((KERNEL<20, WPB, 2>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 83: hipLaunchKernelGGL((KERNEL<20, WPB, 3>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
     case 160: hipLaunchKernelGGL((KERNEL<40, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
     case 161: hipLaunchKernelGGL((KERNEL<40, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
     case 162: hipLaunchKernelGGL((KERNEL<40, WPB, 2>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 163: hipLaunchKernelGGL((KERNEL<40, WPB, 3>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
     case 240: hipLaunchKernelGGL((KERNEL<60, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
     case 241: hipLaunchKernelGGL((KERNEL<60, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
     case 242: hipLaunchKernelGGL((KERNEL<60, WPB, 2>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
+    case 243: hipLaunchKernelGGL((KERNEL<60, WPB, 3>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
     default: return 1;                                                                       \
   }
 
@@ -346,14 +370,14 @@ int dispatch_nf_bdraw(int NF, int bc, dim3 grid, size_t lds, hipStream_t s, cons
 int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
-  const size_t lds = ((size_t)a.mstride + 64 * GS_SWEEP_WPB) * sizeof(double);
+  const size_t lds = ((size_t)a.mstride + GS_SCR_DOUBLES(a.bcast) * GS_SWEEP_WPB) * sizeof(double);
   return dispatch_nf_sweep<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
 
 int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
-  const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) + 64 * GS_SWEEP_WPB) * sizeof(double);
+  const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) + GS_SCR_DOUBLES(a.bcast) * GS_SWEEP_WPB) * sizeof(double);
   return dispatch_nf_bdraw<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
 

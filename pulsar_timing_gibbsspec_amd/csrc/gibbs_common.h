@@ -5,6 +5,10 @@
 
 #define GS_WAVE 64
 
+// per-wave LDS scratch (doubles) of the tile b-draw (gibbs_tile.h): 272 transpose /
+// factor rows + 64 vector + 64 output
+#define GS_TILE_SCR 400
+
 // ---------------------------------------------------------------- cross-lane
 // Broadcast lane `l` of a double to every lane (two v_readlane_b32 -> SGPRs).
 __device__ __forceinline__ double rdlane(double v, int l) {

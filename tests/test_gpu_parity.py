@@ -79,7 +79,7 @@ def test_prefix_matches_oracle(model, replay):
     assert normwise_rel(R, pf["R"]) < 1e-9
 
 
-@pytest.mark.parametrize("bcast", [0, 1, 2])
+@pytest.mark.parametrize("bcast", [0, 1, 2, 3])
 def test_bdraw_matches_reference_draws(ctx, model, replay, bcast):
     """gs_bdraw with rotated normals == the reference's SVD draw (1e-9)."""
     from pulsar_timing_gibbsspec_amd import _lib
@@ -95,7 +95,7 @@ def test_bdraw_matches_reference_draws(ctx, model, replay, bcast):
     for c, k in enumerate(ks):
         b_ref = O.bdraw_svd(replay["TNT"], replay["d"], replay["phiinv"][k], g["z"][k])
         assert normwise_rel(b[c], b_ref) < 1e-9, k
-    ctx.set_option(_lib.OPT_BCAST, 2)
+    ctx.set_option(_lib.OPT_BCAST, 3)
 
 
 def test_bdraw_flags_non_positive_definite(model):
@@ -104,7 +104,7 @@ def test_bdraw_flags_non_positive_definite(model):
     assert int(info[0]) > 0
 
 
-@pytest.mark.parametrize("bcast", [0, 1, 2])
+@pytest.mark.parametrize("bcast", [0, 1, 2, 3])
 def test_fused_sweep_matches_reference_chain(ctx, model, replay, bcast):
     """gs_sweep_freespec with the reference's draws (rotated) reproduces chain/bchain,
     with either broadcast variant of the factorisation."""
@@ -128,7 +128,7 @@ def test_fused_sweep_matches_reference_chain(ctx, model, replay, bcast):
         assert np.all(br[0, c] == 0)
     assert normwise_rel(run.b.cpu().numpy()[0], g["b_final"]) < 1e-9
     assert np.array_equal(xr[:, 0], xr[:, 1]) and np.array_equal(br[:, 0], br[:, 2])
-    ctx.set_option(_lib.OPT_BCAST, 2)
+    ctx.set_option(_lib.OPT_BCAST, 3)
 
 
 def test_sweep_split_and_sharding_invariance(model, replay):
