@@ -15,7 +15,8 @@ import os
 
 import torch  # noqa: F401  (must precede the CDLL load; see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpulsar_gibbs.so")
+LIB_PATH = os.environ.get("GS_LIB_PATH") or \
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpulsar_gibbs.so")
 
 OPT_BCAST = 1
 OPT_PSR_BASE = 2

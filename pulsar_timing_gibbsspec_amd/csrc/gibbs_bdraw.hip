@@ -33,7 +33,10 @@
 
 // min workgroups per CU (launch bounds): the tile variant fits 3 x 4 waves of
 // <= 168 VGPRs and 3 x 52.5 KB of LDS per CU
-#define GS_MINW(bc) ((bc) == GS_BCAST_TILE ? 3 : GS_SWEEP_MINW)
+#ifndef GS_TILE_MINW
+#define GS_TILE_MINW 2
+#endif
+#define GS_MINW(bc) ((bc) == GS_BCAST_TILE ? GS_TILE_MINW : GS_SWEEP_MINW)
 
 // per-wave LDS scratch (doubles) of each factorisation variant
 #define GS_SCR_DOUBLES(bc) ((bc) == GS_BCAST_TILE ? GS_TILE_SCR : 64)
@@ -244,6 +247,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
   const int fi = act ? A.fidx[p * NF + lane] : 0;
   const int mi = actm ? A.midx[p * A.NMX + lane] : 0;
   double* scr = lds + A.mstride + wave * GS_SCR_DOUBLES(BC);
+  GS_PH_INIT(scr)
 
   // state: x replicated on the (sin, cos) lane pair, b split over F/M lanes
   double x = act ? A.x_state[sys * NFR + kf] : 0.0;
@@ -256,6 +260,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
   for (int sw = 0; sw < A.n_sweeps; ++sw) {
     const long long ii = A.it0 + sw;
     const int64_t rec = (int64_t)sw * n_sys + sys;
+    GS_PH_BEGIN
     // record-before-update (pulsar_gibbs.py:658-659)
     if (A.x_rec && act && !(lane & 1)) A.x_rec[rec * NFR + kf] = x;
     if (A.b_rec) {
@@ -295,6 +300,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
         ev = GS_EV_B;
         zrow = rec;
       }
+      GS_PH(6)
       double zF, zM;
       if (zinj) {
         zF = act ? zinj[zrow * A.ldb + fi] : 0.0;
@@ -303,10 +309,12 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
         gs_normal2(gs_counter(lane, ii, gchain, p + A.psr_base, ev), A.key, zF, zM);
       }
       const double phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;
+      GS_PH(7)
       const int f = bdraw_sys<NF, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
       if (!fail) fail = f;
     }
   }
+  GS_PH_FLUSH(scr)
   if (act && !(lane & 1)) A.x_state[sys * NFR + kf] = x;
   if (act) A.b_state[sys * A.ldb + fi] = bF;
   if (actm) A.b_state[sys * A.ldb + mi] = bM;
@@ -337,6 +345,17 @@ __global__ void k_rho_analytic(RhoArgs A) {
   const double rho = tau / ((tau / A.rhomax) - log(1 - eta));
   A.x[sys * A.ldx + k] = 0.5 * log10(rho);
 }
+
+#ifdef GS_PHASE_PROF
+extern "C" int gs_debug_phase_cycles(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs_phase_cyc), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(gs_phase_cyc), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 #define GS_NF_CASES(KERNEL, ARGS)                                                            \
   switch (NF * 4 + bc) {                                                                     \

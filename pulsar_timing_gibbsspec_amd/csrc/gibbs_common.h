@@ -7,7 +7,11 @@
 
 // per-wave LDS scratch (doubles) of the tile b-draw (gibbs_tile.h): 272 transpose /
 // factor rows + 64 vector + 64 output
+#ifdef GS_PHASE_PROF
+#define GS_TILE_SCR 408
+#else
 #define GS_TILE_SCR 400
+#endif
 
 // ---------------------------------------------------------------- cross-lane
 // Broadcast lane `l` of a double to every lane (two v_readlane_b32 -> SGPRs).

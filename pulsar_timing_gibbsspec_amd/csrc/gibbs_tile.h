@@ -27,6 +27,35 @@
 
 typedef double gs_d4 __attribute__((ext_vector_type(4)));
 
+// Phase profiling (variant builds only, -DGS_PHASE_PROF): cycles per phase summed over
+// waves, read back with gs_debug_phase_cycles.
+#ifdef GS_PHASE_PROF
+static __device__ unsigned long long gs_phase_cyc[8];
+// per-wave accumulators in the wave's LDS scratch (doubles 400..407), flushed once
+#define GS_PH_ACC(scr) reinterpret_cast<unsigned long long*>((scr) + 400)
+#define GS_PH_INIT(scr) \
+  if ((threadIdx.x & 63) < 8) GS_PH_ACC(scr)[threadIdx.x & 63] = 0ull;
+#define GS_PH_FLUSH(scr) \
+  if ((threadIdx.x & 63) < 8) atomicAdd(&gs_phase_cyc[threadIdx.x & 63], GS_PH_ACC(scr)[threadIdx.x & 63]);
+#define GS_PH_BEGIN                   \
+  __builtin_amdgcn_sched_barrier(0); \
+  unsigned long long _ph_t = clock64(); \
+  __builtin_amdgcn_sched_barrier(0);
+#define GS_PH(i)                                                             \
+  {                                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+    const unsigned long long _t = clock64();                                 \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&GS_PH_ACC(scr)[i], _t - _ph_t); \
+    _ph_t = _t;                                                              \
+  }
+#else
+#define GS_PH_INIT(scr)
+#define GS_PH_FLUSH(scr)
+#define GS_PH_BEGIN
+#define GS_PH(i)
+#endif
+
 namespace gtile {
 
 // compiler-level ordering of the wave's LDS traffic (the hardware executes a
@@ -69,6 +98,87 @@ __device__ __forceinline__ gs_d4 to_row(double v, double* vb, int q, int c) {
   return o;
 }
 
+// v from row group g (lanes 16g..16g+15) to all four row groups, same column:
+// v_permlane32_swap then v_permlane16_swap on each 32-bit half (g compile-time)
+__device__ __forceinline__ double bcast_group(double v, int g) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  unsigned w[2] = {(unsigned)u, (unsigned)(u >> 32)};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const auto a = __builtin_amdgcn_permlane32_swap(w[h], w[h], false, false);
+    const unsigned y = (g < 2) ? a[0] : a[1];
+    const auto b = __builtin_amdgcn_permlane16_swap(y, y, false, false);
+    w[h] = (g & 1) ? b[1] : b[0];
+  }
+  return __longlong_as_double((long long)(((unsigned long long)w[1] << 32) | w[0]));
+}
+
+// lane n of each 16-lane row to the whole row (DPP row_newbcast, n compile-time)
+template <int N>
+__device__ __forceinline__ double newbcast_c(double v) {
+  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + N, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double newbcast(double v, int n) {
+  switch (n) {  // n is constant after unrolling: the switch folds away
+    case 0: return newbcast_c<0>(v);
+    case 1: return newbcast_c<1>(v);
+    case 2: return newbcast_c<2>(v);
+    case 3: return newbcast_c<3>(v);
+    case 4: return newbcast_c<4>(v);
+    case 5: return newbcast_c<5>(v);
+    case 6: return newbcast_c<6>(v);
+    case 7: return newbcast_c<7>(v);
+    case 8: return newbcast_c<8>(v);
+    case 9: return newbcast_c<9>(v);
+    case 10: return newbcast_c<10>(v);
+    case 11: return newbcast_c<11>(v);
+    case 12: return newbcast_c<12>(v);
+    case 13: return newbcast_c<13>(v);
+    case 14: return newbcast_c<14>(v);
+    default: return newbcast_c<15>(v);
+  }
+}
+
+// acc + (lane n of this 16-lane row's v) * m as ONE v_fmac_f64_dpp row_newbcast:n.
+// The s_nop covers the VALU-write -> DPP-read hazard (the compiler cannot see into asm).
+template <int N>
+__device__ __forceinline__ double fmac_nb_c(double acc, double v, double m) {
+  asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+               : "+v"(acc)
+               : "v"(v), "v"(m), "n"(N));
+  return acc;
+}
+__device__ __forceinline__ double fmac_nb(double acc, double v, double m, int n) {
+  switch (n) {
+    case 0: return fmac_nb_c<0>(acc, v, m);
+    case 1: return fmac_nb_c<1>(acc, v, m);
+    case 2: return fmac_nb_c<2>(acc, v, m);
+    case 3: return fmac_nb_c<3>(acc, v, m);
+    case 4: return fmac_nb_c<4>(acc, v, m);
+    case 5: return fmac_nb_c<5>(acc, v, m);
+    case 6: return fmac_nb_c<6>(acc, v, m);
+    case 7: return fmac_nb_c<7>(acc, v, m);
+    case 8: return fmac_nb_c<8>(acc, v, m);
+    case 9: return fmac_nb_c<9>(acc, v, m);
+    case 10: return fmac_nb_c<10>(acc, v, m);
+    case 11: return fmac_nb_c<11>(acc, v, m);
+    case 12: return fmac_nb_c<12>(acc, v, m);
+    case 13: return fmac_nb_c<13>(acc, v, m);
+    case 14: return fmac_nb_c<14>(acc, v, m);
+    default: return fmac_nb_c<15>(acc, v, m);
+  }
+}
+
+// x^-1/2: v_rsq_f64 + two Newton steps (x > 0 normal; NaN/inf/<= 0 propagate to a
+// non-finite or non-positive result, caught by the pivot ballot)
+__device__ __forceinline__ double rsq_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  y = y * fma(-hx * y, y, 1.5);
+  y = y * fma(-hx * y, y, 1.5);
+  return y;
+}
+
 // sum over the four lanes of a column (q = 0..3)
 __device__ __forceinline__ double qsum(double p) {
   p += __shfl_xor(p, 16);
@@ -93,6 +203,7 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
   constexpr int LD = NF + 1;
   constexpr int NTILE = NT * (NT + 1) / 2;
   const int q = lane >> 4, c = lane & 15;
+  GS_PH_BEGIN
   double* tb = scr;        // 272
   double* vb = scr + 272;  // 64
   double* ob = scr + 336;  // 64
@@ -132,52 +243,94 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
     }
   }
 
+  GS_PH(0)
   // ---- factorisation
   int fail = 0;
 #pragma unroll
   for (int K = 0; K < NT; ++K) {
+    // diag tile: column elimination on [T_KK ; I] -> B = E (unit upper), with
+    // T_KK E lower triangular; U_KK^-1 = E diag(pivot^-1/2).  Column c of both
+    // lives in lane column c, so the pivot scale is lane-local; A[r][k], B[r][k]
+    // come from lane k of the same 16-lane row (DPP row_newbcast) and row k of A
+    // from row group k&3 (permlane swaps): no LDS, no transpose.
     gs_d4 A = t[tix(K, K, NT)], B;
 #pragma unroll
     for (int s = 0; s < 4; ++s) B[s] = (4 * s + q == c) ? 1.0 : 0.0;
-    double rsd[4] = {0.0, 0.0, 0.0, 0.0};
+#if !defined(GS_DIAG_V1) && !defined(GS_DIAG_V2)
+    // Step k: pivot A[k][k] by DPP from row k (replicated in every row group),
+    // -1/pivot by v_rcp_f64 + one Newton step, then every column update is one
+    // v_fmac_f64_dpp.  Row k+1 (as before step k) is broadcast off the critical path
+    // and updated by the same column operation.  Steps on identity padding
+    // (columns >= NF - 16K) are skipped; pivots are kept per lane column and
+    // turned into pivot^-1/2 once per tile.
+    constexpr int KMAX_LAST = NF - 16 * (NT - 1);
+    const int KMAX = (K == NT - 1) ? KMAX_LAST : 16;
+    double piv = 1.0;
+    double akc = bcast_group(A[0], 0);  // row 0
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (k < KMAX) {
+        const int k1 = k >> 2;
+        const double akk = newbcast(akc, k);  // A[k][k]
+        piv = (c == k) ? akk : piv;
+        if (k + 1 < KMAX) {
+          const double i0 = __builtin_amdgcn_rcp(akk);
+          const double ninv = fma(akk, i0, -2.0) * i0;   // -1/A[k][k]
+          const double ng = (c > k) ? akc * ninv : 0.0;  // -A[k][c]/A[k][k]
+          const double rn = bcast_group(A[(k + 1) >> 2], (k + 1) & 3);  // row k+1 before step k
+          akc = fmac_nb(rn, rn, ng, k);                                  // row k+1 after step k
+#pragma unroll
+          for (int s = k1; s < 4; ++s) A[s] = fmac_nb(A[s], A[s], ng, k);
+#pragma unroll
+          for (int s = 0; s <= k1; ++s) B[s] = fmac_nb(B[s], B[s], ng, k);
+        }
+      }
+    }
+    const double rsd = rsq_nr(piv);
+#elif defined(GS_DIAG_V2)
+    double rsd = 0.0;  // pivot^-1/2 of this lane's column
+    // Critical path per step: g_k -> row k+1 (one FMA) -> pivot (DPP) -> rsqrt -> g_{k+1}.
+    // Row k+1 as it stood before step k is broadcast off the critical path.
+    double akc = bcast_group(A[0], 0);  // row 0
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int k1 = k >> 2;
+      const double akk = newbcast(akc, k);  // A[k][k]
+      const double rs = rsq_nr(akk);
+      rsd = (c == k) ? rs : rsd;
+      const double g = (c > k) ? akc * (rs * rs) : 0.0;
+      if (k < 15) {
+        const double rn = bcast_group(A[(k + 1) >> 2], (k + 1) & 3);  // row k+1 after step k-1
+        akc = fma(-newbcast(rn, k), g, rn);                            // row k+1 after step k
+      }
+#pragma unroll
+      for (int s = k1; s < 4; ++s) A[s] = fma(-newbcast(A[s], k), g, A[s]);
+#pragma unroll
+      for (int s = 0; s <= k1; ++s) B[s] = fma(-newbcast(B[s], k), g, B[s]);
+    }
+#else
+    double rsd = 0.0;  // pivot^-1/2 of this lane's column
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int k0 = k & 3, k1 = k >> 2;
-      lds_fence();
-      tb[q * 16 + c] = A[k1];
-      tb[64 + q * 16 + c] = B[k1];
-      lds_fence();
-      const double akk = tb[k0 * 16 + k];
-      const double akc = tb[k0 * 16 + c];
-      const double bkc = tb[64 + k0 * 16 + c];
-      double akr[4];
-#pragma unroll
-      for (int s = k1; s < 4; ++s) akr[s] = tb[k0 * 16 + 4 * s + q];
-      lds_fence();
+      const double akc = bcast_group(A[k1], k0);  // A[k][c]
+      const double akk = newbcast(akc, k);        // A[k][k]
       const double rs = rsqrt(akk);
-      const double inv = rs * rs;
-      rsd[k1] = (q == k0) ? rs : rsd[k1];
-      const double ga = akc * inv, gb = bkc * inv;
+      rsd = (c == k) ? rs : rsd;
+      const double g = (c > k) ? akc * (rs * rs) : 0.0;
 #pragma unroll
-      for (int s = k1; s < 4; ++s) {
-        const double cf = (s == k1) ? ((q > k0) ? akr[s] : 0.0) : akr[s];
-        A[s] = fma(-cf, ga, A[s]);
-        B[s] = fma(-cf, gb, B[s]);
-      }
+      for (int s = k1; s < 4; ++s) A[s] = fma(-newbcast(A[s], k), g, A[s]);
+#pragma unroll
+      for (int s = 0; s <= k1; ++s) B[s] = fma(-newbcast(B[s], k), g, B[s]);
     }
-    // W = U_KK^-T (row r scaled by 1/sqrt(pivot_r)); first bad pivot of this tile
-    gs_d4 W;
-    unsigned long long badrow = 0;  // bit r: pivot r not > 0
+#endif
+    GS_PH(1)
+    // first bad pivot of this tile (columns c of row group 0)
+    const unsigned long long badm = __ballot(!(rsd > 0.0 && rsd < __builtin_inf())) & 0xffffull;
+    if (!fail && badm) fail = 16 * K + __ffsll((long long)badm);
+    gs_d4 V;  // U_KK^-1
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      W[s] = B[s] * rsd[s];
-      const unsigned long long bm = __ballot(!(rsd[s] > 0.0 && rsd[s] < __builtin_inf()));
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq)
-        if ((bm >> (16 * qq)) & 0xffffull) badrow |= 1ull << (4 * s + qq);
-    }
-    if (!fail && badrow) fail = 16 * K + __ffsll((long long)badrow);
-    const gs_d4 V = transpose(W, tb, q, c);  // U_KK^-1
+    for (int s = 0; s < 4; ++s) V[s] = B[s] * rsd;
     t[tix(K, K, NT)] = V;
     // TRSM: U_KJ = U_KK^-T T_KJ
 #pragma unroll
@@ -192,6 +345,7 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
 #pragma unroll
       for (int J = I; J < NT; ++J) t[tix(I, J, NT)] = mfma_tn(t[tix(I, J, NT)], nx, t[tix(K, J, NT)]);
     }
+    GS_PH(2)
   }
 
   // ---- forward: U^T y = dF   (y_K = U_KK^-T (dF_K - sum_{I<K} U_IK^T y_I))
@@ -215,6 +369,7 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
     if (K + 1 < NT) yrow[K] = to_row(ycol[K], vb, q, c);
   }
 
+  GS_PH(3)
   // ---- backward: U x = y + zF   (x_K = U_KK^-1 (w_K - sum_{J>K} U_KJ x_J))
   double xcol[NT];
   gs_d4 xrow[NT];
@@ -243,6 +398,7 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
   bF = (lane < NF) ? ob[lane] : 0.0;
   lds_fence();
 
+  GS_PH(4)
   // ---- fixed-prior block: x_M = h + R z_M - G x_F, 16 rows per chunk
   vb[lane] = (lane < nM) ? zM : 0.0;
   lds_fence();
@@ -272,5 +428,6 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
   lds_fence();
   bM = (lane < nM) ? ob[lane] : 0.0;
   lds_fence();
+  GS_PH(5)
   return fail;
 }
