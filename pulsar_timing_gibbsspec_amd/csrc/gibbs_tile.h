@@ -113,10 +113,34 @@ __device__ __forceinline__ double bcast_group(double v, int g) {
   return __longlong_as_double((long long)(((unsigned long long)w[1] << 32) | w[0]));
 }
 
+// Same broadcast through the LDS crossbar (ds_bpermute_b32 x2): no VALU slots and no
+// operand copies; the latency is hidden when the row is requested a step ahead.
+__device__ __forceinline__ double bcast_group_bp(double v, int g, int c) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const int addr = (16 * g + c) * 4;
+  const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)u);
+  const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// v of lane `src` (per-lane source) through the LDS crossbar
+__device__ __forceinline__ double bcast_lane_bp(double v, int src) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(src * 4, (int)(unsigned)u);
+  const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src * 4, (int)(unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// an SGPR copy of a compile-time int the compiler cannot see through
+__device__ __forceinline__ int opq(int v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
 // lane n of each 16-lane row to the whole row (DPP row_newbcast, n compile-time)
 template <int N>
 __device__ __forceinline__ double newbcast_c(double v) {
-  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + N, 0xf, 0xf, false);
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + N, 0xf, 0xf, false);  // no "old": every lane is written
 }
 __device__ __forceinline__ double newbcast(double v, int n) {
   switch (n) {  // n is constant after unrolling: the switch folds away
@@ -141,9 +165,11 @@ __device__ __forceinline__ double newbcast(double v, int n) {
 
 // acc + (lane n of this 16-lane row's v) * m as ONE v_fmac_f64_dpp row_newbcast:n.
 // The s_nop covers the VALU-write -> DPP-read hazard (the compiler cannot see into asm).
+// Not volatile: a pure function of its operands, so the scheduler may hoist the
+// row broadcast (ds_bpermute) of the next step above it.
 template <int N>
 __device__ __forceinline__ double fmac_nb_c(double acc, double v, double m) {
-  asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+  asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
                : "+v"(acc)
                : "v"(v), "v"(m), "n"(N));
   return acc;
@@ -265,19 +291,29 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
     // turned into pivot^-1/2 once per tile.
     constexpr int KMAX_LAST = NF - 16 * (NT - 1);
     const int KMAX = (K == NT - 1) ? KMAX_LAST : 16;
-    double piv = 1.0;
     double akc = bcast_group(A[0], 0);  // row 0
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       if (k < KMAX) {
         const int k1 = k >> 2;
+        // row k+1 as before step k, requested first so the crossbar latency overlaps
+        // the pivot chain below (the barrier keeps the scheduler from sinking it)
+        double rn = 0.0;
+        if (k + 1 < KMAX) {
+#ifdef GS_ROW_PERMLANE
+          rn = bcast_group(A[(k + 1) >> 2], (k + 1) & 3);
+#else
+          rn = bcast_group_bp(A[(k + 1) >> 2], (k + 1) & 3, c);
+#endif
+        }
+        __builtin_amdgcn_sched_barrier(0);
         const double akk = newbcast(akc, k);  // A[k][k]
-        piv = (c == k) ? akk : piv;
         if (k + 1 < KMAX) {
           const double i0 = __builtin_amdgcn_rcp(akk);
-          const double ninv = fma(akk, i0, -2.0) * i0;   // -1/A[k][k]
-          const double ng = (c > k) ? akc * ninv : 0.0;  // -A[k][c]/A[k][k]
-          const double rn = bcast_group(A[(k + 1) >> 2], (k + 1) & 3);  // row k+1 before step k
+          const double ninv = fma(akk, i0, -2.0) * i0;  // -1/A[k][k]
+          // lane mask c > k from an opaque k: one v_cmp per step instead of 60
+          // loop-invariant 64-bit masks held in (spilled) SGPRs across the sweep loop
+          const double ng = (c > opq(k)) ? akc * ninv : 0.0;  // -A[k][c]/A[k][k]
           akc = fmac_nb(rn, rn, ng, k);                                  // row k+1 after step k
 #pragma unroll
           for (int s = k1; s < 4; ++s) A[s] = fmac_nb(A[s], A[s], ng, k);
@@ -286,6 +322,12 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
         }
       }
     }
+    // column elimination leaves A[k][k] = pivot k on the diagonal: lane (c&3, c) holds
+    // it in register c>>2; fetch it for every lane of column c
+    double dg = A[0];
+#pragma unroll
+    for (int s = 1; s < 4; ++s) dg = ((c >> 2) == s) ? A[s] : dg;
+    const double piv = bcast_lane_bp(dg, 16 * (c & 3) + c);
     const double rsd = rsq_nr(piv);
 #elif defined(GS_DIAG_V2)
     double rsd = 0.0;  // pivot^-1/2 of this lane's column
