@@ -273,6 +273,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
     for (int pass = (ii == 0) ? 0 : 1; pass < 2; ++pass) {
       const double* zinj = A.z0_inj;
       int ev = GS_EV_B0;
+      double phinv = 0.0;
       int64_t zrow = sys;
       if (pass == 1) {
         // rho|b analytic (pulsar_gibbs.py:208-216, 236)
@@ -286,10 +287,22 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
           double u2;
           gs_uniform2(gs_counter(kf, ii, gchain, p + A.psr_base, GS_EV_RHO), A.key, U, u2);
         }
-        const double hi = 1 - exp((tau / rhomax) - (tau / rhomin));
+        const double t1 = tau / rhomax;
+        const double arg = t1 - (tau / rhomin);
+        // 1 - exp(arg) rounds to exactly 1 for arg < -37.5: skip the exp when every
+        // lane is there (the usual case, tau >> rhomin)
+        double hi = 1.0;
+        if (__ballot(act && !(arg < -40.0))) hi = 1 - exp(arg);
         const double eta = 0.0 + hi * U;
-        const double rho = tau / ((tau / rhomax) - log(1 - eta));
+        const double den = t1 - log(1 - eta);
+        const double rho = tau / den;
         const double xnew = act ? 0.5 * log10(rho) : 0.0;
+        // phiinv of the new rho: 1/rho (rcp + two Newton steps) instead of the
+        // reference's 1/10**(2 x) round trip through log10 (equal to a few ulp)
+        double ri = __builtin_amdgcn_rcp(rho);
+        ri = fma(ri, fma(-rho, ri, 1.0), ri);
+        ri = fma(ri, fma(-rho, ri, 1.0), ri);
+        phinv = act ? ri : 0.0;
         // gate: all(xnew != x_old[-1])  (pulsar_gibbs.py:697)
         const double xlast = rdlane(x, NF - 1);
         const bool same = act && (xnew == xlast);
@@ -308,7 +321,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
       } else {
         gs_normal2(gs_counter(lane, ii, gchain, p + A.psr_base, ev), A.key, zF, zM);
       }
-      const double phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;
+      if (pass == 0) phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;  // first draw from xs
       GS_PH(7)
       const int f = bdraw_sys<NF, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
       if (!fail) fail = f;

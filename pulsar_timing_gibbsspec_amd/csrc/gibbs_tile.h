@@ -164,6 +164,8 @@ __device__ __forceinline__ double newbcast(double v, int n) {
 }
 
 // acc + (lane n of this 16-lane row's v) * m as ONE v_fmac_f64_dpp row_newbcast:n.
+// fmac_nb: the s_nop only at step 0 of a tile (the DPP sources of later steps were
+// written by the previous step); fmac_nb_safe: always.
 // The s_nop covers the VALU-write -> DPP-read hazard (the compiler cannot see into asm).
 // Not volatile: a pure function of its operands, so the scheduler may hoist the
 // row broadcast (ds_bpermute) of the next step above it.
@@ -174,7 +176,36 @@ __device__ __forceinline__ double fmac_nb_c(double acc, double v, double m) {
                : "v"(v), "v"(m), "n"(N));
   return acc;
 }
+// Same without the s_nop, for a DPP source last written by VALU at least two
+// instructions earlier (the previous elimination step).
+template <int N>
+__device__ __forceinline__ double fmac_nb_c_nn(double acc, double v, double m) {
+  asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+      : "+v"(acc)
+      : "v"(v), "v"(m), "n"(N));
+  return acc;
+}
 __device__ __forceinline__ double fmac_nb(double acc, double v, double m, int n) {
+  switch (n) {
+    case 0: return fmac_nb_c<0>(acc, v, m);
+    case 1: return fmac_nb_c_nn<1>(acc, v, m);
+    case 2: return fmac_nb_c_nn<2>(acc, v, m);
+    case 3: return fmac_nb_c_nn<3>(acc, v, m);
+    case 4: return fmac_nb_c_nn<4>(acc, v, m);
+    case 5: return fmac_nb_c_nn<5>(acc, v, m);
+    case 6: return fmac_nb_c_nn<6>(acc, v, m);
+    case 7: return fmac_nb_c_nn<7>(acc, v, m);
+    case 8: return fmac_nb_c_nn<8>(acc, v, m);
+    case 9: return fmac_nb_c_nn<9>(acc, v, m);
+    case 10: return fmac_nb_c_nn<10>(acc, v, m);
+    case 11: return fmac_nb_c_nn<11>(acc, v, m);
+    case 12: return fmac_nb_c_nn<12>(acc, v, m);
+    case 13: return fmac_nb_c_nn<13>(acc, v, m);
+    case 14: return fmac_nb_c_nn<14>(acc, v, m);
+    default: return fmac_nb_c_nn<15>(acc, v, m);
+  }
+}
+__device__ __forceinline__ double fmac_nb_safe(double acc, double v, double m, int n) {
   switch (n) {
     case 0: return fmac_nb_c<0>(acc, v, m);
     case 1: return fmac_nb_c<1>(acc, v, m);
@@ -314,7 +345,11 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
           // lane mask c > k from an opaque k: one v_cmp per step instead of 60
           // loop-invariant 64-bit masks held in (spilled) SGPRs across the sweep loop
           const double ng = (c > opq(k)) ? akc * ninv : 0.0;  // -A[k][c]/A[k][k]
-          akc = fmac_nb(rn, rn, ng, k);                                  // row k+1 after step k
+#ifdef GS_ROW_PERMLANE
+          akc = fmac_nb_safe(rn, rn, ng, k);  // rn written by VALU (permlane) just before
+#else
+          akc = fmac_nb(rn, rn, ng, k);  // row k+1 after step k (rn from the crossbar)
+#endif
 #pragma unroll
           for (int s = k1; s < 4; ++s) A[s] = fmac_nb(A[s], A[s], ng, k);
 #pragma unroll
