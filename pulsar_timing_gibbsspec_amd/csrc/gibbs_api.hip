@@ -182,11 +182,10 @@ __global__ __launch_bounds__(256) void k_prefix(const gs_prefix_desc* desc, int 
   double* R = h + NMX;
   for (int q = tid; q < NF * (NF + 1); q += nt) {
     const int f = q / (NF + 1), g = q % (NF + 1);
-    double s = 0.0;
-    if (g < NF) {
-      s = A[(int64_t)Fi[f] * m + Fi[g]];
-      for (int i = 0; i < nM; ++i) s -= W[i * ldw + f] * W[i * ldw + g];
-    }
+    // column NF (padding of the odd row stride) carries dF[f]: the tile b-draw
+    // factorises the system augmented by dF (gibbs_tile.h)
+    double s = (g < NF) ? A[(int64_t)Fi[f] * m + Fi[g]] : dv[Fi[f]];
+    for (int i = 0; i < nM; ++i) s -= W[i * ldw + f] * W[i * ldw + g];
     S0[q] = s;
   }
   for (int f = tid; f < NF; f += nt) {

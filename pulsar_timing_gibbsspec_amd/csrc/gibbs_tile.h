@@ -283,6 +283,17 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
   // S0 loads inside the caller's sweep loop instead of hoisting 80 VGPRs out of it.
   int z0 = 0;
   asm volatile("" : "+s"(z0));
+  // Augmented system: with NF % 16 != 0 the first padding row/column (index NF,
+  // local column CP of the last tile) carries dF, so the factorisation of
+  // [[S, dF], [dF^T, 1]] yields y = U^-T dF on the way (column CP of U_I,last for
+  // I < last; row CP of the eliminated last diagonal tile scaled by the pivots^-1/2):
+  // no forward solve.  S0 stores dF in its padding column NF (gs_prefix).
+#if !defined(GS_DIAG_V1) && !defined(GS_DIAG_V2)
+  constexpr bool AUG = (NF % 16) != 0;
+#else
+  constexpr bool AUG = false;
+#endif
+  constexpr int CP = NF - 16 * (NT - 1);  // local index of the augmented column
   gs_d4 t[NTILE];
 #pragma unroll
   for (int I = 0; I < NT; ++I) {
@@ -293,6 +304,10 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
       for (int s = 0; s < 4; ++s) {
         const int r = 16 * I + 4 * s + q, col = 16 * J + c;
         double e = (r < NF && col < NF) ? M.S0[r * LD + col + z0] : 0.0;
+        if (AUG && J == NT - 1) {
+          if (r < NF && col == NF) e = M.S0[r * LD + NF + z0];     // dF[r]
+          if (r == NF && col < NF) e = M.S0[col * LD + NF + z0];   // dF[col]
+        }
         if (I == J) e += (4 * s + q == c) ? phc[I] : 0.0;
         v[s] = e;
       }
@@ -303,6 +318,7 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
   GS_PH(0)
   // ---- factorisation
   int fail = 0;
+  double ylast = 0.0;  // AUG: y of the last tile row, column layout
 #pragma unroll
   for (int K = 0; K < NT; ++K) {
     // diag tile: column elimination on [T_KK ; I] -> B = E (unit upper), with
@@ -362,8 +378,14 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
     double dg = A[0];
 #pragma unroll
     for (int s = 1; s < 4; ++s) dg = ((c >> 2) == s) ? A[s] : dg;
-    const double piv = bcast_lane_bp(dg, 16 * (c & 3) + c);
+    double piv = bcast_lane_bp(dg, 16 * (c & 3) + c);
+    if (K == NT - 1) piv = (c >= KMAX) ? 1.0 : piv;  // padding (incl. the augmented pivot)
     const double rsd = rsq_nr(piv);
+    if (AUG && K == NT - 1) {
+      // y_last[k] = (row CP of the eliminated tile)[k] * pivot_k^-1/2, k < CP
+      const double yl = bcast_group_bp(A[CP >> 2], CP & 3, c);
+      ylast = (c < CP) ? yl * rsd : 0.0;
+    }
 #elif defined(GS_DIAG_V2)
     double rsd = 0.0;  // pivot^-1/2 of this lane's column
     // Critical path per step: g_k -> row k+1 (one FMA) -> pivot (DPP) -> rsqrt -> g_{k+1}.
@@ -428,6 +450,14 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
   // ---- forward: U^T y = dF   (y_K = U_KK^-T (dF_K - sum_{I<K} U_IK^T y_I))
   double ycol[NT];
   gs_d4 yrow[NT];
+  if constexpr (AUG) {
+    // y_I (row layout) = lane column CP of U_I,last, broadcast along each 16-lane row
+#pragma unroll
+    for (int I = 0; I + 1 < NT; ++I)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) yrow[I][s] = newbcast(t[tix(I, NT - 1, NT)][s], CP);
+    ycol[NT - 1] = ylast;
+  } else
 #pragma unroll
   for (int K = 0; K < NT; ++K) {
     double p = 0.0;
@@ -460,7 +490,14 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
       for (int s = 0; s < 4; ++s) p = fma(ut[s], xrow[J][s], p);
     }
     if (K + 1 < NT) p = qsum(p);
-    const gs_d4 sr = to_row(ycol[K] + zfc[K] - p, vb, q, c);
+    gs_d4 sr;
+    if (AUG && K + 1 < NT) {
+      sr = to_row(zfc[K] - p, vb, q, c);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) sr[s] += yrow[K][s];
+    } else {
+      sr = to_row(ycol[K] + zfc[K] - p, vb, q, c);
+    }
     const gs_d4 W = transpose(t[tix(K, K, NT)], tb, q, c);
     double p2 = 0.0;
 #pragma unroll
