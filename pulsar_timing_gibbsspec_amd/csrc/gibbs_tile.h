@@ -303,11 +303,14 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int r = 16 * I + 4 * s + q, col = 16 * J + c;
-        double e = (r < NF && col < NF) ? M.S0[r * LD + col + z0] : 0.0;
+        // one LDS load per element: S0[r][col], or dF (S0's column NF) on the
+        // augmented row/column of the last tile column
+        int a = (r < NF && col < NF) ? r * LD + col : -1;
         if (AUG && J == NT - 1) {
-          if (r < NF && col == NF) e = M.S0[r * LD + NF + z0];     // dF[r]
-          if (r == NF && col < NF) e = M.S0[col * LD + NF + z0];   // dF[col]
+          if (r < NF && col == NF) a = r * LD + NF;    // dF[r]
+          if (r == NF && col < NF) a = col * LD + NF;  // dF[col]
         }
+        double e = (a >= 0) ? M.S0[a + z0] : 0.0;
         if (I == J) e += (4 * s + q == c) ? phc[I] : 0.0;
         v[s] = e;
       }
@@ -317,6 +320,8 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
 
   GS_PH(0)
   // ---- factorisation
+  double ycol[NT];
+  gs_d4 yrow[NT];
   int fail = 0;
   double ylast = 0.0;  // AUG: y of the last tile row, column layout
 #pragma unroll
@@ -437,6 +442,8 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
       const gs_d4 z = {0.0, 0.0, 0.0, 0.0};
       t[tix(K, J, NT)] = mfma_tn(z, V, t[tix(K, J, NT)]);
     }
+    // the backward solve wants U_KK^-T: transpose in place while the MFMAs run
+    if constexpr (AUG) t[tix(K, K, NT)] = transpose(V, tb, q, c);
     // trailing update: T_IJ -= U_KI^T U_KJ
 #pragma unroll
     for (int I = K + 1; I < NT; ++I) {
@@ -444,18 +451,19 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
 #pragma unroll
       for (int J = I; J < NT; ++J) t[tix(I, J, NT)] = mfma_tn(t[tix(I, J, NT)], nx, t[tix(K, J, NT)]);
     }
+    if constexpr (AUG) {
+      // block row K is final: keep U_KJ^T (what the backward solve reads)
+#pragma unroll
+      for (int J = K + 1; J < NT; ++J) t[tix(K, J, NT)] = transpose(t[tix(K, J, NT)], tb, q, c);
+    }
     GS_PH(2)
   }
 
   // ---- forward: U^T y = dF   (y_K = U_KK^-T (dF_K - sum_{I<K} U_IK^T y_I))
-  double ycol[NT];
-  gs_d4 yrow[NT];
   if constexpr (AUG) {
-    // y_I (row layout) = lane column CP of U_I,last, broadcast along each 16-lane row
+    // y_K = column CP of U_K,last = row CP of the stored U_K,last^T (row group CP&3)
 #pragma unroll
-    for (int I = 0; I + 1 < NT; ++I)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) yrow[I][s] = newbcast(t[tix(I, NT - 1, NT)][s], CP);
+    for (int K = 0; K + 1 < NT; ++K) ycol[K] = bcast_group_bp(t[tix(K, NT - 1, NT)][CP >> 2], CP & 3, c);
     ycol[NT - 1] = ylast;
   } else
 #pragma unroll
@@ -485,20 +493,13 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
     double p = 0.0;
 #pragma unroll
     for (int J = K + 1; J < NT; ++J) {
-      const gs_d4 ut = transpose(t[tix(K, J, NT)], tb, q, c);
+      const gs_d4 ut = AUG ? t[tix(K, J, NT)] : transpose(t[tix(K, J, NT)], tb, q, c);
 #pragma unroll
       for (int s = 0; s < 4; ++s) p = fma(ut[s], xrow[J][s], p);
     }
     if (K + 1 < NT) p = qsum(p);
-    gs_d4 sr;
-    if (AUG && K + 1 < NT) {
-      sr = to_row(zfc[K] - p, vb, q, c);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) sr[s] += yrow[K][s];
-    } else {
-      sr = to_row(ycol[K] + zfc[K] - p, vb, q, c);
-    }
-    const gs_d4 W = transpose(t[tix(K, K, NT)], tb, q, c);
+    const gs_d4 sr = to_row(ycol[K] + zfc[K] - p, vb, q, c);
+    const gs_d4 W = AUG ? t[tix(K, K, NT)] : transpose(t[tix(K, K, NT)], tb, q, c);
     double p2 = 0.0;
 #pragma unroll
     for (int s = 0; s < 4; ++s) p2 = fma(W[s], sr[s], p2);
