@@ -211,6 +211,7 @@ __device__ __forceinline__ void stage_white(const WhiteTntArgs& A, const gs_whit
 }
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef d4 gs_d4_t;
 
 // TNT_c: grid (n_sys, nb (nb + 1) / 2) lower 16 x 16 tile pairs, mirrored on store;
 // 4 wavefronts split the TOAs, v_mfma_f64_16x16x4f64 (layout as k_tnt).
@@ -265,6 +266,137 @@ __global__ __launch_bounds__(256) void k_white_tnt(WhiteTntArgs A) {
   }
 }
 
+// ---------------------------------------------------------------- batched SYRK
+// TNT_c and d_c in ONE pass over T per system (configs 5 and white-noise pulsars):
+// the system's T is augmented by r as column m, so the lower 16 x 16 tiles of
+// [T | r]^T N_c^-1 [T | r] hold TNT_c and, in row m, d_c.  One workgroup (8 waves)
+// per system streams T through LDS in chunks of SY_TC TOAs (double-buffered, one
+// barrier per chunk); wave w accumulates tiles w, w + 8, ... in registers with
+// v_mfma_f64_16x16x4f64 (A = T[t][bi*16+i] / N[t], B = T[t][bj*16+i]; the k_tnt
+// layout).  Workgroups are mapped XCD-major so the chains of one pulsar share an
+// XCD's L2 for T.  Roofline: fp64 MFMA (n m^2 flop per system against 8 n m bytes).
+constexpr int SY_WAVES = 8;
+constexpr int SY_TC = 16;
+
+__host__ __device__ constexpr int sy_ld(int nb) { return 16 * nb + ((nb & 1) ? 0 : 16); }
+
+template <int MAXT>
+__global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
+  extern __shared__ double lds[];
+  __shared__ double sb[3][GS_WHITE_MAX_BK + 1];
+  const int64_t n_sys = (int64_t)A.n_psr * A.n_chain;
+  // XCD-major: consecutive workgroup ids go round-robin over the 8 XCDs
+  const int64_t per = (n_sys + 7) / 8;
+  const int64_t sys = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (sys >= n_sys) return;  // uniform over the workgroup
+  const int p = (int)(sys / A.n_chain), c = (int)(sys % A.n_chain);
+  const gs_tnt_desc D = A.tdesc[p];
+  const gs_white_desc W = A.wdesc[p];
+  stage_white(A, W, c, sb[0], sb[1], sb[2]);
+  const int m = (int)D.m, nb = (m + 1 + 15) / 16, ld = sy_ld(nb), wcols = 16 * nb;
+  const int ntile = nb * (nb + 1) / 2;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, i = l & 15, k = l >> 4;
+  const int64_t n = D.n_toa;
+  const double* Tp = A.T + D.T_off;
+  const double* rp = A.r + D.toa_off;
+  const double* s2 = A.sigma2 + D.toa_off;
+  const int32_t* bk = A.bk + D.toa_off;
+  double* buf0 = lds;
+  double* buf1 = lds + SY_TC * ld + SY_TC;  // [SY_TC x ld] chunk + SY_TC inverse N
+
+  int ti[MAXT], tj[MAXT];
+  gs_d4_t acc[MAXT];
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    const int tl = w + SY_WAVES * j;
+    int bi = (int)((sqrt(8.0 * tl + 1.0) - 1.0) * 0.5);
+    while ((bi + 1) * (bi + 2) / 2 <= tl) ++bi;
+    while (bi * (bi + 1) / 2 > tl) --bi;
+    ti[j] = (tl < ntile) ? bi : -1;
+    tj[j] = tl - bi * (bi + 1) / 2;
+    acc[j] = gs_d4_t{0.0, 0.0, 0.0, 0.0};
+  }
+
+  // chunk loader: thread tid owns column tid & 255 of rows (tid >> 8) + 2 e, e < 8
+  // (coalesced along the row; no index division)
+  const int lcol = tid & 255, lrow = tid >> 8;
+  const bool colok = lcol < wcols;
+  double reg[SY_TC / 2];
+  double rinv = 0.0;
+  auto load = [&](int64_t t0) {
+#pragma unroll
+    for (int e = 0; e < SY_TC / 2; ++e) {
+      const int64_t t = t0 + lrow + 2 * e;
+      double v = 0.0;
+      if (colok && t < n) v = (lcol < m) ? Tp[t * m + lcol] : ((lcol == m) ? rp[t] : 0.0);
+      reg[e] = v;
+    }
+    if (tid < SY_TC) {
+      const int64_t t = t0 + tid;
+      rinv = 0.0;
+      if (t < n) {
+        const int kb = bk[t];
+        rinv = 1.0 / (sb[0][kb] * (s2[t] + sb[1][kb]) + sb[2][kb]);
+      }
+    }
+  };
+  auto store = [&](double* b) {
+    if (colok)
+#pragma unroll
+      for (int e = 0; e < SY_TC / 2; ++e) b[(lrow + 2 * e) * ld + lcol] = reg[e];
+    if (tid < SY_TC) b[SY_TC * ld + tid] = rinv;
+  };
+
+  const int64_t nch = (n + SY_TC - 1) / SY_TC;
+  load(0);
+  store(buf0);
+  __syncthreads();
+  for (int64_t ch = 0; ch < nch; ++ch) {
+    double* cur = (ch & 1) ? buf1 : buf0;
+    double* nxt = (ch & 1) ? buf0 : buf1;
+    if (ch + 1 < nch) load((ch + 1) * SY_TC);
+#pragma unroll
+    for (int kk = 0; kk < SY_TC / 4; ++kk) {
+      const int tr = 4 * kk + k;
+      const double* row = cur + tr * ld;
+      const double iv = cur[SY_TC * ld + tr];
+#pragma unroll
+      for (int j = 0; j < MAXT; ++j) {
+        if (ti[j] >= 0) {
+          const double a = row[ti[j] * 16 + i] * iv;
+          const double b = row[tj[j] * 16 + i];
+          acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[j], 0, 0, 0);
+        }
+      }
+    }
+    if (ch + 1 < nch) store(nxt);
+    __syncthreads();
+  }
+
+  double* out = A.TNT + D.tnt_off + (int64_t)c * A.tnt_cstride;
+  double* dout = A.d + D.d_off + (int64_t)c * A.d_cstride;
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    if (ti[j] < 0) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = ti[j] * 16 + k + 4 * r, col = tj[j] * 16 + i;
+      const double v = acc[j][r];
+      if (row < m && col < m) {
+        out[(int64_t)row * m + col] = v;
+        out[(int64_t)col * m + row] = v;
+      } else if (row == m && col < m) {
+        dout[col] = v;
+      }
+    }
+  }
+}
+
+size_t sy_lds_bytes(int m_max) {
+  const int nb = (m_max + 1 + 15) / 16;
+  return (size_t)2 * (SY_TC * sy_ld(nb) + SY_TC) * sizeof(double);
+}
+
 // d_c = T^T (r / N_c): grid (n_sys, ceil(m_max / 64)).
 __global__ __launch_bounds__(256) void k_white_tnr(WhiteTntArgs A) {
   __shared__ double red[4][64];
@@ -309,9 +441,33 @@ int launch_white_resid(hipStream_t s, const WhiteResidArgs& a) {
   return 0;
 }
 
+template <int MAXT>
+static void launch_syrk(hipStream_t s, const WhiteTntArgs& a, int64_t n_sys, size_t lds) {
+  static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (nb = 16)
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_white_syrk<MAXT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sy_lds_bytes(255));
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_white_syrk<MAXT>, dim3((unsigned)(((n_sys + 7) / 8) * 8)), dim3(64 * SY_WAVES), lds, s, a);
+}
+
 int launch_white_tnt(hipStream_t s, const WhiteTntArgs& a) {
   const int nb = (a.m_max + 15) / 16;
   const int64_t n_sys = (int64_t)a.n_psr * a.n_chain;
+  // one-pass batched SYRK for m + 1 <= 256 (tiles per wave by the augmented block count)
+  const int nba = (a.m_max + 1 + 15) / 16;
+  if (nba <= 16) {
+    const int per_wave = (nba * (nba + 1) / 2 + SY_WAVES - 1) / SY_WAVES;
+    const size_t lds = sy_lds_bytes(a.m_max);
+    if (per_wave <= 2) launch_syrk<2>(s, a, n_sys, lds);
+    else if (per_wave <= 4) launch_syrk<4>(s, a, n_sys, lds);
+    else if (per_wave <= 7) launch_syrk<7>(s, a, n_sys, lds);
+    else if (per_wave <= 10) launch_syrk<10>(s, a, n_sys, lds);
+    else if (per_wave <= 14) launch_syrk<14>(s, a, n_sys, lds);
+    else launch_syrk<17>(s, a, n_sys, lds);
+    return 0;
+  }
   hipLaunchKernelGGL(k_white_tnt, dim3((unsigned)n_sys, (unsigned)(nb * (nb + 1) / 2)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_white_tnr, dim3((unsigned)n_sys, (unsigned)((a.m_max + 63) / 64)), dim3(256), 0, s, a);
   return 0;

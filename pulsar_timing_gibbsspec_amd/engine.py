@@ -19,7 +19,10 @@ SUPPORTED_NF = (20, 40, 60)
 
 
 def _t(a, dtype, device):
-    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).to(device)
+    a = np.ascontiguousarray(a)
+    if not a.flags.writeable:          # torch.as_tensor warns on read-only numpy buffers
+        a = a.copy()
+    return torch.as_tensor(a, dtype=dtype).to(device)
 
 
 class DeviceModel:
