@@ -53,8 +53,14 @@ enum {
   GS_OPT_BCAST = 1,   /* b-draw factorisation variant: 0 = lane-row, v_readlane -> SGPR;
                          1 = lane-row, LDS broadcast; 2 = lane-row, v_readlane in batches
                          of 8 SGPR pairs; 3 = 16x16 fp64 MFMA tiles (default) */
-  GS_OPT_PSR_BASE = 2 /* global index of this context's pulsar 0 (Philox counters of a
+  GS_OPT_PSR_BASE = 2, /* global index of this context's pulsar 0 (Philox counters of a
                          pulsar-sharded run); default 0 */
+  GS_OPT_X_PER_SYS = 3 /* 0 (default): x holds one row per chain (a PTA's parameter vector,
+                         pta_gibbs.py); 1: one row per (pulsar, chain) system, row
+                         p * n_chain + c (independent pulsars, each its own
+                         PulsarBlockGibbs, config 5).  Read by gs_white_mh, gs_white_tnt;
+                         with 1, gs_bdraw*'s chain_mask and gs_white_mh's nsteps_chain
+                         are indexed by system too. */
 };
 
 typedef struct gs_ctx gs_ctx;
@@ -121,12 +127,15 @@ int gs_prefix(gs_ctx* ctx, int n_psr, int NF, int NMX, const gs_prefix_desc* des
 /*
  * (a1, a5) Batched b|rho draw: Sigma = TNT + diag(phiinv) -> Cholesky ->
  * b = Sigma^-1 d + L^-T z for n_psr x n_chain systems, one wavefront each.
+ * NF = 20, 40, 60: register tiles; even NF in 66..254 (config 5: 200): tiles in a
+ * workspace the context allocates on first use (NF/16+1)(NF/16+2)/2 * 2 KB per
+ * system; Philox slot j then gives the packed normals 2j, 2j+1 of [z_F | z_M].
  * Replaces PulsarBlockGibbs.update_b (pulsar_gibbs.py:489-520) and
  * PTABlockGibbs.update_b (pta_gibbs.py:512-548).
  * phiinv_F: [n_sys x NF] phiinv of the free-spectrum columns (fidx order);
  * nm: [n_psr] fixed-prior column count; z: [n_sys x ldb] injected normals
  * indexed by ORIGINAL column (NULL: Philox, event `event`, sweep `sweep`);
- * chain_mask: [n_chain] or NULL; systems of chains with mask 0 keep b (the
+ * chain_mask: [n_chain] ([n_sys] under GS_OPT_X_PER_SYS) or NULL; masked systems keep b (the
  * b-update gate, pta_gibbs.py:703).  b: [n_sys x ldb] output in original column order.
  */
 int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,

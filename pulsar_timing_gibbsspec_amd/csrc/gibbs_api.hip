@@ -12,6 +12,9 @@ struct gs_ctx {
   uint64_t seed;
   int bcast;     // GS_OPT_BCAST
   int psr_base;  // GS_OPT_PSR_BASE: global index of this shard's pulsar 0 (RNG counters)
+  int x_per_sys = 0;  // GS_OPT_X_PER_SYS
+  double* ws = nullptr;  // tile workspace of the large-NF b-draw (grown on demand)
+  size_t ws_bytes = 0;
 };
 
 namespace {
@@ -249,6 +252,10 @@ int gs_ctx_create(int device, uint64_t seed, void* stream, gs_ctx** out) {
 }
 
 int gs_ctx_destroy(gs_ctx* ctx) {
+  if (ctx && ctx->ws) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->ws);
+  }
   delete ctx;
   return 0;
 }
@@ -276,6 +283,10 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
       if (value < 0 || value > (1 << 23)) return fail_arg(3, "GS_OPT_PSR_BASE out of range");
       ctx->psr_base = value;
       return 0;
+    case GS_OPT_X_PER_SYS:
+      if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_X_PER_SYS must be 0 or 1");
+      ctx->x_per_sys = value;
+      return 0;
     default:
       return fail_arg(2, "unknown option");
   }
@@ -285,6 +296,7 @@ int gs_ctx_get_option(gs_ctx* ctx, int option) {
   if (!ctx) return -1;
   if (option == GS_OPT_BCAST) return ctx->bcast;
   if (option == GS_OPT_PSR_BASE) return ctx->psr_base;
+  if (option == GS_OPT_X_PER_SYS) return ctx->x_per_sys;
   return -1;
 }
 
@@ -322,7 +334,7 @@ int gs_prefix_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const gs
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_psr < 0) return fail_arg(2, "n_psr < 0");
   if (n_chain < 0) return fail_arg(3, "n_chain < 0");
-  if (NF <= 0 || NF > 64 || (NF & 1)) return fail_arg(4, "NF must be even and <= 64");
+  if (NF <= 0 || NF > 254 || (NF & 1)) return fail_arg(4, "NF must be even and <= 254");
   if (NMX <= 0 || NMX > 64) return fail_arg(5, "NMX must be in 1..64");
   if (!desc) return fail_arg(6, "desc is NULL");
   if (tnt_cstride < 0) return fail_arg(7, "tnt_cstride < 0");
@@ -344,7 +356,7 @@ int gs_prefix(gs_ctx* ctx, int n_psr, int NF, int NMX, const gs_prefix_desc* des
               const double* phiinv_fixed, double* model, int32_t* info) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_psr < 0) return fail_arg(2, "n_psr < 0");
-  if (NF <= 0 || NF > 64 || (NF & 1)) return fail_arg(3, "NF must be even and <= 64");
+  if (NF <= 0 || NF > 254 || (NF & 1)) return fail_arg(3, "NF must be even and <= 254");
   if (NMX <= 0 || NMX > 64) return fail_arg(4, "NMX must be in 1..64");
   if (!desc || !TNT || !d || !fidx || !midx || !phiinv_fixed || !model)
     return fail_arg(5, "NULL array");
@@ -357,11 +369,25 @@ static int bdraw_impl(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
                       const int32_t* chain_mask, double* b, int32_t* info, int per_sys) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
-  if (!nf_supported(NF)) return fail_arg(4, "NF must be one of 20, 40, 60");
+  const bool big = big_nf_supported(NF);
+  if (!nf_supported(NF) && !big) return fail_arg(4, "NF must be 20, 40, 60 or even in 66..254");
   if (NMX <= 0 || NMX > 64) return fail_arg(5, "NMX must be in 1..64");
   if (ldb < NF + 1) return fail_arg(6, "ldb too small");
   if (!model || !fidx || !midx || !nm || !phiinv_F || !b) return fail_arg(7, "NULL array");
   if (n_psr == 0 || n_chain == 0) return 0;
+  if (big) {
+    const size_t need = (size_t)n_psr * n_chain * big_ws_doubles_per_sys(NF) * sizeof(double);
+    if (need > ctx->ws_bytes) {
+      int rc = check_hip(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+      if (rc) return rc;
+      if (ctx->ws) (void)hipFree(ctx->ws);
+      ctx->ws = nullptr;
+      ctx->ws_bytes = 0;
+      rc = check_hip(hipMalloc((void**)&ctx->ws, need), "hipMalloc(b-draw workspace)");
+      if (rc) return rc;
+      ctx->ws_bytes = need;
+    }
+  }
   BdrawArgs a;
   a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.ldb = ldb; a.event = event;
   a.mstride = model_stride_doubles(NF, NMX); a.sweep = sweep; a.chain_base = chain_base;
@@ -369,6 +395,11 @@ static int bdraw_impl(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.phiinv_F = phiinv_F; a.z = z;
   a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = ctx->bcast; a.psr_base = ctx->psr_base;
   a.model_per_sys = per_sys;
+  a.mask_per_sys = ctx->x_per_sys;
+  if (big) {
+    launch_bdraw_big(ctx->stream, a, ctx->ws);
+    return after_launch("k_bdraw_big");
+  }
   if (launch_bdraw(ctx->stream, a)) return fail_arg(4, "unsupported NF");
   return after_launch("k_bdraw");
 }
@@ -573,6 +604,7 @@ int gs_white_mh(gs_ctx* ctx, int n_psr, int n_chain, const gs_white_desc* wdesc,
   if (n_steps < 0) return fail_arg(15, "n_steps < 0");
   if (n_psr == 0 || n_chain == 0) return 0;
   WhiteMhArgs a;
+  a.x_per_sys = ctx->x_per_sys;
   a.n_psr = n_psr; a.n_chain = n_chain; a.ldx = ldx; a.n_steps = n_steps; a.psr_base = ctx->psr_base;
   a.ldy = ldy; a.sweep = sweep; a.chain_base = chain_base;
   a.wdesc = wdesc; a.wcol = wcol; a.wkind = wkind; a.wbk = wbk; a.nsteps_chain = nsteps_chain;
@@ -599,6 +631,7 @@ int gs_white_tnt(gs_ctx* ctx, int n_psr, int n_chain, int m_max, const gs_tnt_de
   if (!TNT || !d) return fail_arg(18, "NULL TNT / d");
   if (n_psr == 0 || n_chain == 0) return 0;
   WhiteTntArgs a;
+  a.x_per_sys = ctx->x_per_sys;
   a.n_psr = n_psr; a.n_chain = n_chain; a.m_max = m_max; a.ldx = ldx;
   a.tnt_cstride = tnt_cstride; a.d_cstride = d_cstride; a.tdesc = tdesc; a.wdesc = wdesc;
   a.wcol = wcol; a.wkind = wkind; a.wbk = wbk; a.bk = bk; a.T = T; a.sigma2 = sigma2; a.r = r; a.x = x;

@@ -203,8 +203,8 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
   // runs, TNT differs per chain) are read from global memory (L2) directly
   if (!A.model_per_sys) stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
   if (c >= A.n_chain) return;
-  if (A.chain_mask && A.chain_mask[c] == 0) return;  // gate closed: keep b
   const int64_t sys = (int64_t)p * A.n_chain + c;
+  if (A.chain_mask && A.chain_mask[A.mask_per_sys ? sys : (int64_t)c] == 0) return;  // gate closed: keep b
   const ModelLds M = A.model_per_sys ? model_view(A.model + sys * A.mstride, NF, A.NMX)
                                      : model_view(lds, NF, A.NMX);
   const int nM = A.nm[p];

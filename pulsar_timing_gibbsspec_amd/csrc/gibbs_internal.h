@@ -20,6 +20,7 @@ inline int64_t model_stride_doubles(int NF, int NMX) {
 struct BdrawArgs {
   int n_psr, n_chain, NF, NMX, ldb, event, bcast, psr_base;
   int model_per_sys;  // 1: model block per (pulsar, chain) system, read from global
+  int mask_per_sys;   // chain_mask indexed by system (GS_OPT_X_PER_SYS)
   int64_t mstride, sweep, chain_base;
   const double* model;
   const int32_t *fidx, *midx, *nm, *chain_mask;
@@ -53,6 +54,10 @@ struct RhoArgs {
 
 int launch_sweep_freespec(hipStream_t s, const SweepArgs& a);
 int launch_bdraw(hipStream_t s, const BdrawArgs& a);
+// large free-spectrum blocks (64 < NF <= 255), tiles in a context-owned workspace
+bool big_nf_supported(int NF);
+int64_t big_ws_doubles_per_sys(int NF);
+int launch_bdraw_big(hipStream_t s, const BdrawArgs& a, double* ws);
 int launch_rho_analytic(hipStream_t s, const RhoArgs& a);
 
 struct TauArgs {
@@ -91,6 +96,7 @@ int launch_pta_gate_phiinv(hipStream_t s, const PtaGateArgs& a);
 
 struct WhiteMhArgs {
   int n_psr, n_chain, ldx, n_steps, psr_base;
+  int x_per_sys;  // GS_OPT_X_PER_SYS
   int64_t ldy, sweep, chain_base;
   const gs_white_desc* wdesc;
   const int32_t *wcol, *wkind, *wbk, *nsteps_chain;
@@ -110,6 +116,7 @@ struct WhiteResidArgs {
 
 struct WhiteTntArgs {
   int n_psr, n_chain, m_max, ldx;
+  int x_per_sys;  // GS_OPT_X_PER_SYS
   int64_t tnt_cstride, d_cstride;
   const gs_tnt_desc* tdesc;
   const gs_white_desc* wdesc;

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(64 * MH_WPB) void k_white_mh(WhiteMhArgs A) {
   const int64_t woff = D->w_off;
   const double* s2 = A.sigma2 + D->toa_off;
   const double* y = A.y + c * A.ldy + D->toa_off;
-  double* x = A.x + (int64_t)c * A.ldx;
+  double* x = A.x + (A.x_per_sys ? sys : (int64_t)c) * A.ldx;
   const int32_t* wcol = A.wcol + woff;
   const int32_t* wkind = A.wkind + woff;
   const int32_t* wbk = A.wbk + woff;
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(64 * MH_WPB) void k_white_mh(WhiteMhArgs A) {
   }
   __builtin_amdgcn_wave_barrier();
 
-  const int steps = A.nsteps_chain ? A.nsteps_chain[c] : A.n_steps;
+  const int steps = A.nsteps_chain ? A.nsteps_chain[A.x_per_sys ? sys : (int64_t)c] : A.n_steps;
   const double sig = 0.05 * nw;  // sigmas = 0.05 * len(wind)  (:376)
   int nacc = 0;
   for (int st = 0; st < steps; ++st) {
@@ -189,7 +189,9 @@ __global__ __launch_bounds__(256) void k_white_resid(WhiteResidArgs A) {
 }
 
 // Per-backend noise values of system (p, c) into LDS (whole workgroup).
-__device__ __forceinline__ void stage_white(const WhiteTntArgs& A, const gs_white_desc& W, int c,
+// xrow: the row of x holding this system's white parameters (chain c, or system
+// p * n_chain + c under GS_OPT_X_PER_SYS)
+__device__ __forceinline__ void stage_white(const WhiteTntArgs& A, const gs_white_desc& W, int64_t xrow,
                                             double* ef2, double* t2, double* tn) {
   const int tid = threadIdx.x;
   if (tid < W.n_bk) {
@@ -202,7 +204,7 @@ __device__ __forceinline__ void stage_white(const WhiteTntArgs& A, const gs_whit
     const int64_t o = W.w_off + tid;
     const int k = A.wbk[o], kind = A.wkind[o];
     double e = 1.0, t = 0.0, q = 0.0;
-    apply_white(kind, A.x[(int64_t)c * A.ldx + A.wcol[o]], e, t, q);
+    apply_white(kind, A.x[xrow * A.ldx + A.wcol[o]], e, t, q);
     if (kind == GS_WHITE_EFAC) ef2[k] = e;
     else if (kind == GS_WHITE_TNEQUAD) tn[k] = q;
     else t2[k] = t;
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(256) void k_white_tnt(WhiteTntArgs A) {
   const gs_white_desc W = A.wdesc[p];
   const int m = (int)D.m;
   if (bi * 16 >= m) return;
-  stage_white(A, W, c, sb[0], sb[1], sb[2]);
+  stage_white(A, W, A.x_per_sys ? sys : (int64_t)c, sb[0], sb[1], sb[2]);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int i = l & 15, k = l >> 4;
   const int ci = bi * 16 + i, cj = bj * 16 + i;
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
   const int p = (int)(sys / A.n_chain), c = (int)(sys % A.n_chain);
   const gs_tnt_desc D = A.tdesc[p];
   const gs_white_desc W = A.wdesc[p];
-  stage_white(A, W, c, sb[0], sb[1], sb[2]);
+  stage_white(A, W, A.x_per_sys ? sys : (int64_t)c, sb[0], sb[1], sb[2]);
   const int m = (int)D.m, nb = (m + 1 + 15) / 16, ld = sy_ld(nb), wcols = 16 * nb;
   const int ntile = nb * (nb + 1) / 2;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, i = l & 15, k = l >> 4;
@@ -405,7 +407,7 @@ __global__ __launch_bounds__(256) void k_white_tnr(WhiteTntArgs A) {
   const int p = (int)(sys / A.n_chain), c = (int)(sys % A.n_chain);
   const gs_tnt_desc D = A.tdesc[p];
   const gs_white_desc W = A.wdesc[p];
-  stage_white(A, W, c, sb[0], sb[1], sb[2]);
+  stage_white(A, W, A.x_per_sys ? sys : (int64_t)c, sb[0], sb[1], sb[2]);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int m = (int)D.m;
   const int j = blockIdx.y * 64 + l;

@@ -15,7 +15,13 @@ import torch
 from . import _lib
 from ._lib import check, ptr
 
-SUPPORTED_NF = (20, 40, 60)
+SUPPORTED_NF = (20, 40, 60)      # register-tile b-draw and the fused sweep kernel
+BIG_NF = (66, 254)               # even NF in this range: workspace-tile b-draw (config 5)
+
+
+def nf_supported(NF):
+    """NF = 2 n_f the b-draw handles (gs_bdraw, gs_bdraw_sys)."""
+    return NF in SUPPORTED_NF or (BIG_NF[0] <= NF <= BIG_NF[1] and NF % 2 == 0)
 
 
 def _t(a, dtype, device):
@@ -40,8 +46,8 @@ class DeviceModel:
         NF = len(fidx_list[0])
         if any(len(f) != NF for f in fidx_list):
             raise ValueError("every pulsar must have the same number of free-spectrum columns")
-        if NF not in SUPPORTED_NF:
-            raise NotImplementedError(f"NF = 2*n_f = {NF}; supported: {SUPPORTED_NF}")
+        if not nf_supported(NF):
+            raise NotImplementedError(f"NF = 2*n_f = {NF}; supported: {SUPPORTED_NF} or even {BIG_NF}")
         self.P, self.NF = P, NF
         self.m = np.array([t.shape[1] for t in T_list], np.int64)
         self.n_toa = np.array([t.shape[0] for t in T_list], np.int64)
@@ -132,6 +138,9 @@ class FreeSpectrumChains:
     """
 
     def __init__(self, model: DeviceModel, rhomin, rhomax, n_chain, x0, chain_base=0):
+        if model.NF not in SUPPORTED_NF:
+            raise NotImplementedError(f"the fused sweep needs NF in {SUPPORTED_NF}; "
+                                      f"NF = {model.NF} runs through gs_bdraw + gs_rho_analytic")
         self.model = model
         self.ctx = model.ctx
         self.n_chain = int(n_chain)

@@ -386,3 +386,55 @@ def array_pta(kind="curn_red", n_f=30, n_psr=None, gw_prior=(-9.0, -4.0), red_pr
                                 log10_A, gamma, red=(-14.5, 3.0) if kind == "curn_red" else None)
         models.append(PulsarModel(n, toas, r, sigs))
     return PTA(models)
+
+
+def config5_array(n_psr=200, n_toa=10_000, n_f=100, n_tm=16, n_bk=4, span_yr=15.0, seed=0,
+                  rho_prior=(-9.0, -4.0), efac_prior=(0.5, 2.0), equad_prior=(-8.5, -5.0),
+                  log10_A=np.log10(2e-15), gamma=13.0 / 3.0):
+    """BASELINE configs[4]: n_psr independent synthetic pulsars, each its own
+    PulsarBlockGibbs model ``ef/equad per backend + gw free spectrum + tm``
+    (SURVEY.md §8d item 5): TOAs uniform over span_yr, sigma log-uniform in
+    [0.05, 5] us, n_bk backends per pulsar (contiguous TOA blocks) with true EFAC in
+    efac_prior and log10 EQUAD in equad_prior, n_f free-spectrum bins (f_k = k/span),
+    an orthonormalised n_tm-column timing model; residuals = power-law red process +
+    white noise.  Basis order [F | M] (signal order white, gw, tm), gwid = 0..2 n_f - 1.
+
+    Parameter vector of every pulsar, sorted by name as enterprise does:
+    ``{psr}_b{k}_efac, {psr}_b{k}_log10_tnequad`` (k = 0..n_bk-1), then
+    ``{psr}_gw_log10_rho`` (n_f) -> white columns 0..2 n_bk - 1, gw columns after.
+    Returns dict with per-pulsar lists T, r, sigma, backend and the shared layout
+    (fidx, phiinv_fixed, white: [(col, kind, backend, pmin, pmax)], gw_cols, n_param,
+    x0 (n_psr, n_param) drawn from the priors, names)."""
+    rng = np.random.default_rng(seed)
+    Tspan = span_yr * 365.25 * DAY
+    T, R, S, B = [], [], [], []
+    for p in range(n_psr):
+        toas = np.sort(rng.uniform(0.0, Tspan, n_toa))
+        sigma = 10 ** rng.uniform(np.log10(0.05e-6), np.log10(5e-6), n_toa)
+        bk = np.minimum((np.arange(n_toa) * n_bk) // n_toa, n_bk - 1).astype(np.int32)
+        F, f = fourier_basis(toas, n_f, Tspan)
+        M = synthetic_design_matrix(toas, n_tm)
+        M, _ = np.linalg.qr(M)
+        ef = rng.uniform(*efac_prior, n_bk)[bk]
+        eq = 10 ** rng.uniform(*equad_prior, n_bk)[bk]
+        sig_w = np.sqrt(ef ** 2 * sigma ** 2 + eq ** 2)
+        r = _simulate_residuals(rng, F, f, Tspan, M, sig_w, log10_A, gamma)
+        T.append(np.ascontiguousarray(np.concatenate([F, M], axis=1)))
+        R.append(r)
+        S.append(sigma)
+        B.append(bk)
+    white, names = [], []
+    for k in range(n_bk):
+        white.append((2 * k, 0, k, *efac_prior))       # efac
+        white.append((2 * k + 1, 1, k, *equad_prior))  # log10_tnequad
+        names += [f"b{k}_efac", f"b{k}_log10_tnequad"]
+    gw_cols = np.arange(2 * n_bk, 2 * n_bk + n_f)
+    names += [f"gw_log10_rho_{i}" for i in range(n_f)]
+    n_param = 2 * n_bk + n_f
+    x0 = np.empty((n_psr, n_param))
+    for col, kind, k, lo, hi in white:
+        x0[:, col] = rng.uniform(lo, hi, n_psr)
+    x0[:, gw_cols] = rng.uniform(*rho_prior, (n_psr, n_f))
+    return dict(T=T, r=R, sigma=S, backend=B, fidx=np.arange(2 * n_f), phiinv_fixed=np.full(n_tm, 1e-40),
+                white=white, gw_cols=gw_cols, n_param=n_param, x0=x0, names=names,
+                rhomin=10 ** (2 * rho_prior[0]), rhomax=10 ** (2 * rho_prior[1]))

@@ -25,7 +25,7 @@ import torch
 from . import _lib
 from ._lib import check, ptr
 from .diagnostics import white_aclength
-from .engine import SUPPORTED_NF, _t
+from .engine import BIG_NF, SUPPORTED_NF, _t, nf_supported
 
 MAX_BK = 15
 MAX_W = 32
@@ -66,8 +66,8 @@ class WhiteNoiseModel:
         NF = len(fidx_list[0])
         if any(len(f) != NF for f in fidx_list):
             raise ValueError("every pulsar must have the same number of free-spectrum columns")
-        if NF not in SUPPORTED_NF:
-            raise NotImplementedError(f"NF = 2*n_f = {NF}; supported: {SUPPORTED_NF}")
+        if not nf_supported(NF):
+            raise NotImplementedError(f"NF = 2*n_f = {NF}; supported: {SUPPORTED_NF} or even {BIG_NF}")
         self.P, self.C, self.NF = P, C, NF
         self.m = np.array([t.shape[1] for t in T_list], np.int64)
         self.n_toa = np.array([t.shape[0] for t in T_list], np.int64)
@@ -277,3 +277,78 @@ class WhiteFreeSpectrumChains:
                  chain_base=self.chain_base, chain_mask=self.gate)  # :698
         self.it += 1
 
+
+
+class WhiteArrayChains:
+    """n_chain chains of each of P independent pulsars, each pulsar its own
+    PulsarBlockGibbs (white-noise MH + analytic free spectrum): config 5.
+
+    The (pulsar, chain) systems are independent, so x is laid out one row per system,
+    x (P * n_chain, n_param) with row p * n_chain + c (GS_OPT_X_PER_SYS on the
+    context, which this engine then owns), b (P * n_chain, ldb) in original column
+    order.  Every pulsar has the same parameter layout: gw_cols the n_f log10_rho
+    columns (contiguous), the white columns given to the WhiteNoiseModel.
+
+    Per sweep, all systems at once (pulsar_gibbs.py:656-698 steady state):
+    record -> [ii == 0: TNT, prefix, b from x0] -> y = r - T b -> aclength white MH
+    steps -> rho|b -> gate -> TNT_c, d_c (batched SYRK) + prefix -> gated b|rho.
+    The reference's 1000-step warm-up (acor) is replaced by a given aclength.
+    """
+
+    def __init__(self, wm: WhiteNoiseModel, n_param, gw_cols, rhomin, rhomax, x0, aclength, chain_base=0):
+        self.wm, self.ctx = wm, wm.ctx
+        dev = self.ctx.device
+        self.ctx.set_option(_lib.OPT_X_PER_SYS, 1)
+        self.P, self.C = wm.P, wm.C
+        self.n_sys = wm.P * wm.C
+        self.n_param = int(n_param)
+        self.n_f = wm.NF // 2
+        gw_cols = np.asarray(gw_cols, np.int64)
+        if not np.array_equal(gw_cols, gw_cols[0] + np.arange(self.n_f)):
+            raise NotImplementedError("log10_rho columns must be contiguous in x")
+        self.gw0 = int(gw_cols[0])
+        self.gw_col = _t(gw_cols.astype(np.int32), torch.int32, dev)
+        self.rhomin, self.rhomax = float(rhomin), float(rhomax)
+        self.chain_base = int(chain_base)
+        self.aclength = int(aclength)
+        self.x = _t(np.broadcast_to(np.asarray(x0, float), (self.n_sys, self.n_param)), torch.float64, dev)
+        self.b = torch.zeros(self.n_sys, wm.ldb, dtype=torch.float64, device=dev)
+        self.phiinv_F = torch.empty(self.n_sys, wm.NF, dtype=torch.float64, device=dev)
+        self.gate = torch.ones(self.n_sys, dtype=torch.int32, device=dev)
+        self.xlast = torch.empty(self.n_sys, dtype=torch.float64, device=dev)
+        self.info = torch.zeros(self.n_sys, dtype=torch.int32, device=dev)
+        self.n_acc = torch.zeros(self.n_sys, dtype=torch.int32, device=dev)
+        self.it = 0
+
+    def _gate_phiinv(self, with_gate):
+        check(self.ctx.lib.gs_pta_gate_phiinv(
+            self.ctx.handle, 1, self.n_sys, self.n_f, self.n_param, ptr(self.x),
+            ptr(self.xlast) if with_gate else None, ptr(self.gw_col), None,
+            ptr(self.phiinv_F), ptr(self.gate)), "gs_pta_gate_phiinv")
+
+    def sweep(self, x_rec=None, b_rec=None, z0=None, z=None, u=None, mh_inj=None):
+        """One sweep of every system.  Injected draws (parity mode): z0/z (n_sys, ldb),
+        u (n_sys, n_f), mh_inj (aclength, n_sys, 4)."""
+        wm, lib, h = self.wm, self.ctx.lib, self.ctx.handle
+        ii = self.it
+        check(lib.gs_pta_record(h, self.n_sys, self.n_param, ptr(self.x), ptr(x_rec), ptr(self.xlast)),
+              "gs_pta_record")                                     # pulsar_gibbs.py:658
+        if b_rec is not None:
+            b_rec.copy_(self.b)                                    # :659
+        if ii == 0:                                                # :661-662
+            wm.refresh(self.x, self.n_param)
+            self._gate_phiinv(with_gate=False)
+            wm.bdraw(self.phiinv_F, self.b, self.info, z=z0, sweep=ii, event=_lib.EV_B0,
+                     chain_base=self.chain_base)
+        wm.resid(self.b)                                           # :534-535
+        wm.mh(self.x, self.n_param, self.aclength, ii, self.chain_base, inj=mh_inj,
+              n_acc=self.n_acc)                                    # :373-404
+        check(lib.gs_rho_analytic(h, self.P, self.C, wm.NF, wm.ldb, ptr(wm.fidx), ptr(self.b), ptr(u), ii,
+                                  self.chain_base, self.rhomin, self.rhomax,
+                                  ctypes.c_void_p(self.x.data_ptr() + 8 * self.gw0), self.n_param),
+              "gs_rho_analytic")                                   # :206-216, 236
+        self._gate_phiinv(with_gate=True)                          # :697
+        wm.refresh(self.x, self.n_param)
+        wm.bdraw(self.phiinv_F, self.b, self.info, z=z, sweep=ii, event=_lib.EV_B,
+                 chain_base=self.chain_base, chain_mask=self.gate)  # :698
+        self.it += 1
