@@ -185,6 +185,112 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx):
                 chains_per_gpu=C, n_psr=len(T), n_param=len(names))
 
 
+def config5_cpu_baseline(seconds=10.0):
+    """The oracle's restatement of one PulsarBlockGibbs sweep with white noise
+    (pulsar_gibbs.py:656-698: TNT, SVD draw, aclength=20 white MH steps each recomputing
+    r - T b and the white likelihood as :523-546 does, analytic rho) on ONE pulsar of the
+    config-5 array (10^4 TOAs, m = 216), 1 thread; reported as array sweeps/s = 1 /
+    (200 x the per-pulsar sweep time)."""
+    from oracle import gibbs_oracle as O
+    from pulsar_timing_gibbsspec_amd import synthetic
+    d = synthetic.config5_array(n_psr=1, seed=1)
+    T, r, sig, bk = d["T"][0], d["r"][0], d["sigma"][0], d["backend"][0]
+    rng = np.random.default_rng(0)
+    x = d["x0"][0].copy()
+    gw = d["gw_cols"]
+    wind = [w[0] for w in d["white"]]
+    nb = len(wind) // 2
+    lo = np.array([w[3] for w in d["white"]])
+    hi = np.array([w[4] for w in d["white"]])
+    m = T.shape[1]
+    n_tm = m - 2 * gw.size
+
+    def N_of(xx):
+        return O.ndiag_white(sig, bk, xx[[2 * k for k in range(nb)]], xx[[2 * k + 1 for k in range(nb)]])
+    b = np.zeros(m)
+    it, t0 = 0, time.perf_counter()
+    while True:
+        N = N_of(x)
+        TNT, dd = O.tnt(T, N, r)
+        ph = np.full(m, 1e-40)
+        ph[:gw.size * 2] = 1 / np.repeat(10 ** (2 * x[gw]), 2)
+        b = O.bdraw_svd(TNT, dd, ph, rng.standard_normal(m))
+        ll0 = O.lnlike_white(r, T, b, N_of(x))
+        for _ in range(20):
+            q = x.copy()
+            j = rng.integers(len(wind))
+            q[wind[j]] += rng.standard_normal() * 0.05 * len(wind) * rng.choice([0.1, 0.5, 1, 3, 10])
+            if lo[j] <= q[wind[j]] <= hi[j]:
+                ll1 = O.lnlike_white(r, T, b, N_of(q))
+                if ll1 - ll0 > np.log(rng.random()):
+                    x, ll0 = q, ll1
+        tau = O.tau_half(b, np.arange(2 * gw.size))
+        x[gw] = 0.5 * np.log10(O.rho_analytic(tau, rng.random(gw.size), d["rhomin"], d["rhomax"]))
+        it += 1
+        el = time.perf_counter() - t0
+        if el > seconds:
+            break
+    per_psr = el / it
+    return dict(value=1.0 / (200 * per_psr), unit="iters/s", cores=1, kind="port",
+                sample=f"{it} single-pulsar sweeps (10^4 TOAs, m={m}, n_tm={n_tm}, 20 white MH steps) of the "
+                       f"oracle restatement of pulsar_gibbs.py:656-698 + :373-404 in {el:.1f} s, "
+                       f"{per_psr * 1e3:.0f} ms/pulsar, scaled to the 200-pulsar array")
+
+
+def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, aclength=20, reps=5):
+    """BASELINE configs[4]: n_psr independent pulsars x C chains per GPU, white-noise MH
+    (aclength steps) forcing the per-chain TNT (batched SYRK) every sweep."""
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd.white import WhiteArrayChains, WhiteNoiseModel
+    d = synthetic.config5_array(n_psr=n_psr, n_toa=n_toa, n_f=n_f, seed=0)
+    ctx = _lib.Context(dev.index, seed=20251016)
+    ctx.set_option(_lib.OPT_X_PER_SYS, 1)
+    wm = WhiteNoiseModel(ctx, d["T"], d["r"], d["sigma"], d["backend"], [d["fidx"]] * n_psr,
+                         [d["phiinv_fixed"]] * n_psr, [d["white"]] * n_psr, C)
+    m = int(wm.m[0])
+    del d["T"]
+    eng = WhiteArrayChains(wm, d["n_param"], d["gw_cols"], d["rhomin"], d["rhomax"],
+                           np.repeat(d["x0"], C, axis=0), aclength=aclength, chain_base=rank * C)
+    for _ in range(W):
+        eng.sweep()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        eng.sweep()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if eng.info.cpu().numpy().any() or int(wm.pinfo.abs().sum()):
+        raise RuntimeError("non-PD system in the config-5 bench")
+    # the dominant kernel: gs_white_tnt (k_white_syrk), timed alone on the ctx stream
+    stream = ctx.stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        wm.refresh(eng.x, eng.n_param)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    refresh_ms = e0.elapsed_time(e1) / reps
+    n_sys = n_psr * C
+    flops = n_sys * (n_toa * m * (m + 1) + 2 * n_toa * m)      # SURVEY 8(d): SYRK + TNr per system
+    tflops = flops / (refresh_ms * 1e-3) / 1e12
+    return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+                chains_per_gpu=C, n_psr=n_psr, n_toa=n_toa, m=m, aclength=aclength,
+                roofline={"bound": "mfma", "kernel": "k_white_syrk + k_prefix (gs_white_tnt + gs_prefix_sys)",
+                          "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": tflops / FP64_PEAK_TFLOPS, "kernel_avg_ms": refresh_ms,
+                          "alg_flops_per_launch": flops,
+                          "note": "per-chain TNT/d of all 200 pulsars (n m (m+1) + 2 n m flop per system) "
+                                  "over the HIP-event time of one refresh (SYRK + prefix)"})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -199,6 +305,9 @@ def main():
                     "curn | curn_red | none")
     ap.add_argument("--pta-chains", type=int, default=256)
     ap.add_argument("--pta-steps", type=int, default=20)
+    ap.add_argument("--config5", type=int, default=1, help="measure BASELINE configs[4] too (1/0)")
+    ap.add_argument("--c5-chains", type=int, default=16)
+    ap.add_argument("--c5-steps", type=int, default=5)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -305,7 +414,15 @@ def main():
                             "free spectrum, chain-sharded"
             if not args.no_cpu_baseline:
                 sec["cpu_baseline"] = pta_cpu_baseline(args.pta, args.cpu_seconds)
-            out["secondary"] = {args.pta: sec}
+            out.setdefault("secondary", {})[args.pta] = sec
+    if args.config5:
+        sec = bench_config5(args.c5_chains, args.c5_steps, 1, rank, world, dev)
+        if rank == 0:
+            sec["config"] = ("configs[4]: 200 synthetic pulsars x 10^4 TOAs x 100 frequencies (m=216), "
+                             "white-noise MH (20 steps) + per-chain TNT recompute every sweep, chain-sharded")
+            if not args.no_cpu_baseline:
+                sec["cpu_baseline"] = config5_cpu_baseline(args.cpu_seconds)
+            out.setdefault("secondary", {})["config5"] = sec
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
