@@ -282,10 +282,17 @@ constexpr int SY_TC = 16;
 
 __host__ __device__ constexpr int sy_ld(int nb) { return 16 * nb + ((nb & 1) ? 0 : 16); }
 
-template <int MAXT>
+// Tile ownership: block rows are paired (w, NB-1-w), so wave w owns the lower tiles
+// (w, 0..w) and (NB-1-w, 0..NB-1-w): NB+1 tiles, one scaled A operand per row and one
+// B operand per block column per 4-TOA step shared by both rows (NB+2 LDS reads and 2
+// multiplies per NB+1 MFMAs).  The wave index is made uniform (readfirstlane) so the
+// ownership tests are scalar branches and the MFMAs issue back to back.
+template <int NB>
 __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
   extern __shared__ double lds[];
   __shared__ double sb[3][GS_WHITE_MAX_BK + 1];
+  constexpr int NH = (NB + 1) / 2;  // waves with tiles
+  constexpr int LDC = sy_ld(NB), WC = 16 * NB;
   const int64_t n_sys = (int64_t)A.n_psr * A.n_chain;
   // XCD-major: consecutive workgroup ids go round-robin over the 8 XCDs
   const int64_t per = (n_sys + 7) / 8;
@@ -295,34 +302,29 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
   const gs_tnt_desc D = A.tdesc[p];
   const gs_white_desc W = A.wdesc[p];
   stage_white(A, W, A.x_per_sys ? sys : (int64_t)c, sb[0], sb[1], sb[2]);
-  const int m = (int)D.m, nb = (m + 1 + 15) / 16, ld = sy_ld(nb), wcols = 16 * nb;
-  const int ntile = nb * (nb + 1) / 2;
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, i = l & 15, k = l >> 4;
+  const int m = (int)D.m;
+  const int tid = threadIdx.x, l = tid & 63, i = l & 15, k = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r1 = w, r2 = NB - 1 - w;  // owned block rows (r1 <= r2 for w < NH)
+  const bool act = w < NH;
+  const bool two = act && r2 != r1;
   const int64_t n = D.n_toa;
   const double* Tp = A.T + D.T_off;
   const double* rp = A.r + D.toa_off;
   const double* s2 = A.sigma2 + D.toa_off;
   const int32_t* bk = A.bk + D.toa_off;
   double* buf0 = lds;
-  double* buf1 = lds + SY_TC * ld + SY_TC;  // [SY_TC x ld] chunk + SY_TC inverse N
+  double* buf1 = lds + SY_TC * LDC + SY_TC;  // [SY_TC x LDC] chunk + SY_TC inverse N
 
-  int ti[MAXT], tj[MAXT];
-  gs_d4_t acc[MAXT];
+  // NB + 1 accumulator slots: tile (r2, j) in slot j (j <= r2), tile (r1, j) in slot
+  // NB - j (j <= r1 < r2): disjoint, and both slot indices are static in the j loop
+  gs_d4_t acc[NB + 1];
 #pragma unroll
-  for (int j = 0; j < MAXT; ++j) {
-    const int tl = w + SY_WAVES * j;
-    int bi = (int)((sqrt(8.0 * tl + 1.0) - 1.0) * 0.5);
-    while ((bi + 1) * (bi + 2) / 2 <= tl) ++bi;
-    while (bi * (bi + 1) / 2 > tl) --bi;
-    ti[j] = (tl < ntile) ? bi : -1;
-    tj[j] = tl - bi * (bi + 1) / 2;
-    acc[j] = gs_d4_t{0.0, 0.0, 0.0, 0.0};
-  }
+  for (int j = 0; j <= NB; ++j) acc[j] = gs_d4_t{0.0, 0.0, 0.0, 0.0};
 
   // chunk loader: thread tid owns column tid & 255 of rows (tid >> 8) + 2 e, e < 8
-  // (coalesced along the row; no index division)
   const int lcol = tid & 255, lrow = tid >> 8;
-  const bool colok = lcol < wcols;
+  const bool colok = lcol < WC;
   double reg[SY_TC / 2];
   double rinv = 0.0;
   auto load = [&](int64_t t0) {
@@ -345,8 +347,8 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
   auto store = [&](double* b) {
     if (colok)
 #pragma unroll
-      for (int e = 0; e < SY_TC / 2; ++e) b[(lrow + 2 * e) * ld + lcol] = reg[e];
-    if (tid < SY_TC) b[SY_TC * ld + tid] = rinv;
+      for (int e = 0; e < SY_TC / 2; ++e) b[(lrow + 2 * e) * LDC + lcol] = reg[e];
+    if (tid < SY_TC) b[SY_TC * LDC + tid] = rinv;
   };
 
   const int64_t nch = (n + SY_TC - 1) / SY_TC;
@@ -354,36 +356,41 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
   store(buf0);
   __syncthreads();
   for (int64_t ch = 0; ch < nch; ++ch) {
-    double* cur = (ch & 1) ? buf1 : buf0;
+    const double* cur = (ch & 1) ? buf1 : buf0;
     double* nxt = (ch & 1) ? buf0 : buf1;
     if (ch + 1 < nch) load((ch + 1) * SY_TC);
+    // keep the next chunk's global loads here, ahead of the MFMAs: their latency is
+    // hidden behind this chunk's math (the scheduler would otherwise sink them)
+    __builtin_amdgcn_sched_barrier(0);
+    if (act) {
 #pragma unroll
-    for (int kk = 0; kk < SY_TC / 4; ++kk) {
-      const int tr = 4 * kk + k;
-      const double* row = cur + tr * ld;
-      const double iv = cur[SY_TC * ld + tr];
+      for (int kk = 0; kk < SY_TC / 4; ++kk) {
+        const double* row = cur + (4 * kk + k) * LDC + i;
+        const double iv = cur[SY_TC * LDC + 4 * kk + k];
+        const double a1 = row[16 * r1] * iv;
+        const double a2 = row[16 * r2] * iv;
+        double bv[NB];  // every B operand of the step in flight at once
 #pragma unroll
-      for (int j = 0; j < MAXT; ++j) {
-        if (ti[j] >= 0) {
-          const double a = row[ti[j] * 16 + i] * iv;
-          const double b = row[tj[j] * 16 + i];
-          acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[j], 0, 0, 0);
+        for (int j = 0; j < NB; ++j) bv[j] = row[16 * j];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          if (j <= r2) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, bv[j], acc[j], 0, 0, 0);
+          if (two && j <= r1) acc[NB - j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bv[j], acc[NB - j], 0, 0, 0);
         }
       }
     }
     if (ch + 1 < nch) store(nxt);
     __syncthreads();
   }
+  if (!act) return;
 
   double* out = A.TNT + D.tnt_off + (int64_t)c * A.tnt_cstride;
   double* dout = A.d + D.d_off + (int64_t)c * A.d_cstride;
-#pragma unroll
-  for (int j = 0; j < MAXT; ++j) {
-    if (ti[j] < 0) continue;
+  auto emit = [&](int bi, int bj, const gs_d4_t v4) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = ti[j] * 16 + k + 4 * r, col = tj[j] * 16 + i;
-      const double v = acc[j][r];
+      const int row = bi * 16 + k + 4 * r, col = bj * 16 + i;
+      const double v = v4[r];
       if (row < m && col < m) {
         out[(int64_t)row * m + col] = v;
         out[(int64_t)col * m + row] = v;
@@ -391,12 +398,12 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
         dout[col] = v;
       }
     }
+  };
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    if (j <= r2) emit(r2, j, acc[j]);
+    if (two && j <= r1) emit(r1, j, acc[NB - j]);
   }
-}
-
-size_t sy_lds_bytes(int m_max) {
-  const int nb = (m_max + 1 + 15) / 16;
-  return (size_t)2 * (SY_TC * sy_ld(nb) + SY_TC) * sizeof(double);
 }
 
 // d_c = T^T (r / N_c): grid (n_sys, ceil(m_max / 64)).
@@ -443,31 +450,41 @@ int launch_white_resid(hipStream_t s, const WhiteResidArgs& a) {
   return 0;
 }
 
-template <int MAXT>
-static void launch_syrk(hipStream_t s, const WhiteTntArgs& a, int64_t n_sys, size_t lds) {
-  static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (nb = 16)
+template <int NB>
+static void launch_syrk(hipStream_t s, const WhiteTntArgs& a, int64_t n_sys) {
+  static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (NB = 16)
+  const size_t lds = (size_t)2 * (SY_TC * sy_ld(NB) + SY_TC) * sizeof(double);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_white_syrk<MAXT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sy_lds_bytes(255));
+    (void)hipFuncSetAttribute((const void*)k_white_syrk<NB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL(k_white_syrk<MAXT>, dim3((unsigned)(((n_sys + 7) / 8) * 8)), dim3(64 * SY_WAVES), lds, s, a);
+  hipLaunchKernelGGL(k_white_syrk<NB>, dim3((unsigned)(((n_sys + 7) / 8) * 8)), dim3(64 * SY_WAVES), lds, s, a);
 }
 
 int launch_white_tnt(hipStream_t s, const WhiteTntArgs& a) {
   const int nb = (a.m_max + 15) / 16;
   const int64_t n_sys = (int64_t)a.n_psr * a.n_chain;
-  // one-pass batched SYRK for m + 1 <= 256 (tiles per wave by the augmented block count)
+  // one-pass batched SYRK for m + 1 <= 256 (block count of the r-augmented T)
   const int nba = (a.m_max + 1 + 15) / 16;
   if (nba <= 16) {
-    const int per_wave = (nba * (nba + 1) / 2 + SY_WAVES - 1) / SY_WAVES;
-    const size_t lds = sy_lds_bytes(a.m_max);
-    if (per_wave <= 2) launch_syrk<2>(s, a, n_sys, lds);
-    else if (per_wave <= 4) launch_syrk<4>(s, a, n_sys, lds);
-    else if (per_wave <= 7) launch_syrk<7>(s, a, n_sys, lds);
-    else if (per_wave <= 10) launch_syrk<10>(s, a, n_sys, lds);
-    else if (per_wave <= 14) launch_syrk<14>(s, a, n_sys, lds);
-    else launch_syrk<17>(s, a, n_sys, lds);
+    switch (nba) {
+      case 1: launch_syrk<1>(s, a, n_sys); break;
+      case 2: launch_syrk<2>(s, a, n_sys); break;
+      case 3: launch_syrk<3>(s, a, n_sys); break;
+      case 4: launch_syrk<4>(s, a, n_sys); break;
+      case 5: launch_syrk<5>(s, a, n_sys); break;
+      case 6: launch_syrk<6>(s, a, n_sys); break;
+      case 7: launch_syrk<7>(s, a, n_sys); break;
+      case 8: launch_syrk<8>(s, a, n_sys); break;
+      case 9: launch_syrk<9>(s, a, n_sys); break;
+      case 10: launch_syrk<10>(s, a, n_sys); break;
+      case 11: launch_syrk<11>(s, a, n_sys); break;
+      case 12: launch_syrk<12>(s, a, n_sys); break;
+      case 13: launch_syrk<13>(s, a, n_sys); break;
+      case 14: launch_syrk<14>(s, a, n_sys); break;
+      case 15: launch_syrk<15>(s, a, n_sys); break;
+      default: launch_syrk<16>(s, a, n_sys); break;
+    }
     return 0;
   }
   hipLaunchKernelGGL(k_white_tnt, dim3((unsigned)n_sys, (unsigned)(nb * (nb + 1) / 2)), dim3(256), 0, s, a);
