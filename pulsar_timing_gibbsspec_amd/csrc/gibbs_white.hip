@@ -278,7 +278,7 @@ __global__ __launch_bounds__(256) void k_white_tnt(WhiteTntArgs A) {
 // layout).  Workgroups are mapped XCD-major so the chains of one pulsar share an
 // XCD's L2 for T.  Roofline: fp64 MFMA (n m^2 flop per system against 8 n m bytes).
 constexpr int SY_WAVES = 8;
-constexpr int SY_TC = 16;
+constexpr int SY_TC = 32;
 
 __host__ __device__ constexpr int sy_ld(int nb) { return 16 * nb + ((nb & 1) ? 0 : 16); }
 
