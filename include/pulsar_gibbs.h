@@ -194,6 +194,20 @@ int gs_rho_curn(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau,
                 int ngrid, const double* grid3, const double* u, int64_t sweep, int64_t chain_base,
                 double* x, int ldx, const int32_t* xcol, int32_t* idx_out);
 /*
+ * (a6, sufficient statistic) CURN without per-pulsar red noise: the common pdf depends on
+ * tau only through S[k][c] = sum_p tau[p][k][c] (pta_gibbs.py:194-205 with irn = 0), so a
+ * pulsar-sharded run all-reduces S instead of gathering tau.
+ * gs_tau_sum: S [n_f x n_chain] = sum over the n_psr local pulsars (sequential order).
+ * gs_rho_curn_sum: the grid-CDF draw of pta_gibbs.py:181-214 from S and the GLOBAL
+ * pulsar count n_psr, in log space (log pdf = -n_psr log rho_g - S / (2 rho_g));
+ * equal to gs_rho_curn up to pdf rounding (1e-15 relative).  ngrid <= 2048.
+ */
+int gs_tau_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, double* S);
+int gs_rho_curn_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* S, int ngrid,
+                    const double* grid3, const double* u, int64_t sweep, int64_t chain_base, double* x,
+                    int ldx, const int32_t* xcol, int32_t* idx_out);
+
+/*
  * (a7) per-pulsar red free spectrum conditioned on phi_gw (pta_gibbs.py:252-276):
  *   tau [n_psr x n_f x n_chain], gw [n_f x n_chain] = phi_gw of the sin columns,
  *   u [n_chain x n_psr x n_f] or NULL (Philox GS_EV_RED); xcol [n_psr x n_f].

@@ -176,6 +176,20 @@ def rho_grid_cdf_curn(tau, irn, U, rhomin, rhomax):
     return np.take_along_axis(rho_tmp, idx, axis=0), idx
 
 
+def rho_grid_cdf_curn_sum(S, n_psr, U, rhomin, rhomax):
+    """The CURN grid-CDF draw without intrinsic red noise from the sufficient statistic
+    S_k = sum_p tau_p,k (pta_gibbs.py:194-212 with irn = 0): prod_p ratio e^(-ratio/2)
+    ln10 = const * rho^-P e^(-S/(2 rho)); the constant cancels in cdf / max.  Log space,
+    relative to the row maximum.  S, U: (n_f,)."""
+    rho_tmp = rho_grid(rhomin, rhomax)
+    lp = -n_psr * np.log(rho_tmp)[None, :] - np.asarray(S)[:, None] / (2.0 * rho_tmp[None, :])
+    pdf = np.exp(lp - lp.max(axis=1)[:, None])
+    cdf = np.cumsum(pdf, axis=1)
+    cdf /= cdf.max(axis=1)[:, None]
+    idx = _cdf_index(cdf, U)
+    return np.take_along_axis(rho_tmp, idx, axis=0), idx
+
+
 def rho_grid_cdf_red(tau, gw, U, rhomin, rhomax):
     """Per-pulsar red free spectrum, grid CDF conditioned on the common phi_gw
     (pta_gibbs.py:254-276).  tau, U: (P, n_f); gw: (n_f,)."""

@@ -50,6 +50,8 @@ SIGNATURES = {
     "gs_tau": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _P]),
     "gs_rho_curn": (_I, [_P, _I, _I, _I, _P, _P, _I, _P, _P, _I64, _I64, _P, _I, _P, _P]),
     "gs_rho_red": (_I, [_P, _I, _I, _I, _P, _P, _I, _P, _P, _I64, _I64, _P, _I, _P, _P]),
+    "gs_tau_sum": (_I, [_P, _I, _I, _I, _P, _P]),
+    "gs_rho_curn_sum": (_I, [_P, _I, _I, _I, _P, _I, _P, _P, _I64, _I64, _P, _I, _P, _P]),
     "gs_rho_gumbel": (_I, [_P, _I, _I, _P, _P, _I, _P, _P, _I64, _I64, _P, _I, _P, _P]),
     "gs_phi_from_x": (_I, [_P, _I, _I, _P, _I, _P, _P]),
     "gs_pta_record": (_I, [_P, _I, _I, _P, _P, _P]),

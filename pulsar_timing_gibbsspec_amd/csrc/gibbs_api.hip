@@ -524,6 +524,26 @@ int gs_rho_curn(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau,
   return after_launch("k_rho_curn");
 }
 
+int gs_tau_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, double* S) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0 || n_f < 0) return fail_arg(2, "negative batch");
+  if (!tau || !S) return fail_arg(5, "NULL tau / S");
+  launch_tau_sum(ctx->stream, n_psr, (int64_t)n_f * n_chain, tau, S);
+  return after_launch("k_tau_sum");
+}
+
+int gs_rho_curn_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* S, int ngrid,
+                    const double* grid3, const double* u, int64_t sweep, int64_t chain_base, double* x,
+                    int ldx, const int32_t* xcol, int32_t* idx_out) {
+  if (ngrid > 64 * 32) return fail_arg(6, "ngrid > 2048");
+  GridArgs a;
+  int rc = grid_common(ctx, a, n_psr, n_chain, n_f, S, nullptr, ngrid, grid3, u, sweep, chain_base, x, ldx,
+                       xcol, idx_out);
+  if (rc) return rc;
+  launch_rho_curn_sum(ctx->stream, a);
+  return after_launch("k_rho_curn_sum");
+}
+
 int gs_rho_red(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, const double* gw,
                int ngrid, const double* grid3, const double* u, int64_t sweep, int64_t chain_base,
                double* x, int ldx, const int32_t* xcol, int32_t* idx_out) {

@@ -122,6 +122,87 @@ __global__ __launch_bounds__(64 * GS_CURN_WPB) void k_rho_curn(GridArgs A) {
   }
 }
 
+// ------------------------------------------------------------ a6': CURN from tau sums
+// Without per-pulsar red noise the common pdf depends on tau only through
+// S_k = sum_p tau_p,k: prod_p (tau_p/rho) e^(-tau_p/(2 rho)) ln10 = const * rho^-P
+// e^(-S/(2 rho)), and the constant cancels in cdf / max.  So a pulsar-sharded run
+// exchanges S (one all-reduce of n_f x n_chain doubles) instead of every tau, and the
+// draw is O(1) per grid point: log pdf = -P log rho_g - S / (2 rho_g), evaluated
+// against its maximum (no underflow for any P).  Same draw as k_rho_curn up to
+// rounding of the pdf (1e-15 relative: an index can only differ when u falls within
+// that of a cdf value).  One wavefront per row; lane l owns the contiguous grid
+// points [l G, (l+1) G), G = ceil(ngrid / 64); wave scan of the lane sums.
+__global__ __launch_bounds__(256) void k_tau_sum(int n_psr, int64_t nrow, const double* tau, double* S) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrow) return;
+  double s = 0.0;
+  for (int p = 0; p < n_psr; ++p) s += tau[p * nrow + r];  // sequential in pulsar order
+  S[r] = s;
+}
+
+constexpr int CS_MAXG = 32;  // grid points per lane (ngrid <= 2048)
+
+__global__ __launch_bounds__(256) void k_rho_curn_sum(GridArgs A) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t nrow = (int64_t)A.n_f * A.n_chain;
+  if (r >= nrow) return;
+  const int c = (int)(r % A.n_chain), k = (int)(r / A.n_chain);
+  const double S = A.tau[r];
+  const double P = (double)A.n_psr;
+  const int G = (A.ngrid + 63) / 64;
+  const int g0 = lane * G;
+  double lp[CS_MAXG];
+  double mx = -__builtin_inf();
+#pragma unroll
+  for (int j = 0; j < CS_MAXG; ++j) {
+    const int g = g0 + j;
+    lp[j] = -__builtin_inf();
+    if (j < G && g < A.ngrid) {
+      lp[j] = -P * A.grid3[A.ngrid + g] - S / (2.0 * A.grid3[g]);
+      mx = fmax(mx, lp[j]);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+  double loc = 0.0;  // this lane's cumulative sums, kept in lp[]
+#pragma unroll
+  for (int j = 0; j < CS_MAXG; ++j) {
+    if (j < G) {
+      loc += exp(lp[j] - mx);  // exp(-inf) = 0 past the grid
+      lp[j] = loc;
+    }
+  }
+  // inclusive wave scan of the lane totals
+  double incl = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  const double off = incl - loc;
+  const double total = __shfl(incl, 63);
+  double u;
+  if (A.u) {
+    u = A.u[(int64_t)c * A.n_f + k];
+  } else {
+    double u2;
+    gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, 0, GS_EV_CURN), A.key, u, u2);
+  }
+  int cnt = 0;  // searchsorted(cdf / total, u, 'left'): points with cdf / total < u
+#pragma unroll
+  for (int j = 0; j < CS_MAXG; ++j)
+    if (j < G && g0 + j < A.ngrid) cnt += ((off + lp[j]) / total < u) ? 1 : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if (lane == 0) {
+    int idx = cnt - 1;
+    if (idx < 0) idx += A.ngrid;
+    if (A.idx_out) A.idx_out[r] = idx;
+    A.x[(int64_t)c * A.ldx + A.xcol[k]] = A.grid3[2 * A.ngrid + idx];
+  }
+}
+
 // ------------------------------------------------------------ a7: red CDF
 // rows r = (p * n_f + k) * n_chain + c, one LANE per row; gw [n_f][n_chain] = phi_gw.
 // One pass over the grid keeps the (sequential, exact) running sum at 16 chunk
@@ -278,6 +359,19 @@ int launch_rho_curn(hipStream_t s, const GridArgs& a) {
   if (n == 0) return 0;
   const size_t lds = (size_t)GS_CURN_WPB * a.ngrid * sizeof(double);
   hipLaunchKernelGGL(k_rho_curn, grid1(n, GS_CURN_WPB), dim3(64 * GS_CURN_WPB), lds, s, a);
+  return 0;
+}
+
+int launch_tau_sum(hipStream_t s, int n_psr, int64_t nrow, const double* tau, double* S) {
+  if (nrow == 0) return 0;
+  hipLaunchKernelGGL(k_tau_sum, grid1(nrow, 256), dim3(256), 0, s, n_psr, nrow, tau, S);
+  return 0;
+}
+
+int launch_rho_curn_sum(hipStream_t s, const GridArgs& a) {
+  const int64_t n = (int64_t)a.n_f * a.n_chain;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_rho_curn_sum, grid1(n, 4), dim3(256), 0, s, a);
   return 0;
 }
 

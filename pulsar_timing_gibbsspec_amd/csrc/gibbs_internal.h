@@ -77,6 +77,9 @@ struct GridArgs {
   gs_key key;
 };
 
+int launch_tau_sum(hipStream_t s, int n_psr, int64_t nrow, const double* tau, double* S);
+int launch_rho_curn_sum(hipStream_t s, const GridArgs& a);
+
 struct PtaGateArgs {
   int n_psr, n_chain, n_f, n_param;
   const double *x, *xlast;

@@ -90,6 +90,21 @@ class PulsarAllGather:
         return res
 
 
+class TauSumAllReduce:
+    """The CURN exchange without per-pulsar red noise: each rank holds the partial sums
+    S_k = sum over its pulsars of tau_p,k [n_f, n_chain]; one all-reduce (RCCL over xGMI
+    for backend 'nccl') leaves the global sums on every rank, identical on all ranks, so
+    every rank draws the common rho from the same Philox counters (north_star: the only
+    collective of the CURN config)."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def __call__(self, partial):
+        dist.all_reduce(partial, op=dist.ReduceOp.SUM, group=self.group)
+        return partial
+
+
 def max_over_ranks(value, device="cpu"):
     """Max of a float over ranks (the bench's job time)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:

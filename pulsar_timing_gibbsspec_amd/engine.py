@@ -199,10 +199,16 @@ class PTAChains:
     [psr_lo, psr_lo + P_local) of P_global; ``gather`` (distributed.PulsarAllGather)
     exchanges the [tau | x_red] slabs so the common draw sees every pulsar in global
     order.  ``sweep_begin`` / ``sweep_end`` expose the two halves around the exchange.
+
+    curn_mode='sum' (no per-pulsar red noise only): the common draw uses the sufficient
+    statistic S_k = sum_p tau_p,k (gs_tau_sum, gs_rho_curn_sum); a pulsar-sharded run
+    then exchanges S with ``allreduce`` (distributed.TauSumAllReduce, one RCCL
+    all-reduce of n_f x n_chain doubles per sweep) instead of gathering tau.
     """
 
     def __init__(self, model: DeviceModel, n_param, gw_col, red_col, gw_bounds, red_bounds, n_chain, x0,
-                 chain_base=0, ngrid=1000, P_global=None, psr_lo=0, gather=None):
+                 chain_base=0, ngrid=1000, P_global=None, psr_lo=0, gather=None, curn_mode="exact",
+                 allreduce=None):
         self.model, self.ctx = model, model.ctx
         dev = self.ctx.device
         P, C = model.P, int(n_chain)
@@ -211,8 +217,16 @@ class PTAChains:
         self.psr_lo = int(psr_lo)
         self.sharded = self.PG != P
         self.gather = gather
-        if self.sharded and gather is None:
+        if curn_mode not in ("exact", "sum"):
+            raise ValueError("curn_mode must be 'exact' or 'sum'")
+        if curn_mode == "sum" and red_col is not None:
+            raise ValueError("curn_mode='sum' needs irn = 0 (no per-pulsar red noise)")
+        self.curn_mode = curn_mode
+        self.allreduce = allreduce
+        if self.sharded and curn_mode == "exact" and gather is None:
             raise ValueError("a pulsar-sharded PTAChains needs a gather")
+        if self.sharded and curn_mode == "sum" and allreduce is None:
+            raise ValueError("a pulsar-sharded curn_mode='sum' PTAChains needs an allreduce")
         self.n_f = model.NF // 2
         self.chain_base = int(chain_base)
         self.ngrid = ngrid
@@ -235,6 +249,7 @@ class PTAChains:
         self.tau = torch.empty(P, self.n_f, C, dtype=torch.float64, device=dev)
         self.tau_g = torch.empty(self.PG, self.n_f, C, dtype=torch.float64, device=dev) if self.sharded \
             else self.tau
+        self.S = torch.empty(self.n_f, C, dtype=torch.float64, device=dev)   # curn_mode='sum' 
         self.gwphi = torch.empty(self.n_f, C, dtype=torch.float64, device=dev)
         self.irn = torch.empty(self.PG, self.n_f, C, dtype=torch.float64, device=dev) if self.red else None
         self.phiinv_F = torch.empty(P * C, model.NF, dtype=torch.float64, device=dev)
@@ -275,6 +290,9 @@ class PTAChains:
             check(lib.gs_rho_red(h, self.P, self.C, self.n_f, ptr(self.tau), ptr(self.gwphi), self.ngrid,
                                  ptr(self.grid_red), ptr(u_red), ii, self.chain_base, ptr(self.x),
                                  self.n_param, ptr(self.red_col), None), "gs_rho_red")
+        if self.curn_mode == "sum":                            # sufficient statistic S_k
+            check(lib.gs_tau_sum(h, self.P, self.C, self.n_f, ptr(self.tau), ptr(self.S)), "gs_tau_sum")
+            return self.S if self.sharded else None
         if not self.sharded:
             return None
         parts = [self.tau.unsqueeze(1)]
@@ -287,6 +305,16 @@ class PTAChains:
         """Common draw on the global inputs, gate, gated b|rho."""
         lib, h = self.ctx.lib, self.ctx.handle
         ii = self.it
+        if self.curn_mode == "sum":
+            if self.sharded and slab_g is not None and slab_g.data_ptr() != self.S.data_ptr():
+                self.S.copy_(slab_g)
+            check(lib.gs_rho_curn_sum(h, self.PG, self.C, self.n_f, ptr(self.S), self.ngrid, ptr(self.grid_gw),
+                                      ptr(u_curn), ii, self.chain_base, ptr(self.x), self.n_param,
+                                      ptr(self.gw_col), None), "gs_rho_curn_sum")
+            self._gate_phiinv(with_gate=True)
+            self._bdraw(z, _lib.EV_B, self.gate)
+            self.it += 1
+            return
         if self.sharded:
             self.tau_g.copy_(slab_g[:, 0])
             if self.red:
@@ -307,4 +335,6 @@ class PTAChains:
         z0/z: (P*n_chain, ldb) injected normals (original column order); u_red
         (n_chain, P, n_f) and u_curn (n_chain, n_f): injected uniforms."""
         slab = self.sweep_begin(x_rec=x_rec, z0=z0, u_red=u_red)
-        self.sweep_end(self.gather(slab) if self.sharded else None, z=z, u_curn=u_curn)
+        if self.sharded:
+            slab = self.allreduce(slab) if self.curn_mode == "sum" else self.gather(slab)
+        self.sweep_end(slab, z=z, u_curn=u_curn)

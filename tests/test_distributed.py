@@ -89,3 +89,21 @@ def test_pulsar_allgather_gloo_world2():
 def test_pulsar_allgather_uneven_lpt_gloo_world2():
     out = run_world(_gather_lpt_case, 2)
     assert all(out.values())
+
+
+def _allreduce_case(rank, world):
+    n_f, C, P = 5, 3, 9
+    tau = torch.rand(P, n_f, C, generator=torch.Generator().manual_seed(1), dtype=torch.float64)
+    lo, hi = D.shard_range(P, rank, world)
+    partial = tau[lo:hi].sum(dim=0)
+    out = D.TauSumAllReduce()(partial.clone())
+    return out.numpy().tolist(), float(torch.max(torch.abs(out - tau.sum(dim=0))))
+
+
+def test_tau_sum_allreduce_gloo_world2():
+    """The CURN exchange without red noise: per-rank partial tau sums all-reduce to the
+    global S_k, identical on every rank."""
+    out = run_world(_allreduce_case)
+    assert out[0][0] == out[1][0]
+    assert out[0][1] < 1e-12
+

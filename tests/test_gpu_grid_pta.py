@@ -226,3 +226,67 @@ def test_pulsar_sharded_engine_bit_identical(kind):
         bs = sh.b.view(hi - lo, C, -1)
         w = bs.shape[2]
         assert torch.equal(bs, bref[lo:hi, :, :w]) and not bref[lo:hi, :, w:].any()
+
+
+def test_curn_sum_kernel_matches_reference(ctx):
+    """gs_tau_sum + gs_rho_curn_sum (the sufficient-statistic CURN draw a sharded run
+    all-reduces for) pick the reference's grid index on every sweep of the fixture."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import grid3
+    g = golden("pta_curn.npz")
+    *_, rec = pta_replay(g, "curn")
+    P, n_f = rec[0]["tau"].shape
+    Gg = grid3(float(g["rhomin_gw"]), float(g["rhomax_gw"]))
+    n_param = g["x0"].size
+    K = Keep()
+    for ii, r in enumerate(rec):
+        S = torch.zeros(n_f, 1, dtype=torch.float64, device="cuda")
+        _lib.check(ctx.lib.gs_tau_sum(ctx.handle, P, 1, n_f, K(r["tau"][:, :, None]), _lib.ptr(S)), "gs_tau_sum")
+        assert np.allclose(S.cpu().numpy()[:, 0], r["tau"].sum(axis=0), rtol=1e-15, atol=0)
+        x = dev(g["chain"][ii][None])
+        idx = torch.zeros(n_f, dtype=torch.int32, device="cuda")
+        _lib.check(ctx.lib.gs_rho_curn_sum(ctx.handle, P, 1, n_f, _lib.ptr(S), 1000, _lib.ptr(Gg),
+                                           K(r["u_curn"][None]), 0, 0, _lib.ptr(x), n_param,
+                                           K(g["rind"].astype(np.int32), torch.int32), _lib.ptr(idx)),
+                   "gs_rho_curn_sum")
+        assert np.array_equal(idx.cpu().numpy(), r["idx_curn"] % 1000), ii
+        assert np.array_equal(x.cpu().numpy()[0], r["x_curn"]), ii
+
+
+def test_curn_sum_sharded_engine_matches_unsharded():
+    """curn_mode='sum': two pulsar shards exchanging partial tau sums (the all-reduce)
+    reproduce the unsharded sum-mode chains under device Philox; the unsharded
+    sum-mode chain itself stays within the exact engine's posterior (same grid)."""
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd.distributed import shard_range
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
+    pta = synthetic.array_pta(kind="curn", n_psr=9, seed=2)
+    T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
+    names = pta.param_names
+    rind = [i for i, n in enumerate(names) if "rho" in n and "gw" in n]
+    gwid = [np.arange(t.shape[1] - 60, t.shape[1]) for t in T]
+    fixed = [np.full(t.shape[1] - 60, 1e-40) for t in T]
+    C, S = 16, 6
+    x0 = np.random.default_rng(0).uniform(-9, -4, (C, len(names)))
+    bounds = ((1e-18, 1e-8), (1e-20, 1e-8))
+    ref = PTAChains(DeviceModel(_lib.Context(0, seed=78), T, N, R, gwid, fixed), len(names), rind, None,
+                    *bounds, C, x0, curn_mode="sum")
+    xr_ref = torch.zeros(S, C, len(names), dtype=torch.float64, device="cuda")
+    for i in range(S):
+        ref.sweep(x_rec=xr_ref[i])
+    shards = []
+    for r in range(2):
+        lo, hi = shard_range(len(T), r, 2)
+        mdl = DeviceModel(_lib.Context(0, seed=78), T[lo:hi], N[lo:hi], R[lo:hi], gwid[lo:hi], fixed[lo:hi])
+        shards.append(PTAChains(mdl, len(names), rind, None, *bounds, C, x0, P_global=len(T), psr_lo=lo,
+                                curn_mode="sum", allreduce=lambda s: s))
+    xr = [torch.zeros(S, C, len(names), dtype=torch.float64, device="cuda") for _ in range(2)]
+    for i in range(S):
+        parts = [sh.sweep_begin(x_rec=xr[j][i]) for j, sh in enumerate(shards)]
+        tot = parts[0] + parts[1]                     # the all-reduce
+        for sh in shards:
+            sh.sweep_end(tot.clone())
+    assert torch.equal(xr[0], xr[1])
+    assert torch.equal(xr[0], xr_ref)
+    gw = xr_ref[:, :, rind].cpu().numpy()
+    assert np.isfinite(gw).all() and (gw >= -9).all() and (gw <= -4).all()

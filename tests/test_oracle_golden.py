@@ -289,3 +289,15 @@ def test_exact_chol_draw_pins_reference_white():
     assert normwise_rel(rp["b_first"], bx) < 5e-9
     TNT, d = O.tnt(g["T"], N, g["r"])
     assert normwise_rel(O.bdraw_chol(TNT, d, ph, rp["z0"], order), bx) < 1e-9
+
+
+def test_curn_sum_statistic_matches_product_draw():
+    """CURN without red noise: the draw from S_k = sum_p tau_p,k (what a sharded run
+    all-reduces) picks the reference's grid index on every sweep of the fixture."""
+    g = golden("pta_curn.npz")
+    *_, rec = pta_replay(g, "curn")
+    lo, hi = float(g["rhomin_gw"]), float(g["rhomax_gw"])
+    for ii, r in enumerate(rec):
+        tau = r["tau"]                                   # (P, n_f)
+        _, idx = O.rho_grid_cdf_curn_sum(tau.sum(axis=0), tau.shape[0], r["u_curn"], lo, hi)
+        assert np.array_equal(idx % 1000, r["idx_curn"] % 1000), ii
