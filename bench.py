@@ -148,7 +148,7 @@ def pta_cpu_baseline(kind, seconds=10.0):
                        f"pta_gibbs.py:664-704, numpy SVD, 1 thread) in {el:.1f} s")
 
 
-def bench_pta(kind, C, K, W, rank, world, dev, ctx):
+def bench_pta(kind, C, K, W, rank, world, dev, ctx, curn_mode="exact"):
     """Configs 4a/4b: PTAChains over the 45 simulated pulsars, C chains per GPU (chain-sharded)."""
     from pulsar_timing_gibbsspec_amd import synthetic
     from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
@@ -161,7 +161,7 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx):
     model = DeviceModel(ctx, T, N, R, gwid, [np.full(t.shape[1] - 60, 1e-40) for t in T])
     x0 = np.random.default_rng(rank).uniform(-9, -4, (C, len(names)))
     eng = PTAChains(model, len(names), rind, hind.reshape(len(T), -1) if kind == "curn_red" else None,
-                    (1e-18, 1e-8), (1e-20, 1e-8), C, x0, chain_base=rank * C)
+                    (1e-18, 1e-8), (1e-20, 1e-8), C, x0, chain_base=rank * C, curn_mode=curn_mode)
     rec = torch.empty(K, C, len(names), dtype=torch.float64, device=dev)
     for _ in range(W):
         eng.sweep(x_rec=rec[0])
@@ -301,8 +301,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--bcast", type=int, default=None, help="GS_OPT_BCAST (0 readlane, 1 LDS, 2 batched)")
-    ap.add_argument("--pta", default="curn_red", help="secondary PTA config measured in the same run: "
-                    "curn | curn_red | none")
+    ap.add_argument("--pta", default="curn_red,curn", help="secondary PTA configs measured in the same run "
+                    "(comma list of curn_red, curn; or none). curn uses the sufficient-statistic draw")
     ap.add_argument("--pta-chains", type=int, default=256)
     ap.add_argument("--pta-steps", type=int, default=20)
     ap.add_argument("--config5", type=int, default=1, help="measure BASELINE configs[4] too (1/0)")
@@ -407,14 +407,15 @@ def main():
         }
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-    if args.pta != "none":
-        sec = bench_pta(args.pta, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx)
+    for kind in [k for k in args.pta.split(",") if k and k != "none"]:
+        mode = "sum" if kind == "curn" else "exact"
+        sec = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, curn_mode=mode)
         if rank == 0:
-            sec["config"] = f"configs[3]: 45-pulsar CURN{' + per-pulsar red' if args.pta == 'curn_red' else ''} " \
-                            "free spectrum, chain-sharded"
+            sec["config"] = (f"configs[3]: 45-pulsar CURN{' + per-pulsar red' if kind == 'curn_red' else ''} "
+                             f"free spectrum, chain-sharded, common draw {mode}")
             if not args.no_cpu_baseline:
-                sec["cpu_baseline"] = pta_cpu_baseline(args.pta, args.cpu_seconds)
-            out.setdefault("secondary", {})[args.pta] = sec
+                sec["cpu_baseline"] = pta_cpu_baseline(kind, args.cpu_seconds)
+            out.setdefault("secondary", {})[kind] = sec
     if args.config5:
         sec = bench_config5(args.c5_chains, args.c5_steps, 1, rank, world, dev)
         if rank == 0:

@@ -176,6 +176,42 @@ class FreeSpectrumChains:
         return x_rec, b_rec
 
 
+class HistoryStreamer:
+    """Chain history to pinned host memory, overlapped with the sampling.
+
+    Two slots of device record buffers; after a block of sweeps is launched on the
+    context stream, ``submit`` queues its device->pinned-host copy on a side stream
+    (ordered after the block by an event) and returns at once, so the copy runs on
+    the copy engine while the next block's sweeps run.  ``fetch`` waits for a slot's
+    copy and returns the pinned host tensors.  A slot is reused only after its fetch."""
+
+    def __init__(self, ctx, shapes, dtype=torch.float64):
+        dev = ctx.device
+        self.ctx = ctx
+        self.dev_bufs = [[torch.empty(s, dtype=dtype, device=dev) for s in shapes] for _ in range(2)]
+        self.host_bufs = [[torch.empty(s, dtype=dtype, pin_memory=True) for s in shapes] for _ in range(2)]
+        self.side = torch.cuda.Stream(device=dev)
+        self.done = [torch.cuda.Event(), torch.cuda.Event()]
+        self.rows = [0, 0]
+
+    def buffers(self, slot, n):
+        return [b[:n] for b in self.dev_bufs[slot]]
+
+    def submit(self, slot, n):
+        ready = torch.cuda.Event()
+        ready.record(self.ctx.stream)
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(ready)
+            for d, h in zip(self.dev_bufs[slot], self.host_bufs[slot]):
+                h[:n].copy_(d[:n], non_blocking=True)
+            self.done[slot].record(self.side)
+        self.rows[slot] = n
+
+    def fetch(self, slot):
+        self.done[slot].synchronize()
+        return [h[:self.rows[slot]] for h in self.host_bufs[slot]]
+
+
 def grid3(rhomin, rhomax, n=1000, device="cuda"):
     """[rho_g | log rho_g | 0.5 log10 rho_g], rho_g = 10**linspace(log10 rhomin, log10 rhomax, n)
     — numpy on the host, so the device sees the reference's exact grid

@@ -30,7 +30,7 @@ import torch
 
 from . import _lib
 from .diagnostics import white_aclength
-from .engine import DeviceModel, FreeSpectrumChains
+from .engine import DeviceModel, FreeSpectrumChains, HistoryStreamer
 from .white import MAX_W, WhiteFreeSpectrumChains, WhiteNoiseModel, white_kind
 
 
@@ -372,27 +372,41 @@ class PulsarBlockGibbs(object):
             runner.run(1, record=False)
         runner.it = max(runner.it, start)
         m = int(model.m[0])
-        ii = start
-        while ii < niter:
-            nxt = min(niter, (ii // save_every + 1) * save_every + 1)
-            n = nxt - ii
-            xr, br = runner.run(n)
-            xh = xr.cpu().numpy()
-            bh = br[:, :, :m].cpu().numpy()
+        blk = max(1, save_every) + 1
+        # block k+1's sweeps run while block k's rows stream to pinned host memory
+        streamer = HistoryStreamer(self.ctx, [(blk, nc, runner.n_f), (blk, nc, model.ldb)])
+
+        def consume(slot, ii, nxt):
+            xh, bh = (t.numpy() for t in streamer.fetch(slot))
+            bh = bh[:, :, :m]
             self.chain[ii:nxt] = xh[:, 0]
             self.bchain[ii:nxt] = bh[:, 0]
             if nc > 1:
                 self.chains[:, ii:nxt] = np.moveaxis(xh, 1, 0)
                 self.bchains[:, ii:nxt] = np.moveaxis(bh, 1, 0)
-            ii = nxt
-            self.iter = ii - 1
-            last = ii - 1
+            self.iter = nxt - 1
+            last = nxt - 1
             if last % save_every == 0 and last > 0:
                 np.save(f"{outdir}/chain.npy", self.chain[:last + 1, :])
                 np.save(f"{outdir}/bchain.npy", self.bchain[:last + 1, :])
                 if nc > 1:
                     np.save(f"{outdir}/chains.npy", self.chains[:, :last + 1])
                     np.save(f"{outdir}/bchains.npy", self.bchains[:, :last + 1])
+
+        ii, slot, pending = start, 0, None
+        while ii < niter:
+            nxt = min(niter, (ii // save_every + 1) * save_every + 1)
+            n = nxt - ii
+            xr, br = streamer.buffers(slot, n)
+            runner.run(n, x_rec=xr, b_rec=br)
+            streamer.submit(slot, n)
+            if pending is not None:
+                consume(*pending)
+            pending = (slot, ii, nxt)
+            slot ^= 1
+            ii = nxt
+        if pending is not None:
+            consume(*pending)
         info = runner.info.cpu().numpy()
         if info.any():
             print(f"WARNING: {int((info != 0).sum())} chains hit a non-positive-definite Sigma")

@@ -7,7 +7,7 @@ OUT=$R/gpurun_out/prof_${TAG:-r01}
 mkdir -p $OUT
 export OPENBLAS_NUM_THREADS=1
 test -f $R/pulsar_timing_gibbsspec_amd/libpulsar_gibbs.so || { echo "build first"; exit 2; }
-ARGS="--no-cpu-baseline --pta none ${BENCH_ARGS:-}"
+ARGS="--no-cpu-baseline --pta none --config5 0 ${BENCH_ARGS:-}"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $R/bench.py $ARGS > $OUT/trace.log 2>&1; rc=$?
 echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
