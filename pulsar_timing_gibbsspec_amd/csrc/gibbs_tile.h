@@ -245,11 +245,14 @@ __device__ __forceinline__ void tile_elim(gs_d4& A, gs_d4& B, double& rsd, int q
     __builtin_amdgcn_sched_barrier(0);
     const double akk = newbcast(akc, k);  // A[k][k]
     if (k + 1 < KMAX) {
-      const double i0 = __builtin_amdgcn_rcp(akk);
-      const double ninv = fma(akk, i0, -2.0) * i0;  // -1/A[k][k]
       // lane mask c > k from an opaque k: one v_cmp per step instead of loop-invariant
-      // 64-bit masks held in (spilled) SGPRs across the caller's sweep loop
-      const double ng = (c > opq(k)) ? akc * ninv : 0.0;  // -A[k][c]/A[k][k]
+      // 64-bit masks held in (spilled) SGPRs across the caller's sweep loop; applied to
+      // the row before the pivot arrives, so it is off the critical path
+      const double akm = (c > opq(k)) ? akc : 0.0;
+      // -A[k][c]/A[k][k] = akm i0 (akk i0 - 2) (one Newton step on v_rcp_f64): the two
+      // products run side by side, 4 dependent ops from pivot to multiplier
+      const double i0 = __builtin_amdgcn_rcp(akk);
+      const double ng = (akm * i0) * fma(akk, i0, -2.0);
       akc = fmac_nb(rn, rn, ng, k);                        // row k+1 after step k
 #pragma unroll
       for (int s = k1; s < 4; ++s) A[s] = fmac_nb(A[s], A[s], ng, k);
