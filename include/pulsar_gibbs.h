@@ -116,6 +116,7 @@ int gs_tnt(gs_ctx* ctx, int n_psr, int m_max, const gs_tnt_desc* desc,
  *   G  [NMX x (NF+1)] L_M^-T W  (row stride NF+1)
  *   h  [NMX]          L_M^-T L_M^-1 d_M
  *   R  [NMX x NMX]    L_M^-T  (upper)
+ *   aux[2]            sum log diag L_M, |L_M^-1 d_M|^2  (gs_lnlike_marg)
  * fidx: [n_psr x NF] column index of each free-spectrum column (gwid);
  * midx: [n_psr x NMX] column index of each fixed-prior column;
  * phiinv_fixed: [n_psr x NMX] their (constant) phiinv (1e-40 for the TM).
@@ -193,6 +194,17 @@ int gs_tau(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const int32_t* 
 int gs_rho_curn(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, const double* irn,
                 int ngrid, const double* grid3, const double* u, int64_t sweep, int64_t chain_base,
                 double* x, int ldx, const int32_t* xcol, int32_t* idx_out);
+/*
+ *  Marginalised likelihood get_lnlikelihood_fullmarg (pulsar_gibbs.py:569-610,
+ * pta_gibbs.py:577-621) for n_psr x n_chain systems from the prefix model blocks (one per
+ * pulsar, or per system with model_per_sys): lnl[sys] = 1/2 (d^T Sigma^-1 d - log det Sigma)
+ * + 1/2 sum_F log phiinv_F, -inf (and info > 0) if Sigma is not positive definite.  The
+ * reference's value adds the model constants -1/2 (sum log N + r^T N^-1 r) + 1/2 sum_M log
+ * phiinv_M.  NF = 20, 40, 60.
+ */
+int gs_lnlike_marg(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const double* model,
+                   int model_per_sys, const int32_t* nm, const double* phiinv_F, double* lnl, int32_t* info);
+
 /*
  * (a6, sufficient statistic) CURN without per-pulsar red noise: the common pdf depends on
  * tau only through S[k][c] = sum_p tau[p][k][c] (pta_gibbs.py:194-205 with irn = 0), so a

@@ -212,7 +212,18 @@ __global__ __launch_bounds__(256) void k_prefix(const gs_prefix_desc* desc, int 
   for (int64_t q = (int64_t)NF * (NF + 1) + NF + NMX * (NF + 1) + NMX + NMX * NMX + tid; q < mstride; q += nt)
     out[q] = 0.0;
   __syncthreads();
-  if (tid == 0 && info) info[sys] = s_fail;
+  if (tid == 0) {
+    // aux for the marginalised likelihood: sum log diag L_M and |e|^2, e = L_M^-1 d_M
+    double lm = 0.0, ee = 0.0;
+    for (int i = 0; i < nM; ++i) {
+      lm += log(L[i * NMX + i]);
+      ee += W[i * ldw + NF] * W[i * ldw + NF];
+    }
+    const int64_t ao = (int64_t)NF * (NF + 1) + NF + NMX * (NF + 1) + NMX + NMX * NMX;
+    out[ao] = lm;
+    out[ao + 1] = ee;
+    if (info) info[sys] = s_fail;
+  }
 }
 
 __global__ void k_philox(int64_t n, const uint32_t* ctr, uint32_t* out, gs_key key) {
@@ -522,6 +533,22 @@ int gs_rho_curn(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau,
   if (rc) return rc;
   launch_rho_curn(ctx->stream, a);
   return after_launch("k_rho_curn");
+}
+
+int gs_lnlike_marg(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const double* model,
+                   int model_per_sys, const int32_t* nm, const double* phiinv_F, double* lnl, int32_t* info) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
+  if (!nf_supported(NF)) return fail_arg(4, "NF must be 20, 40 or 60");
+  if (NMX <= 0 || NMX > 64) return fail_arg(5, "NMX must be in 1..64");
+  if (!model || !nm || !phiinv_F || !lnl) return fail_arg(6, "NULL array");
+  if (n_psr == 0 || n_chain == 0) return 0;
+  LnlArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.model_per_sys = model_per_sys ? 1 : 0;
+  a.mstride = model_stride_doubles(NF, NMX); a.model = model; a.nm = nm; a.phiinv_F = phiinv_F;
+  a.lnl = lnl; a.info = info;
+  launch_lnlike_marg(ctx->stream, a);
+  return after_launch("k_lnlike_marg");
 }
 
 int gs_tau_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, double* S) {

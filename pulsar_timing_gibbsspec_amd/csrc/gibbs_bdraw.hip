@@ -226,6 +226,39 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
   if (A.info && lane == 0) A.info[sys] = fail;
 }
 
+// ------------------------------------------------------------ marginalised likelihood
+//  get_lnlikelihood_fullmarg pulsar_gibbs.py:569-610, phiinv-dependent part:
+//   lnl = 1/2 (d^T Sigma^-1 d - log det Sigma) + 1/2 sum_F log phiinv_F
+// with the prefix: d^T Sigma^-1 d = |e|^2 + |y|^2, log det Sigma = 2 sum log diag L_M +
+// log det S; |y|^2 and log det S come out of the augmented tile factorisation.  The
+// model constants -1/2 (log det N + r^T N^-1 r) - 1/2 sum_M log phi_M are the caller's.
+template <int NF, int WPB>
+__global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
+  extern __shared__ double lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nb = (A.n_chain + WPB - 1) / WPB;
+  const int p = blockIdx.x / nb;
+  const int c = (blockIdx.x % nb) * WPB + wave;
+  if (!A.model_per_sys) stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+  if (c >= A.n_chain) return;
+  const int64_t sys = (int64_t)p * A.n_chain + c;
+  const double* mb = A.model_per_sys ? A.model + sys * A.mstride : lds;
+  const ModelLds M = model_view(mb, NF, A.NMX);
+  const double phinv = lane < NF ? A.phiinv_F[sys * NF + lane] : 1.0;
+  double yy = 0.0, ldS = 0.0;
+  double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * GS_TILE_SCR;
+  const int fail = bdraw_tile<NF, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr);
+  double lph = lane < NF ? log(phinv) : 0.0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lph += __shfl_xor(lph, o);
+  const int64_t ao = model_aux_offset(NF, A.NMX);
+  const double lm = mb[ao], ee = mb[ao + 1];
+  if (lane == 0) {
+    A.lnl[sys] = fail ? -__builtin_inf() : 0.5 * (ee + yy - 2.0 * lm - ldS) + 0.5 * lph;
+    if (A.info) A.info[sys] = fail;
+  }
+}
+
 // ------------------------------------------------------------ fused sweep
 template <int NF, int WPB, int BC>
 __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepArgs A) {
@@ -398,6 +431,19 @@ int dispatch_nf_bdraw(int NF, int bc, dim3 grid, size_t lds, hipStream_t s, cons
 }
 
 }  // namespace
+
+int launch_lnlike_marg(hipStream_t s, const LnlArgs& a) {
+  constexpr int WPB = GS_SWEEP_WPB;
+  const int nb = (a.n_chain + WPB - 1) / WPB;
+  dim3 grid((unsigned)(a.n_psr * nb));
+  const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) + GS_TILE_SCR * WPB) * sizeof(double);
+  switch (a.NF) {
+    case 20: hipLaunchKernelGGL((k_lnlike_marg<20, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 40: hipLaunchKernelGGL((k_lnlike_marg<40, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 60: hipLaunchKernelGGL((k_lnlike_marg<60, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    default: return 1;
+  }
+}
 
 int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;

@@ -12,10 +12,25 @@
 #define GS_SWEEP_WPB 4
 #endif
 
-inline int64_t model_stride_doubles(int NF, int NMX) {
-  const int64_t s = (int64_t)NF * (NF + 1) + NF + (int64_t)NMX * (NF + 1) + NMX + (int64_t)NMX * NMX;
+// model block: S0 | dF | G | h | R | aux[2] (aux: sum log diag L_M, |L_M^-1 d_M|^2)
+__host__ __device__ inline int64_t model_aux_offset(int NF, int NMX) {
+  return (int64_t)NF * (NF + 1) + NF + (int64_t)NMX * (NF + 1) + NMX + (int64_t)NMX * NMX;
+}
+__host__ __device__ inline int64_t model_stride_doubles(int NF, int NMX) {
+  const int64_t s = model_aux_offset(NF, NMX) + 2;
   return (s + 1) & ~int64_t(1);  // 16-byte multiple
 }
+
+struct LnlArgs {
+  int n_psr, n_chain, NF, NMX, model_per_sys;
+  int64_t mstride;
+  const double* model;
+  const int32_t* nm;
+  const double* phiinv_F;
+  double* lnl;
+  int32_t* info;
+};
+int launch_lnlike_marg(hipStream_t s, const LnlArgs& a);
 
 struct BdrawArgs {
   int n_psr, n_chain, NF, NMX, ldb, event, bcast, psr_base;

@@ -272,7 +272,10 @@ __device__ __forceinline__ void tile_elim(gs_d4& A, gs_d4& B, double& rsd, int q
 
 // Model block view (see gibbs_bdraw.hip ModelLds): S0 NF x (NF+1), dF, G NMX x (NF+1),
 // h, R NMX x NMX.  Same interface and outputs as bdraw_wave.
-template <int NF, typename ModelT>
+// LNL = true (the marginalised likelihood, gs_lnlike_marg): stop after the factorisation
+// and return, wave-uniform, bF = |y|^2 = dF^T S^-1 dF and bM = log det S (sum of the log
+// pivots of the real columns).
+template <int NF, bool LNL = false, typename ModelT>
 __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int lane, double phinv,
                                           double zF, double zM, double& bF, double& bM,
                                           double* __restrict__ scr) {
@@ -340,6 +343,8 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
   double ycol[NT];
   gs_d4 yrow[NT];
   int fail = 0;
+  double lpiv = 0.0;   // LNL: sum over this lane's column of log pivot
+  double yyacc = 0.0;  // LNL: sum of y_K^2 over this lane's rows 4s+q (K < NT-1)
   double ylast = 0.0;  // AUG: y of the last tile row, column layout
 #pragma unroll
   for (int K = 0; K < NT; ++K) {
@@ -363,6 +368,7 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
     // first bad pivot of this tile (columns c of row group 0)
     const unsigned long long badm = __ballot(!(rsd > 0.0 && rsd < __builtin_inf())) & 0xffffull;
     if (!fail && badm) fail = 16 * K + __ffsll((long long)badm);
+    if constexpr (LNL) lpiv += (16 * K + c < NF) ? -2.0 * log(rsd) : 0.0;
     gs_d4 V;  // U_KK^-1
 #pragma unroll
     for (int s = 0; s < 4; ++s) V[s] = B[s] * rsd;
@@ -372,6 +378,15 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
     for (int J = K + 1; J < NT; ++J) {
       const gs_d4 z = {0.0, 0.0, 0.0, 0.0};
       t[tix(K, J, NT)] = mfma_tn(z, V, t[tix(K, J, NT)]);
+    }
+    if constexpr (LNL) {
+      // |y_K|^2: y_K = column CP of U_K,last (rows 4s+q in row group q, any column)
+      if (K + 1 < NT)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const double yv = newbcast(t[tix(K, NT - 1, NT)][s], CP);
+          yyacc = fma(yv, yv, yyacc);
+        }
     }
     // the backward solve wants U_KK^-T: transpose in place while the MFMAs run
     if constexpr (AUG) t[tix(K, K, NT)] = transpose(V, tb, q, c);
@@ -416,6 +431,22 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
   }
 
   GS_PH(3)
+  if constexpr (LNL) {
+    static_assert(AUG, "the likelihood mode reads y off the augmented factorisation");
+    // rows of y_0..y_{NT-2}: lane (q, 0) holds rows 4s+q of each (sum over the 4 row
+    // groups); y_last in column layout (sum over the 16 columns of row group 0)
+    double yy = (c == 0) ? yyacc : 0.0;
+    yy += (q == 0) ? ylast * ylast : 0.0;
+    double lp = (q == 0) ? lpiv : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      yy += __shfl_xor(yy, o);
+      lp += __shfl_xor(lp, o);
+    }
+    bF = yy;
+    bM = lp;
+    return fail;
+  }
   // ---- backward: U x = y + zF   (x_K = U_KK^-1 (w_K - sum_{J>K} U_KJ x_J))
   double xcol[NT];
   gs_d4 xrow[NT];

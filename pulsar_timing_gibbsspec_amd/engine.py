@@ -107,6 +107,30 @@ class DeviceModel:
         if info.any():
             raise np.linalg.LinAlgError(f"fixed-prior block not positive definite: info={info}")
 
+    def lnl_constants(self):
+        """-1/2 (sum log N + r^T N^-1 r) + 1/2 sum_M log phiinv_M per pulsar (the model
+        part of get_lnlikelihood_fullmarg, pulsar_gibbs.py:583-600), reduced on device."""
+        dev = self.ctx.device
+        seg = torch.repeat_interleave(torch.arange(self.P, device=dev),
+                                      torch.as_tensor(self.n_toa, device=dev))
+        t = torch.log(self.Nvec) + self.r * self.r / self.Nvec
+        wn = torch.zeros(self.P, dtype=torch.float64, device=dev).index_add_(0, seg, t)
+        nmask = torch.arange(self.NMX, device=dev)[None, :] < self.nm_dev[:, None]
+        lph = torch.where(nmask, torch.log(self.phfix), torch.zeros_like(self.phfix)).sum(dim=1)
+        return -0.5 * wn + 0.5 * lph
+
+    def lnlike_marg(self, phiinv_F, n_chain):
+        """Marginalised likelihood (pulsar_gibbs.py:569-610) of P*n_chain systems:
+        phiinv_F (P*n_chain, NF) device tensor -> (lnl (P*n_chain,), info)."""
+        dev = self.ctx.device
+        n_sys = self.P * n_chain
+        lnl = torch.empty(n_sys, dtype=torch.float64, device=dev)
+        info = torch.zeros(n_sys, dtype=torch.int32, device=dev)
+        check(self.ctx.lib.gs_lnlike_marg(self.ctx.handle, self.P, n_chain, self.NF, self.NMX, ptr(self.model), 0,
+                                          ptr(self.nm_dev), ptr(phiinv_F), ptr(lnl), ptr(info)), "gs_lnlike_marg")
+        const = self.lnl_constants().repeat_interleave(n_chain)
+        return lnl + const, info
+
     def tnt_host(self, p):
         m = int(self.m[p])
         o = int(self.tnt_off[p])

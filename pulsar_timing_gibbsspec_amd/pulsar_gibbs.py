@@ -180,6 +180,15 @@ class PulsarBlockGibbs(object):
                                       "only fixed-prior columns are supported outside gwid")
         return phiinv[self.gwid]
 
+    def get_lnlikelihood_fullmarg(self, xs):
+        """Marginalised likelihood (pulsar_gibbs.py:569-610) on the device: the prefix
+        model block + one augmented tile factorisation (gs_lnlike_marg); -inf when
+        Sigma is not positive definite (the reference's LinAlgError branch, :598-599)."""
+        model = self._model(xs)
+        ph = torch.as_tensor(np.ascontiguousarray(self._phiinv_F(xs))[None], device=self.ctx.device)
+        lnl, info = model.lnlike_marg(ph, 1)
+        return -np.inf if int(info[0]) else float(lnl[0])
+
     # ------------------------------------------------------------ white noise
     def _white_structure(self, xs):
         """Per-TOA sigma^2, backend groups and the white parameter table, discovered

@@ -54,7 +54,8 @@ def test_host_only_calls(lib):
     lib.gs_model_stride.restype = ctypes.c_int64
     lib.gs_model_stride.argtypes = [ctypes.c_int, ctypes.c_int]
     s = lib.gs_model_stride(60, 16)
-    assert s == 60 * 61 + 60 + 16 * 61 + 16 + 256 + ((60 * 61 + 60 + 16 * 61 + 16 + 256) & 1)
+    base = 60 * 61 + 60 + 16 * 61 + 16 + 256 + 2          # S0 | dF | G | h | R | aux[2]
+    assert s == base + (base & 1)
     assert s % 2 == 0
 
 
