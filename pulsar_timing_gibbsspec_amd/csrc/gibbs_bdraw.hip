@@ -129,7 +129,7 @@ __device__ __forceinline__ int bdraw_wave(const ModelLds& M, int NMX, int nM, in
       // column k through the wave's LDS slot: one ds_write_b64 per lane, then
       // same-address (broadcast) ds_read_b128 pairs; DS ops of a wave are in order.
       scr[lane] = f;
-      __builtin_amdgcn_wave_barrier();
+      wave_lds_sync();
 #pragma unroll
       for (int j = (k + 1) & ~1; j < NF; j += 2) {
         const double2 v = *reinterpret_cast<const double2*>(scr + j);
@@ -137,7 +137,7 @@ __device__ __forceinline__ int bdraw_wave(const ModelLds& M, int NMX, int nM, in
         a[j + 1] = fma(-f, v.y, a[j + 1]);
         if ((((j - k) >> 1) % (GS_BCAST_CHUNK / 2)) == 0) __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_lds_sync();
     }
     __builtin_amdgcn_sched_barrier(0);
   }

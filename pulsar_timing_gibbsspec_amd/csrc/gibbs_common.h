@@ -13,6 +13,16 @@
 #define GS_TILE_SCR 400
 #endif
 
+// ---------------------------------------------------------------- intra-wave LDS sync
+// Lanes of one wavefront exchanging data through LDS: wavefront-scope release/acquire
+// fences around the wave barrier (a bare wave barrier does not order the LDS accesses
+// for the compiler backend).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ---------------------------------------------------------------- cross-lane
 // Broadcast lane `l` of a double to every lane (two v_readlane_b32 -> SGPRs).
 __device__ __forceinline__ double rdlane(double v, int l) {

@@ -58,12 +58,12 @@ static __device__ unsigned long long gs_phase_cyc[8];
 
 namespace gtile {
 
-// compiler-level ordering of the wave's LDS traffic (the hardware executes a
-// wave's DS instructions in order, so no s_barrier is needed)
-__device__ __forceinline__ void lds_fence() {
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
-}
+// Ordering of the wave's cross-lane LDS traffic: wavefront-scope release/acquire
+// fences around the wave barrier (the hardware executes a wave's DS instructions in
+// order, so no s_barrier is needed).  A bare wave_barrier + asm memory clobber is NOT
+// enough: the backend scheduler reordered a transpose's LDS reads past another
+// transpose's writes (found by the likelihood tests, tests/test_gpu_lnlike.py).
+__device__ __forceinline__ void lds_fence() { wave_lds_sync(); }
 
 // acc + X^T Y for C-layout tiles X, Y
 __device__ __forceinline__ gs_d4 mfma_tn(gs_d4 acc, const gs_d4 x, const gs_d4 y) {

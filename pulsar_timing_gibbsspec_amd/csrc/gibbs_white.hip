@@ -87,7 +87,7 @@ __global__ __launch_bounds__(64 * MH_WPB) void k_white_mh(WhiteMhArgs A) {
     t2[lane] = 0.0;
     tn[lane] = 0.0;
   }
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   if (lane < nw) {
     const double v = x[wcol[lane]];
     xs[lane] = v;
@@ -98,12 +98,12 @@ __global__ __launch_bounds__(64 * MH_WPB) void k_white_mh(WhiteMhArgs A) {
     else if (wkind[lane] == GS_WHITE_TNEQUAD) tn[k] = q;
     else t2[k] = t;
   }
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   for (int k = 0; k < nbk; ++k) {
     const double s = backend_sum(s2, y, bko[k], bko[k + 1], ef2[k], t2[k], tn[k], lane);
     if (lane == 0) S[k] = s;
   }
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
 
   const int steps = A.nsteps_chain ? A.nsteps_chain[A.x_per_sys ? sys : (int64_t)c] : A.n_steps;
   const double sig = 0.05 * nw;  // sigmas = 0.05 * len(wind)  (:376)
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(64 * MH_WPB) void k_white_mh(WhiteMhArgs A) {
           xs[w] = xq;
         }
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_lds_sync();
     }
   }
   if (lane < nw) x[wcol[lane]] = xs[lane];
