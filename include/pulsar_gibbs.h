@@ -93,6 +93,15 @@ int gs_ctx_set_seed(gs_ctx* ctx, uint64_t seed);
 int gs_ctx_set_option(gs_ctx* ctx, int option, int value);
 int gs_ctx_get_option(gs_ctx* ctx, int option); /* -1 on unknown option / NULL ctx */
 
+/*
+ * Graph replay of sweeps (a8): Philox counters use sweep + *sweep_dev when a device-side
+ * sweep counter is attached (NULL detaches), so a captured sequence of launches draws
+ * fresh numbers on every replay; gs_counter_add(counter, inc) advances it on the stream
+ * (captured with the sweep).  Attach before capturing.
+ */
+int gs_ctx_set_sweep_counter(gs_ctx* ctx, const int64_t* sweep_dev);
+int gs_counter_add(gs_ctx* ctx, int64_t* counter, int64_t inc);
+
 /* Doubles per pulsar in a model buffer (see gs_prefix). */
 int64_t gs_model_stride(int NF, int NMX);
 /* Dynamic LDS bytes per workgroup of the b-draw / sweep kernels for (NF, NMX). */

@@ -13,6 +13,7 @@ struct gs_ctx {
   int bcast;     // GS_OPT_BCAST
   int psr_base;  // GS_OPT_PSR_BASE: global index of this shard's pulsar 0 (RNG counters)
   int x_per_sys = 0;  // GS_OPT_X_PER_SYS
+  const int64_t* sweep_dev = nullptr;  // gs_ctx_set_sweep_counter
   double* ws = nullptr;  // tile workspace of the large-NF b-draw (grown on demand)
   size_t ws_bytes = 0;
 };
@@ -311,6 +312,19 @@ int gs_ctx_get_option(gs_ctx* ctx, int option) {
   return -1;
 }
 
+int gs_ctx_set_sweep_counter(gs_ctx* ctx, const int64_t* sweep_dev) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  ctx->sweep_dev = sweep_dev;
+  return 0;
+}
+
+int gs_counter_add(gs_ctx* ctx, int64_t* counter, int64_t inc) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (!counter) return fail_arg(2, "counter is NULL");
+  launch_counter_add(ctx->stream, counter, inc);
+  return after_launch("k_counter_add");
+}
+
 int64_t gs_model_stride(int NF, int NMX) { return model_stride_doubles(NF, NMX); }
 
 int gs_sweep_lds_bytes(int NF, int NMX) {
@@ -402,6 +416,7 @@ static int bdraw_impl(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   BdrawArgs a;
   a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.ldb = ldb; a.event = event;
   a.mstride = model_stride_doubles(NF, NMX); a.sweep = sweep; a.chain_base = chain_base;
+  a.sweep_dev = ctx->sweep_dev;
   a.model = model; a.fidx = fidx; a.midx = midx; a.nm = nm; a.chain_mask = chain_mask;
   a.phiinv_F = phiinv_F; a.z = z;
   a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = ctx->bcast; a.psr_base = ctx->psr_base;
@@ -462,6 +477,7 @@ int gs_rho_analytic(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const 
   if (ldx < NF / 2) return fail_arg(14, "ldx too small");
   RhoArgs a;
   a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.ldb = ldb; a.ldx = ldx; a.sweep = sweep;
+  a.sweep_dev = ctx->sweep_dev;
   a.chain_base = chain_base; a.rhomin = rhomin; a.rhomax = rhomax; a.fidx = fidx; a.b = b;
   a.u = u; a.x = x; a.key = key_of(ctx); a.psr_base = ctx->psr_base;
   launch_rho_analytic(ctx->stream, a);
@@ -519,6 +535,7 @@ static int grid_common(gs_ctx* ctx, GridArgs& a, int n_psr, int n_chain, int n_f
   if (!grid3) return fail_arg(8, "grid3 is NULL");
   if (!x || !xcol) return fail_arg(12, "x/xcol is NULL");
   a.n_psr = n_psr; a.n_chain = n_chain; a.n_f = n_f; a.ngrid = ngrid; a.ldx = ldx; a.sweep = sweep;
+  a.sweep_dev = ctx->sweep_dev;
   a.chain_base = chain_base; a.tau = tau; a.irn = irn; a.grid3 = grid3; a.u = u; a.xcol = xcol; a.x = x;
   a.idx_out = idx_out; a.key = key_of(ctx); a.psr_base = ctx->psr_base;
   return 0;
@@ -654,6 +671,7 @@ int gs_white_mh(gs_ctx* ctx, int n_psr, int n_chain, const gs_white_desc* wdesc,
   a.x_per_sys = ctx->x_per_sys;
   a.n_psr = n_psr; a.n_chain = n_chain; a.ldx = ldx; a.n_steps = n_steps; a.psr_base = ctx->psr_base;
   a.ldy = ldy; a.sweep = sweep; a.chain_base = chain_base;
+  a.sweep_dev = ctx->sweep_dev;
   a.wdesc = wdesc; a.wcol = wcol; a.wkind = wkind; a.wbk = wbk; a.nsteps_chain = nsteps_chain;
   a.wmin = wmin; a.wmax = wmax; a.sigma2 = sigma2; a.y = y; a.inj = inj;
   a.x = x; a.q_rec = q_rec; a.n_acc = n_acc; a.key = key_of(ctx);

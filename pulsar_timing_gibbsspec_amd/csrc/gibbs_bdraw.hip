@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
     zF = lane < NF ? A.z[sys * A.ldb + fi] : 0.0;
     zM = lane < nM ? A.z[sys * A.ldb + mi] : 0.0;
   } else {
-    gs_normal2(gs_counter(lane, A.sweep, A.chain_base + c, p + A.psr_base, A.event), A.key, zF, zM);
+    gs_normal2(gs_counter(lane, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, p + A.psr_base, A.event), A.key, zF, zM);
   }
   double bF = 0.0, bM = 0.0;
   double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * GS_SCR_DOUBLES(BC);
@@ -384,7 +384,7 @@ __global__ void k_rho_analytic(RhoArgs A) {
     U = A.u[sys * NFR + k];
   } else {
     double u2;
-    gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, p + A.psr_base, GS_EV_RHO), A.key, U, u2);
+    gs_uniform2(gs_counter(k, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, p + A.psr_base, GS_EV_RHO), A.key, U, u2);
   }
   const double hi = 1 - exp((tau / A.rhomax) - (tau / A.rhomin));
   const double eta = 0.0 + hi * U;

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(64 * BIG_WPB) void k_bdraw_big(BdrawArgs A, double*
   } else {
     for (int j = lane; 2 * j < NF + nM; j += 64) {
       double n1, n2;
-      gs_normal2(gs_counter(j, A.sweep, A.chain_base + ch, p + A.psr_base, A.event), A.key, n1, n2);
+      gs_normal2(gs_counter(j, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + ch, p + A.psr_base, A.event), A.key, n1, n2);
       zb[2 * j] = n1;
       if (2 * j + 1 < NF + nM) zb[2 * j + 1] = n2;
     }

@@ -75,6 +75,12 @@ __device__ __forceinline__ gs_u4 gs_counter(uint32_t slot, long long sweep, long
   return c;
 }
 
+// Sweep index of a Philox counter: the launch argument, plus the context's device-side
+// sweep counter when one is attached (graph-captured sweeps advance it on the device).
+__device__ __forceinline__ long long gs_sweep(int64_t s, const int64_t* dev) {
+  return dev ? (long long)(s + *dev) : (long long)s;
+}
+
 // Two uniforms in [0,1) for one counter.
 __device__ __forceinline__ void gs_uniform2(gs_u4 c, gs_key k, double& u1, double& u2) {
   const gs_u4 w = philox4x32_10(c, k.k0, k.k1);

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(64 * GS_CURN_WPB) void k_rho_curn(GridArgs A) {
     u = A.u[(int64_t)c * A.n_f + k];
   } else {
     double u2;
-    gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, 0, GS_EV_CURN), A.key, u, u2);
+    gs_uniform2(gs_counter(k, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, 0, GS_EV_CURN), A.key, u, u2);
   }
   const double total = pdf[A.ngrid - 1];
   int cnt = 0;
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void k_rho_curn_sum(GridArgs A) {
     u = A.u[(int64_t)c * A.n_f + k];
   } else {
     double u2;
-    gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, 0, GS_EV_CURN), A.key, u, u2);
+    gs_uniform2(gs_counter(k, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, 0, GS_EV_CURN), A.key, u, u2);
   }
   int cnt = 0;  // searchsorted(cdf / total, u, 'left'): points with cdf / total < u
 #pragma unroll
@@ -221,7 +221,7 @@ __global__ void k_rho_red(GridArgs A) {
     u = A.u[((int64_t)c * A.n_psr + p) * A.n_f + k];
   } else {
     double u2;
-    gs_uniform2(gs_counter(k, A.sweep, A.chain_base + c, p + A.psr_base, GS_EV_RED), A.key, u, u2);
+    gs_uniform2(gs_counter(k, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, p + A.psr_base, GS_EV_RED), A.key, u, u2);
   }
   const double tau = A.tau[r];
   const double gw = A.irn[(int64_t)k * A.n_chain + c];
@@ -286,7 +286,7 @@ __global__ void k_rho_gumbel(GridArgs A) {
       u = A.u[((int64_t)c * A.n_f + k) * A.ngrid + g];
     } else {
       double u2;
-      gs_uniform2(gs_counter((uint32_t)(k * 1024 + g), A.sweep, A.chain_base + c, 0, GS_EV_GUMBEL), A.key,
+      gs_uniform2(gs_counter((uint32_t)(k * 1024 + g), gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, 0, GS_EV_GUMBEL), A.key,
                   u, u2);
     }
     const double lr = ltau - np_logaddexp(lirn, A.grid3[A.ngrid + g]);
@@ -343,6 +343,10 @@ __global__ void k_pta_gate_phiinv(PtaGateArgs A) {
   }
 }
 
+__global__ void k_counter_add(int64_t* counter, int64_t inc) {
+  if (threadIdx.x == 0) *counter += inc;
+}
+
 inline dim3 grid1(int64_t n, int bs) { return dim3((unsigned)((n + bs - 1) / bs)); }
 
 }  // namespace
@@ -359,6 +363,11 @@ int launch_rho_curn(hipStream_t s, const GridArgs& a) {
   if (n == 0) return 0;
   const size_t lds = (size_t)GS_CURN_WPB * a.ngrid * sizeof(double);
   hipLaunchKernelGGL(k_rho_curn, grid1(n, GS_CURN_WPB), dim3(64 * GS_CURN_WPB), lds, s, a);
+  return 0;
+}
+
+int launch_counter_add(hipStream_t s, int64_t* counter, int64_t inc) {
+  hipLaunchKernelGGL(k_counter_add, dim3(1), dim3(64), 0, s, counter, inc);
   return 0;
 }
 

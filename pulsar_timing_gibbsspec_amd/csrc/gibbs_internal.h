@@ -37,6 +37,7 @@ struct BdrawArgs {
   int model_per_sys;  // 1: model block per (pulsar, chain) system, read from global
   int mask_per_sys;   // chain_mask indexed by system (GS_OPT_X_PER_SYS)
   int64_t mstride, sweep, chain_base;
+  const int64_t* sweep_dev;  // ctx sweep counter (graph replay) or NULL
   const double* model;
   const int32_t *fidx, *midx, *nm, *chain_mask;
   const double *phiinv_F, *z;
@@ -60,6 +61,7 @@ struct SweepArgs {
 struct RhoArgs {
   int n_psr, n_chain, NF, ldb, ldx, psr_base;
   int64_t sweep, chain_base;
+  const int64_t* sweep_dev;  // ctx sweep counter (graph replay) or NULL
   double rhomin, rhomax;
   const int32_t* fidx;
   const double *b, *u;
@@ -85,6 +87,7 @@ struct TauArgs {
 struct GridArgs {
   int n_psr, n_chain, n_f, ngrid, ldx, psr_base;
   int64_t sweep, chain_base;
+  const int64_t* sweep_dev;  // ctx sweep counter (graph replay) or NULL
   const double *tau, *irn, *grid3, *u;
   const int32_t* xcol;
   double* x;
@@ -92,6 +95,7 @@ struct GridArgs {
   gs_key key;
 };
 
+int launch_counter_add(hipStream_t s, int64_t* counter, int64_t inc);
 int launch_tau_sum(hipStream_t s, int n_psr, int64_t nrow, const double* tau, double* S);
 int launch_rho_curn_sum(hipStream_t s, const GridArgs& a);
 
@@ -116,6 +120,7 @@ struct WhiteMhArgs {
   int n_psr, n_chain, ldx, n_steps, psr_base;
   int x_per_sys;  // GS_OPT_X_PER_SYS
   int64_t ldy, sweep, chain_base;
+  const int64_t* sweep_dev;  // ctx sweep counter (graph replay) or NULL
   const gs_white_desc* wdesc;
   const int32_t *wcol, *wkind, *wbk, *nsteps_chain;
   const double *wmin, *wmax, *sigma2, *y, *inj;

@@ -120,9 +120,9 @@ __global__ __launch_bounds__(64 * MH_WPB) void k_white_mh(WhiteMhArgs A) {
     } else {
       double u1, u2, v1, v2, u4;
       const int ps = p + A.psr_base;
-      gs_uniform2(gs_counter(3u * st, A.sweep, gchain, ps, GS_EV_WHITE), A.key, u1, u2);
-      gs_uniform2(gs_counter(3u * st + 1, A.sweep, gchain, ps, GS_EV_WHITE), A.key, v1, v2);
-      gs_uniform2(gs_counter(3u * st + 2, A.sweep, gchain, ps, GS_EV_WHITE), A.key, u, u4);
+      gs_uniform2(gs_counter(3u * st, gs_sweep(A.sweep, A.sweep_dev), gchain, ps, GS_EV_WHITE), A.key, u1, u2);
+      gs_uniform2(gs_counter(3u * st + 1, gs_sweep(A.sweep, A.sweep_dev), gchain, ps, GS_EV_WHITE), A.key, v1, v2);
+      gs_uniform2(gs_counter(3u * st + 2, gs_sweep(A.sweep, A.sweep_dev), gchain, ps, GS_EV_WHITE), A.key, u, u4);
       sc = scale_choice(u1);
       w = min((int)(u2 * nw), nw - 1);
       z = sqrt(-2.0 * log(1.0 - v1)) * cospi(2.0 * v2);

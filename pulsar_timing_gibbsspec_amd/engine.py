@@ -390,6 +390,47 @@ class PTAChains:
         self._bdraw(z, _lib.EV_B, self.gate)                   # pta_gibbs.py:704
         self.it += 1
 
+    def capture(self, n_sweeps):
+        """Capture n_sweeps steady-state sweeps (device Philox, unsharded) into a hipGraph
+        (torch.cuda.CUDAGraph around the C-ABI launches on the context's stream).
+
+        Philox counters take sweep = launch argument + a device counter
+        (gs_ctx_set_sweep_counter), which the graph advances itself (gs_counter_add),
+        so every replay draws the next n_sweeps sweeps: replays are bit-identical to
+        eager sweeps.  The graph records x into ``graph_rec`` (n_sweeps, C, n_param)."""
+        if self.it == 0:
+            raise ValueError("run sweep 0 eagerly first (it draws b from x0, pta_gibbs.py:669-670)")
+        if self.sharded:
+            raise NotImplementedError("graph capture of the pulsar-sharded exchange")
+        lib, h, dev = self.ctx.lib, self.ctx.handle, self.ctx.device
+        n = int(n_sweeps)
+        self.graph_rec = torch.empty(n, self.C, self.n_param, dtype=torch.float64, device=dev)
+        self._gcount = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._gbase, self._gn = self.it, n
+        cap = torch.cuda.Stream(device=dev)
+        old = self.ctx.stream
+        cap.wait_stream(old)
+        self.ctx.set_stream(cap)
+        check(lib.gs_ctx_set_sweep_counter(h, ptr(self._gcount)), "gs_ctx_set_sweep_counter")
+        self.graph = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(self.graph, stream=cap):
+                for i in range(n):
+                    self.sweep(x_rec=self.graph_rec[i])
+                check(lib.gs_counter_add(h, ptr(self._gcount), n), "gs_counter_add")
+        finally:
+            check(lib.gs_ctx_set_sweep_counter(h, None), "gs_ctx_set_sweep_counter")
+            self.ctx.set_stream(old)
+            self.it = self._gbase          # nothing ran during capture
+        return self.graph_rec
+
+    def replay(self):
+        """Run the captured sweeps once (the next n_sweeps sweeps); returns graph_rec."""
+        self._gcount.fill_(self.it - self._gbase)   # stays right if eager sweeps ran between
+        self.graph.replay()
+        self.it += self._gn
+        return self.graph_rec
+
     def sweep(self, x_rec=None, z0=None, z=None, u_red=None, u_curn=None):
         """One PTABlockGibbs sweep for every chain; x_rec: (n_chain, n_param) row or None.
         z0/z: (P*n_chain, ldb) injected normals (original column order); u_red

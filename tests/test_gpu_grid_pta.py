@@ -290,3 +290,40 @@ def test_curn_sum_sharded_engine_matches_unsharded():
     assert torch.equal(xr[0], xr_ref)
     gw = xr_ref[:, :, rind].cpu().numpy()
     assert np.isfinite(gw).all() and (gw >= -9).all() and (gw <= -4).all()
+
+
+@pytest.mark.parametrize("kind,mode", [("curn", "sum"), ("curn_red", "exact")])
+def test_graph_replay_equals_eager_sweeps(kind, mode):
+    """hipGraph-captured sweeps (device sweep counter advanced inside the graph) replay
+    to the same chains as eager sweeps, replay after replay."""
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
+    pta = synthetic.array_pta(kind=kind, n_psr=7, seed=4)
+    T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
+    names = pta.param_names
+    rind = [i for i, n in enumerate(names) if "rho" in n and "gw" in n]
+    hind = np.array([i for i, n in enumerate(names) if "red" in n and "rho" in n])
+    red_col = hind.reshape(len(T), -1) if kind == "curn_red" else None
+    gwid = [np.arange(t.shape[1] - 60, t.shape[1]) for t in T]
+    fixed = [np.full(t.shape[1] - 60, 1e-40) for t in T]
+    C, K = 8, 4
+    x0 = np.random.default_rng(1).uniform(-9, -4, (C, len(names)))
+    bounds = ((1e-18, 1e-8), (1e-20, 1e-8))
+
+    def engine():
+        ctx = _lib.Context(0, seed=5)
+        return PTAChains(DeviceModel(ctx, T, N, R, gwid, fixed), len(names), rind, red_col, *bounds, C, x0,
+                         curn_mode=mode)
+    ref = engine()
+    xr = torch.zeros(1 + 3 * K, C, len(names), dtype=torch.float64, device="cuda")
+    for i in range(1 + 3 * K):
+        ref.sweep(x_rec=xr[i])
+    g = engine()
+    xg = torch.zeros_like(xr)
+    g.sweep(x_rec=xg[0])
+    g.capture(K)
+    for r in range(3):
+        g.replay()
+        xg[1 + r * K:1 + (r + 1) * K].copy_(g.graph_rec)
+    torch.cuda.synchronize()
+    assert torch.equal(xg, xr)
