@@ -148,7 +148,7 @@ def pta_cpu_baseline(kind, seconds=10.0):
                        f"pta_gibbs.py:664-704, numpy SVD, 1 thread) in {el:.1f} s")
 
 
-def bench_pta(kind, C, K, W, rank, world, dev, ctx, curn_mode="exact"):
+def bench_pta(kind, C, K, W, rank, world, dev, ctx, curn_mode="exact", graph=True):
     """Configs 4a/4b: PTAChains over the 45 simulated pulsars, C chains per GPU (chain-sharded)."""
     from pulsar_timing_gibbsspec_amd import synthetic
     from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
@@ -163,14 +163,19 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, curn_mode="exact"):
     eng = PTAChains(model, len(names), rind, hind.reshape(len(T), -1) if kind == "curn_red" else None,
                     (1e-18, 1e-8), (1e-20, 1e-8), C, x0, chain_base=rank * C, curn_mode=curn_mode)
     rec = torch.empty(K, C, len(names), dtype=torch.float64, device=dev)
-    for _ in range(W):
+    for _ in range(max(1, W)):
         eng.sweep(x_rec=rec[0])
+    if graph:                              # the K timed sweeps as one hipGraph replay
+        eng.capture(K)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for i in range(K):
-        eng.sweep(x_rec=rec[i])
+    if graph:
+        eng.replay()
+    else:
+        for i in range(K):
+            eng.sweep(x_rec=rec[i])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -182,7 +187,7 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, curn_mode="exact"):
     if eng.info.cpu().numpy().any():
         raise RuntimeError("non-PD Sigma in the PTA bench")
     return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
-                chains_per_gpu=C, n_psr=len(T), n_param=len(names))
+                chains_per_gpu=C, n_psr=len(T), n_param=len(names), hipgraph=bool(graph))
 
 
 def config5_cpu_baseline(seconds=10.0):
@@ -306,6 +311,8 @@ def main():
     ap.add_argument("--pta-chains", type=int, default=256)
     ap.add_argument("--pta-steps", type=int, default=20)
     ap.add_argument("--config5", type=int, default=1, help="measure BASELINE configs[4] too (1/0)")
+    ap.add_argument("--pta-graph", type=int, default=0, help="time the PTA sweeps as a hipGraph replay (1/0); "
+                    "measured no faster: the sweeps are GPU-bound and eager launches queue ahead")
     ap.add_argument("--c5-chains", type=int, default=16)
     ap.add_argument("--c5-steps", type=int, default=5)
     args = ap.parse_args()
@@ -409,7 +416,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     for kind in [k for k in args.pta.split(",") if k and k != "none"]:
         mode = "sum" if kind == "curn" else "exact"
-        sec = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, curn_mode=mode)
+        sec = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, curn_mode=mode,
+                        graph=bool(args.pta_graph))
         if rank == 0:
             sec["config"] = (f"configs[3]: 45-pulsar CURN{' + per-pulsar red' if kind == 'curn_red' else ''} "
                              f"free spectrum, chain-sharded, common draw {mode}")
