@@ -224,10 +224,12 @@ class PTABlockGibbs(object):
         return eng.x[0].cpu().numpy()
 
     # ------------------------------------------------------------ loop
-    def sample(self, xs, outdir="./", niter=10000, resume=False, save_every=100):
+    def sample(self, xs, outdir="./", niter=10000, resume=False, save_every=100, *, flush_final=False):
         """PTABlockGibbs.sample (pta_gibbs.py:631-713): chain row ii = state before sweep ii;
         chain.txt (chain 0) rewritten with rows [:ii+1] at ii % 100 == 0, ii > 0;
-        with nchains > 1 also chains.npy (leading chain axis)."""
+        with nchains > 1 also chains.npy (leading chain axis).  flush_final=True also
+        writes the rows after the last multiple of save_every (the reference
+        drops them, Appendix A.8)."""
         print(f"Creating chain directory: {outdir}")
         os.makedirs(outdir, exist_ok=True)
         self._check_supported()
@@ -272,6 +274,10 @@ class PTABlockGibbs(object):
                 np.savetxt(f"{outdir}/chain.txt", self.chain[:last + 1, :])
                 if nc > 1:
                     np.save(f"{outdir}/chains.npy", self.chains[:, :last + 1])
+        if flush_final:
+            np.savetxt(f"{outdir}/chain.txt", self.chain[:self.iter + 1, :])
+            if nc > 1:
+                np.save(f"{outdir}/chains.npy", self.chains[:, :self.iter + 1])
         b = eng.b.cpu().numpy()
         self._b = [b[p * eng.C, :eng.model.m[p]] for p in range(eng.P)]
         if eng.info.cpu().numpy().any():

@@ -340,7 +340,7 @@ class PulsarBlockGibbs(object):
         if not self._white_loop() and not np.array_equal(gwind, np.arange(len(self.gwid) // 2)):
             raise NotImplementedError("gw rho parameters must be the whole parameter vector")
 
-    def sample(self, xs, outdir="./", niter=10000, resume=False, save_every=100):
+    def sample(self, xs, outdir="./", niter=10000, resume=False, save_every=100, *, flush_final=False):
         """PulsarBlockGibbs.sample (pulsar_gibbs.py:620-710) as persistent device sweeps.
 
         Chain row ii holds the state BEFORE sweep ii (row 0 = xs, bchain[0] = 0).
@@ -354,7 +354,10 @@ class PulsarBlockGibbs(object):
         np.savetxt(f"{outdir}/pars_bchain.txt", self.b_param_names, fmt="%s")
 
         if self._white_loop():
-            return self._sample_white(xs, outdir, niter, resume, save_every)
+            out = self._sample_white(xs, outdir, niter, resume, save_every)
+            if flush_final:
+                self._flush(outdir)
+            return out
         model = self._model(xs)
         nc = self.nchains
         self.chain = np.zeros((niter, len(xs)))
@@ -421,7 +424,19 @@ class PulsarBlockGibbs(object):
             print(f"WARNING: {int((info != 0).sum())} chains hit a non-positive-definite Sigma")
         self._b = runner.b[0, :m].cpu().numpy()
         self._runner = runner
+        if flush_final:
+            self._flush(outdir)
         return self.chain
+
+    def _flush(self, outdir):
+        """flush_final=True: also write the rows after the last multiple of
+        save_every, which the reference never saves (pulsar_gibbs.py:701-710, Appendix A.8)."""
+        n = self.iter + 1
+        np.save(f"{outdir}/chain.npy", self.chain[:n, :])
+        np.save(f"{outdir}/bchain.npy", self.bchain[:n, :])
+        if self.chains is not None:
+            np.save(f"{outdir}/chains.npy", self.chains[:, :n])
+            np.save(f"{outdir}/bchains.npy", self.bchains[:, :n])
 
     def _sample_white(self, xs, outdir, niter, resume, save_every):
         """sample() with the white-noise MH block (pulsar_gibbs.py:656-698): one device

@@ -196,3 +196,21 @@ def test_pulsar_block_gibbs_surface(tmp_path):
     assert np.array_equal(gb2.chain[0], g["x0"]) and np.all(gb2.bchain[0] == 0)
     assert open(tmp_path / "pars_chain.txt").read().split()[0] == "gw_log10_rho_0"
     assert np.all(np.isfinite(gb2.chain)) and np.all(gb2.chain >= -9.0) and np.all(gb2.chain <= -4.0)
+
+
+def test_sample_flush_final_and_resume(tmp_path):
+    """flush_final writes the trailing partial block; resume continues from
+    the saved rows and reproduces the uninterrupted chain (device Philox counters are
+    indexed by the global sweep)."""
+    from pulsar_timing_gibbsspec_amd import PulsarBlockGibbs, synthetic
+    g = golden("single_j1713.npz")
+    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0)
+    full = PulsarBlockGibbs(pta, seed=8).sample(g["x0"], outdir=str(tmp_path / "a"), niter=260,
+                                                 flush_final=True)
+    assert np.load(tmp_path / "a" / "chain.npy").shape == (260, 30)
+    gb = PulsarBlockGibbs(pta, seed=8)
+    gb.sample(g["x0"], outdir=str(tmp_path / "b"), niter=150)          # saves rows [:101]
+    assert np.load(tmp_path / "b" / "chain.npy").shape == (101, 30)
+    res = PulsarBlockGibbs(pta, seed=8).sample(g["x0"], outdir=str(tmp_path / "b"), niter=260, resume=True,
+                                                flush_final=True)
+    assert np.array_equal(res, full)
