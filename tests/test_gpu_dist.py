@@ -1,0 +1,90 @@
+"""Pulsar-sharded PTA engine across two PROCESSES on the one GPU (gloo carries the
+exchange: distributed.PulsarAllGather for CURN+red, distributed.TauSumAllReduce for
+CURN without red noise), against the unsharded engine.  On a node the same code runs
+one process per GPU over RCCL (backend 'nccl')."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from tests.conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _setup(kind):
+    from pulsar_timing_gibbsspec_amd import synthetic
+    pta = synthetic.array_pta(kind=kind, n_psr=8, seed=3)
+    T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
+    names = pta.param_names
+    rind = [i for i, n in enumerate(names) if "rho" in n and "gw" in n]
+    hind = np.array([i for i, n in enumerate(names) if "red" in n and "rho" in n])
+    red_col = hind.reshape(len(T), -1) if kind == "curn_red" else None
+    gwid = [np.arange(t.shape[1] - 60, t.shape[1]) for t in T]
+    fixed = [np.full(t.shape[1] - 60, 1e-40) for t in T]
+    return T, N, R, names, rind, red_col, gwid, fixed
+
+
+def _worker(rank, world, port, kind, mode, S, out_dir):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pulsar_timing_gibbsspec_amd import _lib
+        from pulsar_timing_gibbsspec_amd.distributed import PulsarAllGather, TauSumAllReduce, shard_range
+        from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
+        T, N, R, names, rind, red_col, gwid, fixed = _setup(kind)
+        C = 8
+        x0 = np.random.default_rng(0).uniform(-9, -4, (C, len(names)))
+        lo, hi = shard_range(len(T), rank, world)
+        ctx = _lib.Context(0, seed=31)
+        mdl = DeviceModel(ctx, T[lo:hi], N[lo:hi], R[lo:hi], gwid[lo:hi], fixed[lo:hi])
+        assign = [np.arange(*shard_range(len(T), r, world)) for r in range(world)]
+        ex = dict(allreduce=TauSumAllReduce()) if mode == "sum" else \
+            dict(gather=PulsarAllGather(assign, ((2 if red_col is not None else 1), 30, C), device="cuda"))
+        eng = PTAChains(mdl, len(names), rind, red_col, (1e-18, 1e-8), (1e-20, 1e-8), C, x0,
+                        P_global=len(T), psr_lo=lo, curn_mode=mode, **ex)
+        xr = torch.zeros(S, C, len(names), dtype=torch.float64, device="cuda")
+        for i in range(S):
+            eng.sweep(x_rec=xr[i])
+        np.save(os.path.join(out_dir, f"x{rank}.npy"), xr.cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,mode", [("curn", "sum"), ("curn_red", "exact")])
+def test_pulsar_sharded_two_processes(tmp_path, kind, mode):
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch
+    import torch.multiprocessing as mp
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
+    S = 5
+    ctxm = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctxm.Process(target=_worker, args=(r, 2, port, kind, mode, S, str(tmp_path))) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    T, N, R, names, rind, red_col, gwid, fixed = _setup(kind)
+    C = 8
+    x0 = np.random.default_rng(0).uniform(-9, -4, (C, len(names)))
+    ref = PTAChains(DeviceModel(_lib.Context(0, seed=31), T, N, R, gwid, fixed), len(names), rind, red_col,
+                    (1e-18, 1e-8), (1e-20, 1e-8), C, x0, curn_mode=mode)
+    xr = torch.zeros(S, C, len(names), dtype=torch.float64, device="cuda")
+    for i in range(S):
+        ref.sweep(x_rec=xr[i])
+    want = xr.cpu().numpy()
+    for r in range(2):
+        assert np.array_equal(np.load(tmp_path / f"x{r}.npy"), want), r
