@@ -148,9 +148,14 @@ def pta_cpu_baseline(kind, seconds=10.0):
                        f"pta_gibbs.py:664-704, numpy SVD, 1 thread) in {el:.1f} s")
 
 
-def bench_pta(kind, C, K, W, rank, world, dev, ctx, curn_mode="exact", graph=True):
-    """Configs 4a/4b: PTAChains over the 45 simulated pulsars, C chains per GPU (chain-sharded)."""
+def bench_pta(kind, C, K, W, rank, world, dev, ctx, curn_mode="exact", graph=True, shard="chain"):
+    """Configs 3/4: PTAChains over the 45 simulated pulsars.  shard='chain': C chains per
+    GPU, no collective (weak).  shard='pulsar' (N > 1): every rank runs the same C chains
+    over its pulsar block (balanced by m^3) and exchanges per sweep over RCCL -- the
+    tau-sum all-reduce for CURN (sufficient statistic) or the [tau | x_red] all-gather for
+    CURN + red (strong scaling over pulsars)."""
     from pulsar_timing_gibbsspec_amd import synthetic
+    from pulsar_timing_gibbsspec_amd.distributed import PulsarAllGather, TauSumAllReduce
     from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
     pta = synthetic.array_pta(kind=kind, seed=0)
     T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
@@ -158,10 +163,26 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, curn_mode="exact", graph=Tru
     rind = [i for i, n in enumerate(names) if "rho" in n and "gw" in n]
     hind = np.array([i for i, n in enumerate(names) if "red" in n and "rho" in n])
     gwid = [np.arange(t.shape[1] - 60, t.shape[1]) for t in T]
-    model = DeviceModel(ctx, T, N, R, gwid, [np.full(t.shape[1] - 60, 1e-40) for t in T])
-    x0 = np.random.default_rng(rank).uniform(-9, -4, (C, len(names)))
-    eng = PTAChains(model, len(names), rind, hind.reshape(len(T), -1) if kind == "curn_red" else None,
-                    (1e-18, 1e-8), (1e-20, 1e-8), C, x0, chain_base=rank * C, curn_mode=curn_mode)
+    fixed = [np.full(t.shape[1] - 60, 1e-40) for t in T]
+    red_col = hind.reshape(len(T), -1) if kind == "curn_red" else None
+    sharded = shard == "pulsar" and world > 1
+    if sharded:
+        lo, hi = _contiguous_balanced(np.array([t.shape[1] ** 3 for t in T], float), rank, world)
+        model = DeviceModel(ctx, T[lo:hi], N[lo:hi], R[lo:hi], gwid[lo:hi], fixed[lo:hi])
+        x0 = np.random.default_rng(0).uniform(-9, -4, (C, len(names)))
+        bounds = [_contiguous_balanced(np.array([t.shape[1] ** 3 for t in T], float), r, world)
+                  for r in range(world)]
+        assign = [np.arange(a, b) for a, b in bounds]
+        ex = dict(allreduce=TauSumAllReduce()) if curn_mode == "sum" else \
+            dict(gather=PulsarAllGather(assign, ((2 if red_col is not None else 1), 30, C), device=dev))
+        eng = PTAChains(model, len(names), rind, red_col, (1e-18, 1e-8), (1e-20, 1e-8), C, x0,
+                        P_global=len(T), psr_lo=lo, curn_mode=curn_mode, **ex)
+        graph = False
+    else:
+        model = DeviceModel(ctx, T, N, R, gwid, fixed)
+        x0 = np.random.default_rng(rank).uniform(-9, -4, (C, len(names)))
+        eng = PTAChains(model, len(names), rind, red_col, (1e-18, 1e-8), (1e-20, 1e-8), C, x0,
+                        chain_base=rank * C, curn_mode=curn_mode)
     rec = torch.empty(K, C, len(names), dtype=torch.float64, device=dev)
     for _ in range(max(1, W)):
         eng.sweep(x_rec=rec[0])
@@ -186,8 +207,22 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, curn_mode="exact", graph=Tru
         el = float(t.item())
     if eng.info.cpu().numpy().any():
         raise RuntimeError("non-PD Sigma in the PTA bench")
-    return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
-                chains_per_gpu=C, n_psr=len(T), n_param=len(names), hipgraph=bool(graph))
+    total_chains = C if sharded else C * world
+    return dict(value=total_chains * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+                chains_per_gpu=C, n_psr=len(T), n_param=len(names), hipgraph=bool(graph),
+                sharding=("pulsars over %d GPUs (RCCL %s per sweep), strong" %
+                          (world, "all-reduce" if curn_mode == "sum" else "all-gather")) if sharded
+                else "chains, weak")
+
+
+def _contiguous_balanced(w, rank, world):
+    """Contiguous pulsar block of this rank with ~equal sum of weights (m^3 ~ b|rho cost)."""
+    cw = np.concatenate([[0.0], np.cumsum(w)])
+    cuts = [int(np.searchsorted(cw, cw[-1] * r / world)) for r in range(world + 1)]
+    cuts[0], cuts[-1] = 0, len(w)
+    for r in range(1, world):                     # every rank keeps at least one pulsar
+        cuts[r] = min(max(cuts[r], cuts[r - 1] + 1), len(w) - (world - r))
+    return cuts[rank], cuts[rank + 1]
 
 
 def config5_cpu_baseline(seconds=10.0):
@@ -313,6 +348,7 @@ def main():
     ap.add_argument("--config5", type=int, default=1, help="measure BASELINE configs[4] too (1/0)")
     ap.add_argument("--pta-graph", type=int, default=0, help="time the PTA sweeps as a hipGraph replay (1/0); "
                     "measured no faster: the sweeps are GPU-bound and eager launches queue ahead")
+    ap.add_argument("--pta-shard", default="chain", help="chain | pulsar: how N > 1 GPUs split the PTA configs")
     ap.add_argument("--c5-chains", type=int, default=16)
     ap.add_argument("--c5-steps", type=int, default=5)
     args = ap.parse_args()
@@ -320,9 +356,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU over RCCL; GS_DIST_BACKEND=gloo (and more ranks than GPUs, ranks
+    # sharing devices round-robin) only to rehearse the multi-rank paths on one GPU
+    backend = os.environ.get("GS_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -417,7 +461,7 @@ def main():
     for kind in [k for k in args.pta.split(",") if k and k != "none"]:
         mode = "sum" if kind == "curn" else "exact"
         sec = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, curn_mode=mode,
-                        graph=bool(args.pta_graph))
+                        graph=bool(args.pta_graph), shard=args.pta_shard)
         if rank == 0:
             sec["config"] = (f"configs[3]: 45-pulsar CURN{' + per-pulsar red' if kind == 'curn_red' else ''} "
                              f"free spectrum, chain-sharded, common draw {mode}")
