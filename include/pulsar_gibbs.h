@@ -55,12 +55,16 @@ enum {
                          of 8 SGPR pairs; 3 = 16x16 fp64 MFMA tiles (default) */
   GS_OPT_PSR_BASE = 2, /* global index of this context's pulsar 0 (Philox counters of a
                          pulsar-sharded run); default 0 */
-  GS_OPT_X_PER_SYS = 3 /* 0 (default): x holds one row per chain (a PTA's parameter vector,
+  GS_OPT_X_PER_SYS = 3, /* 0 (default): x holds one row per chain (a PTA's parameter vector,
                          pta_gibbs.py); 1: one row per (pulsar, chain) system, row
                          p * n_chain + c (independent pulsars, each its own
                          PulsarBlockGibbs, config 5).  Read by gs_white_mh, gs_white_tnt;
                          with 1, gs_bdraw*'s chain_mask and gs_white_mh's nsteps_chain
                          are indexed by system too. */
+  GS_OPT_GRID_EXACT = 4 /* gs_rho_curn: 1 = numpy's operation order (sequential product of
+                         per-pulsar pdfs, sequential cumsum: bit-identical pdfs); 0 (default)
+                         = log-space product (one log + one exp per grid point, rcp for the
+                         ratios), equal pdfs to ~1e-15 relative */
 };
 
 typedef struct gs_ctx gs_ctx;

@@ -21,6 +21,7 @@ LIB_PATH = os.environ.get("GS_LIB_PATH") or \
 OPT_BCAST = 1
 OPT_PSR_BASE = 2
 OPT_X_PER_SYS = 3
+OPT_GRID_EXACT = 4
 EV_B0, EV_RHO, EV_B, EV_RED, EV_CURN, EV_GUMBEL, EV_WHITE, EV_USER = 1, 2, 3, 4, 5, 6, 7, 16
 
 _P = C.c_void_p

@@ -13,6 +13,7 @@ struct gs_ctx {
   int bcast;     // GS_OPT_BCAST
   int psr_base;  // GS_OPT_PSR_BASE: global index of this shard's pulsar 0 (RNG counters)
   int x_per_sys = 0;  // GS_OPT_X_PER_SYS
+  int grid_exact = 0;  // GS_OPT_GRID_EXACT
   const int64_t* sweep_dev = nullptr;  // gs_ctx_set_sweep_counter
   double* ws = nullptr;  // tile workspace of the large-NF b-draw (grown on demand)
   size_t ws_bytes = 0;
@@ -295,6 +296,10 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
       if (value < 0 || value > (1 << 23)) return fail_arg(3, "GS_OPT_PSR_BASE out of range");
       ctx->psr_base = value;
       return 0;
+    case GS_OPT_GRID_EXACT:
+      if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_GRID_EXACT must be 0 or 1");
+      ctx->grid_exact = value;
+      return 0;
     case GS_OPT_X_PER_SYS:
       if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_X_PER_SYS must be 0 or 1");
       ctx->x_per_sys = value;
@@ -309,6 +314,7 @@ int gs_ctx_get_option(gs_ctx* ctx, int option) {
   if (option == GS_OPT_BCAST) return ctx->bcast;
   if (option == GS_OPT_PSR_BASE) return ctx->psr_base;
   if (option == GS_OPT_X_PER_SYS) return ctx->x_per_sys;
+  if (option == GS_OPT_GRID_EXACT) return ctx->grid_exact;
   return -1;
 }
 
@@ -538,6 +544,7 @@ static int grid_common(gs_ctx* ctx, GridArgs& a, int n_psr, int n_chain, int n_f
   a.sweep_dev = ctx->sweep_dev;
   a.chain_base = chain_base; a.tau = tau; a.irn = irn; a.grid3 = grid3; a.u = u; a.xcol = xcol; a.x = x;
   a.idx_out = idx_out; a.key = key_of(ctx); a.psr_base = ctx->psr_base;
+  a.exact = ctx->grid_exact;
   return 0;
 }
 

@@ -203,12 +203,126 @@ __global__ __launch_bounds__(256) void k_rho_curn_sum(GridArgs A) {
   }
 }
 
+// ------------------------------------------------------------ a6 fast: CURN product in log space
+// The same draw as k_rho_curn without numpy's operation order (GS_OPT_GRID_EXACT = 0,
+// the default): log pdf_g = -sum_p log(irn_p + rho_g) - 1/2 sum_p tau_p / (irn_p + rho_g)
+// + const (sum_p log tau_p and P log ln10 cancel in cdf / max).  Per (grid point, pulsar):
+// one add, one v_rcp_f64 + Newton step, one FMA into the ratio sum and one multiply into
+// the product of (irn + rho), renormalised by frexp every 8 pulsars -- instead of a
+// division and an exp; one log and one exp per grid point.  pdf rounding differs from
+// numpy's by ~1e-15 relative, so the index can only differ when u falls that close to a
+// cdf value (tested equal to the reference on every fixture sweep).  One wavefront per
+// row, lane l owns grid points [l G, (l+1) G), wave scan of the lane sums.
+constexpr int CF_MAXG = 16;  // grid points per lane (ngrid <= 1024)
+
+__global__ __launch_bounds__(256) void k_rho_curn_fast(GridArgs A) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t nrow = (int64_t)A.n_f * A.n_chain;
+  if (r >= nrow) return;
+  const int c = (int)(r % A.n_chain), k = (int)(r / A.n_chain);
+  const int G = (A.ngrid + 63) / 64;
+  const int g0 = lane * G;
+  double rg[CF_MAXG], prod[CF_MAXG], sr[CF_MAXG];
+  int ex[CF_MAXG];
+#pragma unroll
+  for (int j = 0; j < CF_MAXG; ++j) {
+    const int g = min(g0 + j, A.ngrid - 1);
+    rg[j] = A.grid3[g];
+    prod[j] = 1.0;
+    sr[j] = 0.0;
+    ex[j] = 0;
+  }
+  const int P = A.n_psr;
+  for (int p = 0; p < P; ++p) {
+    const double tau = A.tau[p * nrow + r];
+    const double irn = A.irn ? A.irn[p * nrow + r] : 0.0;
+#pragma unroll
+    for (int j = 0; j < CF_MAXG; ++j) {
+      const double a = irn + rg[j];
+      double ra = __builtin_amdgcn_rcp(a);
+      ra = fma(ra, fma(-a, ra, 1.0), ra);
+      ra = fma(ra, fma(-a, ra, 1.0), ra);
+      sr[j] = fma(tau, ra, sr[j]);
+      prod[j] *= a;
+    }
+    if ((p & 7) == 7 || p == P - 1) {
+#pragma unroll
+      for (int j = 0; j < CF_MAXG; ++j) {
+        ex[j] += __builtin_amdgcn_frexp_exp(prod[j]);
+        prod[j] = __builtin_amdgcn_frexp_mant(prod[j]);
+      }
+    }
+  }
+  constexpr double LN2 = 0.693147180559945309417232121458176568;
+  double lp[CF_MAXG];
+  double mx = -__builtin_inf();
+#pragma unroll
+  for (int j = 0; j < CF_MAXG; ++j) {
+    lp[j] = -__builtin_inf();
+    if (j < G && g0 + j < A.ngrid) {
+      lp[j] = -(log(prod[j]) + ex[j] * LN2) - 0.5 * sr[j];
+      mx = fmax(mx, lp[j]);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+  double loc = 0.0;
+#pragma unroll
+  for (int j = 0; j < CF_MAXG; ++j) {
+    if (j < G) {
+      loc += exp(lp[j] - mx);
+      lp[j] = loc;
+    }
+  }
+  double incl = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  const double off = incl - loc;
+  const double total = __shfl(incl, 63);
+  double u;
+  if (A.u) {
+    u = A.u[(int64_t)c * A.n_f + k];
+  } else {
+    double u2;
+    gs_uniform2(gs_counter(k, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, 0, GS_EV_CURN), A.key, u, u2);
+  }
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < CF_MAXG; ++j)
+    if (j < G && g0 + j < A.ngrid) cnt += ((off + lp[j]) / total < u) ? 1 : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if (lane == 0) {
+    int idx = cnt - 1;
+    if (idx < 0) idx += A.ngrid;
+    if (A.idx_out) A.idx_out[r] = idx;
+    A.x[(int64_t)c * A.ldx + A.xcol[k]] = A.grid3[2 * A.ngrid + idx];
+  }
+}
+
 // ------------------------------------------------------------ a7: red CDF
 // rows r = (p * n_f + k) * n_chain + c, one LANE per row; gw [n_f][n_chain] = phi_gw.
 // One pass over the grid keeps the (sequential, exact) running sum at 16 chunk
 // ends; the crossing chunk is then recomputed from its exact entry value, so the
 // cumsum seen at every compared position is bit-identical to np.cumsum.
 #define GS_RED_NCH 16
+// EXACT = false (GS_OPT_GRID_EXACT = 0, the default): ratio = tau * rcp(a) refined by two
+// Newton steps instead of the IEEE division (within an ulp of it; same index unless u falls
+// within ~1e-16 of a cdf value).
+template <bool EXACT>
+__device__ __forceinline__ double red_ratio(double tau, double a) {
+  if (EXACT) return tau / a;
+  double ra = __builtin_amdgcn_rcp(a);
+  ra = fma(ra, fma(-a, ra, 1.0), ra);
+  ra = fma(ra, fma(-a, ra, 1.0), ra);
+  return tau * ra;
+}
+
+template <bool EXACT>
 __global__ void k_rho_red(GridArgs A) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nrow = (int64_t)A.n_psr * A.n_f * A.n_chain;
@@ -232,7 +346,7 @@ __global__ void k_rho_red(GridArgs A) {
   for (int j = 0; j < GS_RED_NCH; ++j) {
     const int g1 = min(A.ngrid, (j + 1) * ch);
     for (int g = j * ch; g < g1; ++g) {
-      const double ratio = tau / (gw + A.grid3[g]);
+      const double ratio = red_ratio<EXACT>(tau, gw + A.grid3[g]);
       cum += ratio * exp(-ratio / 2) * LN10;
     }
     ck[j] = cum;
@@ -256,7 +370,7 @@ __global__ void k_rho_red(GridArgs A) {
     double cc = entry;
     const int g1 = min(A.ngrid, (jx + 1) * ch);
     for (int g = jx * ch; g < g1; ++g) {
-      const double ratio = tau / (gw + A.grid3[g]);
+      const double ratio = red_ratio<EXACT>(tau, gw + A.grid3[g]);
       cc += ratio * exp(-ratio / 2) * LN10;
       cnt += (cc / total < u) ? 1 : 0;
     }
@@ -361,6 +475,10 @@ int launch_tau(hipStream_t s, const TauArgs& a) {
 int launch_rho_curn(hipStream_t s, const GridArgs& a) {
   const int64_t n = (int64_t)a.n_f * a.n_chain;
   if (n == 0) return 0;
+  if (!a.exact && a.ngrid <= 64 * CF_MAXG) {
+    hipLaunchKernelGGL(k_rho_curn_fast, grid1(n, 4), dim3(256), 0, s, a);
+    return 0;
+  }
   const size_t lds = (size_t)GS_CURN_WPB * a.ngrid * sizeof(double);
   hipLaunchKernelGGL(k_rho_curn, grid1(n, GS_CURN_WPB), dim3(64 * GS_CURN_WPB), lds, s, a);
   return 0;
@@ -387,7 +505,10 @@ int launch_rho_curn_sum(hipStream_t s, const GridArgs& a) {
 int launch_rho_red(hipStream_t s, const GridArgs& a) {
   const int64_t n = (int64_t)a.n_psr * a.n_f * a.n_chain;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(k_rho_red, grid1(n, 64), dim3(64), 0, s, a);
+  if (a.exact)
+    hipLaunchKernelGGL(k_rho_red<true>, grid1(n, 64), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_rho_red<false>, grid1(n, 64), dim3(64), 0, s, a);
   return 0;
 }
 

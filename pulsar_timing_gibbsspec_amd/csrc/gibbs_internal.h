@@ -86,6 +86,7 @@ struct TauArgs {
 
 struct GridArgs {
   int n_psr, n_chain, n_f, ngrid, ldx, psr_base;
+  int exact;  // GS_OPT_GRID_EXACT: numpy's operation order (bit-exact pdfs)
   int64_t sweep, chain_base;
   const int64_t* sweep_dev;  // ctx sweep counter (graph replay) or NULL
   const double *tau, *irn, *grid3, *u;

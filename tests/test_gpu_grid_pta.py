@@ -62,10 +62,16 @@ def test_gumbel_kernel_exact(ctx):
     assert np.array_equal(x.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("grid_exact", [1, 0])
 @pytest.mark.parametrize("kind", ["curn", "curn_red"])
-def test_grid_cdf_kernels_exact(ctx, kind):
-    """a6 (and a7) on every sweep's recorded inputs: indices bit-exact."""
+def test_grid_cdf_kernels_exact(ctx, kind, grid_exact, request):
+    """a6 (and a7) on every sweep's recorded inputs: indices equal to the reference's.
+    grid_exact=1: numpy's operation order (bit-identical pdfs/cdfs); grid_exact=0 (the
+    default): log-space CURN product and rcp-Newton ratios (pdfs within ~1e-15 relative:
+    an index could differ only for u within that of a cdf value — none on the fixtures)."""
     from pulsar_timing_gibbsspec_amd import _lib
+    _lib.check(ctx.lib.gs_ctx_set_option(ctx.handle, _lib.OPT_GRID_EXACT, grid_exact), "set_option")
+    request.addfinalizer(lambda: ctx.lib.gs_ctx_set_option(ctx.handle, _lib.OPT_GRID_EXACT, 0))
     from pulsar_timing_gibbsspec_amd.engine import grid3
     g = golden(f"pta_{kind}.npz")
     *_, rec = pta_replay(g, kind)
