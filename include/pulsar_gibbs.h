@@ -45,6 +45,7 @@ enum {
   GS_EV_CURN = 5,   /* common grid-CDF uniforms          (pta_gibbs.py:209)        */
   GS_EV_GUMBEL = 6, /* Gumbel-max uniforms               (pulsar_gibbs.py:233)     */
   GS_EV_WHITE = 7,  /* white-noise MH draws              (pulsar_gibbs.py:377-398) */
+  GS_EV_REDMH = 8,  /* power-law red-noise MH draws      (pulsar_gibbs.py:312-319) */
   GS_EV_USER = 16   /* first id free for callers                                    */
 };
 
@@ -248,6 +249,33 @@ int gs_rho_red(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, 
 int gs_rho_gumbel(gs_ctx* ctx, int n_chain, int n_f, const double* tau, const double* irn, int ngrid,
                   const double* grid3, const double* u, int64_t sweep, int64_t chain_base, double* x,
                   int ldx, const int32_t* xcol, int32_t* idx_out);
+
+/*
+ *  Power-law intrinsic red noise, single pulsar (PulsarBlockGibbs with a red
+ * signal, pulsar_gibbs.py:271-329, 549-566).  One wavefront per chain.
+ * gs_red_mh: nsteps Metropolis steps on (log10_A, gamma) = x[c][red_col[0]], x[c][red_col[1]]
+ *   under the red-only likelihood get_lnlikelihood_red (:549-566)
+ *     lnL = sum_k lr_k - exp(lr_k),  lr_k = log tau_k - logaddexp(log irn_k, log 10^(2 x[c][gw_col[k]]))
+ *   with log irn_k = lnphi[k] + lnphi[n_f + k] log10_A + lnphi[2 n_f + k] gamma (the power law,
+ *   log-linear; lnphi [3 x n_f] probed on the host from the signal's get_phi) and tau
+ *   [n_f x n_chain] in the half convention (gs_tau half = 1).  Proposals (symmetric):
+ *   jump[12] = {U00, U01, U10, U11, sqrt S0, sqrt S1, P(SCAM), P(SCAM) + P(AM), lo_A, hi_A,
+ *   lo_gamma, hi_gamma} (U, S: SVD of the block's proposal covariance; the remainder of the
+ *   probability is the DE jump over de [nde x 2], nde >= 2 when used).  anchor = 1: every step
+ *   is accepted against the block's starting lnL (the reference discards PTMCMCOneStep's
+ *   returned state, :318-319); anchor = 0: against the current state.  Outputs: x (in place),
+ *   irn [n_f x n_chain] = phi_red at the final state (or NULL), lnl [n_chain] = lnL at the final
+ *   state (or NULL), n_acc [n_chain] accepted steps (or NULL).  nsteps = 0 evaluates only.
+ *   Philox event GS_EV_REDMH, slots 4 s .. 4 s + 3 of step s.  n_f <= 256.
+ * gs_gate_phiinv_irn: gs_pta_gate_phiinv for one pulsar with phi_F = 10**(2 x_gw) + irn
+ *   (enterprise sums the phis of signals sharing the Fourier basis).
+ */
+int gs_red_mh(gs_ctx* ctx, int n_chain, int n_f, int nsteps, int anchor, double* x, int ldx,
+              const int32_t* red_col, const int32_t* gw_col, const double* tau, const double* lnphi,
+              const double* jump, const double* de, int nde, int64_t sweep, int64_t chain_base, double* irn,
+              double* lnl, int32_t* n_acc);
+int gs_gate_phiinv_irn(gs_ctx* ctx, int n_chain, int n_f, int n_param, const double* x, const double* xlast,
+                       const int32_t* gw_col, const double* irn, double* phiinv_F, int32_t* gate);
 
 /* out[j][c] = 10**(2 x[c * ldx + cols[j]]): free-spectrum phi (sin column) from log10 rho. */
 int gs_phi_from_x(gs_ctx* ctx, int n_chain, int ncol, const double* x, int ldx, const int32_t* cols,

@@ -359,3 +359,82 @@ def white_mh(x, wind, steps, lnlike, lnprior):
         if diff > np.log(u):
             xnew, l0, p0 = q, l1, p1
     return xnew
+
+
+# ============================================================== power-law red MH
+EV_REDMH = 8
+
+
+def lnlike_red(b, gwid, irn, gwphi):
+    """get_lnlikelihood_red (pulsar_gibbs.py:549-566): tau = (b_sin^2 + b_cos^2)/2,
+    lr = log tau - logaddexp(log irn, log phi_gw), lnL = sum(lr - exp(lr))."""
+    tau = np.asarray(b)[gwid] ** 2
+    tau = (tau[::2] + tau[1::2]) / 2
+    logratio = np.log(tau) - np.logaddexp(np.log(irn), np.log(gwphi))
+    return np.sum(logratio - np.exp(logratio))
+
+
+def powerlaw_lnirn(lnphi, la, ga):
+    """log irn_k = (a_k la + c_k) + g_k ga: the power law's log-linear form (lnphi rows c, a, g)."""
+    return (lnphi[1] * la + lnphi[0]) + lnphi[2] * ga
+
+
+def red_mh_philox(x, ia, ig, gw_col, tau_half, lnphi, jump, de, nsteps, anchor, key, sweep, chain):
+    """The device red-noise Metropolis block (gs_red_mh) restated on the same Philox
+    stream.  Steady state of update_red_params (pulsar_gibbs.py:312-319): nsteps symmetric
+    jumps (SCAM / AM / DE mix restating PTMCMCSampler's, which is absent — parity of the
+    proposal law unpinned), each accepted if lnL(q) - lnL(ref) > log u with ref = the
+    block's starting point when anchor (the reference discards PTMCMCOneStep's returned
+    state, :318-319) or the current one.  Returns (x, lnL, n_acc, margins) where
+    margins[s] = |lnL(q) - lnL(ref) - log u| of each step (near-ties, for tests)."""
+    x = np.asarray(x, float).copy()
+    ltau = np.log(np.asarray(tau_half, float))
+    lgw = np.log(10.0 ** (2.0 * x[gw_col]))
+
+    def L(a, g):
+        lr = ltau - np.logaddexp(powerlaw_lnirn(lnphi, a, g), lgw)
+        return float(np.sum(lr - np.exp(lr)))
+
+    U00, U01, U10, U11, s0, s1, w_scam, w_am, lo0, hi0, lo1, hi1 = [float(v) for v in jump]
+    qa, qg = float(x[ia]), float(x[ig])
+    L0 = Lc = L(qa, qg)
+    acc, margins = 0, []
+    key = np.asarray(key, np.uint32)
+
+    def uni(slot):
+        ctr = np.array([slot, sweep & 0xffffffff, chain & 0xffffffff, EV_REDMH], np.uint32)
+        u1, u2 = philox_uniform_pair(ctr, key)
+        return float(u1), float(u2)
+
+    for s in range(nsteps):
+        u_kind, u_scale = uni(4 * s)
+        u_a, u_b = uni(4 * s + 1)
+        n1, n2 = (float(v) for v in box_muller(*uni(4 * s + 2)))
+        u_acc, u_de = uni(4 * s + 3)
+        scale = 10.0 if u_scale > 0.97 else (0.2 if u_scale > 0.9 else 1.0)
+        if u_kind < w_scam:
+            d1 = u_a >= 0.5
+            cd = 1.6970562748477141 * scale * (s1 if d1 else s0) * n1
+            da, dg = cd * (U01 if d1 else U00), cd * (U11 if d1 else U10)
+        elif u_kind < w_am:
+            cd = 1.2 * scale
+            z0, z1 = n1 * s0, n2 * s1
+            da, dg = cd * (U00 * z0 + U01 * z1), cd * (U10 * z0 + U11 * z1)
+        else:
+            n = len(de)
+            i = min(int(u_a * n), n - 1)
+            k = min(int(u_b * (n - 1)), n - 2)
+            k += k >= i
+            sc = 1.0 if u_de < 0.5 else u_scale * 1.2
+            da, dg = sc * (de[i][0] - de[k][0]), sc * (de[i][1] - de[k][1])
+        pa, pg = qa + da, qg + dg
+        inb = lo0 <= pa <= hi0 and lo1 <= pg <= hi1
+        L1 = L(pa, pg) if inb else -np.inf
+        ref = L0 if anchor else Lc
+        diff = L1 - ref
+        margins.append(abs(diff - np.log(u_acc)) if np.isfinite(diff) else np.inf)
+        if diff > np.log(u_acc):
+            qa, qg, Lc = pa, pg, L1
+            acc += 1
+    x[ia], x[ig] = qa, qg
+    return x, Lc, acc, np.array(margins)

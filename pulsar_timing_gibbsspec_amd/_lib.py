@@ -22,7 +22,7 @@ OPT_BCAST = 1
 OPT_PSR_BASE = 2
 OPT_X_PER_SYS = 3
 OPT_GRID_EXACT = 4
-EV_B0, EV_RHO, EV_B, EV_RED, EV_CURN, EV_GUMBEL, EV_WHITE, EV_USER = 1, 2, 3, 4, 5, 6, 7, 16
+EV_B0, EV_RHO, EV_B, EV_RED, EV_CURN, EV_GUMBEL, EV_WHITE, EV_REDMH, EV_USER = 1, 2, 3, 4, 5, 6, 7, 8, 16
 
 _P = C.c_void_p
 _I = C.c_int
@@ -65,6 +65,8 @@ SIGNATURES = {
     "gs_white_resid": (_I, [_P, _I, _I, _I64, _I, _P, _P, _P, _P, _I64, _P]),
     "gs_white_mh": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _I, _I, _P, _I64, _I64,
                          _P, _P, _P]),
+    "gs_red_mh": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _I, _I64, _I64, _P, _P, _P]),
+    "gs_gate_phiinv_irn": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "gs_white_tnt": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I64, _I64, _P, _P]),
 }
 

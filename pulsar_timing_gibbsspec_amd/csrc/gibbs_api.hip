@@ -644,9 +644,45 @@ int gs_pta_gate_phiinv(gs_ctx* ctx, int n_psr, int n_chain, int n_f, int n_param
   if (!x || !gw_col || !phiinv_F || !gate) return fail_arg(6, "NULL array");
   PtaGateArgs a;
   a.n_psr = n_psr; a.n_chain = n_chain; a.n_f = n_f; a.n_param = n_param; a.x = x; a.xlast = xlast;
-  a.gw_col = gw_col; a.red_col = red_col; a.phiinv_F = phiinv_F; a.gate = gate;
+  a.gw_col = gw_col; a.red_col = red_col; a.irn = nullptr; a.phiinv_F = phiinv_F; a.gate = gate;
   launch_pta_gate_phiinv(ctx->stream, a);
   return after_launch("k_pta_gate_phiinv");
+}
+
+int gs_gate_phiinv_irn(gs_ctx* ctx, int n_chain, int n_f, int n_param, const double* x, const double* xlast,
+                       const int32_t* gw_col, const double* irn, double* phiinv_F, int32_t* gate) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_chain < 0 || n_f <= 0 || n_param <= 0) return fail_arg(2, "bad size");
+  if (!x || !gw_col || !irn || !phiinv_F || !gate) return fail_arg(5, "NULL array");
+  PtaGateArgs a;
+  a.n_psr = 1; a.n_chain = n_chain; a.n_f = n_f; a.n_param = n_param; a.x = x; a.xlast = xlast;
+  a.gw_col = gw_col; a.red_col = nullptr; a.irn = irn; a.phiinv_F = phiinv_F; a.gate = gate;
+  launch_pta_gate_phiinv(ctx->stream, a);
+  return after_launch("k_pta_gate_phiinv");
+}
+
+int gs_red_mh(gs_ctx* ctx, int n_chain, int n_f, int nsteps, int anchor, double* x, int ldx,
+              const int32_t* red_col, const int32_t* gw_col, const double* tau, const double* lnphi,
+              const double* jump, const double* de, int nde, int64_t sweep, int64_t chain_base, double* irn,
+              double* lnl, int32_t* n_acc) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_chain < 0) return fail_arg(2, "n_chain < 0");
+  if (n_f <= 0 || n_f > 256) return fail_arg(3, "n_f must be in 1..256");
+  if (nsteps < 0 || nsteps > (1 << 20)) return fail_arg(4, "nsteps out of range");
+  if (anchor != 0 && anchor != 1) return fail_arg(5, "anchor must be 0 or 1");
+  if (!x) return fail_arg(6, "x is NULL");
+  if (!red_col || !gw_col) return fail_arg(8, "red_col/gw_col is NULL");
+  if (!tau || !lnphi) return fail_arg(10, "tau/lnphi is NULL");
+  if (nsteps > 0 && !jump) return fail_arg(12, "jump is NULL");
+  if (nde < 0 || (nde > 0 && !de)) return fail_arg(14, "bad DE buffer");
+  if (n_chain == 0) return 0;
+  RedMhArgs a;
+  a.n_chain = n_chain; a.n_f = n_f; a.ldx = ldx; a.nsteps = nsteps; a.anchor = anchor; a.nde = nde;
+  a.sweep = sweep; a.chain_base = chain_base; a.sweep_dev = ctx->sweep_dev; a.key = key_of(ctx);
+  a.red_col = red_col; a.gw_col = gw_col; a.tau = tau; a.lnphi = lnphi; a.jump = jump; a.de = de;
+  a.x = x; a.irn = irn; a.lnl = lnl; a.n_acc = n_acc;
+  launch_red_mh(ctx->stream, a);
+  return after_launch("k_red_mh");
 }
 
 int gs_philox(gs_ctx* ctx, int64_t n, const uint32_t* ctr, uint32_t* out) {

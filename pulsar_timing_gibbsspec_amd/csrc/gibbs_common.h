@@ -98,3 +98,13 @@ __device__ __forceinline__ void gs_normal2(gs_u4 c, gs_key k, double& n1, double
   n1 = r * co;
   n2 = r * s;
 }
+
+// ---------------------------------------------------------------- numpy npy_logaddexp
+__device__ __forceinline__ double np_logaddexp(double x, double y) {
+  if (x == y) return x + 0.693147180559945309417232121458176568;  // x + log(2)
+  const double t = x - y;
+  if (t > 0) return x + log1p(exp(-t));
+  if (t <= 0) return y + log1p(exp(t));
+  return t;  // NaN
+}
+

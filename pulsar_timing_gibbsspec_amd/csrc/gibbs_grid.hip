@@ -19,15 +19,6 @@ namespace {
 
 constexpr double LN10 = 2.302585092994045684;  // np.log(10)
 
-// numpy npy_logaddexp
-__device__ __forceinline__ double np_logaddexp(double x, double y) {
-  if (x == y) return x + 0.693147180559945309417232121458176568;  // x + log(2)
-  const double t = x - y;
-  if (t > 0) return x + log1p(exp(-t));
-  if (t <= 0) return y + log1p(exp(t));
-  return t;  // NaN
-}
-
 // ------------------------------------------------------------ tau
 // tau[p][k][c] = (b_sin^2 + b_cos^2) * scale  (scale 1: pta_gibbs.py:194-195; 0.5: pulsar_gibbs.py:209)
 __global__ void k_tau(TauArgs A) {
@@ -450,6 +441,7 @@ __global__ void k_pta_gate_phiinv(PtaGateArgs A) {
     const int p = t / A.n_f, k = t % A.n_f;
     double phi = pow(10.0, 2.0 * xc[A.gw_col[k]]);
     if (A.red_col) phi = phi + pow(10.0, 2.0 * xc[A.red_col[p * A.n_f + k]]);
+    if (A.irn) phi = phi + A.irn[(int64_t)k * A.n_chain + c];
     const double pinv = 1.0 / phi;
     double* o = A.phiinv_F + ((int64_t)p * A.n_chain + c) * (2 * A.n_f);
     o[2 * k] = pinv;

@@ -104,6 +104,7 @@ struct PtaGateArgs {
   int n_psr, n_chain, n_f, n_param;
   const double *x, *xlast;
   const int32_t *gw_col, *red_col;
+  const double* irn;  // [n_f x n_chain] power-law red phi added to every pulsar's phi, or NULL
   double* phiinv_F;
   int32_t* gate;
 };
@@ -150,5 +151,18 @@ struct WhiteTntArgs {
 };
 
 int launch_white_mh(hipStream_t s, const WhiteMhArgs& a);
+
+// power-law red-noise Metropolis block (gibbs_red.hip)
+struct RedMhArgs {
+  int n_chain, n_f, ldx, nsteps, anchor, nde;
+  int64_t sweep, chain_base;
+  const int64_t* sweep_dev;
+  gs_key key;
+  const int32_t *red_col, *gw_col;
+  const double *tau, *lnphi, *jump, *de;
+  double *x, *irn, *lnl;
+  int32_t* n_acc;
+};
+int launch_red_mh(hipStream_t s, const RedMhArgs& a);
 int launch_white_resid(hipStream_t s, const WhiteResidArgs& a);
 int launch_white_tnt(hipStream_t s, const WhiteTntArgs& a);

@@ -95,6 +95,7 @@ class DeviceModel:
 
     def refresh(self, Nvec=None):
         """(Re)compute TNT/d and the prefix on device (e.g. after a white-noise change)."""
+        self._lnl_const = None
         if Nvec is not None:
             self.Nvec.copy_(_t(np.concatenate(Nvec), torch.float64, self.ctx.device))
         lib, h = self.ctx.lib, self.ctx.handle
@@ -110,6 +111,8 @@ class DeviceModel:
     def lnl_constants(self):
         """-1/2 (sum log N + r^T N^-1 r) + 1/2 sum_M log phiinv_M per pulsar (the model
         part of get_lnlikelihood_fullmarg, pulsar_gibbs.py:583-600), reduced on device."""
+        if getattr(self, "_lnl_const", None) is not None:
+            return self._lnl_const
         dev = self.ctx.device
         seg = torch.repeat_interleave(torch.arange(self.P, device=dev),
                                       torch.as_tensor(self.n_toa, device=dev))
@@ -117,7 +120,8 @@ class DeviceModel:
         wn = torch.zeros(self.P, dtype=torch.float64, device=dev).index_add_(0, seg, t)
         nmask = torch.arange(self.NMX, device=dev)[None, :] < self.nm_dev[:, None]
         lph = torch.where(nmask, torch.log(self.phfix), torch.zeros_like(self.phfix)).sum(dim=1)
-        return -0.5 * wn + 0.5 * lph
+        self._lnl_const = -0.5 * wn + 0.5 * lph
+        return self._lnl_const
 
     def lnlike_marg(self, phiinv_F, n_chain):
         """Marginalised likelihood (pulsar_gibbs.py:569-610) of P*n_chain systems:

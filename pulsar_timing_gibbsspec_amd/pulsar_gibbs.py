@@ -17,9 +17,12 @@ the same chain files.  The arithmetic runs on the GPU through the C-ABI:
 
 Extensions (keyword-only, reference-equivalent defaults): ``nchains``
 (independent chains, chain 0 is written in the reference layout), ``device``,
-``seed`` (Philox key).  Models with other Metropolis blocks (power-law red
-noise via PTMCMC, ECORR) are outside the device hot path and raise
-``NotImplementedError`` from ``sample``.
+``seed`` (Philox key).
+
+* power-law intrinsic red noise: ``update_red_params`` /
+  ``get_lnlikelihood_red`` -> gs_red_mh (:271-329, :549-566), rho|b -> gs_rho_gumbel
+  (:218-236), and ``sample`` runs rednoise.RedNoiseChains.  ECORR blocks stay out of
+  scope and raise ``NotImplementedError`` from ``sample``.
 """
 from __future__ import annotations
 
@@ -30,7 +33,9 @@ import torch
 
 from . import _lib
 from .diagnostics import white_aclength
-from .engine import DeviceModel, FreeSpectrumChains, HistoryStreamer
+from .engine import DeviceModel, FreeSpectrumChains, HistoryStreamer, grid3
+from .rednoise import (DE_BUFFER, RED_STEPS, RedJumps, RedNoiseChains, powerlaw_loglinear,
+                       warmup as red_warmup)
 from .white import MAX_W, WhiteFreeSpectrumChains, WhiteNoiseModel, white_kind
 
 
@@ -301,19 +306,35 @@ class PulsarBlockGibbs(object):
         return b[0, :model.m[0]].cpu().numpy()
 
     def update_gwrho_params(self, xs, u=None):
-        """rho | b (pulsar_gibbs.py:199-268); analytic branch on the GPU."""
+        """rho | b (pulsar_gibbs.py:199-268) on the GPU: the analytic draw, or with an
+        intrinsic red signal the grid + Gumbel-max draw (:218-234; ``u``: the (n_f, 1000)
+        uniforms behind the Gumbels in parity mode)."""
         gwind = self.get_gwrho_param_indices()
         xnew = xs.copy()
         if self.hypersample != "conditional":
             print("ERROR: Only conditional draws on rho for now...")
             return xnew
-        if self.red_sig is not None:
-            raise NotImplementedError("grid + Gumbel rho|b with intrinsic red noise: use the "
-                                      "device grid kernel (not yet exposed here)")
         dev = self.ctx.device
         n_f = len(self.gwid) // 2
         b = torch.as_tensor(self._b[None, :], dtype=torch.float64, device=dev)
         fidx = torch.as_tensor(np.asarray(self.gwid, np.int32)[None, :], device=dev)
+        if self.red_sig is not None:
+            irn = np.array(self.red_sig.get_phi(self.map_params(xnew)))[::2]        # :223
+            tau = torch.empty(n_f, 1, dtype=torch.float64, device=dev)
+            _lib.check(self.ctx.lib.gs_tau(self.ctx.handle, 1, 1, 2 * n_f, b.shape[1], _lib.ptr(fidx),
+                                           _lib.ptr(b), 1, _lib.ptr(tau)), "gs_tau")
+            irt = torch.as_tensor(np.ascontiguousarray(irn[:, None]), dtype=torch.float64, device=dev)
+            ut = None if u is None else torch.as_tensor(np.ascontiguousarray(np.asarray(u, float)[None]),
+                                                        dtype=torch.float64, device=dev)
+            x = torch.empty(1, n_f, dtype=torch.float64, device=dev)
+            cols = torch.arange(n_f, dtype=torch.int32, device=dev)
+            grid = grid3(self.rhomin, self.rhomax, device=dev)
+            _lib.check(self.ctx.lib.gs_rho_gumbel(self.ctx.handle, 1, n_f, _lib.ptr(tau), _lib.ptr(irt), 1000,
+                                                  _lib.ptr(grid), _lib.ptr(ut), self._ndraw, 0, _lib.ptr(x),
+                                                  n_f, _lib.ptr(cols), None), "gs_rho_gumbel")
+            self._ndraw += 1
+            xnew[gwind] = x[0].cpu().numpy()
+            return xnew
         ut = None if u is None else torch.as_tensor(np.asarray(u, float)[None, :], dtype=torch.float64,
                                                     device=dev)
         x = torch.empty(1, n_f, dtype=torch.float64, device=dev)
@@ -324,13 +345,99 @@ class PulsarBlockGibbs(object):
         xnew[gwind] = x[0].cpu().numpy()
         return xnew
 
+    # ------------------------------------------------------------ power-law red noise (8f-2)
+    def _red_setup(self, xs):
+        """(ia, ig, lnphi, bounds): the log10_A / gamma indices, the power law's log-linear
+        coefficients probed from red_sig.get_phi, and their Uniform prior bounds."""
+        if getattr(self, "_red_info", None) is not None:
+            return self._red_info
+        rind = self.get_red_param_indices()
+        names = self.param_names
+        ia = [i for i in rind if "log10_A" in names[i]]
+        ig = [i for i in rind if "gamma" in names[i]]
+        if len(rind) != 2 or len(ia) != 1 or len(ig) != 1:
+            raise NotImplementedError(f"power-law red noise needs one log10_A and one gamma, got "
+                                      f"{[names[i] for i in rind]}")
+        ia, ig = int(ia[0]), int(ig[0])
+        x = np.asarray(xs, float).copy()
+
+        def phi_of(la, ga):
+            x[ia], x[ig] = la, ga
+            return np.array(self.red_sig.get_phi(self.map_params(x)))[::2]
+        lnphi = powerlaw_loglinear(phi_of)
+        by_index = [p for p in self.params for _ in range(p.size or 1)]
+        bounds = (_parse_uniform_bounds(by_index[ia]), _parse_uniform_bounds(by_index[ig]))
+        self._red_info = (ia, ig, lnphi, bounds)
+        return self._red_info
+
+    def _param_bounds(self):
+        lo, hi = [], []
+        for p in self.params:
+            a, b = _parse_uniform_bounds(p)
+            lo += [a] * (p.size or 1)
+            hi += [b] * (p.size or 1)
+        return np.array(lo), np.array(hi)
+
+    def _red_engine(self, xs, n_chain, jumps=None, x_first=None):
+        ia, ig, lnphi, bounds = self._red_setup(xs)
+        if jumps is None:
+            jumps = getattr(self, "_red_jumps", None) or RedJumps(np.eye(2) * 0.01, np.zeros((0, 2)), bounds,
+                                                                  self.ctx.device)
+        return RedNoiseChains(self._model(xs), len(xs), self.get_gwrho_param_indices(),
+                              (ia, ig), lnphi, jumps, self.rhomin, self.rhomax, n_chain, xs, x_first=x_first)
+
+    def get_lnlikelihood_red(self, xs):
+        """get_lnlikelihood_red (pulsar_gibbs.py:549-566) on the device at (xs, self._b)."""
+        eng = self._red_engine(xs, 1)
+        eng.b[0, :len(self._b)] = torch.as_tensor(self._b, device=self.ctx.device)
+        return float(eng.lnlike_red()[0])
+
+    def update_red_params(self, xs, iters=None):
+        """update_red_params (pulsar_gibbs.py:271-329).  iters: the sweep-0 warm-up on the
+        device's marginalised likelihood (rednoise.warmup), which learns the red block's
+        proposal covariance and DE buffer and returns the joint step's state; None: one
+        20-step Metropolis block on the red-only likelihood (gs_red_mh)."""
+        rind = self.get_red_param_indices()
+        xnew = np.asarray(xs, float).copy()
+        ia, ig, _, bounds = self._red_setup(xnew)
+        if iters is not None:
+            lo, hi = self._param_bounds()
+            rng = np.random.default_rng(np.random.SeedSequence([int(self.ctx.seed), 0x7ed]))
+
+            def lnprob(x):
+                return self.get_lnlikelihood_fullmarg(x) + self.get_lnprior(x)
+            x1, cov, chain = red_warmup(lnprob, xnew, int(iters), rng, lo, hi)
+            sub = [ia, ig]
+            self.cov_red = cov[np.ix_(sub, sub)]
+            de = chain[-DE_BUFFER:][:, sub] if len(chain) else np.zeros((0, 2))
+            self._red_jumps = RedJumps(self.cov_red, de, bounds, self.ctx.device)
+            self._red_warm_chain = chain
+            return x1
+        if rind.size == 0:
+            return xnew
+        eng = self._red_engine(xnew, 1)
+        eng.b[0, :len(self._b)] = torch.as_tensor(self._b, device=self.ctx.device)
+        eng.it = self._ndraw
+        eng._tau()
+        eng.red_block(RED_STEPS)
+        self._ndraw += 1
+        return eng.x[0].cpu().numpy()
+
     # ------------------------------------------------------------ loop
+    def _red_loop(self):
+        if self.red_sig is None:
+            return False
+        extra = [n for n in self.param_names if "rho" not in n]
+        return bool(extra) and all(("log10_A" in n or "gamma" in n) for n in extra)
+
     def _white_loop(self):
         names = self.param_names
         extra = [n for n in names if "rho" not in n]
         return bool(extra) and all(("efac" in n or "equad" in n) for n in extra)
 
     def _check_device_loop(self, xs):
+        if self._red_loop() and self.hypersample == "conditional":
+            return
         extra = [n for n in self.param_names if "rho" not in n and not self._white_loop()]
         if extra or self.red_sig is not None or self.hypersample != "conditional":
             raise NotImplementedError(
@@ -353,6 +460,11 @@ class PulsarBlockGibbs(object):
         np.savetxt(f"{outdir}/pars_chain.txt", self.param_names, fmt="%s")
         np.savetxt(f"{outdir}/pars_bchain.txt", self.b_param_names, fmt="%s")
 
+        if self._red_loop():
+            out = self._sample_red(xs, outdir, niter, resume, save_every)
+            if flush_final:
+                self._flush(outdir)
+            return out
         if self._white_loop():
             out = self._sample_white(xs, outdir, niter, resume, save_every)
             if flush_final:
@@ -504,6 +616,73 @@ class PulsarBlockGibbs(object):
         info = runner.info.cpu().numpy()
         if info.any():
             print(f"WARNING: {int((info != 0).sum())} chains hit a non-positive-definite Sigma")
+        self._b = runner.b[0, :m].cpu().numpy()
+        self._runner = runner
+        return self.chain
+
+    def _sample_red(self, xs, outdir, niter, resume, save_every):
+        """sample() with power-law red noise (pulsar_gibbs.py:656-698): sweep 0 runs the
+        warm-up (update_red_params(iters=10000), :689-690) on the host with the device
+        likelihood; every sweep is then one launch sequence for all chains
+        (rednoise.RedNoiseChains)."""
+        nc = self.nchains
+        dev = self.ctx.device
+        n_param = len(xs)
+        model = self._model(xs)
+        m = int(model.m[0])
+        self.chain = np.zeros((niter, n_param))
+        self.bchain = np.zeros((niter, len(self._b)))
+        self.chains = np.zeros((nc, niter, n_param)) if nc > 1 else None
+        self.bchains = np.zeros((nc, niter, len(self._b))) if nc > 1 else None
+        start = 0
+        x0 = np.asarray(xs, float)
+        if resume and os.path.exists(f"{outdir}/chain.npy"):
+            print("Resuming from previous run...")
+            c0 = np.load(f"{outdir}/chain.npy")
+            b0 = np.load(f"{outdir}/bchain.npy")
+            start = min(c0.shape[0], b0.shape[0])
+            self.chain[:start] = c0[:start]
+            self.bchain[:start] = b0[:start]
+        x_first = None
+        if start == 0 and getattr(self, "_red_jumps", None) is None:
+            x_first = self.update_red_params(x0, iters=getattr(self, "red_warmup_iters", 10000))
+        elif getattr(self, "_red_jumps", None) is None:
+            raise NotImplementedError("resume of a red-noise run needs the warm-up's proposal (_red_jumps)")
+        runner = self._red_engine(x0, nc, x_first=x_first)
+        if start > 0:
+            runner.x.copy_(torch.as_tensor(self.chain[start - 1][None, :], device=dev).expand(nc, -1))
+            runner.b[:, :m] = torch.as_tensor(self.bchain[start - 1], device=dev)
+            runner.it = start
+        blk = max(1, save_every)
+        xr = torch.empty(blk + 1, nc, n_param, dtype=torch.float64, device=dev)
+        br = torch.empty(blk + 1, nc, model.ldb, dtype=torch.float64, device=dev)
+        ii = start
+        while ii < niter:
+            nxt = min(niter, (ii // blk + 1) * blk + 1)
+            n = nxt - ii
+            for k in range(n):
+                runner.sweep(x_rec=xr[k], b_rec=br[k])
+            xh = xr[:n].cpu().numpy()
+            bh = br[:n, :, :m].cpu().numpy()
+            self.chain[ii:nxt] = xh[:, 0]
+            self.bchain[ii:nxt] = bh[:, 0]
+            if nc > 1:
+                self.chains[:, ii:nxt] = np.moveaxis(xh, 1, 0)
+                self.bchains[:, ii:nxt] = np.moveaxis(bh, 1, 0)
+            ii = nxt
+            self.iter = ii - 1
+            last = ii - 1
+            if last % save_every == 0 and last > 0:
+                np.save(f"{outdir}/chain.npy", self.chain[:last + 1, :])
+                np.save(f"{outdir}/bchain.npy", self.bchain[:last + 1, :])
+                if nc > 1:
+                    np.save(f"{outdir}/chains.npy", self.chains[:, :last + 1])
+                    np.save(f"{outdir}/bchains.npy", self.bchains[:, :last + 1])
+        info = runner.info.cpu().numpy()
+        if info.any():
+            print(f"WARNING: {int((info != 0).sum())} chains hit a non-positive-definite Sigma")
+        steps = runner.n_blocks * runner.nsteps
+        self.red_acceptance = (runner.acc_total.cpu().numpy() / steps) if steps else None
         self._b = runner.b[0, :m].cpu().numpy()
         self._runner = runner
         return self.chain

@@ -186,6 +186,37 @@ def single_pulsar_gumbel(ref, out, ncalls=2):
     print("gumbel:", out)
 
 
+def red_likelihood(ref, out, npts=16):
+    """get_lnlikelihood_red (pulsar_gibbs.py:549-566) of the power-law red-noise model at
+    random (b, log10_A, gamma, rho) points, plus the reference's log-probability gate
+    inputs: the values the device red MH block must reproduce."""
+    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0, powerlaw_red=True)
+    np.random.seed(5)
+    g = _quiet(ref.PulsarBlockGibbs, pta)
+    x0 = np.concatenate([p.sample().flatten() for p in g.params])
+    rs = np.random.RandomState(6)
+    rind = g.get_red_param_indices()
+    names = list(g.param_names)
+    ia = [i for i in rind if "log10_A" in names[i]][0]
+    ig = [i for i in rind if "gamma" in names[i]][0]
+    bs, xs, lnl, irn, gwphi = [], [], [], [], []
+    for _ in range(npts):
+        b = rs.standard_normal(len(g._b)) * 10 ** rs.uniform(-8, -6.5, len(g._b))
+        x = x0.copy()
+        x[g.get_gwrho_param_indices()] = rs.uniform(-9, -4, len(g.get_gwrho_param_indices()))
+        x[ia], x[ig] = rs.uniform(-16, -12), rs.uniform(1, 6)
+        g._b = b
+        lnl.append(g.get_lnlikelihood_red(x))
+        prm = g.map_params(x)
+        irn.append(np.array(g.red_sig.get_phi(prm))[::2])
+        gwphi.append(np.array(g.gw_sig.get_phi(prm))[::2])
+        bs.append(b), xs.append(x)
+    np.savez_compressed(out, b=np.stack(bs), x=np.stack(xs), lnl=np.array(lnl), irn=np.stack(irn),
+                        gwphi=np.stack(gwphi), gwid=np.asarray(g.gwid), rind=rind, ia=ia, ig=ig,
+                        gwind=g.get_gwrho_param_indices(), param_names=np.array(names))
+    print("red likelihood:", out)
+
+
 def pta_run(ref, out, kind, niter, n_psr=None):
     """Configs 4a/4b: PTABlockGibbs CURN (+ per-pulsar red free spectrum, conditional)."""
     pta = synthetic.array_pta(kind=kind, n_psr=n_psr, seed=0)
@@ -326,6 +357,9 @@ def main(root):
     mods = load_reference(root)
     PB = mods["pulsar_gibbs"]
     PT = mods["pta_gibbs"]
+    if "--only-red" in sys.argv:
+        red_likelihood(PB, os.path.join(HERE, "red_lnlike_j1713.npz"))
+        return
     single_pulsar(PB, os.path.join(HERE, "single_j1713.npz"))
     single_pulsar_gumbel(PB, os.path.join(HERE, "gumbel_j1713.npz"))
     likelihoods(PB, os.path.join(HERE, "likelihoods_j1713.npz"))
@@ -333,6 +367,7 @@ def main(root):
     pta_run(PT, os.path.join(HERE, "pta_curn_red.npz"), "curn_red", niter=12)
     pta_sample_check(PT, os.path.join(HERE, "pta_sample_small.npz"))
     white_mh(PB, os.path.join(HERE, "white_mh_j1713.npz"))
+    red_likelihood(PB, os.path.join(HERE, "red_lnlike_j1713.npz"))
     if "--long" in sys.argv:
         single_pulsar_long(PB, os.path.join(HERE, "long_j1713.npz"))
 

@@ -301,3 +301,34 @@ def test_curn_sum_statistic_matches_product_draw():
         tau = r["tau"]                                   # (P, n_f)
         _, idx = O.rho_grid_cdf_curn_sum(tau.sum(axis=0), tau.shape[0], r["u_curn"], lo, hi)
         assert np.array_equal(idx % 1000, r["idx_curn"] % 1000), ii
+
+
+def test_lnlike_red_matches_reference():
+    """oracle.lnlike_red == the reference's get_lnlikelihood_red (pulsar_gibbs.py:549-566)
+    on its own values; the power law's log-linear form (the device's irn) agrees too."""
+    from pulsar_timing_gibbsspec_amd import synthetic
+    from pulsar_timing_gibbsspec_amd.rednoise import powerlaw_loglinear
+    g = golden("red_lnlike_j1713.npz")
+    gwid = g["gwid"]
+    for b, want, irn, gw in zip(g["b"], g["lnl"], g["irn"], g["gwphi"]):
+        assert O.lnlike_red(b, gwid, irn, gw) == pytest.approx(want, rel=1e-14)
+    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0, powerlaw_red=True)
+    red = [s for s in pta.signals.values() if s.name == "red"][0]
+    pa, pg = red.params
+    lnphi = powerlaw_loglinear(lambda la, ga: red.get_phi({pa.name: la, pg.name: ga})[::2])
+    ia, ig = int(g["ia"]), int(g["ig"])
+    for x, irn in zip(g["x"], g["irn"]):
+        np.testing.assert_allclose(np.exp(O.powerlaw_lnirn(lnphi, x[ia], x[ig])), irn, rtol=1e-12)
+
+
+def test_red_warmup_learns_covariance():
+    """rednoise.warmup (the sweep-0 adaptive Metropolis restatement) on a correlated
+    2-D Gaussian recovers its covariance."""
+    from pulsar_timing_gibbsspec_amd.rednoise import warmup
+    cov = np.array([[0.5, 0.3], [0.3, 0.4]])
+    P = np.linalg.inv(cov)
+    rng = np.random.default_rng(0)
+    x1, c, chain = warmup(lambda x: -0.5 * x @ P @ x, np.zeros(2), 8000, rng,
+                          np.full(2, -50.0), np.full(2, 50.0))
+    np.testing.assert_allclose(c, cov, atol=0.12)
+    assert chain.shape == (7999, 2) and x1.shape == (2,)
