@@ -438,3 +438,56 @@ def red_mh_philox(x, ia, ig, gw_col, tau_half, lnphi, jump, de, nsteps, anchor, 
             acc += 1
     x[ia], x[ig] = qa, qg
     return x, Lc, acc, np.array(margins)
+
+
+# ============================================================== basis ECORR
+def ecorr_schur(TNT, d, ecid, phi_E):
+    """Eliminate the ECORR epoch columns (ecid) of Sigma = TNT + diag(phiinv) first.
+    U^T N^-1 U is diagonal (each TOA sits in at most one epoch), so with
+    a_e = TNT_ee + 1/phi_e, B = TNT[ecid, R] and R the remaining columns in order:
+        Sigma_R' = TNT_RR - B^T diag(1/a) B,   d_R' = d_R - B^T (d_E / a)
+    and log det Sigma = sum log a + log det(Sigma_R' + diag(phiinv_R)),
+    d^T Sigma^-1 d = sum d_E^2 / a + d_R'^T (Sigma_R' + diag(phiinv_R))^-1 d_R'.
+    Restates, in block form, the Sigma of get_lnlikelihood_fullmarg (pulsar_gibbs.py:592)
+    and update_b (:505) with the ECORR phiinv of get_phiinv.  Returns
+    (rcols, TNT_R', d_R', sum log a, sum d_E^2 / a)."""
+    m = TNT.shape[0]
+    ecid = np.asarray(ecid)
+    rc = np.setdiff1d(np.arange(m), ecid)
+    a = np.diag(TNT)[ecid] + 1.0 / np.asarray(phi_E, float)
+    B = TNT[np.ix_(ecid, rc)]
+    dE = d[ecid]
+    S = TNT[np.ix_(rc, rc)] - B.T @ (B / a[:, None])
+    dR = d[rc] - B.T @ (dE / a)
+    return rc, S, dR, float(np.sum(np.log(a))), float(np.sum(dE ** 2 / a))
+
+
+def lnlike_ecorr_marg(r, Nvec, TNT, d, ecid, phiinv, logdet_phi):
+    """get_lnlikelihood_fullmarg (pulsar_gibbs.py:569-610) through ecorr_schur: equal to
+    lnlike_fullmarg up to rounding (the ECORR block is diagonal)."""
+    ll = -0.5 * (np.sum(np.log(Nvec)) + np.sum(r ** 2 / Nvec))
+    rc, S, dR, sla, sdw = ecorr_schur(TNT, d, ecid, 1.0 / phiinv[ecid])
+    try:
+        cf = sl.cho_factor(S + np.diag(phiinv[rc]))
+    except np.linalg.LinAlgError:
+        return -np.inf
+    ev = sl.cho_solve(cf, dR)
+    ld = sla + np.sum(2 * np.log(np.diag(cf[0])))
+    return ll + 0.5 * (sdw + np.dot(dR, ev) - ld - logdet_phi)
+
+
+def bdraw_ecorr(TNT, d, ecid, phiinv, zR, zE):
+    """b | rho with the ECORR block eliminated first: b_R ~ N(S^-1 d_R', S^-1) drawn as
+    S^-1 d_R' + L^-T zR (S = Sigma_R' + diag(phiinv_R) = L L^T), then the epochs
+    b_E | b_R ~ N((d_E - B b_R) / a, 1/a) = (d_E - B b_R)/a + zE / sqrt(a).  Same
+    distribution as update_b (pulsar_gibbs.py:489-520); returns b in original column order."""
+    m = TNT.shape[0]
+    ecid = np.asarray(ecid)
+    rc, S, dR, _, _ = ecorr_schur(TNT, d, ecid, 1.0 / phiinv[ecid])
+    L = np.linalg.cholesky(S + np.diag(phiinv[rc]))
+    bR = sl.cho_solve((L, True), dR) + sl.solve_triangular(L.T, zR, lower=False)
+    a = np.diag(TNT)[ecid] + phiinv[ecid]
+    bE = (d[ecid] - TNT[np.ix_(ecid, rc)] @ bR) / a + zE / np.sqrt(a)
+    b = np.empty(m)
+    b[rc], b[ecid] = bR, bE
+    return b

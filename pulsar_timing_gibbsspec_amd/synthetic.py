@@ -174,6 +174,58 @@ class MeasurementNoise:
         return ef[self.backends] ** 2 * self.sigma ** 2 + eq[self.backends]
 
 
+def quantization_matrix(toas_s, dt=1.0, nmin=2):
+    """Epoch (quantisation) matrix U [n_toa x n_epoch]: TOAs closer than dt seconds to
+    the first TOA of their bucket share an epoch; epochs with fewer than nmin TOAs get no
+    column (enterprise's create_quantization_matrix, *[upstream, not vendored]*)."""
+    order = np.argsort(toas_s, kind="stable")
+    buckets, ref = [], None
+    for i in order:
+        if ref is None or toas_s[i] - ref >= dt:
+            buckets.append([i])
+            ref = toas_s[i]
+        else:
+            buckets[-1].append(i)
+    buckets = [b for b in buckets if len(b) >= nmin]
+    U = np.zeros((toas_s.size, len(buckets)))
+    for j, b in enumerate(buckets):
+        U[b, j] = 1.0
+    return U
+
+
+class EcorrBasisGP:
+    """Basis ECORR (enterprise EcorrBasisModel, selection by backend): one epoch column per
+    quantisation bucket of each backend's TOAs, backends in order, phi = 10**(2 log10_ecorr_k)
+    for the epochs of backend k.  The reference finds these columns by 'ecorr' in the
+    signal name (pulsar_gibbs.py:98-99) and their prior by 'ecorr' in a parameter name
+    (:111-118)."""
+
+    def __init__(self, psrname, toas_s, backends, params, dt=1.0, nmin=2):
+        self.psrname = psrname
+        self.name = "basis_ecorr"
+        self.signal_id = f"{psrname}_{self.name}"
+        self.params = list(params)
+        backends = np.asarray(backends, np.int64)
+        cols, ebk = [], []
+        for k in range(len(self.params)):
+            sel = np.nonzero(backends == k)[0]
+            Uk = quantization_matrix(toas_s[sel], dt, nmin)
+            full = np.zeros((toas_s.size, Uk.shape[1]))
+            full[sel] = Uk
+            cols.append(full)
+            ebk += [k] * Uk.shape[1]
+        self._U = np.hstack(cols)
+        self.epoch_backend = np.asarray(ebk, np.int64)
+        self.basis_key = ("ecorr", psrname)
+
+    def get_basis(self, params=None):
+        return self._U
+
+    def get_phi(self, params):
+        v = np.array([10.0 ** (2.0 * float(_value(params, p))) for p in self.params])
+        return v[self.epoch_backend]
+
+
 # --------------------------------------------------------------------------- models
 class PulsarModel:
     """Signal collection of one pulsar (enterprise SignalCollection analogue)."""
@@ -354,7 +406,39 @@ def single_pulsar_pta(psr="J1713+0747", n_f=30, rho_prior=(-9.0, -4.0), log10_A=
     return PTA([PulsarModel(psr, toas, r, sigs)])
 
 
-def array_pta(kind="curn_red", n_f=30, n_psr=None, gw_prior=(-9.0, -4.0), red_prior=(-10.0, -4.0),
+def ecorr_pulsar_pta(psr="J1713+0747", n_epoch=160, n_sub=(1, 6), n_backends=2, n_f=30,
+                     rho_prior=(-9.0, -4.0), ecorr_prior=(-8.5, -5.0), log10_ecorr=-6.3,
+                     log10_A=np.log10(2e-15), gamma=13.0 / 3.0, span_yr=15.0, n_tm=16, seed=0):
+    """Single pulsar with basis ECORR (pta_gibbs_freespec.ipynb's
+    J1713 model ``model_general(..., white_vary=True, select='backend')`` with fixed
+    EFAC/EQUAD): n_epoch observing epochs over span_yr, each recorded by one backend
+    (epoch % n_backends) as a burst of n_sub[0]..n_sub[1] sub-band TOAs a few tenths of a
+    second apart (single-TOA epochs get no ECORR column, nmin = 2).  Signals in order
+    [white, basis_ecorr, gw, tm]: T = [U | F | M], ecid = 0..n_e-1, gwid after.
+    Parameters (sorted by name): ``{psr}_basis_ecorr_b{k}_log10_ecorr`` then
+    ``gw_log10_rho`` (n_f).  Residuals: power-law GWB + TM + white + epoch jitter."""
+    rng = np.random.default_rng(seed)
+    Tspan0 = span_yr * 365.25 * DAY
+    t_ep = np.sort(rng.uniform(0.0, Tspan0, n_epoch)) + 53000.0 * DAY
+    nsub = rng.integers(n_sub[0], n_sub[1] + 1, n_epoch)
+    toas = np.concatenate([t + 0.2 * np.arange(k) for t, k in zip(t_ep, nsub)])
+    backends = np.concatenate([np.full(k, e % n_backends) for e, k in enumerate(nsub)])
+    sigma = 10 ** rng.uniform(np.log10(1e-7), np.log10(2e-6), toas.size)
+    Tspan = toas.max() - toas.min()
+    white = MeasurementNoise(psr, sigma, backends)
+    ep = [Uniform(f"{psr}_basis_ecorr_b{k}_log10_ecorr", *ecorr_prior) for k in range(n_backends)]
+    ecorr = EcorrBasisGP(psr, toas, backends, ep)
+    rho = Uniform("gw_log10_rho", rho_prior[0], rho_prior[1], size=n_f)
+    gw = FourierGP(psr, "gw", toas, Tspan, n_f, "spectrum", [rho])
+    tm = TimingModelGP(psr, synthetic_design_matrix(toas, n_tm), use_svd=True)
+    r = _simulate_residuals(rng, gw.get_basis(), gw.freqs, Tspan, tm.get_basis(), sigma,
+                            log10_A, gamma)
+    U = ecorr.get_basis()
+    r = r + U @ (rng.standard_normal(U.shape[1]) * 10.0 ** log10_ecorr)
+    return PTA([PulsarModel(psr, toas, r, [white, ecorr, gw, tm])])
+
+
+def array_pta(kind="curn_red",n_f=30, n_psr=None, gw_prior=(-9.0, -4.0), red_prior=(-10.0, -4.0),
               log10_A=np.log10(2e-15), gamma=13.0 / 3.0, seed=0):
     """Config 3/4 models over the simulated array (model_definition.py:184-234 order: TM, CRN, red, white).
 

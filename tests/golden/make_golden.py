@@ -353,10 +353,68 @@ def white_mh(ref, out, nsweep=6, acl=40):
     print("white:", out, len(log))
 
 
+def ecorr_mh(ref, out, nsweep=6, acl=30, nlike=8):
+    """Basis-ECORR Metropolis block: PulsarBlockGibbs.update_ecorr_params
+    (pulsar_gibbs.py:409-486, steady-state branch) whose self.get_lnlikelihood the .py never
+    defines -- bound here to the reference's own get_lnlikelihood_fullmarg (:569-610), the
+    same code as the notebook's get_lnlikelihood (pta_gibbs_freespec.ipynb, cell 2) -- inside
+    the notebook's sweep order (ECORR block, rho|b, gated b).  aclength_ecorr is set directly
+    (its warm-up needs `acor`, absent).  Also the marginalised likelihood at prior draws."""
+    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=0)
+    np.random.seed(21)
+    g = _quiet(ref.PulsarBlockGibbs, pta)
+    g.get_lnlikelihood = g.get_lnlikelihood_fullmarg
+    x0 = np.concatenate([p.sample().flatten() for p in g.params])
+    eind = g.get_ecorr_indices()
+    g.aclength_ecorr = acl
+    rs = np.random.RandomState(22)
+    xl, ll = [], []
+    for i in range(nlike):
+        x = np.concatenate([p.sample().flatten() for p in g.params])
+        if i == nlike - 1:
+            x[eind] = [p.pmin for p in g.params if "ecorr" in p.name]   # prior edge
+        g.TNT = g.d = None
+        xl.append(x), ll.append(g.get_lnlikelihood_fullmarg(x))
+    chain, bhist, e_in, e_out = [], [], [], []
+    xnew = x0.copy()
+    with Capture() as cap:
+        np.random.seed(23)
+        for ii in range(nsweep):
+            chain.append(xnew.copy())
+            bhist.append(g._b.copy())
+            if ii == 0:
+                g._b = g.update_b(x0)
+            g.TNT = g.d = None
+            e_in.append(xnew.copy())
+            xnew = g.update_ecorr_params(xnew, iters=None)
+            e_out.append(xnew.copy())
+            xnew = g.update_gwrho_params(xnew)
+            if np.all(xnew != chain[ii][-1]):
+                g._b = g.update_b(xnew)
+    log = cap.log
+    sig = pta.signals["J1713+0747_basis_ecorr"]
+    np.savez_compressed(out, x0=x0, chain=np.stack(chain), bhist=np.stack(bhist), b_final=g._b,
+                        e_in=np.stack(e_in), e_out=np.stack(e_out),
+                        kinds=np.array([k for k, _ in log]),
+                        vals=np.concatenate([np.atleast_1d(v).ravel() for _, v in log]),
+                        lens=np.array([np.atleast_1d(v).size for _, v in log]),
+                        T=pta.get_basis()[0], r=pta.get_residuals()[0], Nvec=pta.get_ndiag()[0],
+                        epoch_backend=sig.epoch_backend, eind=eind, ecid=np.asarray(g.ecid),
+                        aclength=acl, gwid=np.asarray(g.gwid), rhomin=g.rhomin, rhomax=g.rhomax,
+                        ecorrmin=g.ecorrmin, ecorrmax=g.ecorrmax, param_names=np.array(g.param_names),
+                        x_like=np.stack(xl), lnlike=np.array(ll),
+                        pmin=np.array([p.pmin for p in g.params for _ in range(p.size or 1)]),
+                        pmax=np.array([p.pmax for p in g.params for _ in range(p.size or 1)]))
+    print("ecorr:", out, len(log))
+
+
 def main(root):
     mods = load_reference(root)
     PB = mods["pulsar_gibbs"]
     PT = mods["pta_gibbs"]
+    if "--only-ecorr" in sys.argv:
+        ecorr_mh(PB, os.path.join(HERE, "ecorr_mh_j1713.npz"))
+        return
     if "--only-red" in sys.argv:
         red_likelihood(PB, os.path.join(HERE, "red_lnlike_j1713.npz"))
         return
@@ -368,6 +426,7 @@ def main(root):
     pta_sample_check(PT, os.path.join(HERE, "pta_sample_small.npz"))
     white_mh(PB, os.path.join(HERE, "white_mh_j1713.npz"))
     red_likelihood(PB, os.path.join(HERE, "red_lnlike_j1713.npz"))
+    ecorr_mh(PB, os.path.join(HERE, "ecorr_mh_j1713.npz"))
     if "--long" in sys.argv:
         single_pulsar_long(PB, os.path.join(HERE, "long_j1713.npz"))
 

@@ -332,3 +332,102 @@ def test_red_warmup_learns_covariance():
                           np.full(2, -50.0), np.full(2, 50.0))
     np.testing.assert_allclose(c, cov, atol=0.12)
     assert chain.shape == (7999, 2) and x1.shape == (2,)
+
+
+# ----------------------------------------------------------------- basis ECORR
+def _ecorr_setup(g):
+    T, r, N = g["T"], g["r"], g["Nvec"]
+    TNT, d = O.tnt(T, N, r)
+    ecid, ebk, eind = g["ecid"], g["epoch_backend"], g["eind"]
+    gwid = g["gwid"]
+    gwind = np.array([i for i, n in enumerate(g["param_names"]) if "rho" in n])
+    pmin, pmax = g["pmin"], g["pmax"]
+
+    def phi_of(x):
+        ph = np.full(T.shape[1], 1e40)
+        ph[ecid] = np.array([10.0 ** (2.0 * float(x[eind[k]])) for k in range(len(eind))])[ebk]
+        ph[gwid] = np.repeat(10.0 ** (2.0 * x[gwind]), 2)
+        return ph
+
+    def lnprior(x):
+        inside = np.all((x >= pmin) & (x <= pmax))
+        return float(-np.sum(np.log(pmax - pmin))) if inside else -np.inf
+
+    return TNT, d, phi_of, lnprior, gwind
+
+
+def test_ecorr_likelihood_and_block_form():
+    """get_lnlikelihood_fullmarg at prior draws with basis ECORR: the oracle's Cholesky form
+    reproduces the reference to rounding, and the ECORR-eliminated block form agrees."""
+    g = golden("ecorr_mh_j1713.npz")
+    TNT, d, phi_of, _, _ = _ecorr_setup(g)
+    r, N = g["r"], g["Nvec"]
+    for x, ref in zip(g["x_like"], g["lnlike"]):
+        ph = phi_of(x)
+        full = O.lnlike_fullmarg(r, N, TNT, d, 1.0 / ph, np.sum(np.log(ph)))
+        blk = O.lnlike_ecorr_marg(r, N, TNT, d, g["ecid"], 1.0 / ph, np.sum(np.log(ph)))
+        assert abs(full - ref) < 1e-9 * abs(ref), (full, ref)
+        assert abs(blk - ref) < 1e-8 * abs(ref), (blk, ref)
+
+
+def test_ecorr_mh_loop_bitwise():
+    """Sweeps with the basis-ECORR MH block (update_ecorr_params, pulsar_gibbs.py:456-484, with
+    the reference's get_lnlikelihood_fullmarg) replayed by the oracle on the reference's draws:
+    every ECORR block output, chain row and b bit for bit."""
+    g = golden("ecorr_mh_j1713.npz")
+    TNT, d, phi_of, lnprior, gwind = _ecorr_setup(g)
+    r, N = g["r"], g["Nvec"]
+    eind, acl, gwid = g["eind"], int(g["aclength"]), g["gwid"]
+    items = iter(split_draws(g))
+
+    def draw_b(x):
+        k, z = next(items)
+        assert k == "randn"
+        return O.bdraw_svd(TNT, d, 1.0 / phi_of(x), z)
+
+    def lnl(x):
+        ph = phi_of(x)
+        return O.lnlike_fullmarg(r, N, TNT, d, 1.0 / ph, np.sum(np.log(ph)))
+
+    x = g["x0"].copy()
+    b = np.zeros(TNT.shape[0])
+    for ii in range(g["chain"].shape[0]):
+        assert np.array_equal(x, g["chain"][ii]) and np.array_equal(b, g["bhist"][ii]), ii
+        if ii == 0:
+            b = draw_b(g["x0"])
+        steps = []
+        for _ in range(acl):
+            (k1, s), (k2, p), (k3, z), (k4, u) = next(items), next(items), next(items), next(items)
+            assert (k1, k2, k3, k4) == ("choice", "choice", "randn", "rand")
+            steps.append((s[0], p[0], z[0], u[0]))
+        xe = O.white_mh(x, eind, steps, lnl, lnprior)
+        assert np.array_equal(xe, g["e_out"][ii]), ii
+        k, U = next(items)
+        xn = xe.copy()
+        xn[gwind] = 0.5 * np.log10(O.rho_analytic(O.tau_half(b, gwid), U, float(g["rhomin"]),
+                                                  float(g["rhomax"])))
+        if np.all(xn != x[-1]):
+            b = draw_b(xn)
+        x = xn
+    assert np.array_equal(b, g["b_final"])
+
+
+def test_ecorr_block_draw_distribution():
+    """bdraw_ecorr is an exact draw from N(Sigma^-1 d, Sigma^-1): zero normals give the mean,
+    and the map z -> b - mean, G, satisfies G^T Sigma G = I."""
+    g = golden("ecorr_mh_j1713.npz")
+    TNT, d, phi_of, _, _ = _ecorr_setup(g)
+    ph = 1.0 / phi_of(g["x0"])
+    ecid = g["ecid"]
+    m = TNT.shape[0]
+    rc = np.setdiff1d(np.arange(m), ecid)
+    Sig = TNT + np.diag(ph)
+    mean = O.bdraw_ecorr(TNT, d, ecid, ph, np.zeros(rc.size), np.zeros(ecid.size))
+    ref = np.linalg.solve(Sig, d)
+    assert np.linalg.norm(mean - ref) < 1e-8 * np.linalg.norm(ref)
+    G = np.empty((m, m))
+    for j in range(m):
+        z = np.zeros(m)
+        z[j] = 1.0
+        G[:, j] = O.bdraw_ecorr(TNT, d, ecid, ph, z[:rc.size], z[rc.size:]) - mean
+    assert np.abs(G.T @ Sig @ G - np.eye(m)).max() < 1e-6
