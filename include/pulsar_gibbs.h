@@ -46,6 +46,9 @@ enum {
   GS_EV_GUMBEL = 6, /* Gumbel-max uniforms               (pulsar_gibbs.py:233)     */
   GS_EV_WHITE = 7,  /* white-noise MH draws              (pulsar_gibbs.py:377-398) */
   GS_EV_REDMH = 8,  /* power-law red-noise MH draws      (pulsar_gibbs.py:312-319) */
+  GS_EV_ECORR = 9,  /* basis-ECORR MH draws              (pulsar_gibbs.py:458-470) */
+  GS_EV_ECORR_B = 10, /* epoch coefficients of a gated b draw (b_E | b_R)          */
+  GS_EV_ECORR_B0 = 11, /* epoch coefficients of the first b draw                   */
   GS_EV_USER = 16   /* first id free for callers                                    */
 };
 
@@ -372,6 +375,50 @@ int gs_bdraw_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,
                  const double* model, const int32_t* fidx, const int32_t* midx, const int32_t* nm,
                  const double* phiinv_F, const double* z, int64_t sweep, int event,
                  int64_t chain_base, const int32_t* chain_mask, double* b, int32_t* info);
+
+/* ------------------------------------------------------------------------
+ *  Basis ECORR, single pulsar, n_chain chains
+ * (PulsarBlockGibbs.update_ecorr_params pulsar_gibbs.py:409-486 on get_lnlikelihood_fullmarg
+ * :569-610; the b draw of update_b :489-520 with the epoch columns; the sweep order of
+ * pta_gibbs_freespec.ipynb's sampler: ECORR block, rho|b, gated b).
+ *
+ * The ne epoch columns E (ecid) of a basis-ECORR signal have a diagonal TNT block, so the
+ * ECORR state enters only through a_e = TNT_ee + 1/phi_e, phi_e = 10**(2 x[c][xcol[ebk[e]]]).
+ * R = the other mR columns in increasing order (rcol).  Caller-built, chain-independent:
+ *   Bx [ne x ldbx] rows [TNT[e, R] | d_e | 0 ...], ldbx = 16 ceil((mR + 1) / 16) <= 96;
+ *   Dg [ne] = TNT_ee;  A [mR x mR] = TNT_RR;  dR [mR] = d_R;  ebk [ne] backend of each epoch;
+ *   xcol [n_bk] x column of each backend's log10_ecorr (n_bk <= GS_WHITE_MAX_BK).
+ * gs_ecorr_schur: per chain TNT [c][mR x mR] = A - B^T diag(1/a) B, d [c][mR] = dR - B^T (d_E/a),
+ *   aux [c][4] = {sum log a, sum d_E^2 / a, sum log phi_E, 0}.  The marginalised likelihood is
+ *   then gs_lnlike_marg on the R system (gs_prefix_sys of TNT, d) + (aux1 - aux0 - aux2) / 2
+ *   + the model constants.
+ * gs_ecorr_propose: one Metropolis proposal per chain at step `step` (:458-462): xq = x with
+ *   x[ecol[p]] += z (0.05 n_e) scale; prop [n_chain x 4] scratch.  inj [steps x n_chain x 4]
+ *   (scale value, parameter index, normal, uniform) or NULL (Philox GS_EV_ECORR).
+ *   emin/emax [n_e]: the Uniform prior of each ECORR parameter.
+ * gs_ecorr_accept: lnL1 = lnl + (aux1 - aux0 - aux2)/2 (-inf if info or pinfo is nonzero);
+ *   init = 1 stores lnL1 in lnl0 (the block's starting value); otherwise accepts
+ *   (x[c][col] = proposed value, lnl0 = lnL1, n_acc += 1) when lnL1 - lnl0 > log U and the
+ *   proposal is inside the prior (:465-472).  q_rec [n_chain x n_e] = q[eind] or NULL.
+ * gs_ecorr_bdraw_e: b_E = (d_E - B b_R)/a + z/sqrt(a) and b[rcol[j]] = bR[j]: the full b
+ *   [n_chain x ldb] in original column order from the R draw bR [n_chain x ldbR] (gs_bdraw_sys
+ *   on the Schur systems).  z [n_chain x m] injected normals by original column, or NULL
+ *   (Philox event `event`: GS_EV_ECORR_B / GS_EV_ECORR_B0).  chain_mask as in gs_bdraw.
+ */
+int gs_ecorr_schur(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const double* Bx, const double* Dg,
+                   const int32_t* ebk, int n_bk, const int32_t* xcol, const double* x, int ldx,
+                   const double* A, const double* dR, double* TNT, double* d, double* aux);
+int gs_ecorr_propose(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, const double* emin,
+                     const double* emax, const double* x, int ldx, int n_param, double* xq, int step,
+                     int64_t sweep, int64_t chain_base, const double* inj, double* prop);
+int gs_ecorr_accept(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, int init, const double* lnl,
+                    const int32_t* info, const int32_t* pinfo, const double* aux, const double* prop,
+                    const double* xq, double* x, int ldx, double* lnl0, double* q_rec, int32_t* n_acc);
+int gs_ecorr_bdraw_e(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const double* Bx, const double* Dg,
+                     const int32_t* ebk, const int32_t* xcol, const double* x, int ldx, const double* bR,
+                     int ldbR, const int32_t* ecid, const int32_t* rcol, int m, const double* z,
+                     int64_t sweep, int event, int64_t chain_base, const int32_t* chain_mask, double* b,
+                     int ldb);
 
 /*
  * Philox4x32-10 test hook: out[i] = the 4 words for counter

@@ -23,6 +23,7 @@ OPT_PSR_BASE = 2
 OPT_X_PER_SYS = 3
 OPT_GRID_EXACT = 4
 EV_B0, EV_RHO, EV_B, EV_RED, EV_CURN, EV_GUMBEL, EV_WHITE, EV_REDMH, EV_USER = 1, 2, 3, 4, 5, 6, 7, 8, 16
+EV_ECORR, EV_ECORR_B, EV_ECORR_B0 = 9, 10, 11
 
 _P = C.c_void_p
 _I = C.c_int
@@ -68,6 +69,11 @@ SIGNATURES = {
     "gs_red_mh": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _I, _I64, _I64, _P, _P, _P]),
     "gs_gate_phiinv_irn": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "gs_white_tnt": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I64, _I64, _P, _P]),
+    "gs_ecorr_schur": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P]),
+    "gs_ecorr_propose": (_I, [_P, _I, _I, _P, _P, _P, _P, _I, _I, _P, _I, _I64, _I64, _P, _P]),
+    "gs_ecorr_accept": (_I, [_P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P]),
+    "gs_ecorr_bdraw_e": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P, _I, _P, _P, _I, _P, _I64, _I,
+                              _I64, _P, _P, _I]),
 }
 
 _lib = None

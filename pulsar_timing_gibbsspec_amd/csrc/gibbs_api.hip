@@ -747,4 +747,91 @@ int gs_white_tnt(gs_ctx* ctx, int n_psr, int n_chain, int m_max, const gs_tnt_de
   launch_white_tnt(ctx->stream, a);
   return after_launch("k_white_tnt");
 }
+
+// ------------------------------------------------------------------ basis ECORR
+int gs_ecorr_schur(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const double* Bx, const double* Dg,
+                   const int32_t* ebk, int n_bk, const int32_t* xcol, const double* x, int ldx,
+                   const double* A, const double* dR, double* TNT, double* d, double* aux) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_chain < 0) return fail_arg(2, "n_chain < 0");
+  if (mR <= 0) return fail_arg(3, "mR <= 0");
+  if (ne < 0) return fail_arg(4, "ne < 0");
+  if (ldbx % 16 || ldbx < mR + 1 || !ecorr_nb_supported(ldbx / 16) || ldbx > 16 * ((mR + 1 + 15) / 16))
+    return fail_arg(5, "ldbx must be 16 ceil((mR + 1) / 16) <= 96");
+  if (!Bx || !Dg || !ebk) return fail_arg(6, "NULL Bx / Dg / ebk");
+  if (n_bk <= 0 || n_bk > GS_WHITE_MAX_BK) return fail_arg(9, "n_bk must be in 1..15");
+  if (!xcol || !x || ldx <= 0) return fail_arg(10, "xcol / x / ldx");
+  if (!A || !dR || !TNT || !d || !aux) return fail_arg(13, "NULL A / dR / TNT / d / aux");
+  if (n_chain == 0) return 0;
+  EcorrSchurArgs a;
+  a.n_chain = n_chain; a.mR = mR; a.ne = ne; a.ldbx = ldbx; a.ldx = ldx; a.n_bk = n_bk;
+  a.Bx = Bx; a.Dg = Dg; a.A = A; a.dR = dR; a.x = x; a.ebk = ebk; a.xcol = xcol;
+  a.TNT = TNT; a.d = d; a.aux = aux;
+  launch_ecorr_schur(ctx->stream, a);
+  return after_launch("k_ecorr_schur");
+}
+
+int gs_ecorr_propose(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, const double* emin,
+                     const double* emax, const double* x, int ldx, int n_param, double* xq, int step,
+                     int64_t sweep, int64_t chain_base, const double* inj, double* prop) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_chain < 0) return fail_arg(2, "n_chain < 0");
+  if (n_e <= 0) return fail_arg(3, "n_e <= 0");
+  if (!ecol || !emin || !emax) return fail_arg(4, "NULL ecol / emin / emax");
+  if (!x || ldx <= 0 || n_param <= 0 || n_param > ldx) return fail_arg(7, "x / ldx / n_param");
+  if (!xq || !prop) return fail_arg(10, "NULL xq / prop");
+  if (step < 0) return fail_arg(11, "step < 0");
+  if (n_chain == 0) return 0;
+  EcorrMhArgs a = {};
+  a.n_chain = n_chain; a.n_e = n_e; a.ldx = ldx; a.n_param = n_param; a.step = step;
+  a.sweep = sweep; a.chain_base = chain_base; a.sweep_dev = ctx->sweep_dev; a.key = key_of(ctx);
+  a.ecol = ecol; a.emin = emin; a.emax = emax; a.inj = inj;
+  a.x = const_cast<double*>(x); a.xq = xq; a.prop = prop;
+  launch_ecorr_propose(ctx->stream, a);
+  return after_launch("k_ecorr_propose");
+}
+
+int gs_ecorr_accept(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, int init, const double* lnl,
+                    const int32_t* info, const int32_t* pinfo, const double* aux, const double* prop,
+                    const double* xq, double* x, int ldx, double* lnl0, double* q_rec, int32_t* n_acc) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_chain < 0) return fail_arg(2, "n_chain < 0");
+  if (n_e <= 0 || !ecol) return fail_arg(3, "n_e / ecol");
+  if (!lnl || !aux) return fail_arg(6, "NULL lnl / aux");
+  if (!init && (!prop || !xq || !x || ldx <= 0)) return fail_arg(10, "prop / xq / x / ldx");
+  if (!lnl0) return fail_arg(14, "NULL lnl0");
+  if (n_chain == 0) return 0;
+  EcorrMhArgs a = {};
+  a.n_chain = n_chain; a.n_e = n_e; a.ldx = ldx; a.init = init ? 1 : 0;
+  a.ecol = ecol; a.lnl = lnl; a.info = info; a.pinfo = pinfo; a.aux = aux;
+  a.prop = const_cast<double*>(prop); a.xq = const_cast<double*>(xq); a.x = x; a.lnl0 = lnl0;
+  a.q_rec = q_rec; a.n_acc = n_acc;
+  launch_ecorr_accept(ctx->stream, a);
+  return after_launch("k_ecorr_accept");
+}
+
+int gs_ecorr_bdraw_e(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const double* Bx, const double* Dg,
+                     const int32_t* ebk, const int32_t* xcol, const double* x, int ldx, const double* bR,
+                     int ldbR, const int32_t* ecid, const int32_t* rcol, int m, const double* z,
+                     int64_t sweep, int event, int64_t chain_base, const int32_t* chain_mask, double* b,
+                     int ldb) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_chain < 0 || mR <= 0 || ne < 0) return fail_arg(2, "n_chain / mR / ne");
+  if (ldbx < mR + 1) return fail_arg(5, "ldbx < mR + 1");
+  if (!Bx || !Dg || !ebk || !xcol) return fail_arg(6, "NULL Bx / Dg / ebk / xcol");
+  if (!x || ldx <= 0) return fail_arg(10, "x / ldx");
+  if (!bR || ldbR < mR) return fail_arg(12, "bR / ldbR");
+  if (!ecid || !rcol) return fail_arg(14, "NULL ecid / rcol");
+  if (m != mR + ne) return fail_arg(16, "m != mR + ne");
+  if (!b || ldb < m) return fail_arg(22, "b / ldb");
+  if (n_chain == 0) return 0;
+  EcorrBArgs a;
+  a.n_chain = n_chain; a.mR = mR; a.ne = ne; a.ldbx = ldbx; a.ldx = ldx; a.ldbR = ldbR; a.m = m; a.ldb = ldb;
+  a.event = event; a.sweep = sweep; a.chain_base = chain_base; a.sweep_dev = ctx->sweep_dev; a.key = key_of(ctx);
+  a.Bx = Bx; a.Dg = Dg; a.x = x; a.bR = bR; a.z = z; a.ebk = ebk; a.xcol = xcol; a.ecid = ecid; a.rcol = rcol;
+  a.chain_mask = chain_mask; a.b = b;
+  launch_ecorr_bdraw_e(ctx->stream, a);
+  return after_launch("k_ecorr_bdraw_e");
+}
+
 }  // extern "C"

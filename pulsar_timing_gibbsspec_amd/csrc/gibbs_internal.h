@@ -166,3 +166,36 @@ struct RedMhArgs {
 int launch_red_mh(hipStream_t s, const RedMhArgs& a);
 int launch_white_resid(hipStream_t s, const WhiteResidArgs& a);
 int launch_white_tnt(hipStream_t s, const WhiteTntArgs& a);
+
+// basis-ECORR block (gibbs_ecorr.hip)
+struct EcorrSchurArgs {
+  int n_chain, mR, ne, ldbx, ldx, n_bk;
+  const double *Bx, *Dg, *A, *dR, *x;
+  const int32_t *ebk, *xcol;
+  double *TNT, *d, *aux;
+};
+struct EcorrMhArgs {
+  int n_chain, n_e, ldx, n_param, step, init;
+  int64_t sweep, chain_base;
+  const int64_t* sweep_dev;
+  gs_key key;
+  const int32_t* ecol;
+  const double *emin, *emax, *inj, *lnl, *aux;
+  const int32_t *info, *pinfo;
+  double *x, *xq, *prop, *lnl0, *q_rec;
+  int32_t* n_acc;
+};
+struct EcorrBArgs {
+  int n_chain, mR, ne, ldbx, ldx, ldbR, m, ldb, event;
+  int64_t sweep, chain_base;
+  const int64_t* sweep_dev;
+  gs_key key;
+  const double *Bx, *Dg, *x, *bR, *z;
+  const int32_t *ebk, *xcol, *ecid, *rcol, *chain_mask;
+  double* b;
+};
+bool ecorr_nb_supported(int nb);
+int launch_ecorr_schur(hipStream_t s, const EcorrSchurArgs& a);
+int launch_ecorr_propose(hipStream_t s, const EcorrMhArgs& a);
+int launch_ecorr_accept(hipStream_t s, const EcorrMhArgs& a);
+int launch_ecorr_bdraw_e(hipStream_t s, const EcorrBArgs& a);

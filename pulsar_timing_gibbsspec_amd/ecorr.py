@@ -1,0 +1,261 @@
+"""Basis ECORR on the device.
+
+The reference's ECORR block is ``PulsarBlockGibbs.update_ecorr_params``
+(pulsar_gibbs.py:409-486): single-parameter Metropolis steps on the per-backend
+log10_ecorr values under the marginalised likelihood (``self.get_lnlikelihood``, which
+the .py never defines -- its sample loop prints 'ERROR: No ECORR for now...' and skips
+the block (:675-683); the working sampler is the notebook's
+(pta_gibbs_freespec.ipynb, cell 2: ``get_lnlikelihood`` = the code of
+``get_lnlikelihood_fullmarg`` :569-610, sweep order white -> ECORR -> rho|b -> gated b).
+
+Device form (csrc/gibbs_ecorr.hip): the epoch columns E of the ECORR basis have a
+diagonal TNT block, so every likelihood evaluation and b draw works on the Schur
+complement over the remaining columns R = [timing model | free spectrum]:
+``gs_ecorr_schur`` (batched fp64-MFMA SYRK over epochs, all chains) ->
+``gs_prefix_sys`` -> ``gs_lnlike_marg`` per Metropolis step, and ``gs_bdraw_sys`` on the
+R system + ``gs_ecorr_bdraw_e`` for the epochs per b draw.  White noise is fixed (the
+configuration of SURVEY 8f-4's J1713 run: efac/equad from a noise dictionary).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, ptr
+from .engine import SUPPORTED_NF, _t
+
+
+class EcorrModel:
+    """One pulsar with a basis-ECORR signal, n_chain chains, fixed white noise.
+
+    T (n_toa x m), Nvec, r: host arrays; ecid: the ECORR epoch columns; epoch_backend[e]:
+    backend of each epoch (index into ecol); gwid: the NF free-spectrum columns in
+    (sin, cos) order; every other column is a fixed-prior (timing-model) column with
+    phiinv_fixed (scalar, or one value per such column in increasing column order).
+    ecol / emin / emax: x column and Uniform prior of each backend's
+    log10_ecorr (eind order).
+    """
+
+    def __init__(self, ctx, T, Nvec, r, ecid, epoch_backend, gwid, ecol, emin, emax, n_param, n_chain,
+                 phiinv_fixed=1e-40):
+        self.ctx = ctx
+        dev = ctx.device
+        lib, h = ctx.lib, ctx.handle
+        T = np.ascontiguousarray(T, float)
+        n_toa, m = T.shape
+        ecid = np.asarray(ecid, np.int64)
+        gwid = np.asarray(gwid, np.int64)
+        NF = gwid.size
+        if NF not in SUPPORTED_NF:
+            raise NotImplementedError(f"ECORR path needs NF in {SUPPORTED_NF}, got {NF}")
+        self.m, self.ne, self.NF = m, ecid.size, NF
+        self.C = int(n_chain)
+        self.n_param = int(n_param)
+        rc = np.setdiff1d(np.arange(m), ecid)
+        self.mR = mR = rc.size
+        self.ldbx = 16 * ((mR + 2 + 14) // 16)
+        if self.ldbx > 96:
+            raise NotImplementedError(f"ECORR Schur kernel supports mR <= 95 (got {mR})")
+        pos = {c: i for i, c in enumerate(rc)}
+        fR = np.array([pos[c] for c in gwid], np.int32)
+        mR_idx = np.array([i for i, c in enumerate(rc) if c not in set(gwid.tolist())], np.int32)
+        self.nm = mR - NF
+        if not 0 < self.nm <= 64:
+            raise NotImplementedError("need 1..64 fixed-prior columns")
+        self.NMX = self.nm
+        self.rc_host, self.ecid_host = rc, ecid
+        # TNT / d of the whole basis once (N fixed), then the chain-independent pieces
+        tdesc = np.array([[n_toa, m, 0, 0, 0, 0]], np.int64)
+        Td, Nd, rd = _t(T.ravel(), torch.float64, dev), _t(Nvec, torch.float64, dev), _t(r, torch.float64, dev)
+        TNT = torch.empty(m * m, dtype=torch.float64, device=dev)
+        d = torch.empty(m, dtype=torch.float64, device=dev)
+        check(lib.gs_tnt(h, 1, m, ptr(_t(tdesc, torch.int64, dev)), ptr(Td), ptr(Nd), ptr(rd), ptr(TNT), ptr(d)),
+              "gs_tnt")
+        TNT = TNT.view(m, m)
+        e_t = torch.as_tensor(ecid, device=dev)
+        r_t = torch.as_tensor(rc, device=dev)
+        Bx = torch.zeros(self.ne, self.ldbx, dtype=torch.float64, device=dev)
+        Bx[:, :mR] = TNT[e_t][:, r_t]
+        Bx[:, mR] = d[e_t]
+        self.Bx = Bx.contiguous()
+        self.Dg = TNT[e_t, e_t].contiguous()
+        self.A = TNT[r_t][:, r_t].contiguous()
+        self.dR = d[r_t].contiguous()
+        self.TNT_full, self.d_full = TNT, d
+        self.ebk = _t(np.asarray(epoch_backend, np.int32), torch.int32, dev)
+        self.ecol = _t(np.asarray(ecol, np.int32), torch.int32, dev)
+        self.ecol_host = np.asarray(ecol, np.int64)
+        self.n_bk = len(ecol)
+        self.emin = _t(np.asarray(emin, float), torch.float64, dev)
+        self.emax = _t(np.asarray(emax, float), torch.float64, dev)
+        self.ecid = _t(ecid.astype(np.int32), torch.int32, dev)
+        self.rcol = _t(rc.astype(np.int32), torch.int32, dev)
+        # R system: prefix over the fixed-prior columns, free spectrum last
+        self.fidx = _t(fR[None, :], torch.int32, dev)
+        self.midx = _t(mR_idx[None, :], torch.int32, dev)
+        self.nm_dev = _t(np.array([self.nm], np.int32), torch.int32, dev)
+        phf = np.broadcast_to(np.asarray(phiinv_fixed, float), (self.NMX,))
+        self.phfix = _t(phf[None, :], torch.float64, dev)
+        self.pdesc = _t(np.array([[mR, self.nm, 0, 0]], np.int64), torch.int64, dev)
+        self.mstride = int(lib.gs_model_stride(NF, self.NMX))
+        C = self.C
+        self.TNTc = torch.empty(C * mR * mR, dtype=torch.float64, device=dev)
+        self.dc = torch.empty(C * mR, dtype=torch.float64, device=dev)
+        self.aux = torch.empty(C, 4, dtype=torch.float64, device=dev)
+        self.model = torch.empty(C * self.mstride, dtype=torch.float64, device=dev)
+        self.pinfo = torch.zeros(C, dtype=torch.int32, device=dev)
+        self.lnl = torch.empty(C, dtype=torch.float64, device=dev)
+        self.linfo = torch.zeros(C, dtype=torch.int32, device=dev)
+        self.lnl0 = torch.empty(C, dtype=torch.float64, device=dev)
+        self.xq = torch.empty(C, self.n_param, dtype=torch.float64, device=dev)
+        self.prop = torch.empty(C, 4, dtype=torch.float64, device=dev)
+        self.bR = torch.zeros(C, mR, dtype=torch.float64, device=dev)
+        self.binfo = torch.zeros(C, dtype=torch.int32, device=dev)
+        # -1/2 (sum log N + r^T N^-1 r) + 1/2 sum_M log phiinv_M (get_lnlikelihood_fullmarg :583-600)
+        Nh, rh = np.asarray(Nvec, float), np.asarray(r, float)
+        self.lnl_const = float(-0.5 * (np.sum(np.log(Nh)) + np.sum(rh ** 2 / Nh)) + 0.5 * np.sum(np.log(phf)))
+
+    # ----------------------------------------------------------------- kernels
+    def factor(self, x):
+        """Schur complement of every chain's ECORR state in x (C, n_param) + R prefix."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        check(lib.gs_ecorr_schur(h, self.C, self.mR, self.ne, self.ldbx, ptr(self.Bx), ptr(self.Dg), ptr(self.ebk),
+                                 self.n_bk, ptr(self.ecol), ptr(x), x.shape[1], ptr(self.A), ptr(self.dR),
+                                 ptr(self.TNTc), ptr(self.dc), ptr(self.aux)), "gs_ecorr_schur")
+        check(lib.gs_prefix_sys(h, 1, self.C, self.NF, self.NMX, ptr(self.pdesc), self.mR * self.mR, self.mR,
+                                ptr(self.TNTc), ptr(self.dc), ptr(self.fidx), ptr(self.midx), ptr(self.phfix),
+                                ptr(self.model), ptr(self.pinfo)), "gs_prefix_sys")
+
+    def _lnl_R(self, phiinv_F):
+        check(self.ctx.lib.gs_lnlike_marg(self.ctx.handle, 1, self.C, self.NF, self.NMX, ptr(self.model), 1,
+                                          ptr(self.nm_dev), ptr(phiinv_F), ptr(self.lnl), ptr(self.linfo)),
+              "gs_lnlike_marg")
+
+    def lnlike(self, x, phiinv_F):
+        """get_lnlikelihood_fullmarg (pulsar_gibbs.py:569-610) of every chain: (C,) tensor."""
+        self.factor(x)
+        self._lnl_R(phiinv_F)
+        a = self.aux
+        ok = (self.pinfo == 0) & (self.linfo == 0)
+        val = self.lnl + 0.5 * (a[:, 1] - a[:, 0] - a[:, 2]) + self.lnl_const
+        return torch.where(ok, val, torch.full_like(val, -np.inf))
+
+    def mh(self, x, phiinv_F, n_steps, sweep=0, chain_base=0, inj=None, q_rec=None, n_acc=None):
+        """n_steps Metropolis steps of update_ecorr_params (pulsar_gibbs.py:456-484) for every
+        chain, x (C, n_param) updated in place.  inj (n_steps, C, 4) or None (Philox);
+        q_rec (n_steps, C, n_e) proposals or None."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        ne_p = self.n_bk
+        self.factor(x)
+        self._lnl_R(phiinv_F)
+        check(lib.gs_ecorr_accept(h, self.C, ne_p, ptr(self.ecol), 1, ptr(self.lnl), ptr(self.linfo),
+                                  ptr(self.pinfo), ptr(self.aux), None, None, ptr(x), x.shape[1], ptr(self.lnl0),
+                                  None, None), "gs_ecorr_accept")
+        for s in range(int(n_steps)):
+            check(lib.gs_ecorr_propose(h, self.C, ne_p, ptr(self.ecol), ptr(self.emin), ptr(self.emax), ptr(x),
+                                       x.shape[1], self.n_param, ptr(self.xq), s, sweep, chain_base, ptr(inj),
+                                       ptr(self.prop)), "gs_ecorr_propose")
+            self.factor(self.xq)
+            self._lnl_R(phiinv_F)
+            qr = q_rec[s] if q_rec is not None else None
+            check(lib.gs_ecorr_accept(h, self.C, ne_p, ptr(self.ecol), 0, ptr(self.lnl), ptr(self.linfo),
+                                      ptr(self.pinfo), ptr(self.aux), ptr(self.prop), ptr(self.xq), ptr(x),
+                                      x.shape[1], ptr(self.lnl0), ptr(qr), ptr(n_acc)), "gs_ecorr_accept")
+
+    def bdraw(self, x, phiinv_F, b, z=None, sweep=0, first=False, chain_base=0, chain_mask=None):
+        """b | rho, ECORR of every chain (update_b, pulsar_gibbs.py:489-520): b (C, ldb >= m)
+        written in original column order (masked chains keep theirs).  z (C, m) injected
+        normals by original column, or None (Philox)."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        self.factor(x)
+        zR = z[:, torch.as_tensor(self.rc_host, device=z.device)].contiguous() if z is not None else None
+        ev_r = _lib.EV_B0 if first else _lib.EV_B
+        ev_e = _lib.EV_ECORR_B0 if first else _lib.EV_ECORR_B
+        check(lib.gs_bdraw_sys(h, 1, self.C, self.NF, self.NMX, self.mR, ptr(self.model), ptr(self.fidx),
+                               ptr(self.midx), ptr(self.nm_dev), ptr(phiinv_F), ptr(zR), sweep, ev_r, chain_base,
+                               ptr(chain_mask), ptr(self.bR), ptr(self.binfo)), "gs_bdraw_sys")
+        check(lib.gs_ecorr_bdraw_e(h, self.C, self.mR, self.ne, self.ldbx, ptr(self.Bx), ptr(self.Dg), ptr(self.ebk),
+                                   ptr(self.ecol), ptr(x), x.shape[1], ptr(self.bR), self.mR, ptr(self.ecid),
+                                   ptr(self.rcol), self.m, ptr(z), sweep, ev_e, chain_base, ptr(chain_mask), ptr(b),
+                                   b.shape[1]), "gs_ecorr_bdraw_e")
+        return b
+
+
+class EcorrFreeSpectrumChains:
+    """n_chain chains of one pulsar with the basis-ECORR MH block and the analytic free
+    spectrum, in the notebook sampler's order (pta_gibbs_freespec.ipynb cell 2 sample();
+    pulsar_gibbs.py:656-698 with the ECORR block of :675-683 enabled):
+
+        record x, b -> [ii == 0: b from x0] -> ECORR MH (aclength_ecorr steps) -> rho|b
+        -> gate all(xnew != x_old[-1]) -> b|rho
+    """
+
+    WARMUP = 1000   # update_ecorr_params(xnew, iters=1000) at ii == 0 (notebook sample())
+
+    def __init__(self, em: EcorrModel, gw_cols, gwid, rhomin, rhomax, x0, aclength=None, chain_base=0):
+        self.em = em
+        self.ctx = em.ctx
+        dev = self.ctx.device
+        C = em.C
+        self.gw_cols = _t(np.asarray(gw_cols, np.int32), torch.int32, dev)
+        self.gw_cols_host = np.asarray(gw_cols, np.int64)
+        self.gw0 = int(self.gw_cols_host[0])
+        if not np.array_equal(self.gw_cols_host, self.gw0 + np.arange(em.NF // 2)):
+            raise NotImplementedError("the gw log10_rho columns must be contiguous in x")
+        self.fidx_full = _t(np.asarray(gwid, np.int32)[None, :], torch.int32, dev)
+        self.rhomin, self.rhomax = float(rhomin), float(rhomax)
+        self.aclength = None if aclength is None else int(aclength)
+        self.short_chain = None
+        self.chain_base = int(chain_base)
+        self.x = _t(np.broadcast_to(np.asarray(x0, float), (C, em.n_param)), torch.float64, dev)
+        self.ldb = em.m
+        self.b = torch.zeros(C, self.ldb, dtype=torch.float64, device=dev)
+        self.phiinv_F = torch.empty(C, em.NF, dtype=torch.float64, device=dev)
+        self.xlast = torch.empty(C, dtype=torch.float64, device=dev)
+        self.gate = torch.empty(C, dtype=torch.int32, device=dev)
+        self.n_acc = torch.zeros(C, dtype=torch.int32, device=dev)
+        self.it = 0
+
+    def _phiinv(self, with_gate):
+        check(self.ctx.lib.gs_pta_gate_phiinv(self.ctx.handle, 1, self.em.C, self.em.NF // 2, self.em.n_param,
+                                              ptr(self.x), ptr(self.xlast) if with_gate else None,
+                                              ptr(self.gw_cols), None, ptr(self.phiinv_F), ptr(self.gate)),
+              "gs_pta_gate_phiinv")
+
+    def sweep(self, x_rec=None, b_rec=None, z0=None, z=None, u=None, mh_inj=None):
+        """One sweep of every chain; x_rec / b_rec (C, n_param) / (C, ldb) get the state
+        before the update (pulsar_gibbs.py:658-659)."""
+        em, lib, h = self.em, self.ctx.lib, self.ctx.handle
+        ii = self.it
+        if x_rec is not None:
+            x_rec.copy_(self.x)
+        if b_rec is not None:
+            b_rec.copy_(self.b)
+        self.xlast.copy_(self.x[:, -1])
+        if ii == 0:  # first b from xs (:661-662)
+            self._phiinv(False)
+            em.bdraw(self.x, self.phiinv_F, self.b, z=z0, sweep=ii, first=True, chain_base=self.chain_base)
+        self._phiinv(False)
+        if self.aclength is None:
+            # warm-up (update_ecorr_params iters=1000, pulsar_gibbs.py:422-451): the proposals
+            # q[eind] form short_chain; aclength_ecorr = max acor over its columns after 100
+            # (chain 0's value is used by every chain)
+            from .diagnostics import white_aclength
+            q_rec = torch.empty(self.WARMUP, em.C, em.n_bk, dtype=torch.float64, device=self.ctx.device)
+            em.mh(self.x, self.phiinv_F, self.WARMUP, sweep=ii, chain_base=self.chain_base, q_rec=q_rec,
+                  n_acc=self.n_acc)
+            self.short_chain = q_rec[:, 0].cpu().numpy()
+            self.aclength = int(white_aclength(self.short_chain))
+        else:
+            em.mh(self.x, self.phiinv_F, self.aclength, sweep=ii, chain_base=self.chain_base, inj=mh_inj,
+                  n_acc=self.n_acc)
+        # rho|b writes the n_f log10_rho columns of x in place (:206-216, 236)
+        xg = ctypes.c_void_p(self.x.data_ptr() + 8 * self.gw0)
+        check(lib.gs_rho_analytic(h, 1, em.C, em.NF, self.ldb, ptr(self.fidx_full), ptr(self.b), ptr(u), ii,
+                                  self.chain_base, self.rhomin, self.rhomax, xg, em.n_param), "gs_rho_analytic")
+        self._phiinv(True)
+        em.bdraw(self.x, self.phiinv_F, self.b, z=z, sweep=ii, chain_base=self.chain_base, chain_mask=self.gate)
+        self.it += 1

@@ -21,8 +21,13 @@ Extensions (keyword-only, reference-equivalent defaults): ``nchains``
 
 * power-law intrinsic red noise: ``update_red_params`` /
   ``get_lnlikelihood_red`` -> gs_red_mh (:271-329, :549-566), rho|b -> gs_rho_gumbel
-  (:218-236), and ``sample`` runs rednoise.RedNoiseChains.  ECORR blocks stay out of
-  scope and raise ``NotImplementedError`` from ``sample``.
+  (:218-236), and ``sample`` runs rednoise.RedNoiseChains.
+* basis ECORR: ``update_ecorr_params`` (:409-486) with
+  ``get_lnlikelihood`` = the marginalised likelihood (the notebook's definition; the .py
+  calls it without defining it), ``update_b`` / ``get_lnlikelihood_fullmarg`` through the
+  ECORR-eliminated Schur systems (ecorr.EcorrModel), and ``sample`` runs the notebook
+  sampler's order (ECORR block, rho|b, gated b; ecorr.EcorrFreeSpectrumChains) where the
+  .py prints 'ERROR: No ECORR for now...' and skips the block (:675-683).
 """
 from __future__ import annotations
 
@@ -33,6 +38,7 @@ import torch
 
 from . import _lib
 from .diagnostics import white_aclength
+from .ecorr import EcorrFreeSpectrumChains, EcorrModel
 from .engine import DeviceModel, FreeSpectrumChains, HistoryStreamer, grid3
 from .rednoise import (DE_BUFFER, RED_STEPS, RedJumps, RedNoiseChains, powerlaw_loglinear,
                        warmup as red_warmup)
@@ -99,6 +105,19 @@ class PulsarBlockGibbs(object):
             print("Basis count is good")
         else:
             print("WARNING: Miscounted basis entries. Maybe red noise and GW do not share a design matrix.")
+
+        if self.ecid is not None:
+            # prior bounds of the ECORR parameters (pulsar_gibbs.py:111-118)
+            ind = None
+            for ct, par in enumerate([p.name for p in self.params]):
+                if "ecorr" in par:
+                    ind = ct
+            lo, hi = _parse_uniform_bounds(self.params[ind].params[0])
+            self.ecorrmin, self.ecorrmax = 10 ** (2 * lo), 10 ** (2 * hi)
+            if self.ecorrsample == "conditional":
+                # the reference's epoch selection needs enterprise's selections.by_backend
+                # (:121-127) and its conditional draw is commented out ('NEEDS TO BE FIXED')
+                raise NotImplementedError("ecorrsample='conditional' is not implemented in the reference")
 
         self.red_sig = None
         self.gw_sig = None
@@ -188,11 +207,95 @@ class PulsarBlockGibbs(object):
     def get_lnlikelihood_fullmarg(self, xs):
         """Marginalised likelihood (pulsar_gibbs.py:569-610) on the device: the prefix
         model block + one augmented tile factorisation (gs_lnlike_marg); -inf when
-        Sigma is not positive definite (the reference's LinAlgError branch, :598-599)."""
+        Sigma is not positive definite (the reference's LinAlgError branch, :598-599).
+        With basis ECORR: the ECORR-eliminated Schur system (ecorr.EcorrModel.lnlike)."""
+        if self.ecid is not None:
+            em = self._ecorr_model1(xs)
+            x = torch.as_tensor(np.asarray(xs, float)[None, :], device=self.ctx.device).contiguous()
+            ph = torch.as_tensor(np.ascontiguousarray(self._ecorr_phiinv_F(xs))[None], device=self.ctx.device)
+            return float(em.lnlike(x, ph)[0])
         model = self._model(xs)
         ph = torch.as_tensor(np.ascontiguousarray(self._phiinv_F(xs))[None], device=self.ctx.device)
         lnl, info = model.lnlike_marg(ph, 1)
         return -np.inf if int(info[0]) else float(lnl[0])
+
+    def get_lnlikelihood(self, xs):
+        """The likelihood update_ecorr_params calls (pulsar_gibbs.py:420, 463) and the .py
+        never defines; the notebook's get_lnlikelihood is get_lnlikelihood_fullmarg's code."""
+        return self.get_lnlikelihood_fullmarg(xs)
+
+    # ------------------------------------------------------------ basis ECORR (8f-4)
+    def _ecorr_loop(self):
+        extra = [n for n in self.param_names if "rho" not in n]
+        return self.ecid is not None and bool(extra) and all("ecorr" in n for n in extra)
+
+    def _ecorr_structure(self, xs):
+        """(eind, epoch_backend, emin, emax) through the PTA contract: the ECORR columns
+        whose phi moves with each ECORR parameter; phi_E = 10**(2 log10_ecorr) is verified."""
+        eind = self.get_ecorr_indices()
+        x0 = np.asarray(xs, float)
+        ec = np.asarray(self.ecid)
+        ph0 = 1.0 / self.pta.get_phiinv(self.map_params(x0), logdet=False)[0][ec]
+        ebk = np.full(ec.size, -1, np.int64)
+        for k, j in enumerate(eind):
+            xp = x0.copy()
+            xp[j] += 0.5
+            mv = 1.0 / self.pta.get_phiinv(self.map_params(xp), logdet=False)[0][ec] != ph0
+            if (ebk[mv] != -1).any():
+                raise NotImplementedError("ECORR selections overlap")
+            ebk[mv] = k
+        if (ebk == -1).any():
+            raise NotImplementedError("ECORR epoch column not driven by any ECORR parameter")
+        want = np.array([10.0 ** (2.0 * float(x0[j])) for j in eind])[ebk]
+        if np.max(np.abs(ph0 - want) / want) > 1e-12:
+            raise NotImplementedError("ECORR phi is not 10**(2 log10_ecorr) per epoch")
+        bounds = []
+        for p in self.params:
+            lo, hi = _parse_uniform_bounds(p)
+            bounds += [(lo, hi)] * (p.size or 1)
+        emin = np.array([bounds[j][0] for j in eind])
+        emax = np.array([bounds[j][1] for j in eind])
+        return eind, ebk, emin, emax
+
+    def _ecorr_model(self, xs, n_chain):
+        params = self.map_params(xs)
+        T = self.pta.get_basis(params)[0]
+        Nvec = self.pta.get_ndiag(params)[0]
+        phiinv = self.pta.get_phiinv(params, logdet=False)[0]
+        eind, ebk, emin, emax = self._ecorr_structure(xs)
+        fixed = np.setdiff1d(np.arange(T.shape[1]), np.concatenate([self.ecid, self.gwid]))
+        return EcorrModel(self.ctx, T, Nvec, self._residuals, self.ecid, ebk, self.gwid, eind, emin, emax,
+                          len(xs), n_chain, phiinv_fixed=phiinv[fixed])
+
+    def _ecorr_model1(self, xs):
+        if getattr(self, "_em1", None) is None:
+            self._em1 = self._ecorr_model(xs, 1)
+        return self._em1
+
+    def _ecorr_phiinv_F(self, xs):
+        return self.pta.get_phiinv(self.map_params(xs), logdet=False)[0][self.gwid]
+
+    def update_ecorr_params(self, xs, iters=None, inj=None):
+        """Basis-ECORR Metropolis block (pulsar_gibbs.py:409-486) on the GPU: with ``iters``
+        the warm-up (cov_ecorr, sigma_ecorr, svd_ecorr and aclength_ecorr from acor of the
+        proposal chain after 100 steps, :448-451), else ``aclength_ecorr`` steps.  ``inj``
+        (steps, 4): injected (scale, parameter index within eind, normal, uniform)."""
+        dev = self.ctx.device
+        em = self._ecorr_model1(xs)
+        x = torch.as_tensor(np.asarray(xs, float)[None, :], device=dev).contiguous()
+        ph = torch.as_tensor(np.ascontiguousarray(self._ecorr_phiinv_F(xs))[None], device=dev)
+        n = int(iters) if iters is not None else int(self.aclength_ecorr)
+        q_rec = torch.empty(n, 1, em.n_bk, dtype=torch.float64, device=dev) if iters is not None else None
+        it = None if inj is None else torch.as_tensor(np.asarray(inj, float).reshape(n, 1, 4), device=dev)
+        em.mh(x, ph, n, sweep=self._ndraw, inj=it, q_rec=q_rec)
+        self._ndraw += 1
+        if iters is not None:
+            short_chain = q_rec[:, 0].cpu().numpy()
+            self.cov_ecorr = np.cov(short_chain[100:, :], rowvar=False)
+            self.sigma_ecorr = np.diag(np.atleast_2d(self.cov_ecorr)) ** 0.5
+            self.svd_ecorr = np.linalg.svd(np.atleast_2d(self.cov_ecorr))
+            self.aclength_ecorr = white_aclength(short_chain)
+        return x[0].cpu().numpy()
 
     # ------------------------------------------------------------ white noise
     def _white_structure(self, xs):
@@ -292,7 +395,20 @@ class PulsarBlockGibbs(object):
         """b | rho, data (pulsar_gibbs.py:489-520) on the GPU.
 
         ``z`` (optional, length m): standard normals in the Cholesky draw's
-        coordinates (parity mode); default: device Philox."""
+        coordinates (parity mode); default: device Philox.  With basis ECORR: the
+        ECORR-eliminated draw (ecorr.EcorrModel.bdraw; z by original column)."""
+        if self.ecid is not None:
+            dev = self.ctx.device
+            em = self._ecorr_model1(xs)
+            x = torch.as_tensor(np.asarray(xs, float)[None, :], device=dev).contiguous()
+            ph = torch.as_tensor(np.ascontiguousarray(self._ecorr_phiinv_F(xs))[None], device=dev)
+            zt = None if z is None else torch.as_tensor(np.asarray(z, float)[None, :em.m], device=dev).contiguous()
+            b = torch.zeros(1, em.m, dtype=torch.float64, device=dev)
+            em.bdraw(x, ph, b, z=zt, sweep=self._ndraw, first=False)
+            self._ndraw += 1
+            if int(em.binfo[0]) != 0:
+                raise np.linalg.LinAlgError(f"Sigma not positive definite (leading minor {int(em.binfo[0])})")
+            return b[0].cpu().numpy()
         model = self._model(xs)
         self.TNT, self.d = model.tnt_host(0)
         dev = self.ctx.device
@@ -436,7 +552,7 @@ class PulsarBlockGibbs(object):
         return bool(extra) and all(("efac" in n or "equad" in n) for n in extra)
 
     def _check_device_loop(self, xs):
-        if self._red_loop() and self.hypersample == "conditional":
+        if (self._red_loop() or self._ecorr_loop()) and self.hypersample == "conditional":
             return
         extra = [n for n in self.param_names if "rho" not in n and not self._white_loop()]
         if extra or self.red_sig is not None or self.hypersample != "conditional":
@@ -462,6 +578,11 @@ class PulsarBlockGibbs(object):
 
         if self._red_loop():
             out = self._sample_red(xs, outdir, niter, resume, save_every)
+            if flush_final:
+                self._flush(outdir)
+            return out
+        if self._ecorr_loop():
+            out = self._sample_ecorr(xs, outdir, niter, resume, save_every)
             if flush_final:
                 self._flush(outdir)
             return out
@@ -616,6 +737,72 @@ class PulsarBlockGibbs(object):
         info = runner.info.cpu().numpy()
         if info.any():
             print(f"WARNING: {int((info != 0).sum())} chains hit a non-positive-definite Sigma")
+        self._b = runner.b[0, :m].cpu().numpy()
+        self._runner = runner
+        return self.chain
+
+    def _sample_ecorr(self, xs, outdir, niter, resume, save_every):
+        """sample() with the basis-ECORR MH block in the notebook sampler's order (ECORR
+        block, rho|b, gated b; pulsar_gibbs.py:656-698 with :675-683 enabled): one device
+        launch sequence per sweep for all chains (ecorr.EcorrFreeSpectrumChains)."""
+        nc = self.nchains
+        dev = self.ctx.device
+        em = self._ecorr_model(xs, nc)
+        m, n_param = em.m, len(xs)
+        self.chain = np.zeros((niter, n_param))
+        self.bchain = np.zeros((niter, len(self._b)))
+        self.chains = np.zeros((nc, niter, n_param)) if nc > 1 else None
+        self.bchains = np.zeros((nc, niter, len(self._b))) if nc > 1 else None
+        start = 0
+        x0 = np.asarray(xs, float)
+        if resume and os.path.exists(f"{outdir}/chain.npy"):
+            print("Resuming from previous run...")
+            c0 = np.load(f"{outdir}/chain.npy")
+            b0 = np.load(f"{outdir}/bchain.npy")
+            start = min(c0.shape[0], b0.shape[0])
+            self.chain[:start] = c0[:start]
+            self.bchain[:start] = b0[:start]
+        runner = EcorrFreeSpectrumChains(em, self.get_gwrho_param_indices(), self.gwid, self.rhomin, self.rhomax,
+                                         x0, aclength=getattr(self, "aclength_ecorr", None))
+        if start > 0:
+            if runner.aclength is None:
+                raise NotImplementedError("resume of an ECORR run needs aclength_ecorr")
+            runner.x.copy_(torch.as_tensor(self.chain[start - 1][None, :], device=dev).expand(nc, -1))
+            runner.b[:, :m] = torch.as_tensor(self.bchain[start - 1], device=dev)
+            runner.it = start
+        blk = max(1, save_every)
+        xr = torch.empty(blk + 1, nc, n_param, dtype=torch.float64, device=dev)
+        br = torch.empty(blk + 1, nc, m, dtype=torch.float64, device=dev)
+        ii = start
+        while ii < niter:
+            nxt = min(niter, (ii // blk + 1) * blk + 1)
+            n = nxt - ii
+            for k in range(n):
+                runner.sweep(x_rec=xr[k], b_rec=br[k])
+            xh = xr[:n].cpu().numpy()
+            bh = br[:n].cpu().numpy()
+            self.chain[ii:nxt] = xh[:, 0]
+            self.bchain[ii:nxt] = bh[:, 0]
+            if nc > 1:
+                self.chains[:, ii:nxt] = np.moveaxis(xh, 1, 0)
+                self.bchains[:, ii:nxt] = np.moveaxis(bh, 1, 0)
+            ii = nxt
+            self.iter = ii - 1
+            last = ii - 1
+            if last % save_every == 0 and last > 0:
+                np.save(f"{outdir}/chain.npy", self.chain[:last + 1, :])
+                np.save(f"{outdir}/bchain.npy", self.bchain[:last + 1, :])
+                if nc > 1:
+                    np.save(f"{outdir}/chains.npy", self.chains[:, :last + 1])
+                    np.save(f"{outdir}/bchains.npy", self.bchains[:, :last + 1])
+        if runner.short_chain is not None:
+            sc = runner.short_chain
+            self.cov_ecorr = np.cov(sc[100:, :], rowvar=False)
+            self.sigma_ecorr = np.diag(np.atleast_2d(self.cov_ecorr)) ** 0.5
+            self.svd_ecorr = np.linalg.svd(np.atleast_2d(self.cov_ecorr))
+        self.aclength_ecorr = runner.aclength
+        if int(em.binfo.max()) != 0:
+            print("WARNING: chains hit a non-positive-definite Sigma")
         self._b = runner.b[0, :m].cpu().numpy()
         self._runner = runner
         return self.chain

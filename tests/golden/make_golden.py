@@ -408,12 +408,40 @@ def ecorr_mh(ref, out, nsweep=6, acl=30, nlike=8):
     print("ecorr:", out, len(log))
 
 
+def ecorr_long(ref, out, niter=6000, thin=5, acl=10):
+    """Long reference run of the ECORR sweep (ecorr_mh's loop, no draw capture) for the
+    posterior comparison: x thinned by `thin`."""
+    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=0)
+    np.random.seed(31)
+    g = _quiet(ref.PulsarBlockGibbs, pta)
+    g.get_lnlikelihood = g.get_lnlikelihood_fullmarg
+    g.aclength_ecorr = acl
+    x0 = np.concatenate([p.sample().flatten() for p in g.params])
+    xnew = x0.copy()
+    rows = []
+    for ii in range(niter):
+        if ii % thin == 0:
+            rows.append(xnew.copy())
+        xold_last = xnew[-1]
+        if ii == 0:
+            g._b = g.update_b(x0)
+        g.TNT = g.d = None
+        xnew = g.update_ecorr_params(xnew, iters=None)
+        xnew = g.update_gwrho_params(xnew)
+        if np.all(xnew != xold_last):
+            g._b = g.update_b(xnew)
+    np.savez_compressed(out, x0=x0, chain=np.stack(rows), thin=thin, aclength=acl)
+    print("ecorr long:", out, len(rows))
+
+
 def main(root):
     mods = load_reference(root)
     PB = mods["pulsar_gibbs"]
     PT = mods["pta_gibbs"]
     if "--only-ecorr" in sys.argv:
         ecorr_mh(PB, os.path.join(HERE, "ecorr_mh_j1713.npz"))
+        if "--long" in sys.argv:
+            ecorr_long(PB, os.path.join(HERE, "ecorr_long_j1713.npz"))
         return
     if "--only-red" in sys.argv:
         red_likelihood(PB, os.path.join(HERE, "red_lnlike_j1713.npz"))
@@ -429,6 +457,7 @@ def main(root):
     ecorr_mh(PB, os.path.join(HERE, "ecorr_mh_j1713.npz"))
     if "--long" in sys.argv:
         single_pulsar_long(PB, os.path.join(HERE, "long_j1713.npz"))
+        ecorr_long(PB, os.path.join(HERE, "ecorr_long_j1713.npz"))
 
 
 if __name__ == "__main__":

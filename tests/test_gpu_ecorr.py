@@ -1,0 +1,180 @@
+""" Basis ECORR on the GPU, through the C-ABI, against the reference's own run
+(tests/golden/ecorr_mh_j1713.npz: PulsarBlockGibbs.update_ecorr_params on its
+get_lnlikelihood_fullmarg inside the notebook sampler's sweep order, every draw captured;
+tests/golden/ecorr_long_j1713.npz: a long reference chain).
+
+* marginalised likelihood at prior draws: |device - reference| < 1e-7 (values ~7e3; the
+  device eliminates the diagonal epoch block first, the reference factors all 212 columns);
+* the Metropolis block fed the reference's draws: accept/reject decisions coincide, so the
+  ECORR parameters come out bit-identical;
+* b | rho: the zero-normal draw is the conditional mean (1e-9 normwise vs the oracle's block
+  form, 1e-8 vs a dense solve) and the normal -> b map G satisfies G^T Sigma G = I;
+* the sampler (Philox draws, many chains): per-parameter KS test against the reference chain.
+"""
+import numpy as np
+import pytest
+
+from tests.conftest import golden, gpu_available
+from oracle import gibbs_oracle as O
+from tests.parity_data import normwise_rel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    from pulsar_timing_gibbsspec_amd import _lib
+    return _lib.Context(0, seed=11)
+
+
+def _items(g):
+    kinds, vals, lens = g["kinds"], g["vals"], g["lens"]
+    off = np.concatenate([[0], np.cumsum(lens)])
+    return [(kinds[i], vals[off[i]:off[i + 1]]) for i in range(kinds.size)]
+
+
+def _model(ctx, g, C):
+    from pulsar_timing_gibbsspec_amd.ecorr import EcorrModel
+    eind = np.asarray(g["eind"])
+    return EcorrModel(ctx, g["T"], g["Nvec"], g["r"], g["ecid"], g["epoch_backend"], g["gwid"], eind,
+                      g["pmin"][eind], g["pmax"][eind], len(g["param_names"]), C)
+
+
+def _gwind(g):
+    return np.array([i for i, n in enumerate(g["param_names"]) if "rho" in n])
+
+
+def _dev(a, dtype=None):
+    import torch
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype or torch.float64, device="cuda")
+
+
+def _phiinv_F(g, X):
+    return 1.0 / np.repeat(10.0 ** (2.0 * X[:, _gwind(g)]), 2, axis=1)
+
+
+def test_ecorr_lnlike_matches_reference(ctx):
+    g = golden("ecorr_mh_j1713.npz")
+    X = g["x_like"]
+    em = _model(ctx, g, X.shape[0])
+    got = em.lnlike(_dev(X), _dev(_phiinv_F(g, X))).cpu().numpy()
+    err = np.abs(got - g["lnlike"])
+    assert err.max() < 1e-7, (got, g["lnlike"])
+
+
+def test_ecorr_mh_matches_reference(ctx):
+    """Every sweep's ECORR block of the reference run, one chain per sweep, fed the
+    reference's (scale, parameter, normal, uniform) draws: outputs bit-identical."""
+    g = golden("ecorr_mh_j1713.npz")
+    eind = list(np.asarray(g["eind"]))
+    acl = int(g["aclength"])
+    n = g["e_in"].shape[0]
+    items = iter(_items(g))
+    inj = np.zeros((acl, n, 4))
+    for ii in range(n):
+        if ii == 0:
+            assert next(items)[0] == "randn"      # first b
+        for s in range(acl):
+            (k1, sc), (k2, p), (k3, z), (k4, u) = next(items), next(items), next(items), next(items)
+            assert (k1, k2, k3, k4) == ("choice", "choice", "randn", "rand")
+            inj[s, ii] = (sc[0], eind.index(int(p[0])), z[0], u[0])
+        assert next(items)[0] == "uniform"       # rho|b
+        k, _ = next(items)                       # gated b
+        assert k == "randn"
+    em = _model(ctx, g, n)
+    x = _dev(g["e_in"])
+    import torch
+    n_acc = torch.zeros(n, dtype=torch.int32, device="cuda")
+    em.mh(x, _dev(_phiinv_F(g, g["e_in"])), acl, inj=_dev(inj), n_acc=n_acc)
+    out = x.cpu().numpy()
+    assert np.array_equal(out, g["e_out"]), np.abs(out - g["e_out"]).max()
+    assert n_acc.cpu().numpy().min() > 0
+
+
+def test_ecorr_bdraw_is_exact_conditional(ctx):
+    import torch
+    g = golden("ecorr_mh_j1713.npz")
+    T, N, r = g["T"], g["Nvec"], g["r"]
+    TNT, d = O.tnt(T, N, r)
+    m = T.shape[1]
+    x0 = g["x0"]
+    eind, ecid, ebk, gwid = g["eind"], g["ecid"], g["epoch_backend"], g["gwid"]
+    ph = np.full(m, 1e40)
+    ph[ecid] = np.array([10.0 ** (2.0 * float(x0[e])) for e in eind])[ebk]
+    ph[gwid] = np.repeat(10.0 ** (2.0 * x0[_gwind(g)]), 2)
+    phiinv = 1.0 / ph
+    C = m + 1
+    em = _model(ctx, g, C)
+    X = np.broadcast_to(x0, (C, x0.size))
+    Z = np.zeros((C, m))
+    Z[1:] = np.eye(m)
+    b = torch.zeros(C, m, dtype=torch.float64, device="cuda")
+    em.bdraw(_dev(X), _dev(_phiinv_F(g, X)), b, z=_dev(Z))
+    B = b.cpu().numpy()
+    rc = np.setdiff1d(np.arange(m), ecid)
+    mean_o = O.bdraw_ecorr(TNT, d, ecid, phiinv, np.zeros(rc.size), np.zeros(ecid.size))
+    assert normwise_rel(B[0], mean_o) < 1e-9
+    Sig = TNT + np.diag(phiinv)
+    assert normwise_rel(B[0], np.linalg.solve(Sig, d)) < 1e-8
+    G = (B[1:] - B[0]).T
+    assert np.abs(G.T @ Sig @ G - np.eye(m)).max() < 1e-6
+    assert int(em.binfo.max()) == 0
+
+
+def test_ecorr_sampler_posterior_ks(ctx):
+    """Device sampler (Philox) vs the reference's long chain: per-parameter two-sample KS on
+    the ECORR parameters and every log10_rho bin (reference thinned to ~independent draws)."""
+    import torch
+    from scipy.stats import ks_2samp
+    from pulsar_timing_gibbsspec_amd.ecorr import EcorrFreeSpectrumChains
+    g = golden("ecorr_mh_j1713.npz")
+    L = golden("ecorr_long_j1713.npz")
+    C, n_sweep, burn = 1024, 60, 40
+    em = _model(ctx, g, C)
+    run = EcorrFreeSpectrumChains(em, _gwind(g), g["gwid"], float(g["rhomin"]), float(g["rhomax"]),
+                                  L["x0"], int(L["aclength"]))
+    x_rec = torch.empty(n_sweep, C, len(g["param_names"]), dtype=torch.float64, device="cuda")
+    for ii in range(n_sweep):
+        run.sweep(x_rec=x_rec[ii])
+    dev = x_rec[burn:].cpu().numpy()
+    assert np.isfinite(dev).all()
+    ref = L["chain"][200:]        # thinned by 5, burn-in 1000 sweeps
+    ref = ref[::5]
+    pmin = 1.0
+    for j in list(np.asarray(g["eind"])) + list(_gwind(g)):
+        p = ks_2samp(dev[-1, :, j], ref[:, j]).pvalue
+        pmin = min(pmin, p)
+    # 32 tests: family-wise threshold
+    assert pmin > 1e-4, pmin
+
+
+def test_pulsar_block_gibbs_ecorr_surface(ctx, tmp_path):
+    """PulsarBlockGibbs on the ECORR model: prior parsing (:111-118), the notebook's
+    get_lnlikelihood, update_ecorr_params fed the reference's first-sweep draws, and a
+    short multi-chain sample() through the warm-up (chain files, finite rows)."""
+    from pulsar_timing_gibbsspec_amd import synthetic
+    from pulsar_timing_gibbsspec_amd.pulsar_gibbs import PulsarBlockGibbs
+    g = golden("ecorr_mh_j1713.npz")
+    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=0)
+    gb = PulsarBlockGibbs(pta, nchains=64, seed=3)
+    assert np.allclose([gb.ecorrmin, gb.ecorrmax], [g["ecorrmin"], g["ecorrmax"]], rtol=0, atol=0)
+    assert np.array_equal(gb.ecid, g["ecid"]) and np.array_equal(gb.gwid, g["gwid"])
+    for x, ref in zip(g["x_like"], g["lnlike"]):
+        assert abs(gb.get_lnlikelihood(x) - ref) < 1e-7
+    eind = list(np.asarray(g["eind"]))
+    items = iter(_items(g))
+    assert next(items)[0] == "randn"
+    acl = int(g["aclength"])
+    inj = []
+    for _ in range(acl):
+        (_, sc), (_, p), (_, z), (_, u) = next(items), next(items), next(items), next(items)
+        inj.append((sc[0], eind.index(int(p[0])), z[0], u[0]))
+    gb.aclength_ecorr = acl
+    assert np.array_equal(gb.update_ecorr_params(g["e_in"][0], inj=np.array(inj)), g["e_out"][0])
+    del gb.aclength_ecorr
+    chain = gb.sample(g["x0"], outdir=str(tmp_path), niter=12, save_every=5)
+    assert chain.shape == (12, len(g["param_names"])) and np.isfinite(chain).all()
+    assert gb.chains.shape[0] == 64 and 1 <= gb.aclength_ecorr < 1000
+    assert np.load(tmp_path / "chain.npy").shape[0] == 11
