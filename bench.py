@@ -331,6 +331,120 @@ def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, a
                                   "over the HIP-event time of one refresh (SYRK + prefix)"})
 
 
+def ecorr_cpu_baseline(seconds=10.0, aclength=10):
+    """The oracle's restatement of the ECORR sweep (notebook order; update_ecorr_params
+    :456-484 on get_lnlikelihood_fullmarg :569-610 with TNT recomputed each sweep as the
+    reference does, :664-665; SVD b draw :489-520), one chain, 1 thread."""
+    from oracle import gibbs_oracle as O
+    from pulsar_timing_gibbsspec_amd import synthetic
+    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=0)
+    T, r, N = pta.get_basis()[0], pta.get_residuals()[0], pta.get_ndiag()[0]
+    names = pta.param_names
+    sig = pta.signals["J1713+0747_basis_ecorr"]
+    ebk = sig.epoch_backend
+    eind = [i for i, n in enumerate(names) if "ecorr" in n]
+    gw = np.array([i for i, n in enumerate(names) if "rho" in n])
+    m = T.shape[1]
+    ne = ebk.size
+    gwid = ne + np.arange(2 * gw.size)
+    rng = np.random.default_rng(0)
+    x = np.concatenate([[-6.3] * len(eind), rng.uniform(-9, -4, gw.size)])
+
+    def phi(xx):
+        ph = np.full(m, 1e40)
+        ph[:ne] = (10.0 ** (2.0 * xx[eind]))[ebk]
+        ph[gwid] = np.repeat(10.0 ** (2.0 * xx[gw]), 2)
+        return ph
+    TNT, dd = O.tnt(T, N, r)
+    b = O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m))    # first b from xs
+    it, t0 = 0, time.perf_counter()
+    while True:
+        TNT, dd = O.tnt(T, N, r)
+
+        def lnl(xx):
+            ph = phi(xx)
+            return O.lnlike_fullmarg(r, N, TNT, dd, 1.0 / ph, np.sum(np.log(ph)))
+        steps = [(rng.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]), rng.choice(eind),
+                  rng.standard_normal(), rng.random()) for _ in range(aclength)]
+        x = O.white_mh(x, eind, steps, lnl, lambda xx: 0.0 if np.all((xx[eind] >= -8.5) & (xx[eind] <= -5)) else -np.inf)
+        x[gw] = 0.5 * np.log10(O.rho_analytic(O.tau_half(b, gwid), rng.random(gw.size), 1e-18, 1e-8))
+        b = O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m))
+        it += 1
+        el = time.perf_counter() - t0
+        if el > seconds:
+            break
+    return dict(value=it / el, unit="iters/s", cores=1, kind="port",
+                sample=f"{it} sweeps of the single-chain ECORR loop (m={m}, {ne} epochs, {aclength} ECORR MH steps, "
+                       f"oracle restatement, numpy/LAPACK, 1 thread) in {el:.1f} s")
+
+
+def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
+    """single pulsar with basis ECORR (J1713-like, 2 backends, 136 epochs,
+    m = 212), C chains per GPU, aclength ECORR MH steps per sweep (each a batched
+    likelihood evaluation: k_ecorr_schur + prefix + lnlike), analytic rho|b, gated b."""
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd.ecorr import EcorrFreeSpectrumChains, EcorrModel
+    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=0)
+    names = pta.param_names
+    sig = pta.signals["J1713+0747_basis_ecorr"]
+    ebk = sig.epoch_backend
+    ne = ebk.size
+    eind = [i for i, n in enumerate(names) if "ecorr" in n]
+    gw = [i for i, n in enumerate(names) if "rho" in n]
+    T = pta.get_basis()[0]
+    m = T.shape[1]
+    gwid = ne + np.arange(2 * len(gw))
+    ctx = _lib.Context(dev.index, seed=20251017)
+    em = EcorrModel(ctx, T, pta.get_ndiag()[0], pta.get_residuals()[0], np.arange(ne), ebk, gwid, eind,
+                    [-8.5] * len(eind), [-5.0] * len(eind), len(names), C)
+    rng = np.random.default_rng(rank)
+    x0 = np.concatenate([np.full((C, len(eind)), -6.3), rng.uniform(-9, -4, (C, len(gw)))], axis=1)
+    eng = EcorrFreeSpectrumChains(em, gw, gwid, 1e-18, 1e-8, x0, aclength=aclength, chain_base=rank * C)
+    for _ in range(W):
+        eng.sweep()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        eng.sweep()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if int(em.binfo.abs().sum()) or int(em.pinfo.abs().sum()):
+        raise RuntimeError("non-PD system in the ECORR bench")
+    # dominant kernel: gs_ecorr_schur, timed alone on the ctx stream
+    stream = ctx.stream
+    lib, h = ctx.lib, ctx.handle
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        _lib.check(lib.gs_ecorr_schur(h, C, em.mR, em.ne, em.ldbx, _lib.ptr(em.Bx), _lib.ptr(em.Dg),
+                                      _lib.ptr(em.ebk), em.n_bk, _lib.ptr(em.ecol), _lib.ptr(eng.x),
+                                      eng.x.shape[1], _lib.ptr(em.A), _lib.ptr(em.dR), _lib.ptr(em.TNTc),
+                                      _lib.ptr(em.dc), _lib.ptr(em.aux)), "gs_ecorr_schur")
+    e1.record(stream)
+    torch.cuda.synchronize()
+    k_ms = e0.elapsed_time(e1) / reps
+    mR = em.mR
+    flops = C * ne * (mR + 1) * (mR + 2)       # lower triangle of [B | d_E]^T W [B | d_E]
+    tflops = flops / (k_ms * 1e-3) / 1e12
+    return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+                chains_per_gpu=C, m=m, n_epoch=ne, m_R=mR, aclength=aclength,
+                roofline={"bound": "mfma", "kernel": "k_ecorr_schur", "achieved": tflops,
+                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tflops / FP64_PEAK_TFLOPS,
+                          "kernel_avg_ms": k_ms, "alg_flops_per_launch": flops,
+                          "note": "ne (mR+1)(mR+2) flop per chain (epoch-weighted SYRK, lower triangle with the "
+                                  "d_E row) over the HIP-event time of one all-chain launch"},
+                config="SURVEY 8f-4: J1713-like pulsar, basis ECORR (2 backends, 136 epochs) + 30-bin free "
+                       "spectrum + 16-col TM, ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -349,6 +463,9 @@ def main():
     ap.add_argument("--pta-graph", type=int, default=0, help="time the PTA sweeps as a hipGraph replay (1/0); "
                     "measured no faster: the sweeps are GPU-bound and eager launches queue ahead")
     ap.add_argument("--pta-shard", default="chain", help="chain | pulsar: how N > 1 GPUs split the PTA configs")
+    ap.add_argument("--ecorr", type=int, default=1, help="measure the basis-ECORR path (SURVEY 8f-4) too (1/0)")
+    ap.add_argument("--ecorr-chains", type=int, default=4096)
+    ap.add_argument("--ecorr-steps", type=int, default=10)
     ap.add_argument("--c5-chains", type=int, default=16)
     ap.add_argument("--c5-steps", type=int, default=5)
     args = ap.parse_args()
@@ -468,6 +585,13 @@ def main():
             if not args.no_cpu_baseline:
                 sec["cpu_baseline"] = pta_cpu_baseline(kind, args.cpu_seconds)
             out.setdefault("secondary", {})[kind] = sec
+    if args.ecorr:
+        sec = bench_ecorr(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev)
+        if rank == 0:
+            sec["sharding"] = "chains, weak"
+            if not args.no_cpu_baseline and world == 1:
+                sec["cpu_baseline"] = ecorr_cpu_baseline(args.cpu_seconds)
+            out.setdefault("secondary", {})["ecorr"] = sec
     if args.config5:
         sec = bench_config5(args.c5_chains, args.c5_steps, 1, rank, world, dev)
         if rank == 0:

@@ -408,6 +408,18 @@ int gs_bdraw_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,
 int gs_ecorr_schur(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const double* Bx, const double* Dg,
                    const int32_t* ebk, int n_bk, const int32_t* xcol, const double* x, int ldx,
                    const double* A, const double* dR, double* TNT, double* d, double* aux);
+/*
+ * gs_ecorr_prefix: gs_ecorr_schur + gs_prefix_sys fused (no per-chain TNT in HBM): writes each
+ * chain's model block (gs_prefix layout, model + c * gs_model_stride(NF, NMX)) and aux [c][4]
+ * as gs_ecorr_schur.  Columns reordered [M | F | d]: Bx [ne x ldbx] rows
+ * [TNT[e, M] (nM <= 16, zero-padded to 16) | TNT[e, F] (fidx order, NF) | d_e | 0 ...];
+ * Ap [ldbx x ldbx] the same ordering of TNT with phiinv_M added on the M diagonal, d as row and
+ * column 16 + NF, (d, d) = 0 and 1 on the padded M diagonal; ldbx = 16 (1 + ceil((NF + 1) / 16))
+ * in {48, 64, 80} (NF = 20, 40, 60).  info [c] > 0: the k-th pivot of the M block failed.
+ */
+int gs_ecorr_prefix(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, int ldbx, const double* Bx,
+                    const double* Dg, const int32_t* ebk, int n_bk, const int32_t* xcol, const double* x,
+                    int ldx, const double* Ap, double* model, double* aux, int32_t* info);
 int gs_ecorr_propose(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, const double* emin,
                      const double* emax, const double* x, int ldx, int n_param, double* xq, int step,
                      int64_t sweep, int64_t chain_base, const double* inj, double* prop);

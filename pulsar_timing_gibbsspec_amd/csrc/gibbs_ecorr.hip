@@ -11,6 +11,7 @@
 // get_lnlikelihood_fullmarg (:569-610): k_ecorr_propose / k_ecorr_accept bracket one
 // batched likelihood evaluation per step.
 #include "gibbs_internal.h"
+#include "gibbs_tile.h"
 
 namespace {
 
@@ -153,6 +154,235 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
   }
 }
 
+
+// Fused ECORR Schur complement + fixed-prior prefix, written straight into the b-draw /
+// likelihood model block (gs_prefix's layout) -- no per-chain TNT round trip through HBM
+// and no separate k_prefix launch.  Bx / Ap columns are ordered [M (nM <= 16, padded to
+// 16) | F (NF) | d | pad], Ap = TNT of that ordering with phiinv_M on the M diagonal, the
+// d row/column and an identity on the M padding.  Tiles: (0,0) = A_MM, (0,r) = A_M,Rr
+// (block row M computed as (0, r) so its C layout is the B operand of L_M^-1 A_M,R), and
+// (r,j), r >= j >= 1.  Epilogue per wavefront: 16x16 Cholesky of T_00 in LDS,
+// W_r = L_M^-1 T_0r and G_r = L_M^-T W_r (4 MFMA each), S_rj = T_rj - W_r^T W_j (4 MFMA).
+template <int NB>
+__global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs A) {
+  extern __shared__ double lds[];
+  __shared__ double wb[2][EC_WAVES][EC_CH];
+  __shared__ double sinv[EC_WAVES][GS_WHITE_MAX_BK + 1], slog[EC_WAVES][GS_WHITE_MAX_BK + 1];
+  __shared__ double Ls[EC_WAVES][16 * 17];
+  constexpr int LDB = 16 * NB;
+  constexpr int NT = 1 + 2 * (NB - 1) + (NB - 1) * (NB - 2) / 2;  // (0,0), (0,r), (r,j) r>=j>=1
+  const int tid = threadIdx.x, l = tid & 63, c = l & 15, q = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ch_id = blockIdx.x * EC_WAVES + w;
+  const bool live = ch_id < A.n_chain;
+  const int ne = A.ne, NF = A.NF, nM = A.nM;
+  if (l < A.n_bk) {
+    double inv = 0.0, lg = 0.0;
+    if (live) ec_phi(A.x[(int64_t)ch_id * A.ldx + A.xcol[l]], inv, lg);
+    sinv[w][l] = inv;
+    slog[w][l] = lg;
+  }
+  __syncthreads();
+
+  // tile slots: 0 = (0,0); 1..NB-1 = (0,r); then (r,j) r >= j >= 1 at 1 + (NB-1) + (r-1)r/2 + (j-1)
+  gs_d4_t acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = gs_d4_t{0.0, 0.0, 0.0, 0.0};
+  double sla = 0.0, slp = 0.0;
+  double reg[NB];
+  double wreg = 0.0;
+  auto load = [&](int e0) {
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int idx = tid + 64 * EC_WAVES * u;
+      const int e = e0 + idx / LDB;
+      reg[u] = (e < ne) ? A.Bx[(int64_t)e0 * LDB + idx] : 0.0;
+    }
+    wreg = 0.0;
+    if (l < EC_CH && live) {
+      const int e = e0 + l;
+      if (e < ne) {
+        const int kb = A.ebk[e];
+        const double a = A.Dg[e] + sinv[w][kb];
+        wreg = 1.0 / a;
+        sla += log(a);
+        slp += slog[w][kb];
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    double* dst = lds + buf * (EC_CH * LDB);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) dst[tid + 64 * EC_WAVES * u] = reg[u];
+    if (l < EC_CH) wb[buf][w][l] = wreg;
+  };
+  const int nch = (ne + EC_CH - 1) / EC_CH;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int chk = 0; chk < nch; ++chk) {
+    const int cb = chk & 1;
+    if (chk + 1 < nch) load((chk + 1) * EC_CH);
+    __builtin_amdgcn_sched_barrier(0);
+    const double* cur = lds + cb * (EC_CH * LDB);
+#pragma unroll
+    for (int kk = 0; kk < EC_CH / 4; ++kk) {
+      const double* row = cur + (4 * kk + q) * LDB + c;
+      const double wv = wb[cb][w][4 * kk + q];
+      double v[NB];
+#pragma unroll
+      for (int r = 0; r < NB; ++r) v[r] = row[16 * r];
+      const double a0 = v[0] * wv;
+      acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, v[0], acc[0], 0, 0, 0);
+#pragma unroll
+      for (int r = 1; r < NB; ++r) acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, v[r], acc[r], 0, 0, 0);
+#pragma unroll
+      for (int r = 1; r < NB; ++r) {
+        const double av = v[r] * wv;
+#pragma unroll
+        for (int j = 1; j <= r; ++j) {
+          const int t = NB + (r - 1) * r / 2 + (j - 1);
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, v[j], acc[t], 0, 0, 0);
+        }
+      }
+    }
+    if (chk + 1 < nch) store(cb ^ 1);
+    __syncthreads();
+  }
+  sla = ec_wave_sum(sla);
+  slp = ec_wave_sum(slp);
+  if (!live) return;  // no workgroup barriers below
+
+  const int LDA = LDB;
+  auto Aq = [&](int r0, int c0, int s) { return A.Ap[(int64_t)(r0 + 4 * s + q) * LDA + c0 + c]; };
+  // sum d_E^2 / a: the (d, d) element of the accumulated product
+  const int di = 16 + NF;
+  double pdd = 0.0;
+  {
+    const int rd = di / 16, ld = di % 16;  // runtime: select over static tile indices (a
+#pragma unroll                             // dynamic acc[] index would demote acc to scratch)
+    for (int r = 1; r < NB; ++r) {
+      const int t = NB + (r - 1) * r / 2 + (r - 1);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        if (r == rd && c == ld && 4 * s + q == ld) pdd = acc[t][s];
+    }
+    pdd = ec_wave_sum(pdd);
+  }
+  // T = Ap - P in place
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc[0][s] = Aq(0, 0, s) - acc[0][s];
+#pragma unroll
+  for (int r = 1; r < NB; ++r)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc[r][s] = Aq(0, 16 * r, s) - acc[r][s];
+#pragma unroll
+  for (int r = 1; r < NB; ++r)
+#pragma unroll
+    for (int j = 1; j <= r; ++j) {
+      const int t = NB + (r - 1) * r / 2 + (j - 1);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[t][s] = Aq(16 * r, 16 * j, s) - acc[t][s];
+    }
+
+  // T_00 = U^T U (upper Cholesky = L_M^T): tile_elim gives V = U^-1 = L_M^-T in registers
+  // (DPP column elimination, gibbs_tile.h); L_M^-1 = V^T.
+  double* tb = Ls[w];
+  gs_d4_t V, Ecol = acc[0];
+  double rsd;
+  tile_elim<16>(Ecol, V, rsd, q, c);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) V[s] *= rsd;
+  int fail = 0;
+  {
+    const bool bad = (q == 0) && (c < nM) && !(rsd > 0.0 && rsd < INFINITY);
+    const unsigned long long m = __ballot(bad);
+    if (m) fail = __builtin_ctzll(m) + 1;
+  }
+  double ldl = (q == 0 && c < nM) ? -log(rsd) : 0.0;  // sum log diag L_M = -sum log rsd
+  ldl = ec_wave_sum(ldl);
+  const gs_d4_t Vt = gtile::transpose(V, tb, q, c);   // C layout of V^T
+
+  // W_r = L_M^-1 T_0r = V^T T_0r, G_r = L_M^-T W_r = V W_r = (V^T)^T W_r
+  gs_d4_t W[NB];
+#pragma unroll
+  for (int r = 1; r < NB; ++r) W[r] = gtile::mfma_tn(gs_d4_t{0.0, 0.0, 0.0, 0.0}, V, acc[r]);
+  const int NMX = A.NMX, ldw = NF + 1;
+  double* mb = A.model + (int64_t)ch_id * A.mstride;
+  double* S0 = mb;
+  double* dF = S0 + (int64_t)NF * ldw;
+  double* Gm = dF + NF;
+  double* hm = Gm + (int64_t)NMX * ldw;
+  double* Rm = hm + NMX;
+  double* am = Rm + (int64_t)NMX * NMX;
+#pragma unroll
+  for (int r = 1; r < NB; ++r) {
+    const gs_d4_t G = gtile::mfma_tn(gs_d4_t{0.0, 0.0, 0.0, 0.0}, Vt, W[r]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int mr = 4 * s + q, col = 16 * (r - 1) + c;
+      if (mr < nM && col <= NF) {  // G's column NF is zero padding (k_prefix layout); h = L^-T e
+        Gm[(int64_t)mr * ldw + col] = (col < NF) ? G[s] : 0.0;
+        if (col == NF) hm[mr] = G[s];
+      }
+    }
+  }
+  // S_rj = T_rj - W_r^T W_j
+#pragma unroll
+  for (int r = 1; r < NB; ++r)
+#pragma unroll
+    for (int j = 1; j <= r; ++j) {
+      const int t = NB + (r - 1) * r / 2 + (j - 1);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-W[r][s], W[j][s], acc[t], 0, 0, 0);
+    }
+  // |L^-1 d_M|^2: column NF of W
+  double e2 = 0.0;
+  {
+    const int rd = 1 + NF / 16, ld = NF % 16;
+#pragma unroll
+    for (int r = 1; r < NB; ++r)
+      if (r == rd && c == ld)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) e2 += W[r][s] * W[r][s];
+    e2 = ec_wave_sum(e2);
+  }
+
+  // model block (gs_prefix layout): S0 | dF | G | h | R | aux
+#pragma unroll
+  for (int r = 1; r < NB; ++r)
+#pragma unroll
+    for (int j = 1; j <= r; ++j) {
+      const int t = NB + (r - 1) * r / 2 + (j - 1);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int row = 16 * (r - 1) + 4 * s + q, col = 16 * (j - 1) + c;
+        if (row < col) continue;
+        const double v = acc[t][s];
+        if (row < NF) S0[(int64_t)row * ldw + col] = v;
+        if (col < NF && row <= NF && row != col) S0[(int64_t)col * ldw + row] = v;
+        if (row == NF && col < NF) dF[col] = v;
+      }
+    }
+  // R = L_M^-T = V (upper), zero beyond nM
+  for (int idx = l; idx < NMX * NMX; idx += 64) Rm[idx] = 0.0;
+  gtile::lds_fence();
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    if (4 * s + q < nM && c < nM) Rm[(4 * s + q) * NMX + c] = V[s];
+  for (int64_t qq = (am - mb) + 2 + l; qq < A.mstride; qq += 64) mb[qq] = 0.0;
+  if (l == 0) {
+    am[0] = ldl;
+    am[1] = e2;
+    double* ax = A.aux + (int64_t)ch_id * 4;
+    ax[0] = sla;
+    ax[1] = pdd;
+    ax[2] = slp;
+    ax[3] = 0.0;
+    if (A.info) A.info[ch_id] = fail;
+  }
+}
+
 // scale = np.random.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]) (pulsar_gibbs.py:430-433)
 __device__ __forceinline__ double ec_scale(double u) {
   if (u < 0.1) return 0.1;
@@ -268,7 +498,29 @@ void launch_schur_nb(hipStream_t s, const EcorrSchurArgs& a) {
                      dim3(64 * EC_WAVES), lds, s, a);
 }
 
+template <int NB>
+void launch_prefix_nb(hipStream_t s, const EcorrPrefixArgs& a) {
+  static bool attr = false;
+  const size_t lds = (size_t)2 * EC_CH * 16 * NB * sizeof(double);
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_ecorr_prefix<NB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_ecorr_prefix<NB>, dim3((unsigned)((a.n_chain + EC_WAVES - 1) / EC_WAVES)),
+                     dim3(64 * EC_WAVES), lds, s, a);
+}
+
 }  // namespace
+
+int launch_ecorr_prefix(hipStream_t s, const EcorrPrefixArgs& a) {
+  switch (a.ldbx / 16) {
+    case 3: launch_prefix_nb<3>(s, a); break;
+    case 4: launch_prefix_nb<4>(s, a); break;
+    case 5: launch_prefix_nb<5>(s, a); break;
+    default: return 1;
+  }
+  return 0;
+}
 
 bool ecorr_nb_supported(int nb) { return nb >= 1 && nb <= 6; }  // NB 7, 8 spill
 

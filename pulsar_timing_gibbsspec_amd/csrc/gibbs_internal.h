@@ -194,6 +194,15 @@ struct EcorrBArgs {
   const int32_t *ebk, *xcol, *ecid, *rcol, *chain_mask;
   double* b;
 };
+struct EcorrPrefixArgs {
+  int n_chain, NF, NMX, nM, ne, ldbx, ldx, n_bk;
+  int64_t mstride;
+  const double *Bx, *Dg, *Ap, *x;
+  const int32_t *ebk, *xcol;
+  double *model, *aux;
+  int32_t* info;
+};
+int launch_ecorr_prefix(hipStream_t s, const EcorrPrefixArgs& a);
 bool ecorr_nb_supported(int nb);
 int launch_ecorr_schur(hipStream_t s, const EcorrSchurArgs& a);
 int launch_ecorr_propose(hipStream_t s, const EcorrMhArgs& a);

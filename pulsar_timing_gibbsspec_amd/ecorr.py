@@ -101,6 +101,29 @@ class EcorrModel:
         self.phfix = _t(phf[None, :], torch.float64, dev)
         self.pdesc = _t(np.array([[mR, self.nm, 0, 0]], np.int64), torch.int64, dev)
         self.mstride = int(lib.gs_model_stride(NF, self.NMX))
+        # fused path (gs_ecorr_prefix): columns [M (<= 16) | F | d], phiinv_M on the M diagonal
+        self.fused = self.nm <= 16
+        if self.fused:
+            KB = 16 * (1 + (NF + 1 + 15) // 16)
+            self.ldbp = KB
+            mcols = torch.as_tensor(rc[mR_idx], device=dev)
+            fcols = torch.as_tensor(gwid, device=dev)
+            Bp = torch.zeros(self.ne, KB, dtype=torch.float64, device=dev)
+            Bp[:, :self.nm] = TNT[e_t][:, mcols]
+            Bp[:, 16:16 + NF] = TNT[e_t][:, fcols]
+            Bp[:, 16 + NF] = d[e_t]
+            self.Bp = Bp.contiguous()
+            cols = torch.cat([mcols, fcols])
+            idx = torch.cat([torch.arange(self.nm, device=dev), 16 + torch.arange(NF, device=dev)])
+            Ap = torch.zeros(KB, KB, dtype=torch.float64, device=dev)
+            Ap[idx[:, None], idx[None, :]] = TNT[cols][:, cols]
+            Ap[16 + NF, idx] = d[cols]
+            Ap[idx, 16 + NF] = d[cols]
+            dm = torch.arange(self.nm, device=dev)
+            Ap[dm, dm] += self.phfix[0, :self.nm]
+            pad = torch.arange(self.nm, 16, device=dev)
+            Ap[pad, pad] = 1.0
+            self.Ap = Ap.contiguous()
         C = self.C
         self.TNTc = torch.empty(C * mR * mR, dtype=torch.float64, device=dev)
         self.dc = torch.empty(C * mR, dtype=torch.float64, device=dev)
@@ -119,9 +142,17 @@ class EcorrModel:
         self.lnl_const = float(-0.5 * (np.sum(np.log(Nh)) + np.sum(rh ** 2 / Nh)) + 0.5 * np.sum(np.log(phf)))
 
     # ----------------------------------------------------------------- kernels
-    def factor(self, x):
-        """Schur complement of every chain's ECORR state in x (C, n_param) + R prefix."""
+    def factor(self, x, fused=None):
+        """Schur complement of every chain's ECORR state in x (C, n_param) + R prefix: one
+        fused launch (gs_ecorr_prefix) when the fixed-prior block fits one 16-column tile,
+        else gs_ecorr_schur + gs_prefix_sys."""
         lib, h = self.ctx.lib, self.ctx.handle
+        if self.fused if fused is None else fused:
+            check(lib.gs_ecorr_prefix(h, self.C, self.NF, self.NMX, self.nm, self.ne, self.ldbp, ptr(self.Bp),
+                                      ptr(self.Dg), ptr(self.ebk), self.n_bk, ptr(self.ecol), ptr(x), x.shape[1],
+                                      ptr(self.Ap), ptr(self.model), ptr(self.aux), ptr(self.pinfo)),
+                  "gs_ecorr_prefix")
+            return
         check(lib.gs_ecorr_schur(h, self.C, self.mR, self.ne, self.ldbx, ptr(self.Bx), ptr(self.Dg), ptr(self.ebk),
                                  self.n_bk, ptr(self.ecol), ptr(x), x.shape[1], ptr(self.A), ptr(self.dR),
                                  ptr(self.TNTc), ptr(self.dc), ptr(self.aux)), "gs_ecorr_schur")

@@ -55,13 +55,30 @@ def _phiinv_F(g, X):
     return 1.0 / np.repeat(10.0 ** (2.0 * X[:, _gwind(g)]), 2, axis=1)
 
 
-def test_ecorr_lnlike_matches_reference(ctx):
+@pytest.mark.parametrize("fused", [True, False])
+def test_ecorr_lnlike_matches_reference(ctx, fused):
+    """Both device forms (fused gs_ecorr_prefix; gs_ecorr_schur + gs_prefix_sys) against the
+    reference's get_lnlikelihood_fullmarg, and their model blocks against each other."""
     g = golden("ecorr_mh_j1713.npz")
     X = g["x_like"]
     em = _model(ctx, g, X.shape[0])
+    assert em.fused
+    em.fused = fused
     got = em.lnlike(_dev(X), _dev(_phiinv_F(g, X))).cpu().numpy()
     err = np.abs(got - g["lnlike"])
     assert err.max() < 1e-7, (got, g["lnlike"])
+    if fused:
+        em.factor(_dev(X), fused=True)
+        a = em.model.clone()
+        em.factor(_dev(X), fused=False)
+        b = em.model
+        NF, NMX = em.NF, em.NMX
+        sizes = [NF * (NF + 1), NF, NMX * (NF + 1), NMX, NMX * NMX, 2]
+        cut = np.cumsum(sizes)[:-1]
+        A = a.view(X.shape[0], -1).cpu().numpy()[:, :sum(sizes)]
+        B = b.view(X.shape[0], -1).cpu().numpy()[:, :sum(sizes)]
+        for sa, sb in zip(np.split(A, cut, axis=1), np.split(B, cut, axis=1)):
+            assert normwise_rel(sa, sb) < 1e-9
 
 
 def test_ecorr_mh_matches_reference(ctx):
