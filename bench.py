@@ -418,29 +418,28 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
         el = float(t.item())
     if int(em.binfo.abs().sum()) or int(em.pinfo.abs().sum()):
         raise RuntimeError("non-PD system in the ECORR bench")
-    # dominant kernel: gs_ecorr_schur, timed alone on the ctx stream
+    # dominant kernel: gs_ecorr_prefix (fused epoch Schur complement + prefix), timed alone
     stream = ctx.stream
-    lib, h = ctx.lib, ctx.handle
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(reps):
-        _lib.check(lib.gs_ecorr_schur(h, C, em.mR, em.ne, em.ldbx, _lib.ptr(em.Bx), _lib.ptr(em.Dg),
-                                      _lib.ptr(em.ebk), em.n_bk, _lib.ptr(em.ecol), _lib.ptr(eng.x),
-                                      eng.x.shape[1], _lib.ptr(em.A), _lib.ptr(em.dR), _lib.ptr(em.TNTc),
-                                      _lib.ptr(em.dc), _lib.ptr(em.aux)), "gs_ecorr_schur")
+        em.factor(eng.x)
     e1.record(stream)
     torch.cuda.synchronize()
     k_ms = e0.elapsed_time(e1) / reps
-    mR = em.mR
-    flops = C * ne * (mR + 1) * (mR + 2)       # lower triangle of [B | d_E]^T W [B | d_E]
+    mR, NF, nM = em.mR, em.NF, em.nm
+    # epoch-weighted SYRK (lower triangle of [B | d_E]^T W [B | d_E]) + the fixed-prior Schur update
+    flops = C * (ne * (mR + 1) * (mR + 2) + nM * (NF + 1) * (NF + 2))
     tflops = flops / (k_ms * 1e-3) / 1e12
     return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 chains_per_gpu=C, m=m, n_epoch=ne, m_R=mR, aclength=aclength,
-                roofline={"bound": "mfma", "kernel": "k_ecorr_schur", "achieved": tflops,
+                roofline={"bound": "mfma", "kernel": "k_ecorr_prefix" if em.fused else "k_ecorr_schur + k_prefix",
+                          "achieved": tflops,
                           "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tflops / FP64_PEAK_TFLOPS,
                           "kernel_avg_ms": k_ms, "alg_flops_per_launch": flops,
-                          "note": "ne (mR+1)(mR+2) flop per chain (epoch-weighted SYRK, lower triangle with the "
-                                  "d_E row) over the HIP-event time of one all-chain launch"},
+                          "note": "ne (mR+1)(mR+2) + nM (NF+1)(NF+2) flop per chain (epoch-weighted SYRK with the "
+                                  "d_E row + fixed-prior Schur update) over the HIP-event time of one all-chain "
+                                  "launch"},
                 config="SURVEY 8f-4: J1713-like pulsar, basis ECORR (2 backends, 136 epochs) + 30-bin free "
                        "spectrum + 16-col TM, ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
 
