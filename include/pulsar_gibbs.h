@@ -392,8 +392,9 @@ int gs_bdraw_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,
  *   aux [c][4] = {sum log a, sum d_E^2 / a, sum log phi_E, 0}.  The marginalised likelihood is
  *   then gs_lnlike_marg on the R system (gs_prefix_sys of TNT, d) + (aux1 - aux0 - aux2) / 2
  *   + the model constants.
- * gs_ecorr_propose: one Metropolis proposal per chain at step `step` (:458-462): xq = x with
- *   x[ecol[p]] += z (0.05 n_e) scale; prop [n_chain x 4] scratch.  inj [steps x n_chain x 4]
+ * gs_ecorr_propose: one Metropolis proposal per chain at step `step` (:458-462): the ECORR
+ *   columns of xq = those of x with x[ecol[p]] += z (0.05 n_e) scale (other columns of xq are
+ *   not written); prop [n_chain x 4] scratch.  inj [steps x n_chain x 4]
  *   (scale value, parameter index, normal, uniform) or NULL (Philox GS_EV_ECORR).
  *   emin/emax [n_e]: the Uniform prior of each ECORR parameter.
  * gs_ecorr_accept: lnL1 = lnl + (aux1 - aux0 - aux2)/2 (-inf if info or pinfo is nonzero);
@@ -415,11 +416,17 @@ int gs_ecorr_schur(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const dou
  * [TNT[e, M] (nM <= 16, zero-padded to 16) | TNT[e, F] (fidx order, NF) | d_e | 0 ...];
  * Ap [ldbx x ldbx] the same ordering of TNT with phiinv_M added on the M diagonal, d as row and
  * column 16 + NF, (d, d) = 0 and 1 on the padded M diagonal; ldbx = 16 (1 + ceil((NF + 1) / 16))
- * in {48, 64, 80} (NF = 20, 40, 60).  info [c] > 0: the k-th pivot of the M block failed.
+ * in {48, 64, 80} (NF = 20, 40, 60); 1 on every padded diagonal.  info [c] > 0: the k-th pivot failed.
+ * Likelihood mode (lnl != NULL; model unused, may be NULL): phiinv_F [n_chain x NF] (fidx order)
+ * is added and the F block factored in registers; lnl [c] = (d^T Sigma^-1 d - log det S_R -
+ * ... ) / 2 in gs_ecorr_accept's convention with aux [c][1] = 0 (lnL = lnl + (aux1 - aux0 -
+ * aux2) / 2 + constants), so one launch per Metropolis step replaces gs_ecorr_prefix +
+ * gs_lnlike_marg.
  */
 int gs_ecorr_prefix(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, int ldbx, const double* Bx,
                     const double* Dg, const int32_t* ebk, int n_bk, const int32_t* xcol, const double* x,
-                    int ldx, const double* Ap, double* model, double* aux, int32_t* info);
+                    int ldx, const double* Ap, const double* phiinv_F, double* model, double* aux,
+                    double* lnl, int32_t* info);
 int gs_ecorr_propose(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, const double* emin,
                      const double* emax, const double* x, int ldx, int n_param, double* xq, int step,
                      int64_t sweep, int64_t chain_base, const double* inj, double* prop);

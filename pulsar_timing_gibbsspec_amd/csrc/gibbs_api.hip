@@ -773,7 +773,8 @@ int gs_ecorr_schur(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const dou
 
 int gs_ecorr_prefix(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, int ldbx, const double* Bx,
                     const double* Dg, const int32_t* ebk, int n_bk, const int32_t* xcol, const double* x,
-                    int ldx, const double* Ap, double* model, double* aux, int32_t* info) {
+                    int ldx, const double* Ap, const double* phiinv_F, double* model, double* aux,
+                    double* lnl, int32_t* info) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_chain < 0) return fail_arg(2, "n_chain < 0");
   if (NF != 20 && NF != 40 && NF != 60) return fail_arg(3, "NF must be 20, 40 or 60");
@@ -783,12 +784,14 @@ int gs_ecorr_prefix(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, i
   if (!Bx || !Dg || !ebk) return fail_arg(8, "NULL Bx / Dg / ebk");
   if (n_bk <= 0 || n_bk > GS_WHITE_MAX_BK) return fail_arg(11, "n_bk must be in 1..15");
   if (!xcol || !x || ldx <= 0) return fail_arg(12, "xcol / x / ldx");
-  if (!Ap || !model || !aux) return fail_arg(15, "NULL Ap / model / aux");
+  if (!Ap || !aux) return fail_arg(15, "NULL Ap / aux");
+  if (lnl ? !phiinv_F : !model) return fail_arg(16, "likelihood mode needs phiinv_F, block mode needs model");
   if (n_chain == 0) return 0;
   EcorrPrefixArgs a;
   a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.nM = nM; a.ne = ne; a.ldbx = ldbx; a.ldx = ldx; a.n_bk = n_bk;
   a.mstride = model_stride_doubles(NF, NMX);
   a.Bx = Bx; a.Dg = Dg; a.Ap = Ap; a.x = x; a.ebk = ebk; a.xcol = xcol; a.model = model; a.aux = aux; a.info = info;
+  a.phiinv_F = phiinv_F; a.lnl = lnl;
   if (launch_ecorr_prefix(ctx->stream, a)) return fail_arg(7, "unsupported ldbx");
   return after_launch("k_ecorr_prefix");
 }

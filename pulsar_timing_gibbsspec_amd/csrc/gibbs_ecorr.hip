@@ -155,27 +155,37 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
 }
 
 
-// Fused ECORR Schur complement + fixed-prior prefix, written straight into the b-draw /
-// likelihood model block (gs_prefix's layout) -- no per-chain TNT round trip through HBM
-// and no separate k_prefix launch.  Bx / Ap columns are ordered [M (nM <= 16, padded to
-// 16) | F (NF) | d | pad], Ap = TNT of that ordering with phiinv_M on the M diagonal, the
-// d row/column and an identity on the M padding.  Tiles: (0,0) = A_MM, (0,r) = A_M,Rr
-// (block row M computed as (0, r) so its C layout is the B operand of L_M^-1 A_M,R), and
-// (r,j), r >= j >= 1.  Epilogue per wavefront: 16x16 Cholesky of T_00 in LDS,
-// W_r = L_M^-1 T_0r and G_r = L_M^-T W_r (4 MFMA each), S_rj = T_rj - W_r^T W_j (4 MFMA).
-template <int NB>
+// Fused ECORR Schur complement + fixed-prior prefix.  Bx / Ap columns are ordered
+// [M (nM <= 16, padded to 16) | F (NF) | d | pad]: Ap = TNT of that ordering with phiinv_M on
+// the M diagonal, d as row/column 16 + NF, (d, d) = 0 and 1 on every padded diagonal.
+// Accumulated tiles are the UPPER ones, (j, r) for j <= r (block row M first), so the
+// C layout of every off-diagonal tile is directly the B operand of a left product.
+// Epilogue per wavefront, all in registers: T = Ap - P; tile_elim (DPP column
+// elimination, gibbs_tile.h) factors T_MM = U^T U -> V = U^-1 = L_M^-T; W_r = V^T T_0r,
+// S_jr = T_jr - W_j^T W_r (4 MFMA each).
+//   LNL = false: G_r = V W_r and S are written into the model block (gs_prefix layout) that
+//                gs_lnlike_marg / gs_bdraw_sys read;
+//   LNL = true:  the marginalised likelihood directly: phiinv_F is added to the S diagonal
+//                and S (F block + the d row/column) is factored by an upper tile Cholesky
+//                (tile_elim on the diagonal tiles, 4-MFMA TRSM and updates); after the last
+//                F pivot the eliminated (d, d) entry is -(d^T Sigma^-1 d) of the whole
+//                system (Ap_dd = 0), so no solve is needed and nothing per chain but lnl
+//                goes to HBM.
+template <int NB, bool LNL>
 __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs A) {
   extern __shared__ double lds[];
   __shared__ double wb[2][EC_WAVES][EC_CH];
   __shared__ double sinv[EC_WAVES][GS_WHITE_MAX_BK + 1], slog[EC_WAVES][GS_WHITE_MAX_BK + 1];
   __shared__ double Ls[EC_WAVES][16 * 17];
   constexpr int LDB = 16 * NB;
-  constexpr int NT = 1 + 2 * (NB - 1) + (NB - 1) * (NB - 2) / 2;  // (0,0), (0,r), (r,j) r>=j>=1
+  constexpr int NF = 20 * (NB - 2);  // 20, 40, 60 <-> NB = 3, 4, 5
+  constexpr int NTF = NB - 1;        // tile rows of the F + d block
+  constexpr int NT = 1 + 2 * NTF + NTF * (NTF - 1) / 2;
   const int tid = threadIdx.x, l = tid & 63, c = l & 15, q = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ch_id = blockIdx.x * EC_WAVES + w;
   const bool live = ch_id < A.n_chain;
-  const int ne = A.ne, NF = A.NF, nM = A.nM;
+  const int ne = A.ne, nM = A.nM;
   if (l < A.n_bk) {
     double inv = 0.0, lg = 0.0;
     if (live) ec_phi(A.x[(int64_t)ch_id * A.ldx + A.xcol[l]], inv, lg);
@@ -184,7 +194,8 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
   }
   __syncthreads();
 
-  // tile slots: 0 = (0,0); 1..NB-1 = (0,r); then (r,j) r >= j >= 1 at 1 + (NB-1) + (r-1)r/2 + (j-1)
+  // tile slots: 0 = (0,0); r = (0,r) for r = 1..NTF; (j,r), 1 <= j <= r: NB + tix(j-1, r-1)
+  auto ts = [](int j, int r) { return NB + gtile::tix(j - 1, r - 1, NTF); };
   gs_d4_t acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = gs_d4_t{0.0, 0.0, 0.0, 0.0};
@@ -232,17 +243,13 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
       double v[NB];
 #pragma unroll
       for (int r = 0; r < NB; ++r) v[r] = row[16 * r];
-      const double a0 = v[0] * wv;
-      acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, v[0], acc[0], 0, 0, 0);
 #pragma unroll
-      for (int r = 1; r < NB; ++r) acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, v[r], acc[r], 0, 0, 0);
+      for (int j = 0; j < NB; ++j) {
+        const double av = v[j] * wv;
 #pragma unroll
-      for (int r = 1; r < NB; ++r) {
-        const double av = v[r] * wv;
-#pragma unroll
-        for (int j = 1; j <= r; ++j) {
-          const int t = NB + (r - 1) * r / 2 + (j - 1);
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, v[j], acc[t], 0, 0, 0);
+        for (int r = j; r < NB; ++r) {
+          const int t = (j == 0) ? r : ts(j, r);
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, v[r], acc[t], 0, 0, 0);
         }
       }
     }
@@ -253,23 +260,14 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
   slp = ec_wave_sum(slp);
   if (!live) return;  // no workgroup barriers below
 
-  const int LDA = LDB;
-  auto Aq = [&](int r0, int c0, int s) { return A.Ap[(int64_t)(r0 + 4 * s + q) * LDA + c0 + c]; };
-  // sum d_E^2 / a: the (d, d) element of the accumulated product
-  const int di = 16 + NF;
-  double pdd = 0.0;
-  {
-    const int rd = di / 16, ld = di % 16;  // runtime: select over static tile indices (a
-#pragma unroll                             // dynamic acc[] index would demote acc to scratch)
-    for (int r = 1; r < NB; ++r) {
-      const int t = NB + (r - 1) * r / 2 + (r - 1);
+  constexpr int LD_D = NF % 16;            // d's position in the last F tile
+  double pdd = 0.0;                        // sum d_E^2 / a = P_dd
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        if (r == rd && c == ld && 4 * s + q == ld) pdd = acc[t][s];
-    }
-    pdd = ec_wave_sum(pdd);
-  }
-  // T = Ap - P in place
+  for (int s = 0; s < 4; ++s)
+    if (c == LD_D && 4 * s + q == LD_D) pdd = acc[ts(NTF, NTF)][s];
+  pdd = ec_wave_sum(pdd);
+  // T = Ap - P
+  auto Aq = [&](int r0, int c0, int s) { return A.Ap[(int64_t)(r0 + 4 * s + q) * LDB + c0 + c]; };
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc[0][s] = Aq(0, 0, s) - acc[0][s];
 #pragma unroll
@@ -277,17 +275,13 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
 #pragma unroll
     for (int s = 0; s < 4; ++s) acc[r][s] = Aq(0, 16 * r, s) - acc[r][s];
 #pragma unroll
-  for (int r = 1; r < NB; ++r)
+  for (int j = 1; j < NB; ++j)
 #pragma unroll
-    for (int j = 1; j <= r; ++j) {
-      const int t = NB + (r - 1) * r / 2 + (j - 1);
+    for (int r = j; r < NB; ++r)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc[t][s] = Aq(16 * r, 16 * j, s) - acc[t][s];
-    }
+      for (int s = 0; s < 4; ++s) acc[ts(j, r)][s] = Aq(16 * j, 16 * r, s) - acc[ts(j, r)][s];
 
-  // T_00 = U^T U (upper Cholesky = L_M^T): tile_elim gives V = U^-1 = L_M^-T in registers
-  // (DPP column elimination, gibbs_tile.h); L_M^-1 = V^T.
-  double* tb = Ls[w];
+  // T_MM = U^T U: V = U^-1 = L_M^-T (upper), L_M^-1 = V^T
   gs_d4_t V, Ecol = acc[0];
   double rsd;
   tile_elim<16>(Ecol, V, rsd, q, c);
@@ -299,87 +293,142 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
     const unsigned long long m = __ballot(bad);
     if (m) fail = __builtin_ctzll(m) + 1;
   }
-  double ldl = (q == 0 && c < nM) ? -log(rsd) : 0.0;  // sum log diag L_M = -sum log rsd
+  double ldl = (q == 0 && c < nM) ? -log(rsd) : 0.0;  // sum log diag L_M
   ldl = ec_wave_sum(ldl);
-  const gs_d4_t Vt = gtile::transpose(V, tb, q, c);   // C layout of V^T
 
-  // W_r = L_M^-1 T_0r = V^T T_0r, G_r = L_M^-T W_r = V W_r = (V^T)^T W_r
+  // W_r = L_M^-1 T_0r = V^T T_0r;  S_jr = T_jr - W_j^T W_r
   gs_d4_t W[NB];
 #pragma unroll
   for (int r = 1; r < NB; ++r) W[r] = gtile::mfma_tn(gs_d4_t{0.0, 0.0, 0.0, 0.0}, V, acc[r]);
-  const int NMX = A.NMX, ldw = NF + 1;
-  double* mb = A.model + (int64_t)ch_id * A.mstride;
-  double* S0 = mb;
-  double* dF = S0 + (int64_t)NF * ldw;
-  double* Gm = dF + NF;
-  double* hm = Gm + (int64_t)NMX * ldw;
-  double* Rm = hm + NMX;
-  double* am = Rm + (int64_t)NMX * NMX;
 #pragma unroll
-  for (int r = 1; r < NB; ++r) {
-    const gs_d4_t G = gtile::mfma_tn(gs_d4_t{0.0, 0.0, 0.0, 0.0}, Vt, W[r]);
+  for (int j = 1; j < NB; ++j)
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int mr = 4 * s + q, col = 16 * (r - 1) + c;
-      if (mr < nM && col <= NF) {  // G's column NF is zero padding (k_prefix layout); h = L^-T e
-        Gm[(int64_t)mr * ldw + col] = (col < NF) ? G[s] : 0.0;
-        if (col == NF) hm[mr] = G[s];
-      }
+    for (int r = j; r < NB; ++r) {
+      const int t = ts(j, r);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-W[j][s], W[r][s], acc[t], 0, 0, 0);
     }
-  }
-  // S_rj = T_rj - W_r^T W_j
-#pragma unroll
-  for (int r = 1; r < NB; ++r)
-#pragma unroll
-    for (int j = 1; j <= r; ++j) {
-      const int t = NB + (r - 1) * r / 2 + (j - 1);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-W[r][s], W[j][s], acc[t], 0, 0, 0);
-    }
-  // |L^-1 d_M|^2: column NF of W
-  double e2 = 0.0;
-  {
-    const int rd = 1 + NF / 16, ld = NF % 16;
-#pragma unroll
-    for (int r = 1; r < NB; ++r)
-      if (r == rd && c == ld)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) e2 += W[r][s] * W[r][s];
-    e2 = ec_wave_sum(e2);
-  }
 
-  // model block (gs_prefix layout): S0 | dF | G | h | R | aux
+  if constexpr (LNL) {
+    // + phiinv_F on the diagonal, then the upper tile Cholesky of the F block
+    const double* ph = A.phiinv_F + (int64_t)ch_id * NF;
 #pragma unroll
-  for (int r = 1; r < NB; ++r)
-#pragma unroll
-    for (int j = 1; j <= r; ++j) {
-      const int t = NB + (r - 1) * r / 2 + (j - 1);
+    for (int K = 1; K < NB; ++K)
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int row = 16 * (r - 1) + 4 * s + q, col = 16 * (j - 1) + c;
-        if (row < col) continue;
-        const double v = acc[t][s];
-        if (row < NF) S0[(int64_t)row * ldw + col] = v;
-        if (col < NF && row <= NF && row != col) S0[(int64_t)col * ldw + row] = v;
-        if (row == NF && col < NF) dF[col] = v;
+        const int i = 16 * (K - 1) + c;
+        if (4 * s + q == c && i < NF) acc[ts(K, K)][s] += ph[i];
+      }
+    double ldS = 0.0, quad = 0.0;
+#pragma unroll
+    for (int K = 1; K < NB; ++K) {
+      gs_d4_t Vk, Ak = acc[ts(K, K)];
+      double rk;
+      if (K < NTF) {
+        tile_elim<16>(Ak, Vk, rk, q, c);
+      } else {
+        // KMAX = LD_D + 1: tile_elim applies a step's column operation only when a later
+        // row remains, so the d row must be in range for the last F pivot to reach it
+        tile_elim<LD_D + 1>(Ak, Vk, rk, q, c);
+        // column-eliminated (d, d) entry = -(d^T Sigma^-1 d) of the whole system
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          if (c == LD_D && 4 * s + q == LD_D) quad = -Ak[s];
+      }
+      const int lim = (K < NTF) ? 16 : LD_D;
+      const bool badk = (q == 0) && (c < lim) && !(rk > 0.0 && rk < INFINITY);
+      const unsigned long long mk = __ballot(badk);
+      if (mk && fail == 0) fail = 16 * K + __builtin_ctzll(mk) + 1;
+      ldS += (q == 0 && c < lim) ? -2.0 * log(rk) : 0.0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) Vk[s] *= rk;
+      // U_KJ = V_K^T T_KJ (J > K), then T_IJ -= U_KI^T U_KJ (K < I <= J)
+#pragma unroll
+      for (int J = K + 1; J < NB; ++J) acc[ts(K, J)] = gtile::mfma_tn(gs_d4_t{0.0, 0.0, 0.0, 0.0}, Vk, acc[ts(K, J)]);
+#pragma unroll
+      for (int I = K + 1; I < NB; ++I)
+#pragma unroll
+        for (int J = I; J < NB; ++J)
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            acc[ts(I, J)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-acc[ts(K, I)][s], acc[ts(K, J)][s], acc[ts(I, J)], 0, 0, 0);
+    }
+    ldS = ec_wave_sum(ldS);
+    quad = ec_wave_sum(quad);
+    double lph = (l < NF) ? log(ph[l]) : 0.0;
+    lph = ec_wave_sum(lph);
+    if (l == 0) {
+      // in gs_ecorr_accept's convention: lnl + (aux1 - aux0 - aux2) / 2, with aux1 = 0 here
+      A.lnl[ch_id] = 0.5 * (quad - 2.0 * ldl - ldS + lph);
+      double* ax = A.aux + (int64_t)ch_id * 4;
+      ax[0] = sla;
+      ax[1] = 0.0;
+      ax[2] = slp;
+      ax[3] = pdd;
+      if (A.info) A.info[ch_id] = fail;
+    }
+    return;
+  } else {
+    const gs_d4_t Vt = gtile::transpose(V, Ls[w], q, c);  // C layout of V^T
+    const int NMX = A.NMX, ldw = NF + 1;
+    double* mb = A.model + (int64_t)ch_id * A.mstride;
+    double* S0 = mb;
+    double* dF = S0 + (int64_t)NF * ldw;
+    double* Gm = dF + NF;
+    double* hm = Gm + (int64_t)NMX * ldw;
+    double* Rm = hm + NMX;
+    double* am = Rm + (int64_t)NMX * NMX;
+    double e2 = 0.0;  // |L_M^-1 d_M|^2: column d of W
+#pragma unroll
+    for (int r = 1; r < NB; ++r) {
+      if (r == NTF && c == LD_D)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) e2 += W[r][s] * W[r][s];
+      // G_r = L_M^-T W_r = V W_r = (V^T)^T W_r
+      const gs_d4_t G = gtile::mfma_tn(gs_d4_t{0.0, 0.0, 0.0, 0.0}, Vt, W[r]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int mr = 4 * s + q, col = 16 * (r - 1) + c;
+        if (mr < nM && col <= NF) {  // G's column NF is zero padding (k_prefix layout); h = L^-T e
+          Gm[(int64_t)mr * ldw + col] = (col < NF) ? G[s] : 0.0;
+          if (col == NF) hm[mr] = G[s];
+        }
       }
     }
-  // R = L_M^-T = V (upper), zero beyond nM
-  for (int idx = l; idx < NMX * NMX; idx += 64) Rm[idx] = 0.0;
-  gtile::lds_fence();
+    e2 = ec_wave_sum(e2);
+    // S0 (rows < NF, cols <= NF, column NF = dF) from the upper tiles
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
-    if (4 * s + q < nM && c < nM) Rm[(4 * s + q) * NMX + c] = V[s];
-  for (int64_t qq = (am - mb) + 2 + l; qq < A.mstride; qq += 64) mb[qq] = 0.0;
-  if (l == 0) {
-    am[0] = ldl;
-    am[1] = e2;
-    double* ax = A.aux + (int64_t)ch_id * 4;
-    ax[0] = sla;
-    ax[1] = pdd;
-    ax[2] = slp;
-    ax[3] = 0.0;
-    if (A.info) A.info[ch_id] = fail;
+    for (int j = 1; j < NB; ++j)
+#pragma unroll
+      for (int r = j; r < NB; ++r) {
+        const int t = ts(j, r);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int row = 16 * (j - 1) + 4 * s + q, col = 16 * (r - 1) + c;
+          if (row > col) continue;
+          const double v = acc[t][s];
+          if (row < NF && col <= NF) S0[(int64_t)row * ldw + col] = v;
+          if (col < NF && row != col) S0[(int64_t)col * ldw + row] = v;
+          if (col == NF && row < NF) dF[row] = v;
+        }
+      }
+    // R = L_M^-T = V (upper), zero beyond nM
+    for (int idx = l; idx < NMX * NMX; idx += 64) Rm[idx] = 0.0;
+    gtile::lds_fence();
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (4 * s + q < nM && c < nM) Rm[(4 * s + q) * NMX + c] = V[s];
+    for (int64_t qq = (am - mb) + 2 + l; qq < A.mstride; qq += 64) mb[qq] = 0.0;
+    if (l == 0) {
+      am[0] = ldl;
+      am[1] = e2;
+      double* ax = A.aux + (int64_t)ch_id * 4;
+      ax[0] = sla;
+      ax[1] = pdd;
+      ax[2] = slp;
+      ax[3] = 0.0;
+      if (A.info) A.info[ch_id] = fail;
+    }
   }
 }
 
@@ -394,7 +443,8 @@ __device__ __forceinline__ double ec_scale(double u) {
 
 // One Metropolis proposal per chain (pulsar_gibbs.py:458-462): scale, one ECORR parameter
 // uniformly, q[par] += randn * (0.05 n_e) * scale.  xq = x with the jump applied;
-// prop[c] = {x column, log U, inside prior, proposed value}.
+// prop[c] = {x column, log U, inside prior, proposed value}.  Only the ECORR columns of xq
+// are written (the rest of the row is never read).
 __global__ __launch_bounds__(256) void k_ecorr_propose(EcorrMhArgs A) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= A.n_chain) return;
@@ -419,7 +469,8 @@ __global__ __launch_bounds__(256) void k_ecorr_propose(EcorrMhArgs A) {
   }
   const double* xr = A.x + (int64_t)c * A.ldx;
   double* qr = A.xq + (int64_t)c * A.ldx;
-  for (int j = 0; j < A.n_param; ++j) qr[j] = xr[j];
+  // the likelihood kernels read only the ECORR columns of xq
+  for (int j = 0; j < A.n_e; ++j) qr[A.ecol[j]] = xr[A.ecol[j]];
   const int col = A.ecol[p];
   const double qv = xr[col] + (z * (0.05 * A.n_e)) * sc;
   qr[col] = qv;
@@ -498,25 +549,27 @@ void launch_schur_nb(hipStream_t s, const EcorrSchurArgs& a) {
                      dim3(64 * EC_WAVES), lds, s, a);
 }
 
-template <int NB>
+template <int NB, bool LNL>
 void launch_prefix_nb(hipStream_t s, const EcorrPrefixArgs& a) {
   static bool attr = false;
   const size_t lds = (size_t)2 * EC_CH * 16 * NB * sizeof(double);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_ecorr_prefix<NB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_ecorr_prefix<NB, LNL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL(k_ecorr_prefix<NB>, dim3((unsigned)((a.n_chain + EC_WAVES - 1) / EC_WAVES)),
+  hipLaunchKernelGGL((k_ecorr_prefix<NB, LNL>), dim3((unsigned)((a.n_chain + EC_WAVES - 1) / EC_WAVES)),
                      dim3(64 * EC_WAVES), lds, s, a);
 }
 
 }  // namespace
 
 int launch_ecorr_prefix(hipStream_t s, const EcorrPrefixArgs& a) {
+  const bool lnl = a.lnl != nullptr;
   switch (a.ldbx / 16) {
-    case 3: launch_prefix_nb<3>(s, a); break;
-    case 4: launch_prefix_nb<4>(s, a); break;
-    case 5: launch_prefix_nb<5>(s, a); break;
+    case 3: lnl ? launch_prefix_nb<3, true>(s, a) : launch_prefix_nb<3, false>(s, a); break;
+    case 4: lnl ? launch_prefix_nb<4, true>(s, a) : launch_prefix_nb<4, false>(s, a); break;
+    case 5: lnl ? launch_prefix_nb<5, true>(s, a) : launch_prefix_nb<5, false>(s, a); break;
     default: return 1;
   }
   return 0;

@@ -198,8 +198,9 @@ struct EcorrPrefixArgs {
   int n_chain, NF, NMX, nM, ne, ldbx, ldx, n_bk;
   int64_t mstride;
   const double *Bx, *Dg, *Ap, *x;
+  const double* phiinv_F;  // likelihood mode (lnl != NULL): [n_chain x NF]
   const int32_t *ebk, *xcol;
-  double *model, *aux;
+  double *model, *aux, *lnl;
   int32_t* info;
 };
 int launch_ecorr_prefix(hipStream_t s, const EcorrPrefixArgs& a);

@@ -103,6 +103,7 @@ class EcorrModel:
         self.mstride = int(lib.gs_model_stride(NF, self.NMX))
         # fused path (gs_ecorr_prefix): columns [M (<= 16) | F | d], phiinv_M on the M diagonal
         self.fused = self.nm <= 16
+        self.fused_lnl = True   # likelihood-mode launches for the Metropolis steps
         if self.fused:
             KB = 16 * (1 + (NF + 1 + 15) // 16)
             self.ldbp = KB
@@ -121,7 +122,7 @@ class EcorrModel:
             Ap[idx, 16 + NF] = d[cols]
             dm = torch.arange(self.nm, device=dev)
             Ap[dm, dm] += self.phfix[0, :self.nm]
-            pad = torch.arange(self.nm, 16, device=dev)
+            pad = torch.cat([torch.arange(self.nm, 16, device=dev), torch.arange(17 + NF, KB, device=dev)])
             Ap[pad, pad] = 1.0
             self.Ap = Ap.contiguous()
         C = self.C
@@ -132,6 +133,7 @@ class EcorrModel:
         self.pinfo = torch.zeros(C, dtype=torch.int32, device=dev)
         self.lnl = torch.empty(C, dtype=torch.float64, device=dev)
         self.linfo = torch.zeros(C, dtype=torch.int32, device=dev)
+        self._linfo_dirty = False
         self.lnl0 = torch.empty(C, dtype=torch.float64, device=dev)
         self.xq = torch.empty(C, self.n_param, dtype=torch.float64, device=dev)
         self.prop = torch.empty(C, 4, dtype=torch.float64, device=dev)
@@ -150,7 +152,7 @@ class EcorrModel:
         if self.fused if fused is None else fused:
             check(lib.gs_ecorr_prefix(h, self.C, self.NF, self.NMX, self.nm, self.ne, self.ldbp, ptr(self.Bp),
                                       ptr(self.Dg), ptr(self.ebk), self.n_bk, ptr(self.ecol), ptr(x), x.shape[1],
-                                      ptr(self.Ap), ptr(self.model), ptr(self.aux), ptr(self.pinfo)),
+                                      ptr(self.Ap), None, ptr(self.model), ptr(self.aux), None, ptr(self.pinfo)),
                   "gs_ecorr_prefix")
             return
         check(lib.gs_ecorr_schur(h, self.C, self.mR, self.ne, self.ldbx, ptr(self.Bx), ptr(self.Dg), ptr(self.ebk),
@@ -160,6 +162,23 @@ class EcorrModel:
                                 ptr(self.TNTc), ptr(self.dc), ptr(self.fidx), ptr(self.midx), ptr(self.phfix),
                                 ptr(self.model), ptr(self.pinfo)), "gs_prefix_sys")
 
+    def _eval(self, x, phiinv_F):
+        """lnl / aux / info of every chain at x: one fused likelihood-mode launch when
+        available (no model block), else factor + gs_lnlike_marg."""
+        if self.fused and self.fused_lnl:
+            if self._linfo_dirty:   # the likelihood-mode kernel reports through pinfo only
+                self.linfo.zero_()
+                self._linfo_dirty = False
+            check(self.ctx.lib.gs_ecorr_prefix(self.ctx.handle, self.C, self.NF, self.NMX, self.nm, self.ne,
+                                               self.ldbp, ptr(self.Bp), ptr(self.Dg), ptr(self.ebk), self.n_bk,
+                                               ptr(self.ecol), ptr(x), x.shape[1], ptr(self.Ap), ptr(phiinv_F),
+                                               None, ptr(self.aux), ptr(self.lnl), ptr(self.pinfo)),
+                  "gs_ecorr_prefix")
+            return
+        self.factor(x)
+        self._lnl_R(phiinv_F)
+        self._linfo_dirty = True
+
     def _lnl_R(self, phiinv_F):
         check(self.ctx.lib.gs_lnlike_marg(self.ctx.handle, 1, self.C, self.NF, self.NMX, ptr(self.model), 1,
                                           ptr(self.nm_dev), ptr(phiinv_F), ptr(self.lnl), ptr(self.linfo)),
@@ -167,8 +186,7 @@ class EcorrModel:
 
     def lnlike(self, x, phiinv_F):
         """get_lnlikelihood_fullmarg (pulsar_gibbs.py:569-610) of every chain: (C,) tensor."""
-        self.factor(x)
-        self._lnl_R(phiinv_F)
+        self._eval(x, phiinv_F)
         a = self.aux
         ok = (self.pinfo == 0) & (self.linfo == 0)
         val = self.lnl + 0.5 * (a[:, 1] - a[:, 0] - a[:, 2]) + self.lnl_const
@@ -180,8 +198,7 @@ class EcorrModel:
         q_rec (n_steps, C, n_e) proposals or None."""
         lib, h = self.ctx.lib, self.ctx.handle
         ne_p = self.n_bk
-        self.factor(x)
-        self._lnl_R(phiinv_F)
+        self._eval(x, phiinv_F)
         check(lib.gs_ecorr_accept(h, self.C, ne_p, ptr(self.ecol), 1, ptr(self.lnl), ptr(self.linfo),
                                   ptr(self.pinfo), ptr(self.aux), None, None, ptr(x), x.shape[1], ptr(self.lnl0),
                                   None, None), "gs_ecorr_accept")
@@ -189,8 +206,7 @@ class EcorrModel:
             check(lib.gs_ecorr_propose(h, self.C, ne_p, ptr(self.ecol), ptr(self.emin), ptr(self.emax), ptr(x),
                                        x.shape[1], self.n_param, ptr(self.xq), s, sweep, chain_base, ptr(inj),
                                        ptr(self.prop)), "gs_ecorr_propose")
-            self.factor(self.xq)
-            self._lnl_R(phiinv_F)
+            self._eval(self.xq, phiinv_F)
             qr = q_rec[s] if q_rec is not None else None
             check(lib.gs_ecorr_accept(h, self.C, ne_p, ptr(self.ecol), 0, ptr(self.lnl), ptr(self.linfo),
                                       ptr(self.pinfo), ptr(self.aux), ptr(self.prop), ptr(self.xq), ptr(x),

@@ -55,15 +55,18 @@ def _phiinv_F(g, X):
     return 1.0 / np.repeat(10.0 ** (2.0 * X[:, _gwind(g)]), 2, axis=1)
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_ecorr_lnlike_matches_reference(ctx, fused):
-    """Both device forms (fused gs_ecorr_prefix; gs_ecorr_schur + gs_prefix_sys) against the
-    reference's get_lnlikelihood_fullmarg, and their model blocks against each other."""
+@pytest.mark.parametrize("mode", ["lnl", "block", "unfused"])
+def test_ecorr_lnlike_matches_reference(ctx, mode):
+    """The three device forms -- gs_ecorr_prefix in likelihood mode; gs_ecorr_prefix model
+    block + gs_lnlike_marg; gs_ecorr_schur + gs_prefix_sys + gs_lnlike_marg -- against the
+    reference's get_lnlikelihood_fullmarg, and the two model blocks against each other."""
     g = golden("ecorr_mh_j1713.npz")
     X = g["x_like"]
     em = _model(ctx, g, X.shape[0])
     assert em.fused
+    fused = mode != "unfused"
     em.fused = fused
+    em.fused_lnl = mode == "lnl"
     got = em.lnlike(_dev(X), _dev(_phiinv_F(g, X))).cpu().numpy()
     err = np.abs(got - g["lnlike"])
     assert err.max() < 1e-7, (got, g["lnlike"])
