@@ -17,7 +17,10 @@ namespace {
 
 typedef double gs_d4_t __attribute__((ext_vector_type(4)));
 
-constexpr int EC_WAVES = 8;  // chains per workgroup (one wavefront each)
+#ifndef GS_EC_WAVES
+#define GS_EC_WAVES 8
+#endif
+constexpr int EC_WAVES = GS_EC_WAVES;  // chains per workgroup (one wavefront each)
 constexpr int EC_CH = 32;    // epochs per LDS chunk
 
 __device__ __forceinline__ double ec_wave_sum(double v) {
@@ -65,12 +68,13 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
   for (int t = 0; t < NT; ++t) acc[t] = gs_d4_t{0.0, 0.0, 0.0, 0.0};
   double sla = 0.0, slp = 0.0;
 
-  double reg[NB];
+  constexpr int LPT = EC_CH * LDB / (64 * EC_WAVES);  // chunk elements per thread
+  double reg[LPT];
   double wreg = 0.0;
   auto load = [&](int e0) {
 #pragma unroll
-    for (int q = 0; q < NB; ++q) {
-      const int idx = tid + 64 * EC_WAVES * q;  // EC_CH * LDB = 512 NB elements
+    for (int q = 0; q < LPT; ++q) {
+      const int idx = tid + 64 * EC_WAVES * q;
       const int e = e0 + idx / LDB;
       reg[q] = (e < ne) ? A.Bx[(int64_t)e0 * LDB + idx] : 0.0;
     }
@@ -89,7 +93,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
   auto store = [&](int buf) {
     double* dst = lds + buf * (EC_CH * LDB);
 #pragma unroll
-    for (int q = 0; q < NB; ++q) dst[tid + 64 * EC_WAVES * q] = reg[q];
+    for (int q = 0; q < LPT; ++q) dst[tid + 64 * EC_WAVES * q] = reg[q];
     if (l < EC_CH) wb[buf][w][l] = wreg;
   };
 
@@ -102,8 +106,10 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
     if (ch + 1 < nch) load((ch + 1) * EC_CH);
     __builtin_amdgcn_sched_barrier(0);
     const double* cur = lds + cb * (EC_CH * LDB);
+    const int nk = min(EC_CH / 4, (ne - ch * EC_CH + 3) / 4);  // k-steps holding epochs (uniform)
 #pragma unroll
     for (int kk = 0; kk < EC_CH / 4; ++kk) {
+      if (kk >= nk) break;
       const double* row = cur + (4 * kk + k) * LDB + i;
       const double wv = wb[cb][w][4 * kk + k];
       double v[NB];
@@ -200,11 +206,12 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = gs_d4_t{0.0, 0.0, 0.0, 0.0};
   double sla = 0.0, slp = 0.0;
-  double reg[NB];
+  constexpr int LPT = EC_CH * LDB / (64 * EC_WAVES);  // chunk elements per thread
+  double reg[LPT];
   double wreg = 0.0;
   auto load = [&](int e0) {
 #pragma unroll
-    for (int u = 0; u < NB; ++u) {
+    for (int u = 0; u < LPT; ++u) {
       const int idx = tid + 64 * EC_WAVES * u;
       const int e = e0 + idx / LDB;
       reg[u] = (e < ne) ? A.Bx[(int64_t)e0 * LDB + idx] : 0.0;
@@ -224,7 +231,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
   auto store = [&](int buf) {
     double* dst = lds + buf * (EC_CH * LDB);
 #pragma unroll
-    for (int u = 0; u < NB; ++u) dst[tid + 64 * EC_WAVES * u] = reg[u];
+    for (int u = 0; u < LPT; ++u) dst[tid + 64 * EC_WAVES * u] = reg[u];
     if (l < EC_CH) wb[buf][w][l] = wreg;
   };
   const int nch = (ne + EC_CH - 1) / EC_CH;
@@ -236,8 +243,10 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
     if (chk + 1 < nch) load((chk + 1) * EC_CH);
     __builtin_amdgcn_sched_barrier(0);
     const double* cur = lds + cb * (EC_CH * LDB);
+    const int nk = min(EC_CH / 4, (ne - chk * EC_CH + 3) / 4);  // k-steps holding epochs (uniform)
 #pragma unroll
     for (int kk = 0; kk < EC_CH / 4; ++kk) {
+      if (kk >= nk) break;
       const double* row = cur + (4 * kk + q) * LDB + c;
       const double wv = wb[cb][w][4 * kk + q];
       double v[NB];
