@@ -378,6 +378,16 @@ def ecorr_cpu_baseline(seconds=10.0, aclength=10):
                        f"oracle restatement, numpy/LAPACK, 1 thread) in {el:.1f} s")
 
 
+def _ecorr_traffic(C):
+    """HBM bytes per launch of k_ecorr_prefix<likelihood> from the committed PMC passes
+    (tools/gpu_pmc_ecorr.sh -> profiles/pmc_traffic_ecorr.json), same chain count only."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic_ecorr.json")))
+    except (OSError, ValueError):
+        return None
+    return d.get("bytes_per_launch") if d.get("chains") == C else None
+
+
 def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
     """single pulsar with basis ECORR (J1713-like, 2 backends, 136 epochs,
     m = 212), C chains per GPU, aclength ECORR MH steps per sweep (each a batched
@@ -442,6 +452,7 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
                           "achieved": tflops,
                           "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tflops / FP64_PEAK_TFLOPS,
                           "kernel_avg_ms": k_ms, "alg_flops_per_launch": flops,
+                          "traffic": _ecorr_traffic(C),
                           "note": "ne (mR+1)(mR+2) + nM (NF+1)(NF+2) + (NF+1)^3/3 flop per chain (epoch-weighted "
                                   "SYRK with the d_E row + fixed-prior Schur update + F-block Cholesky) over the "
                                   "HIP-event time of one all-chain likelihood launch"},
