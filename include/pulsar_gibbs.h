@@ -402,6 +402,8 @@ int gs_bdraw_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,
  *   (x[c][col] = proposed value, lnl0 = lnL1, n_acc += 1) when lnL1 - lnl0 > log U and the
  *   proposal is inside the prior (:465-472).  q_rec [n_chain x n_e] = q[eind] or NULL.
  * gs_ecorr_bdraw_e: b_E = (d_E - B b_R)/a + z/sqrt(a) and b[rcol[j]] = bR[j]: the full b
+ *   (Bx column t multiplies bR[jmap[t]], skipped when jmap[t] < 0; d_E is column dcol; with the
+ *   gs_ecorr_schur layout jmap = 0..mR-1, dcol = mR)
  *   [n_chain x ldb] in original column order from the R draw bR [n_chain x ldbR] (gs_bdraw_sys
  *   on the Schur systems).  z [n_chain x m] injected normals by original column, or NULL
  *   (Philox event `event`: GS_EV_ECORR_B / GS_EV_ECORR_B0).  chain_mask as in gs_bdraw.
@@ -426,7 +428,18 @@ int gs_ecorr_schur(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const dou
 int gs_ecorr_prefix(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, int ldbx, const double* Bx,
                     const double* Dg, const int32_t* ebk, int n_bk, const int32_t* xcol, const double* x,
                     int ldx, const double* Ap, const double* phiinv_F, double* model, double* aux,
-                    double* lnl, int32_t* info);
+                    double* lnl, int32_t* info, int64_t bx_cstride, int64_t dg_cstride, int64_t ap_cstride);
+/*
+ * White noise sampled with ECORR (per-chain N): Bx / Dg / Ap differ per chain.  gs_ecorr_gather
+ * builds them from per-chain TNT [c][m x m] (tnt_cstride) and d [c][m] (d_cstride), e.g.
+ * gs_white_tnt's output: Bx [c][ne x kb], Dg [c][ne], Ap [c][kb x kb] with colmap [kb] = the
+ * original column of each reordered column, -1 for padding (1 on the Ap diagonal), -2 for d;
+ * phm [16] = phiinv of the fixed-prior columns (added on the Ap diagonal of the first 16).
+ * Pass the per-chain strides (ne kb, ne, kb kb) to gs_ecorr_prefix / gs_ecorr_bdraw_e.
+ */
+int gs_ecorr_gather(gs_ctx* ctx, int n_chain, int m, int ne, int kb, const int32_t* ecid, const int32_t* colmap,
+                    const double* phm, const double* TNT, int64_t tnt_cstride, const double* d,
+                    int64_t d_cstride, double* Bx, double* Dg, double* Ap);
 int gs_ecorr_propose(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, const double* emin,
                      const double* emax, const double* x, int ldx, int n_param, double* xq, int step,
                      int64_t sweep, int64_t chain_base, const double* inj, double* prop);
@@ -437,7 +450,7 @@ int gs_ecorr_bdraw_e(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const d
                      const int32_t* ebk, const int32_t* xcol, const double* x, int ldx, const double* bR,
                      int ldbR, const int32_t* ecid, const int32_t* rcol, int m, const double* z,
                      int64_t sweep, int event, int64_t chain_base, const int32_t* chain_mask, double* b,
-                     int ldb);
+                     int ldb, int64_t bx_cstride, int64_t dg_cstride, int dcol, const int32_t* jmap);
 
 /*
  * Philox4x32-10 test hook: out[i] = the 4 words for counter

@@ -70,11 +70,13 @@ SIGNATURES = {
     "gs_gate_phiinv_irn": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "gs_white_tnt": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I64, _I64, _P, _P]),
     "gs_ecorr_schur": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P]),
-    "gs_ecorr_prefix": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P]),
+    "gs_ecorr_prefix": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P,
+                             _I64, _I64, _I64]),
+    "gs_ecorr_gather": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P]),
     "gs_ecorr_propose": (_I, [_P, _I, _I, _P, _P, _P, _P, _I, _I, _P, _I, _I64, _I64, _P, _P]),
     "gs_ecorr_accept": (_I, [_P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P]),
     "gs_ecorr_bdraw_e": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P, _I, _P, _P, _I, _P, _I64, _I,
-                              _I64, _P, _P, _I]),
+                              _I64, _P, _P, _I, _I64, _I64, _I, _P]),
 }
 
 _lib = None

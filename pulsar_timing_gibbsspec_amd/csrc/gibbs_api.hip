@@ -774,7 +774,7 @@ int gs_ecorr_schur(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const dou
 int gs_ecorr_prefix(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, int ldbx, const double* Bx,
                     const double* Dg, const int32_t* ebk, int n_bk, const int32_t* xcol, const double* x,
                     int ldx, const double* Ap, const double* phiinv_F, double* model, double* aux,
-                    double* lnl, int32_t* info) {
+                    double* lnl, int32_t* info, int64_t bx_cstride, int64_t dg_cstride, int64_t ap_cstride) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_chain < 0) return fail_arg(2, "n_chain < 0");
   if (NF != 20 && NF != 40 && NF != 60) return fail_arg(3, "NF must be 20, 40 or 60");
@@ -792,8 +792,30 @@ int gs_ecorr_prefix(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, i
   a.mstride = model_stride_doubles(NF, NMX);
   a.Bx = Bx; a.Dg = Dg; a.Ap = Ap; a.x = x; a.ebk = ebk; a.xcol = xcol; a.model = model; a.aux = aux; a.info = info;
   a.phiinv_F = phiinv_F; a.lnl = lnl;
+  if (bx_cstride < 0 || dg_cstride < 0 || ap_cstride < 0) return fail_arg(20, "negative per-chain stride");
+  if ((bx_cstride == 0) != (ap_cstride == 0) || (bx_cstride == 0) != (dg_cstride == 0))
+    return fail_arg(20, "per-chain strides must be all zero or all nonzero");
+  a.bx_cs = bx_cstride; a.dg_cs = dg_cstride; a.ap_cs = ap_cstride;
   if (launch_ecorr_prefix(ctx->stream, a)) return fail_arg(7, "unsupported ldbx");
   return after_launch("k_ecorr_prefix");
+}
+
+int gs_ecorr_gather(gs_ctx* ctx, int n_chain, int m, int ne, int kb, const int32_t* ecid, const int32_t* colmap,
+                    const double* phm, const double* TNT, int64_t tnt_cstride, const double* d,
+                    int64_t d_cstride, double* Bx, double* Dg, double* Ap) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_chain < 0 || m <= 0 || ne < 0) return fail_arg(2, "n_chain / m / ne");
+  if (kb <= 16 || kb % 16) return fail_arg(5, "kb must be a multiple of 16 above 16");
+  if (!ecid || !colmap || !phm) return fail_arg(6, "NULL ecid / colmap / phm");
+  if (!TNT || !d || tnt_cstride < (int64_t)m * m || d_cstride < m) return fail_arg(9, "TNT / d / strides");
+  if (!Bx || !Dg || !Ap) return fail_arg(13, "NULL Bx / Dg / Ap");
+  if (n_chain == 0) return 0;
+  EcorrGatherArgs a;
+  a.n_chain = n_chain; a.m = m; a.ne = ne; a.kb = kb; a.nM = 16; a.tnt_cstride = tnt_cstride;
+  a.d_cstride = d_cstride; a.TNT = TNT; a.d = d; a.phm = phm; a.ecid = ecid; a.colmap = colmap;
+  a.Bx = Bx; a.Dg = Dg; a.Ap = Ap;
+  launch_ecorr_gather(ctx->stream, a);
+  return after_launch("k_ecorr_gather");
 }
 
 int gs_ecorr_propose(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, const double* emin,
@@ -839,10 +861,12 @@ int gs_ecorr_bdraw_e(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const d
                      const int32_t* ebk, const int32_t* xcol, const double* x, int ldx, const double* bR,
                      int ldbR, const int32_t* ecid, const int32_t* rcol, int m, const double* z,
                      int64_t sweep, int event, int64_t chain_base, const int32_t* chain_mask, double* b,
-                     int ldb) {
+                     int ldb, int64_t bx_cstride, int64_t dg_cstride, int dcol, const int32_t* jmap) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_chain < 0 || mR <= 0 || ne < 0) return fail_arg(2, "n_chain / mR / ne");
   if (ldbx < mR + 1) return fail_arg(5, "ldbx < mR + 1");
+  if (dcol < 0 || dcol >= ldbx || !jmap) return fail_arg(26, "dcol / jmap");
+  if (bx_cstride < 0 || dg_cstride < 0) return fail_arg(24, "negative per-chain stride");
   if (!Bx || !Dg || !ebk || !xcol) return fail_arg(6, "NULL Bx / Dg / ebk / xcol");
   if (!x || ldx <= 0) return fail_arg(10, "x / ldx");
   if (!bR || ldbR < mR) return fail_arg(12, "bR / ldbR");
@@ -855,6 +879,7 @@ int gs_ecorr_bdraw_e(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const d
   a.event = event; a.sweep = sweep; a.chain_base = chain_base; a.sweep_dev = ctx->sweep_dev; a.key = key_of(ctx);
   a.Bx = Bx; a.Dg = Dg; a.x = x; a.bR = bR; a.z = z; a.ebk = ebk; a.xcol = xcol; a.ecid = ecid; a.rcol = rcol;
   a.chain_mask = chain_mask; a.b = b;
+  a.bx_cs = bx_cstride; a.dg_cs = dg_cstride; a.dcol = dcol; a.jmap = jmap;
   launch_ecorr_bdraw_e(ctx->stream, a);
   return after_launch("k_ecorr_bdraw_e");
 }

@@ -10,6 +10,8 @@
 // PulsarBlockGibbs.update_ecorr_params (pulsar_gibbs.py:409-486) on
 // get_lnlikelihood_fullmarg (:569-610): k_ecorr_propose / k_ecorr_accept bracket one
 // batched likelihood evaluation per step.
+#include <algorithm>
+
 #include "gibbs_internal.h"
 #include "gibbs_tile.h"
 
@@ -177,7 +179,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
 //                F pivot the eliminated (d, d) entry is -(d^T Sigma^-1 d) of the whole
 //                system (Ap_dd = 0), so no solve is needed and nothing per chain but lnl
 //                goes to HBM.
-template <int NB, bool LNL>
+template <int NB, bool LNL, bool PC>
 __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs A) {
   extern __shared__ double lds[];
   __shared__ double wb[2][EC_WAVES][EC_CH];
@@ -234,6 +236,40 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
     for (int u = 0; u < LPT; ++u) dst[tid + 64 * EC_WAVES * u] = reg[u];
     if (l < EC_CH) wb[buf][w][l] = wreg;
   };
+  if constexpr (PC) {
+    // per-chain [B | d_E] (white noise sampled: TNT differs per chain): no LDS sharing,
+    // each wavefront streams its own rows; 1/a and the log sums by the c == 0 lanes
+    if (!live) return;  // no workgroup barriers below
+    const double* Bc = A.Bx + (int64_t)ch_id * A.bx_cs;
+    const double* Dc = A.Dg + (int64_t)ch_id * A.dg_cs;
+#pragma unroll 2
+    for (int e0 = 0; e0 < ne; e0 += 4) {
+      const int e = e0 + q;
+      const bool ok = e < ne;
+      double wv = 0.0;
+      if (ok) {
+        const int kb = A.ebk[e];
+        const double a = Dc[e] + sinv[w][kb];
+        wv = 1.0 / a;
+        if (c == 0) {
+          sla += log(a);
+          slp += slog[w][kb];
+        }
+      }
+      double v[NB];
+#pragma unroll
+      for (int r = 0; r < NB; ++r) v[r] = ok ? Bc[(int64_t)e * LDB + 16 * r + c] : 0.0;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const double av = v[j] * wv;
+#pragma unroll
+        for (int r = j; r < NB; ++r) {
+          const int t = (j == 0) ? r : ts(j, r);
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, v[r], acc[t], 0, 0, 0);
+        }
+      }
+    }
+  } else {
   const int nch = (ne + EC_CH - 1) / EC_CH;
   load(0);
   store(0);
@@ -265,6 +301,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
     if (chk + 1 < nch) store(cb ^ 1);
     __syncthreads();
   }
+  }
   sla = ec_wave_sum(sla);
   slp = ec_wave_sum(slp);
   if (!live) return;  // no workgroup barriers below
@@ -276,7 +313,8 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
     if (c == LD_D && 4 * s + q == LD_D) pdd = acc[ts(NTF, NTF)][s];
   pdd = ec_wave_sum(pdd);
   // T = Ap - P
-  auto Aq = [&](int r0, int c0, int s) { return A.Ap[(int64_t)(r0 + 4 * s + q) * LDB + c0 + c]; };
+  const double* Apc = A.Ap + (int64_t)ch_id * A.ap_cs;
+  auto Aq = [&](int r0, int c0, int s) { return Apc[(int64_t)(r0 + 4 * s + q) * LDB + c0 + c]; };
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc[0][s] = Aq(0, 0, s) - acc[0][s];
 #pragma unroll
@@ -530,10 +568,13 @@ __global__ __launch_bounds__(256) void k_ecorr_bdraw_e(EcorrBArgs A) {
   const int e = j;
   double inv, lg;
   ec_phi(A.x[(int64_t)c * A.ldx + A.xcol[A.ebk[e]]], inv, lg);
-  const double a = A.Dg[e] + inv;
-  const double* row = A.Bx + (int64_t)e * A.ldbx;
-  double s = row[A.mR];
-  for (int t = 0; t < A.mR; ++t) s = fma(-row[t], bR[t], s);
+  const double a = A.Dg[(int64_t)c * A.dg_cs + e] + inv;
+  const double* row = A.Bx + (int64_t)c * A.bx_cs + (int64_t)e * A.ldbx;
+  double s = row[A.dcol];
+  for (int t = 0; t < A.ldbx; ++t) {
+    const int jr = A.jmap[t];
+    if (jr >= 0) s = fma(-row[t], bR[jr], s);
+  }
   double z;
   if (A.z) {
     z = A.z[(int64_t)c * A.m + A.ecid[e]];
@@ -558,17 +599,60 @@ void launch_schur_nb(hipStream_t s, const EcorrSchurArgs& a) {
                      dim3(64 * EC_WAVES), lds, s, a);
 }
 
-template <int NB, bool LNL>
-void launch_prefix_nb(hipStream_t s, const EcorrPrefixArgs& a) {
+template <int NB, bool LNL, bool PC>
+void launch_prefix_nbp(hipStream_t s, const EcorrPrefixArgs& a) {
   static bool attr = false;
-  const size_t lds = (size_t)2 * EC_CH * 16 * NB * sizeof(double);
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_ecorr_prefix<NB, LNL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  const size_t lds = PC ? 0 : (size_t)2 * EC_CH * 16 * NB * sizeof(double);
+  if (!attr && !PC) {
+    (void)hipFuncSetAttribute((const void*)k_ecorr_prefix<NB, LNL, PC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((k_ecorr_prefix<NB, LNL>), dim3((unsigned)((a.n_chain + EC_WAVES - 1) / EC_WAVES)),
+  hipLaunchKernelGGL((k_ecorr_prefix<NB, LNL, PC>), dim3((unsigned)((a.n_chain + EC_WAVES - 1) / EC_WAVES)),
                      dim3(64 * EC_WAVES), lds, s, a);
+}
+
+template <int NB, bool LNL>
+void launch_prefix_nb(hipStream_t s, const EcorrPrefixArgs& a) {
+  if (a.bx_cs) launch_prefix_nbp<NB, LNL, true>(s, a);
+  else launch_prefix_nbp<NB, LNL, false>(s, a);
+}
+
+// per-chain [B | d_E], Dg, Ap from per-chain TNT / d (white noise sampled)
+__global__ __launch_bounds__(256) void k_ecorr_gather(EcorrGatherArgs A) {
+  const int c = blockIdx.y;
+  const int kb = A.kb, ne = A.ne, m = A.m;
+  const double* T = A.TNT + (int64_t)c * A.tnt_cstride;
+  const double* dv = A.d + (int64_t)c * A.d_cstride;
+  const int64_t nB = (int64_t)ne * kb, nA = (int64_t)kb * kb;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nB + nA + ne; i += (int64_t)gridDim.x * 256) {
+    if (i < nB) {
+      const int e = (int)(i / kb), j = (int)(i % kb);
+      const int cj = A.colmap[j];
+      const int ce = A.ecid[e];
+      A.Bx[(int64_t)c * nB + i] = (cj >= 0) ? T[(int64_t)ce * m + cj] : ((cj == -2) ? dv[ce] : 0.0);
+    } else if (i < nB + nA) {
+      const int64_t k = i - nB;
+      const int r = (int)(k / kb), j = (int)(k % kb);
+      const int cr = A.colmap[r], cj = A.colmap[j];
+      double v;
+      if (cr >= 0 && cj >= 0) {
+        v = T[(int64_t)cr * m + cj];
+        if (r == j && r < 16) v += A.phm[r];
+      } else if (cr == -2 && cj >= 0) {
+        v = dv[cj];
+      } else if (cj == -2 && cr >= 0) {
+        v = dv[cr];
+      } else {
+        v = (r == j && cr == -1) ? 1.0 : 0.0;
+      }
+      A.Ap[(int64_t)c * nA + k] = v;
+    } else {
+      const int e = (int)(i - nB - nA);
+      const int ce = A.ecid[e];
+      A.Dg[(int64_t)c * ne + e] = T[(int64_t)ce * m + ce];
+    }
+  }
 }
 
 }  // namespace
@@ -608,6 +692,13 @@ int launch_ecorr_propose(hipStream_t s, const EcorrMhArgs& a) {
 
 int launch_ecorr_accept(hipStream_t s, const EcorrMhArgs& a) {
   hipLaunchKernelGGL(k_ecorr_accept, dim3((unsigned)((a.n_chain + 255) / 256)), dim3(256), 0, s, a);
+  return 0;
+}
+
+int launch_ecorr_gather(hipStream_t s, const EcorrGatherArgs& a) {
+  const int64_t n = (int64_t)a.ne * a.kb + (int64_t)a.kb * a.kb + a.ne;
+  hipLaunchKernelGGL(k_ecorr_gather, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 64), (unsigned)a.n_chain),
+                     dim3(256), 0, s, a);
   return 0;
 }
 

@@ -186,8 +186,9 @@ struct EcorrMhArgs {
   int32_t* n_acc;
 };
 struct EcorrBArgs {
-  int n_chain, mR, ne, ldbx, ldx, ldbR, m, ldb, event;
-  int64_t sweep, chain_base;
+  int n_chain, mR, ne, ldbx, ldx, ldbR, m, ldb, event, dcol;
+  int64_t sweep, chain_base, bx_cs, dg_cs;  // per-chain strides of Bx / Dg (0: shared)
+  const int32_t* jmap;                      // Bx column -> index into bR (-1: skip)
   const int64_t* sweep_dev;
   gs_key key;
   const double *Bx, *Dg, *x, *bR, *z;
@@ -196,7 +197,7 @@ struct EcorrBArgs {
 };
 struct EcorrPrefixArgs {
   int n_chain, NF, NMX, nM, ne, ldbx, ldx, n_bk;
-  int64_t mstride;
+  int64_t mstride, bx_cs, dg_cs, ap_cs;  // per-chain strides of Bx / Dg / Ap (0: shared)
   const double *Bx, *Dg, *Ap, *x;
   const double* phiinv_F;  // likelihood mode (lnl != NULL): [n_chain x NF]
   const int32_t *ebk, *xcol;
@@ -204,6 +205,14 @@ struct EcorrPrefixArgs {
   int32_t* info;
 };
 int launch_ecorr_prefix(hipStream_t s, const EcorrPrefixArgs& a);
+struct EcorrGatherArgs {
+  int n_chain, m, ne, kb, nM;
+  int64_t tnt_cstride, d_cstride;
+  const double *TNT, *d, *phm;
+  const int32_t *ecid, *colmap;
+  double *Bx, *Dg, *Ap;
+};
+int launch_ecorr_gather(hipStream_t s, const EcorrGatherArgs& a);
 bool ecorr_nb_supported(int nb);
 int launch_ecorr_schur(hipStream_t s, const EcorrSchurArgs& a);
 int launch_ecorr_propose(hipStream_t s, const EcorrMhArgs& a);

@@ -40,7 +40,7 @@ class EcorrModel:
     """
 
     def __init__(self, ctx, T, Nvec, r, ecid, epoch_backend, gwid, ecol, emin, emax, n_param, n_chain,
-                 phiinv_fixed=1e-40):
+                 phiinv_fixed=1e-40, per_chain=False):
         self.ctx = ctx
         dev = ctx.device
         lib, h = ctx.lib, ctx.handle
@@ -125,6 +125,32 @@ class EcorrModel:
             pad = torch.cat([torch.arange(self.nm, 16, device=dev), torch.arange(17 + NF, KB, device=dev)])
             Ap[pad, pad] = 1.0
             self.Ap = Ap.contiguous()
+            # column maps of the reordered layout: original column (-1 pad, -2 d) and R index
+            colmap = np.full(KB, -1, np.int32)
+            colmap[:self.nm] = rc[mR_idx]
+            colmap[16:16 + NF] = gwid
+            colmap[16 + NF] = -2
+            jmap = np.full(KB, -1, np.int32)
+            jmap[:self.nm] = mR_idx
+            jmap[16:16 + NF] = fR
+            self.colmap = _t(colmap, torch.int32, dev)
+            self.jmap = _t(jmap, torch.int32, dev)
+            self.dcol = 16 + NF
+            phm = np.ones(16)
+            phm[:self.nm] = np.asarray(phf)[:self.nm]
+            self.phm = _t(phm, torch.float64, dev)
+        # per-chain operands (white noise sampled: N, hence TNT, differs per chain)
+        self.per_chain = bool(per_chain)
+        self.strides = (0, 0, 0)
+        if self.per_chain:
+            if not self.fused:
+                raise NotImplementedError("per-chain ECORR operands need <= 16 fixed-prior columns")
+            KB = self.ldbp
+            C0 = int(n_chain)
+            self.Bp = torch.empty(C0, self.ne, KB, dtype=torch.float64, device=dev)
+            self.Dg = torch.empty(C0, self.ne, dtype=torch.float64, device=dev)
+            self.Ap = torch.empty(C0, KB, KB, dtype=torch.float64, device=dev)
+            self.strides = (self.ne * KB, self.ne, KB * KB)
         C = self.C
         self.TNTc = torch.empty(C * mR * mR, dtype=torch.float64, device=dev)
         self.dc = torch.empty(C * mR, dtype=torch.float64, device=dev)
@@ -152,8 +178,8 @@ class EcorrModel:
         if self.fused if fused is None else fused:
             check(lib.gs_ecorr_prefix(h, self.C, self.NF, self.NMX, self.nm, self.ne, self.ldbp, ptr(self.Bp),
                                       ptr(self.Dg), ptr(self.ebk), self.n_bk, ptr(self.ecol), ptr(x), x.shape[1],
-                                      ptr(self.Ap), None, ptr(self.model), ptr(self.aux), None, ptr(self.pinfo)),
-                  "gs_ecorr_prefix")
+                                      ptr(self.Ap), None, ptr(self.model), ptr(self.aux), None, ptr(self.pinfo),
+                                      *self.strides), "gs_ecorr_prefix")
             return
         check(lib.gs_ecorr_schur(h, self.C, self.mR, self.ne, self.ldbx, ptr(self.Bx), ptr(self.Dg), ptr(self.ebk),
                                  self.n_bk, ptr(self.ecol), ptr(x), x.shape[1], ptr(self.A), ptr(self.dR),
@@ -161,6 +187,12 @@ class EcorrModel:
         check(lib.gs_prefix_sys(h, 1, self.C, self.NF, self.NMX, ptr(self.pdesc), self.mR * self.mR, self.mR,
                                 ptr(self.TNTc), ptr(self.dc), ptr(self.fidx), ptr(self.midx), ptr(self.phfix),
                                 ptr(self.model), ptr(self.pinfo)), "gs_prefix_sys")
+
+    def gather(self, TNT, d, tnt_cstride, d_cstride):
+        """Per-chain [B | d_E], Dg, Ap from per-chain TNT / d (white.WhiteNoiseModel.tnt)."""
+        check(self.ctx.lib.gs_ecorr_gather(self.ctx.handle, self.C, self.m, self.ne, self.ldbp, ptr(self.ecid),
+                                           ptr(self.colmap), ptr(self.phm), ptr(TNT), tnt_cstride, ptr(d),
+                                           d_cstride, ptr(self.Bp), ptr(self.Dg), ptr(self.Ap)), "gs_ecorr_gather")
 
     def _eval(self, x, phiinv_F):
         """lnl / aux / info of every chain at x: one fused likelihood-mode launch when
@@ -172,8 +204,8 @@ class EcorrModel:
             check(self.ctx.lib.gs_ecorr_prefix(self.ctx.handle, self.C, self.NF, self.NMX, self.nm, self.ne,
                                                self.ldbp, ptr(self.Bp), ptr(self.Dg), ptr(self.ebk), self.n_bk,
                                                ptr(self.ecol), ptr(x), x.shape[1], ptr(self.Ap), ptr(phiinv_F),
-                                               None, ptr(self.aux), ptr(self.lnl), ptr(self.pinfo)),
-                  "gs_ecorr_prefix")
+                                               None, ptr(self.aux), ptr(self.lnl), ptr(self.pinfo),
+                                               *self.strides), "gs_ecorr_prefix")
             return
         self.factor(x)
         self._lnl_R(phiinv_F)
@@ -184,12 +216,15 @@ class EcorrModel:
                                           ptr(self.nm_dev), ptr(phiinv_F), ptr(self.lnl), ptr(self.linfo)),
               "gs_lnlike_marg")
 
-    def lnlike(self, x, phiinv_F):
-        """get_lnlikelihood_fullmarg (pulsar_gibbs.py:569-610) of every chain: (C,) tensor."""
+    def lnlike(self, x, phiinv_F, lnl_const=None):
+        """get_lnlikelihood_fullmarg (pulsar_gibbs.py:569-610) of every chain: (C,) tensor.
+        lnl_const: -1/2 (sum log N + r^T N^-1 r) + 1/2 sum_M log phiinv_M per chain when N
+        differs per chain (default: the model's fixed-N value)."""
         self._eval(x, phiinv_F)
         a = self.aux
         ok = (self.pinfo == 0) & (self.linfo == 0)
-        val = self.lnl + 0.5 * (a[:, 1] - a[:, 0] - a[:, 2]) + self.lnl_const
+        const = self.lnl_const if lnl_const is None else lnl_const
+        val = self.lnl + 0.5 * (a[:, 1] - a[:, 0] - a[:, 2]) + const
         return torch.where(ok, val, torch.full_like(val, -np.inf))
 
     def mh(self, x, phiinv_F, n_steps, sweep=0, chain_base=0, inj=None, q_rec=None, n_acc=None):
@@ -224,10 +259,19 @@ class EcorrModel:
         check(lib.gs_bdraw_sys(h, 1, self.C, self.NF, self.NMX, self.mR, ptr(self.model), ptr(self.fidx),
                                ptr(self.midx), ptr(self.nm_dev), ptr(phiinv_F), ptr(zR), sweep, ev_r, chain_base,
                                ptr(chain_mask), ptr(self.bR), ptr(self.binfo)), "gs_bdraw_sys")
-        check(lib.gs_ecorr_bdraw_e(h, self.C, self.mR, self.ne, self.ldbx, ptr(self.Bx), ptr(self.Dg), ptr(self.ebk),
+        if self.fused:   # reordered [M | F | d] rows (shared or per chain)
+            Bx, ldbx, dcol, jmap = self.Bp, self.ldbp, self.dcol, self.jmap
+        else:
+            if not hasattr(self, "_jmap_r"):
+                self._jmap_r = torch.arange(self.mR, dtype=torch.int32, device=x.device)
+                self._jmap_r = torch.cat([self._jmap_r, torch.full((self.ldbx - self.mR,), -1, dtype=torch.int32,
+                                                                   device=x.device)])
+            Bx, ldbx, dcol, jmap = self.Bx, self.ldbx, self.mR, self._jmap_r
+        check(lib.gs_ecorr_bdraw_e(h, self.C, self.mR, self.ne, ldbx, ptr(Bx), ptr(self.Dg), ptr(self.ebk),
                                    ptr(self.ecol), ptr(x), x.shape[1], ptr(self.bR), self.mR, ptr(self.ecid),
                                    ptr(self.rcol), self.m, ptr(z), sweep, ev_e, chain_base, ptr(chain_mask), ptr(b),
-                                   b.shape[1]), "gs_ecorr_bdraw_e")
+                                   b.shape[1], self.strides[0], self.strides[1], dcol, ptr(jmap)),
+              "gs_ecorr_bdraw_e")
         return b
 
 
@@ -302,6 +346,80 @@ class EcorrFreeSpectrumChains:
         # rho|b writes the n_f log10_rho columns of x in place (:206-216, 236)
         xg = ctypes.c_void_p(self.x.data_ptr() + 8 * self.gw0)
         check(lib.gs_rho_analytic(h, 1, em.C, em.NF, self.ldb, ptr(self.fidx_full), ptr(self.b), ptr(u), ii,
+                                  self.chain_base, self.rhomin, self.rhomax, xg, em.n_param), "gs_rho_analytic")
+        self._phiinv(True)
+        em.bdraw(self.x, self.phiinv_F, self.b, z=z, sweep=ii, chain_base=self.chain_base, chain_mask=self.gate)
+        self.it += 1
+
+
+class EcorrWhiteChains:
+    """White noise AND basis ECORR sampled (the notebook's J1713 run, white_vary=True), n_chain
+    chains of one pulsar, in the notebook sampler's order (pta_gibbs_freespec.ipynb cell 2):
+
+        record x, b -> [ii == 0: b from x0] -> white MH on y = r - T b (pulsar_gibbs.py:373-404)
+        -> TNT_c, d_c with the chain's new N (gs_white_tnt: the reference's TNT reset + the
+        recompute inside get_lnlikelihood) -> per-chain ECORR operands (gs_ecorr_gather)
+        -> ECORR MH (:456-484) -> rho|b -> gate -> b|rho
+
+    wm: white.WhiteNoiseModel(prefix=False) over the full basis; em: EcorrModel(per_chain=True).
+    """
+
+    def __init__(self, wm, em: EcorrModel, gw_cols, gwid, rhomin, rhomax, x0, aclength_white,
+                 aclength_ecorr, chain_base=0):
+        if not em.per_chain:
+            raise ValueError("EcorrWhiteChains needs EcorrModel(per_chain=True)")
+        self.wm, self.em, self.ctx = wm, em, em.ctx
+        dev = self.ctx.device
+        C = em.C
+        gw = np.asarray(gw_cols, np.int64)
+        self.gw0 = int(gw[0])
+        if not np.array_equal(gw, self.gw0 + np.arange(em.NF // 2)):
+            raise NotImplementedError("the gw log10_rho columns must be contiguous in x")
+        self.gw_cols = _t(gw.astype(np.int32), torch.int32, dev)
+        self.fidx_full = _t(np.asarray(gwid, np.int32)[None, :], torch.int32, dev)
+        self.rhomin, self.rhomax = float(rhomin), float(rhomax)
+        self.acl_w, self.acl_e = int(aclength_white), int(aclength_ecorr)
+        self.chain_base = int(chain_base)
+        self.x = _t(np.broadcast_to(np.asarray(x0, float), (C, em.n_param)), torch.float64, dev)
+        self.b = torch.zeros(C, em.m, dtype=torch.float64, device=dev)
+        self.phiinv_F = torch.empty(C, em.NF, dtype=torch.float64, device=dev)
+        self.xlast = torch.empty(C, dtype=torch.float64, device=dev)
+        self.gate = torch.empty(C, dtype=torch.int32, device=dev)
+        self.n_acc_white = torch.zeros(C, dtype=torch.int32, device=dev)
+        self.n_acc_ecorr = torch.zeros(C, dtype=torch.int32, device=dev)
+        self.it = 0
+
+    def _phiinv(self, with_gate):
+        em = self.em
+        check(self.ctx.lib.gs_pta_gate_phiinv(self.ctx.handle, 1, em.C, em.NF // 2, em.n_param, ptr(self.x),
+                                              ptr(self.xlast) if with_gate else None, ptr(self.gw_cols), None,
+                                              ptr(self.phiinv_F), ptr(self.gate)), "gs_pta_gate_phiinv")
+
+    def _operands(self):
+        wm, em = self.wm, self.em
+        wm.tnt(self.x, em.n_param)
+        em.gather(wm.TNT, wm.d, wm.tnt_cstride, wm.d_cstride)
+
+    def sweep(self, x_rec=None, b_rec=None, z0=None, z=None, u=None, white_inj=None, ecorr_inj=None):
+        em, wm, lib, h = self.em, self.wm, self.ctx.lib, self.ctx.handle
+        ii = self.it
+        if x_rec is not None:
+            x_rec.copy_(self.x)
+        if b_rec is not None:
+            b_rec.copy_(self.b)
+        self.xlast.copy_(self.x[:, -1])
+        if ii == 0:
+            self._operands()
+            self._phiinv(False)
+            em.bdraw(self.x, self.phiinv_F, self.b, z=z0, sweep=ii, first=True, chain_base=self.chain_base)
+        wm.resid(self.b)
+        wm.mh(self.x, em.n_param, self.acl_w, ii, chain_base=self.chain_base, inj=white_inj, n_acc=self.n_acc_white)
+        self._operands()
+        self._phiinv(False)
+        em.mh(self.x, self.phiinv_F, self.acl_e, sweep=ii, chain_base=self.chain_base, inj=ecorr_inj,
+              n_acc=self.n_acc_ecorr)
+        xg = ctypes.c_void_p(self.x.data_ptr() + 8 * self.gw0)
+        check(lib.gs_rho_analytic(h, 1, em.C, em.NF, em.m, ptr(self.fidx_full), ptr(self.b), ptr(u), ii,
                                   self.chain_base, self.rhomin, self.rhomax, xg, em.n_param), "gs_rho_analytic")
         self._phiinv(True)
         em.bdraw(self.x, self.phiinv_F, self.b, z=z, sweep=ii, chain_base=self.chain_base, chain_mask=self.gate)

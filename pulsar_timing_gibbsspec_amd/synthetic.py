@@ -408,15 +408,17 @@ def single_pulsar_pta(psr="J1713+0747", n_f=30, rho_prior=(-9.0, -4.0), log10_A=
 
 def ecorr_pulsar_pta(psr="J1713+0747", n_epoch=160, n_sub=(1, 6), n_backends=2, n_f=30,
                      rho_prior=(-9.0, -4.0), ecorr_prior=(-8.5, -5.0), log10_ecorr=-6.3,
-                     log10_A=np.log10(2e-15), gamma=13.0 / 3.0, span_yr=15.0, n_tm=16, seed=0):
+                     log10_A=np.log10(2e-15), gamma=13.0 / 3.0, span_yr=15.0, n_tm=16, seed=0,
+                     white_vary=False):
     """Single pulsar with basis ECORR (pta_gibbs_freespec.ipynb's
     J1713 model ``model_general(..., white_vary=True, select='backend')`` with fixed
     EFAC/EQUAD): n_epoch observing epochs over span_yr, each recorded by one backend
     (epoch % n_backends) as a burst of n_sub[0]..n_sub[1] sub-band TOAs a few tenths of a
     second apart (single-TOA epochs get no ECORR column, nmin = 2).  Signals in order
     [white, basis_ecorr, gw, tm]: T = [U | F | M], ecid = 0..n_e-1, gwid after.
-    Parameters (sorted by name): ``{psr}_basis_ecorr_b{k}_log10_ecorr`` then
-    ``gw_log10_rho`` (n_f).  Residuals: power-law GWB + TM + white + epoch jitter."""
+    Parameters (sorted by name): [``{psr}_b{k}_efac``, ``{psr}_b{k}_log10_tnequad`` with
+    ``white_vary``], ``{psr}_basis_ecorr_b{k}_log10_ecorr``, then ``gw_log10_rho`` (n_f).
+    Residuals: power-law GWB + TM + white + epoch jitter."""
     rng = np.random.default_rng(seed)
     Tspan0 = span_yr * 365.25 * DAY
     t_ep = np.sort(rng.uniform(0.0, Tspan0, n_epoch)) + 53000.0 * DAY
@@ -425,7 +427,9 @@ def ecorr_pulsar_pta(psr="J1713+0747", n_epoch=160, n_sub=(1, 6), n_backends=2, 
     backends = np.concatenate([np.full(k, e % n_backends) for e, k in enumerate(nsub)])
     sigma = 10 ** rng.uniform(np.log10(1e-7), np.log10(2e-6), toas.size)
     Tspan = toas.max() - toas.min()
-    white = MeasurementNoise(psr, sigma, backends)
+    efp = [Uniform(f"{psr}_b{k}_efac", 0.1, 5.0) for k in range(n_backends)] if white_vary else []
+    eqp = [Uniform(f"{psr}_b{k}_log10_tnequad", -8.5, -5.0) for k in range(n_backends)] if white_vary else []
+    white = MeasurementNoise(psr, sigma, backends, efp, eqp)
     ep = [Uniform(f"{psr}_basis_ecorr_b{k}_log10_ecorr", *ecorr_prior) for k in range(n_backends)]
     ecorr = EcorrBasisGP(psr, toas, backends, ep)
     rho = Uniform("gw_log10_rho", rho_prior[0], rho_prior[1], size=n_f)

@@ -58,7 +58,7 @@ class WhiteNoiseModel:
     """
 
     def __init__(self, ctx, T_list, r_list, sigma_list, backend_list, fidx_list, phiinv_fixed_list,
-                 white_list, n_chain):
+                 white_list, n_chain, prefix=True):
         self.ctx = ctx
         dev = ctx.device
         P = len(T_list)
@@ -72,7 +72,10 @@ class WhiteNoiseModel:
         self.m = np.array([t.shape[1] for t in T_list], np.int64)
         self.n_toa = np.array([t.shape[0] for t in T_list], np.int64)
         self.nm = (self.m - NF).astype(np.int32)
-        if (self.nm <= 0).any() or (self.nm > 64).any():
+        # prefix=False: per-chain TNT / d, residuals and the white MH only (the basis-ECORR
+        # path factors its own Schur systems, ecorr.EcorrModel(per_chain=True))
+        self.prefix = bool(prefix)
+        if self.prefix and ((self.nm <= 0).any() or (self.nm > 64).any()):
             raise NotImplementedError("need 1..64 fixed-prior columns per pulsar")
         self.NMX = int(self.nm.max())
         self.ldb = int(self.m.max())
@@ -147,11 +150,19 @@ class WhiteNoiseModel:
         self.mstride = int(ctx.lib.gs_model_stride(NF, self.NMX))
         self.TNT = torch.empty(C * self.tnt_cstride, dtype=torch.float64, device=dev)
         self.d = torch.empty(C * self.d_cstride, dtype=torch.float64, device=dev)
-        self.model = torch.empty(P * C * self.mstride, dtype=torch.float64, device=dev)
+        self.model = torch.empty(P * C * self.mstride if self.prefix else 0, dtype=torch.float64, device=dev)
         self.y = torch.empty(C, self.ntot, dtype=torch.float64, device=dev)
         self.pinfo = torch.zeros(P * C, dtype=torch.int32, device=dev)
 
     # ---------------------------------------------------------------- kernels
+    def tnt(self, x, ldx):
+        """TNT_c, d_c from the white parameters in x (pulsar_gibbs.py:495-502)."""
+        check(self.ctx.lib.gs_white_tnt(self.ctx.handle, self.P, self.C, int(self.m.max()), ptr(self.tdesc),
+                                        ptr(self.wdesc), ptr(self.wcol), ptr(self.wkind), ptr(self.wbk),
+                                        ptr(self.T), ptr(self.sigma2), ptr(self.bk), ptr(self.r), ptr(x), ldx,
+                                        self.tnt_cstride, self.d_cstride, ptr(self.TNT), ptr(self.d)),
+              "gs_white_tnt")
+
     def refresh(self, x, ldx):
         """TNT_c, d_c from the white parameters in x, then the per-system prefix."""
         lib, h = self.ctx.lib, self.ctx.handle

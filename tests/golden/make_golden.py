@@ -434,10 +434,68 @@ def ecorr_long(ref, out, niter=6000, thin=5, acl=10):
     print("ecorr long:", out, len(rows))
 
 
+def ecorr_white_mh(ref, out, nsweep=5, acl_w=12, acl_e=12, nlike=6):
+    """White-noise + basis-ECORR blocks together (the notebook J1713 configuration,
+    white_vary=True): per sweep (notebook sample order) record, [first b], TNT reset,
+    update_white_params (:373-404, steady state), update_ecorr_params (:456-484, its
+    get_lnlikelihood = get_lnlikelihood_fullmarg), rho|b, gated b; every draw captured.
+    Also the marginalised likelihood at prior draws of all parameters."""
+    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=0, white_vary=True)
+    np.random.seed(41)
+    g = _quiet(ref.PulsarBlockGibbs, pta)
+    g.get_lnlikelihood = g.get_lnlikelihood_fullmarg
+    x0 = np.concatenate([p.sample().flatten() for p in g.params])
+    wind, eind = g.get_efacequad_indices(), g.get_ecorr_indices()
+    x0[wind] = [1.0 if "efac" in n else -7.0 for n in np.array(g.param_names)[wind]]
+    g.aclength_white, g.aclength_ecorr = acl_w, acl_e
+    xl, ll = [], []
+    for _ in range(nlike):
+        x = np.concatenate([p.sample().flatten() for p in g.params])
+        g.TNT = g.d = None
+        xl.append(x), ll.append(g.get_lnlikelihood_fullmarg(x))
+    chain, bhist, w_in, w_out, e_out = [], [], [], [], []
+    xnew = x0.copy()
+    with Capture() as cap:
+        np.random.seed(43)
+        for ii in range(nsweep):
+            chain.append(xnew.copy())
+            bhist.append(g._b.copy())
+            if ii == 0:
+                g._b = g.update_b(x0)
+            g.TNT = g.d = None
+            w_in.append(xnew.copy())
+            xnew = g.update_white_params(xnew, iters=None)
+            w_out.append(xnew.copy())
+            xnew = g.update_ecorr_params(xnew, iters=None)
+            e_out.append(xnew.copy())
+            xnew = g.update_gwrho_params(xnew)
+            if np.all(xnew != chain[ii][-1]):
+                g._b = g.update_b(xnew)
+    log = cap.log
+    sig = pta.signals["J1713+0747_basis_ecorr"]
+    wn = pta.models[0].white[0]
+    np.savez_compressed(out, x0=x0, chain=np.stack(chain), bhist=np.stack(bhist), b_final=g._b,
+                        w_in=np.stack(w_in), w_out=np.stack(w_out), e_out=np.stack(e_out),
+                        kinds=np.array([k for k, _ in log]),
+                        vals=np.concatenate([np.atleast_1d(v).ravel() for _, v in log]),
+                        lens=np.array([np.atleast_1d(v).size for _, v in log]),
+                        T=pta.get_basis()[0], r=pta.get_residuals()[0], sigma=wn.sigma, backends=wn.backends,
+                        epoch_backend=sig.epoch_backend, eind=eind, wind=wind, ecid=np.asarray(g.ecid),
+                        aclength_white=acl_w, aclength_ecorr=acl_e, gwid=np.asarray(g.gwid),
+                        rhomin=g.rhomin, rhomax=g.rhomax, param_names=np.array(g.param_names),
+                        x_like=np.stack(xl), lnlike=np.array(ll),
+                        pmin=np.array([p.pmin for p in g.params for _ in range(p.size or 1)]),
+                        pmax=np.array([p.pmax for p in g.params for _ in range(p.size or 1)]))
+    print("ecorr+white:", out, len(log))
+
+
 def main(root):
     mods = load_reference(root)
     PB = mods["pulsar_gibbs"]
     PT = mods["pta_gibbs"]
+    if "--only-ecorr-white" in sys.argv:
+        ecorr_white_mh(PB, os.path.join(HERE, "ecorr_white_j1713.npz"))
+        return
     if "--only-ecorr" in sys.argv:
         ecorr_mh(PB, os.path.join(HERE, "ecorr_mh_j1713.npz"))
         if "--long" in sys.argv:
@@ -455,6 +513,7 @@ def main(root):
     white_mh(PB, os.path.join(HERE, "white_mh_j1713.npz"))
     red_likelihood(PB, os.path.join(HERE, "red_lnlike_j1713.npz"))
     ecorr_mh(PB, os.path.join(HERE, "ecorr_mh_j1713.npz"))
+    ecorr_white_mh(PB, os.path.join(HERE, "ecorr_white_j1713.npz"))
     if "--long" in sys.argv:
         single_pulsar_long(PB, os.path.join(HERE, "long_j1713.npz"))
         ecorr_long(PB, os.path.join(HERE, "ecorr_long_j1713.npz"))

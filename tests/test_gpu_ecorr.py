@@ -198,3 +198,125 @@ def test_pulsar_block_gibbs_ecorr_surface(ctx, tmp_path):
     assert chain.shape == (12, len(g["param_names"])) and np.isfinite(chain).all()
     assert gb.chains.shape[0] == 64 and 1 <= gb.aclength_ecorr < 1000
     assert np.load(tmp_path / "chain.npy").shape[0] == 11
+
+
+# ----------------------------------------------------------------- white noise + ECORR
+def _white_setup(ctx, g, C):
+    from pulsar_timing_gibbsspec_amd.ecorr import EcorrModel
+    from pulsar_timing_gibbsspec_amd.white import WhiteNoiseModel
+    names = list(g["param_names"])
+    wind, eind = list(np.asarray(g["wind"])), np.asarray(g["eind"])
+    wl = []
+    for j in wind:
+        k = int(names[j].split("_b")[1].split("_")[0])
+        kind = 0 if names[j].endswith("efac") else 1
+        wl.append((int(j), kind, k, float(g["pmin"][j]), float(g["pmax"][j])))
+    T, gwid = g["T"], np.asarray(g["gwid"])
+    m = T.shape[1]
+    wm = WhiteNoiseModel(ctx, [T], [g["r"]], [g["sigma"]], [g["backends"]], [gwid], [np.full(m - gwid.size, 1e-40)],
+                         [wl], C, prefix=False)
+    em = EcorrModel(ctx, T, g["sigma"] ** 2, g["r"], g["ecid"], g["epoch_backend"], gwid, eind, g["pmin"][eind],
+                    g["pmax"][eind], len(names), C, per_chain=True)
+    return wm, em, wind, eind
+
+
+def _white_N(g, x):
+    names = list(g["param_names"])
+    bk = np.asarray(g["backends"])
+    nb = int(bk.max()) + 1
+    ef = np.array([x[names.index(f"J1713+0747_b{k}_efac")] for k in range(nb)])
+    eq = np.array([10.0 ** (2.0 * float(x[names.index(f"J1713+0747_b{k}_log10_tnequad")])) for k in range(nb)])
+    return ef[bk] ** 2 * g["sigma"] ** 2 + eq[bk]
+
+
+def test_ecorr_white_lnlike_matches_reference(ctx):
+    """Per-chain N (white parameters vary): gs_white_tnt -> gs_ecorr_gather -> likelihood-mode
+    gs_ecorr_prefix against the reference's get_lnlikelihood_fullmarg at prior draws."""
+    import torch
+    g = golden("ecorr_white_j1713.npz")
+    X = g["x_like"]
+    C = X.shape[0]
+    wm, em, _, _ = _white_setup(ctx, g, C)
+    x = _dev(X)
+    wm.tnt(x, x.shape[1])
+    em.gather(wm.TNT, wm.d, wm.tnt_cstride, wm.d_cstride)
+    r = g["r"]
+    const = []
+    for xx in X:
+        N = _white_N(g, xx)
+        const.append(-0.5 * (np.sum(np.log(N)) + np.sum(r ** 2 / N)) + 0.5 * em.nm * np.log(1e-40))
+    got = em.lnlike(x, _dev(_phiinv_F(g, X)), lnl_const=torch.as_tensor(const, device="cuda")).cpu().numpy()
+    assert np.abs(got - g["lnlike"]).max() < 1e-7, (got, g["lnlike"])
+
+
+def test_ecorr_white_blocks_match_reference(ctx):
+    """Sweeps 1.. of the reference's white + ECORR run, one chain per sweep, fed the reference's
+    MH draws: the white block (on y = r - T b with the sweep's b) and then the ECORR block (on
+    the chain's new N) reproduce the reference's outputs bit for bit."""
+    import torch
+    g = golden("ecorr_white_j1713.npz")
+    wind, eind = list(np.asarray(g["wind"])), list(np.asarray(g["eind"]))
+    aw, ae = int(g["aclength_white"]), int(g["aclength_ecorr"])
+    n = g["w_in"].shape[0]
+    items = iter(_items(g))
+    iw = np.zeros((aw, n, 4))
+    ie = np.zeros((ae, n, 4))
+    for ii in range(n):
+        if ii == 0:
+            assert next(items)[0] == "randn"
+        for s in range(aw):
+            (k1, sc), (k2, p), (k3, z), (k4, u) = next(items), next(items), next(items), next(items)
+            assert (k1, k2, k3, k4) == ("choice", "choice", "randn", "rand")
+            iw[s, ii] = (sc[0], wind.index(int(p[0])), z[0], u[0])
+        for s in range(ae):
+            (k1, sc), (k2, p), (k3, z), (k4, u) = next(items), next(items), next(items), next(items)
+            assert (k1, k2, k3, k4) == ("choice", "choice", "randn", "rand")
+            ie[s, ii] = (sc[0], eind.index(int(p[0])), z[0], u[0])
+        assert next(items)[0] == "uniform"
+        assert next(items)[0] == "randn"
+    sel = np.arange(1, n)          # sweep 0's white block used the unrecorded first b
+    C = sel.size
+    wm, em, _, _ = _white_setup(ctx, g, C)
+    x = _dev(g["w_in"][sel])
+    b = _dev(g["bhist"][sel])
+    wm.resid(b)
+    wm.mh(x, x.shape[1], aw, 0, inj=_dev(iw[:, sel]))
+    assert np.array_equal(x.cpu().numpy(), g["w_out"][sel])
+    wm.tnt(x, x.shape[1])
+    em.gather(wm.TNT, wm.d, wm.tnt_cstride, wm.d_cstride)
+    em.mh(x, _dev(_phiinv_F(g, g["w_out"][sel])), ae, inj=_dev(ie[:, sel]))
+    assert np.array_equal(x.cpu().numpy(), g["e_out"][sel])
+
+
+def test_ecorr_white_sampler_runs(ctx):
+    """Philox sampler with both blocks, 256 chains: finite chains, both blocks accept, and
+    the per-chain b draw is the exact conditional mean at zero normals."""
+    import torch
+    from pulsar_timing_gibbsspec_amd.ecorr import EcorrWhiteChains
+    g = golden("ecorr_white_j1713.npz")
+    C = 256
+    wm, em, _, _ = _white_setup(ctx, g, C)
+    run = EcorrWhiteChains(wm, em, _gwind(g), g["gwid"], float(g["rhomin"]), float(g["rhomax"]), g["x0"], 10, 10)
+    x_rec = torch.empty(12, C, len(g["param_names"]), dtype=torch.float64, device="cuda")
+    for ii in range(12):
+        run.sweep(x_rec=x_rec[ii])
+    X = x_rec.cpu().numpy()
+    assert np.isfinite(X).all() and np.isfinite(run.b.cpu().numpy()).all()
+    assert run.n_acc_white.min().item() > 0 and run.n_acc_ecorr.min().item() > 0
+    assert int(em.pinfo.abs().max()) == 0 and int(em.binfo.abs().max()) == 0
+    # exact conditional mean at chain 0's state (zero normals)
+    x0 = run.x[:1].expand(C, -1).contiguous()
+    run.x.copy_(x0)
+    run._operands()
+    run._phiinv(False)
+    bz = torch.zeros(C, em.m, dtype=torch.float64, device="cuda")
+    em.bdraw(run.x, run.phiinv_F, bz, z=torch.zeros(C, em.m, dtype=torch.float64, device="cuda"))
+    xx = run.x[0].cpu().numpy()
+    N = _white_N(g, xx)
+    TNT, d = O.tnt(g["T"], N, g["r"])
+    m = em.m
+    ph = np.full(m, 1e40)
+    ph[np.asarray(g["ecid"])] = np.array([10.0 ** (2 * float(xx[e])) for e in g["eind"]])[g["epoch_backend"]]
+    ph[np.asarray(g["gwid"])] = np.repeat(10.0 ** (2 * xx[_gwind(g)]), 2)
+    ref = np.linalg.solve(TNT + np.diag(1.0 / ph), d)
+    assert normwise_rel(bz[0].cpu().numpy(), ref) < 1e-8
