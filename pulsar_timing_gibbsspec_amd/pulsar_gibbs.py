@@ -38,7 +38,7 @@ import torch
 
 from . import _lib
 from .diagnostics import white_aclength
-from .ecorr import EcorrFreeSpectrumChains, EcorrModel
+from .ecorr import EcorrFreeSpectrumChains, EcorrModel, EcorrWhiteChains
 from .engine import DeviceModel, FreeSpectrumChains, HistoryStreamer, grid3
 from .rednoise import (DE_BUFFER, RED_STEPS, RedJumps, RedNoiseChains, powerlaw_loglinear,
                        warmup as red_warmup)
@@ -213,7 +213,8 @@ class PulsarBlockGibbs(object):
             em = self._ecorr_model1(xs)
             x = torch.as_tensor(np.asarray(xs, float)[None, :], device=self.ctx.device).contiguous()
             ph = torch.as_tensor(np.ascontiguousarray(self._ecorr_phiinv_F(xs))[None], device=self.ctx.device)
-            return float(em.lnlike(x, ph)[0])
+            const = self._ecorr_lnl_const(xs) if self._ecorr_white() else None
+            return float(em.lnlike(x, ph, lnl_const=const)[0])
         model = self._model(xs)
         ph = torch.as_tensor(np.ascontiguousarray(self._phiinv_F(xs))[None], device=self.ctx.device)
         lnl, info = model.lnlike_marg(ph, 1)
@@ -227,7 +228,11 @@ class PulsarBlockGibbs(object):
     # ------------------------------------------------------------ basis ECORR (8f-4)
     def _ecorr_loop(self):
         extra = [n for n in self.param_names if "rho" not in n]
-        return self.ecid is not None and bool(extra) and all("ecorr" in n for n in extra)
+        return (self.ecid is not None and any("ecorr" in n for n in extra)
+                and all(("ecorr" in n or "efac" in n or "equad" in n) for n in extra))
+
+    def _ecorr_white(self):
+        return self.ecid is not None and self.get_efacequad_indices().size > 0
 
     def _ecorr_structure(self, xs):
         """(eind, epoch_backend, emin, emax) through the PTA contract: the ECORR columns
@@ -257,7 +262,7 @@ class PulsarBlockGibbs(object):
         emax = np.array([bounds[j][1] for j in eind])
         return eind, ebk, emin, emax
 
-    def _ecorr_model(self, xs, n_chain):
+    def _ecorr_model(self, xs, n_chain, per_chain=False):
         params = self.map_params(xs)
         T = self.pta.get_basis(params)[0]
         Nvec = self.pta.get_ndiag(params)[0]
@@ -265,12 +270,29 @@ class PulsarBlockGibbs(object):
         eind, ebk, emin, emax = self._ecorr_structure(xs)
         fixed = np.setdiff1d(np.arange(T.shape[1]), np.concatenate([self.ecid, self.gwid]))
         return EcorrModel(self.ctx, T, Nvec, self._residuals, self.ecid, ebk, self.gwid, eind, emin, emax,
-                          len(xs), n_chain, phiinv_fixed=phiinv[fixed])
+                          len(xs), n_chain, phiinv_fixed=phiinv[fixed], per_chain=per_chain)
 
     def _ecorr_model1(self, xs):
+        """The 1-chain ECORR model; with white noise sampled its operands are rebuilt from
+        the TNT of xs's N on every call (the reference's TNT reset + recompute)."""
         if getattr(self, "_em1", None) is None:
-            self._em1 = self._ecorr_model(xs, 1)
+            self._em1 = self._ecorr_model(xs, 1, per_chain=self._ecorr_white())
+            if self._ecorr_white():
+                self._wm1e = self._white_model(xs, 1)
+        if self._ecorr_white():
+            x = torch.as_tensor(np.asarray(xs, float)[None, :], device=self.ctx.device).contiguous()
+            self._wm1e.tnt(x, x.shape[1])
+            self._em1.gather(self._wm1e.TNT, self._wm1e.d, self._wm1e.tnt_cstride, self._wm1e.d_cstride)
         return self._em1
+
+    def _ecorr_lnl_const(self, xs):
+        """-1/2 (sum log N + r^T N^-1 r) + 1/2 sum_M log phiinv_M at xs's white noise."""
+        params = self.map_params(xs)
+        N = self.pta.get_ndiag(params)[0]
+        phiinv = self.pta.get_phiinv(params, logdet=False)[0]
+        fixed = np.setdiff1d(np.arange(phiinv.size), np.concatenate([self.ecid, self.gwid]))
+        r = self._residuals
+        return float(-0.5 * (np.sum(np.log(N)) + np.sum(r ** 2 / N)) + 0.5 * np.sum(np.log(phiinv[fixed])))
 
     def _ecorr_phiinv_F(self, xs):
         return self.pta.get_phiinv(self.map_params(xs), logdet=False)[0][self.gwid]
@@ -360,8 +382,10 @@ class PulsarBlockGibbs(object):
         mask = np.ones(T.shape[1], bool)
         mask[self.gwid] = False
         self._phfix = phiinv[mask].copy()
+        # with basis ECORR the per-chain Schur systems are factored by ecorr.EcorrModel: the
+        # white model only supplies TNT_c / d_c, residuals and the white MH (prefix=False)
         return WhiteNoiseModel(self.ctx, [T], [self._residuals], [np.sqrt(sigma2)], [bk], [self.gwid],
-                               [phiinv[mask]], [wl], n_chain)
+                               [phiinv[mask]], [wl], n_chain, prefix=self.ecid is None)
 
     def update_white_params(self, xs, iters=None, inj=None):
         """White-noise Metropolis block (pulsar_gibbs.py:332-406) on the GPU: with
@@ -747,7 +771,8 @@ class PulsarBlockGibbs(object):
         launch sequence per sweep for all chains (ecorr.EcorrFreeSpectrumChains)."""
         nc = self.nchains
         dev = self.ctx.device
-        em = self._ecorr_model(xs, nc)
+        white = self._ecorr_white()
+        em = self._ecorr_model(xs, nc, per_chain=white)
         m, n_param = em.m, len(xs)
         self.chain = np.zeros((niter, n_param))
         self.bchain = np.zeros((niter, len(self._b)))
@@ -762,8 +787,22 @@ class PulsarBlockGibbs(object):
             start = min(c0.shape[0], b0.shape[0])
             self.chain[:start] = c0[:start]
             self.bchain[:start] = b0[:start]
-        runner = EcorrFreeSpectrumChains(em, self.get_gwrho_param_indices(), self.gwid, self.rhomin, self.rhomax,
-                                         x0, aclength=getattr(self, "aclength_ecorr", None))
+        if white:
+            # both warm-ups (update_white_params / update_ecorr_params iters=1000, notebook
+            # sample() at ii == 0) run once on the 1-chain device models from xs to set the
+            # step counts; every chain then starts from their final state
+            if getattr(self, "aclength_white", None) is None or getattr(self, "aclength_ecorr", None) is None:
+                if not np.any(self._b):
+                    self._b = self.update_b(x0)
+                x0 = self.update_white_params(x0, iters=1000)
+                x0 = self.update_ecorr_params(x0, iters=1000)
+            runner = EcorrWhiteChains(self._white_model(xs, nc), em, self.get_gwrho_param_indices(), self.gwid,
+                                      self.rhomin, self.rhomax, x0, self.aclength_white, self.aclength_ecorr)
+            runner.aclength = self.aclength_ecorr
+            runner.short_chain = None
+        else:
+            runner = EcorrFreeSpectrumChains(em, self.get_gwrho_param_indices(), self.gwid, self.rhomin,
+                                             self.rhomax, x0, aclength=getattr(self, "aclength_ecorr", None))
         if start > 0:
             if runner.aclength is None:
                 raise NotImplementedError("resume of an ECORR run needs aclength_ecorr")

@@ -320,3 +320,40 @@ def test_ecorr_white_sampler_runs(ctx):
     ph[np.asarray(g["gwid"])] = np.repeat(10.0 ** (2 * xx[_gwind(g)]), 2)
     ref = np.linalg.solve(TNT + np.diag(1.0 / ph), d)
     assert normwise_rel(bz[0].cpu().numpy(), ref) < 1e-8
+
+
+def test_pulsar_block_gibbs_ecorr_white_surface(ctx, tmp_path):
+    """PulsarBlockGibbs with white noise and ECORR sampled: get_lnlikelihood at prior draws of
+    every parameter (white included) against the reference, update_white_params followed by
+    update_ecorr_params on the reference's sweep-1 draws, and a short multi-chain sample()."""
+    from pulsar_timing_gibbsspec_amd import synthetic
+    from pulsar_timing_gibbsspec_amd.pulsar_gibbs import PulsarBlockGibbs
+    g = golden("ecorr_white_j1713.npz")
+    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=0, white_vary=True)
+    gb = PulsarBlockGibbs(pta, nchains=32, seed=5)
+    for x, ref in zip(g["x_like"], g["lnlike"]):
+        assert abs(gb.get_lnlikelihood(x) - ref) < 1e-7
+    wind, eind = list(np.asarray(g["wind"])), list(np.asarray(g["eind"]))
+    aw, ae = int(g["aclength_white"]), int(g["aclength_ecorr"])
+    items = iter(_items(g))
+    assert next(items)[0] == "randn"
+    for _ in range(aw + ae):          # sweep 0
+        next(items), next(items), next(items), next(items)
+    next(items), next(items)
+    iw, ie = [], []
+    for _ in range(aw):
+        (_, sc), (_, p), (_, z), (_, u) = next(items), next(items), next(items), next(items)
+        iw.append((sc[0], wind.index(int(p[0])), z[0], u[0]))
+    for _ in range(ae):
+        (_, sc), (_, p), (_, z), (_, u) = next(items), next(items), next(items), next(items)
+        ie.append((sc[0], eind.index(int(p[0])), z[0], u[0]))
+    gb.aclength_white, gb.aclength_ecorr = aw, ae
+    gb._b = g["bhist"][1]
+    xw = gb.update_white_params(g["w_in"][1], inj=np.array(iw))
+    assert np.array_equal(xw, g["w_out"][1])
+    assert np.array_equal(gb.update_ecorr_params(xw, inj=np.array(ie)), g["e_out"][1])
+    del gb.aclength_white, gb.aclength_ecorr
+    gb._b = np.zeros_like(gb._b)
+    chain = gb.sample(g["x0"], outdir=str(tmp_path), niter=8, save_every=4)
+    assert chain.shape == (8, len(g["param_names"])) and np.isfinite(chain).all()
+    assert gb.chains.shape[0] == 32 and gb.aclength_white >= 1 and gb.aclength_ecorr >= 1
