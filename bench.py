@@ -388,6 +388,59 @@ def _ecorr_traffic(C):
     return d.get("bytes_per_launch") if d.get("chains") == C else None
 
 
+def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
+    """SURVEY 8f-4 with white noise sampled too (the notebook's J1713 configuration): per sweep
+    white MH (aclength steps) -> per-chain TNT (gs_white_tnt) -> per-chain ECORR operands ->
+    ECORR MH (aclength steps) -> rho|b -> gated b, C chains per GPU."""
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd.ecorr import EcorrWhiteChains, white_ecorr_models
+    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=0, white_vary=True)
+    names = pta.param_names
+    sig = pta.signals["J1713+0747_basis_ecorr"]
+    wn = pta.models[0].white[0]
+    ebk = sig.epoch_backend
+    ne = ebk.size
+    eind = [i for i, n in enumerate(names) if "ecorr" in n]
+    wind = [i for i, n in enumerate(names) if "efac" in n or "equad" in n]
+    gw = [i for i, n in enumerate(names) if "rho" in n]
+    T = pta.get_basis()[0]
+    m = T.shape[1]
+    gwid = ne + np.arange(2 * len(gw))
+    wl = [(j, 0 if names[j].endswith("efac") else 1, int(names[j].split("_b")[1].split("_")[0]),
+           0.1 if names[j].endswith("efac") else -8.5, 5.0 if names[j].endswith("efac") else -5.0) for j in wind]
+    ctx = _lib.Context(dev.index, seed=20251018)
+    wm, wmR, em = white_ecorr_models(ctx, T, pta.get_residuals()[0], wn.sigma, wn.backends, gwid, wl, np.arange(ne),
+                                     ebk, eind, [-8.5] * len(eind), [-5.0] * len(eind), len(names), C)
+    rng = np.random.default_rng(100 + rank)
+    x0 = np.empty((C, len(names)))
+    x0[:, wind] = [1.0 if names[j].endswith("efac") else -7.0 for j in wind]
+    x0[:, eind] = -6.3
+    x0[:, gw] = rng.uniform(-9, -4, (C, len(gw)))
+    eng = EcorrWhiteChains(wm, em, gw, gwid, 1e-18, 1e-8, x0, aclength, aclength, chain_base=rank * C, wmR=wmR)
+    for _ in range(W):
+        eng.sweep()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        eng.sweep()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if int(em.binfo.abs().sum()) or int(em.pinfo.abs().sum()):
+        raise RuntimeError("non-PD system in the white + ECORR bench")
+    return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+                chains_per_gpu=C, m=m, n_epoch=ne, aclength_white=aclength, aclength_ecorr=aclength,
+                config="SURVEY 8f-4 with EFAC/EQUAD sampled: J1713-like pulsar, 2 backends, 136 ECORR epochs, "
+                       "white MH + per-chain TNT + ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
+
+
 def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
     """single pulsar with basis ECORR (J1713-like, 2 backends, 136 epochs,
     m = 212), C chains per GPU, aclength ECORR MH steps per sweep (each a batched
@@ -607,6 +660,10 @@ def main():
             if not args.no_cpu_baseline and world == 1:
                 sec["cpu_baseline"] = ecorr_cpu_baseline(args.cpu_seconds)
             out.setdefault("secondary", {})["ecorr"] = sec
+        sec = bench_ecorr_white(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev)
+        if rank == 0:
+            sec["sharding"] = "chains, weak"
+            out["secondary"]["ecorr_white"] = sec
     if args.config5:
         sec = bench_config5(args.c5_chains, args.c5_steps, 1, rank, world, dev)
         if rank == 0:

@@ -437,6 +437,19 @@ int gs_ecorr_prefix(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, i
  * phm [16] = phiinv of the fixed-prior columns (added on the Ap diagonal of the first 16).
  * Pass the per-chain strides (ne kb, ne, kb kb) to gs_ecorr_prefix / gs_ecorr_bdraw_e.
  */
+/*
+ * gs_ecorr_epoch_sums: the per-chain [B | d_E] rows and epoch diagonal straight from the TOAs
+ * (white noise sampled): Bx [c][e][j] = sum_{q in eptr[e]..eptr[e+1]} eu[q] T[etoa[q]][colmap[j]]
+ * / N_c, column dcol = sum eu r / N_c, Dg [c][e] = sum eu^2 / N_c, N_c from chain c's white
+ * parameters in x (the gs_white_mh / gs_white_tnt tables of one pulsar; T row-major
+ * n_toa x m, TOAs in the order of sigma2 / bk / r).  With the epoch columns of T being
+ * quantisation indicators this equals TNT[ecid[e], colmap[j]] of the full SYRK.
+ */
+int gs_ecorr_epoch_sums(gs_ctx* ctx, int n_chain, const gs_white_desc* wdesc, const int32_t* wcol,
+                        const int32_t* wkind, const int32_t* wbk, const double* x, int ldx, const double* T, int m,
+                        const double* sigma2, const int32_t* bk, const double* r, int ne, int kb, int dcol,
+                        const int32_t* colmap, const int32_t* eptr, const int32_t* etoa, const double* eu,
+                        double* Bx, double* Dg);
 int gs_ecorr_gather(gs_ctx* ctx, int n_chain, int m, int ne, int kb, const int32_t* ecid, const int32_t* colmap,
                     const double* phm, const double* TNT, int64_t tnt_cstride, const double* d,
                     int64_t d_cstride, double* Bx, double* Dg, double* Ap);

@@ -72,6 +72,8 @@ SIGNATURES = {
     "gs_ecorr_schur": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P]),
     "gs_ecorr_prefix": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P,
                              _I64, _I64, _I64]),
+    "gs_ecorr_epoch_sums": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P,
+                                 _P, _P]),
     "gs_ecorr_gather": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P]),
     "gs_ecorr_propose": (_I, [_P, _I, _I, _P, _P, _P, _P, _I, _I, _P, _I, _I64, _I64, _P, _P]),
     "gs_ecorr_accept": (_I, [_P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P]),

@@ -800,6 +800,31 @@ int gs_ecorr_prefix(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, i
   return after_launch("k_ecorr_prefix");
 }
 
+int gs_ecorr_epoch_sums(gs_ctx* ctx, int n_chain, const gs_white_desc* wdesc, const int32_t* wcol,
+                        const int32_t* wkind, const int32_t* wbk, const double* x, int ldx, const double* T, int m,
+                        const double* sigma2, const int32_t* bk, const double* r, int ne, int kb, int dcol,
+                        const int32_t* colmap, const int32_t* eptr, const int32_t* etoa, const double* eu,
+                        double* Bx, double* Dg) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_chain < 0) return fail_arg(2, "n_chain < 0");
+  if (!wdesc || !wcol || !wkind || !wbk) return fail_arg(3, "NULL white tables");
+  if (!x || ldx <= 0) return fail_arg(7, "x / ldx");
+  if (!T || m <= 0) return fail_arg(9, "T / m");
+  if (!sigma2 || !bk || !r) return fail_arg(11, "NULL sigma2 / bk / r");
+  if (ne < 0 || kb <= 0 || dcol < 0 || dcol >= kb) return fail_arg(14, "ne / kb / dcol");
+  if (!colmap || !eptr || !etoa || !eu) return fail_arg(17, "NULL colmap / epoch lists");
+  if (!Bx || !Dg) return fail_arg(21, "NULL Bx / Dg");
+  if (n_chain == 0 || ne == 0) return 0;
+  EcorrSumArgs a = {};
+  a.w.n_psr = 1; a.w.n_chain = n_chain; a.w.m_max = m; a.w.ldx = ldx; a.w.x_per_sys = 0;
+  a.w.wdesc = wdesc; a.w.wcol = wcol; a.w.wkind = wkind; a.w.wbk = wbk; a.w.bk = bk;
+  a.w.T = T; a.w.sigma2 = sigma2; a.w.r = r; a.w.x = x;
+  a.n_chain = n_chain; a.ne = ne; a.kb = kb; a.dcol = dcol;
+  a.colmap = colmap; a.eptr = eptr; a.etoa = etoa; a.eu = eu; a.Bx = Bx; a.Dg = Dg;
+  launch_ecorr_epoch_sums(ctx->stream, a);
+  return after_launch("k_ecorr_epoch_sums");
+}
+
 int gs_ecorr_gather(gs_ctx* ctx, int n_chain, int m, int ne, int kb, const int32_t* ecid, const int32_t* colmap,
                     const double* phm, const double* TNT, int64_t tnt_cstride, const double* d,
                     int64_t d_cstride, double* Bx, double* Dg, double* Ap) {

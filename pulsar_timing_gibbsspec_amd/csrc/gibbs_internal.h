@@ -152,6 +152,16 @@ struct WhiteTntArgs {
 
 int launch_white_mh(hipStream_t s, const WhiteMhArgs& a);
 
+// ECORR operands with white noise sampled: epoch segment sums (gibbs_white.hip)
+struct EcorrSumArgs {
+  WhiteTntArgs w;  // white tables, x, T (row-major n_toa x m), sigma2, bk, r of pulsar 0
+  int n_chain, ne, kb, dcol;
+  const int32_t *colmap, *eptr, *etoa;
+  const double* eu;
+  double *Bx, *Dg;
+};
+int launch_ecorr_epoch_sums(hipStream_t s, const EcorrSumArgs& a);
+
 // power-law red-noise Metropolis block (gibbs_red.hip)
 struct RedMhArgs {
   int n_chain, n_f, ldx, nsteps, anchor, nde;

@@ -194,6 +194,16 @@ class EcorrModel:
                                            ptr(self.colmap), ptr(self.phm), ptr(TNT), tnt_cstride, ptr(d),
                                            d_cstride, ptr(self.Bp), ptr(self.Dg), ptr(self.Ap)), "gs_ecorr_gather")
 
+    def gather_R(self, TNT_R, d_R, tnt_cstride, d_cstride):
+        """Per-chain Ap from the per-chain TNT / d of the R columns only (rc order)."""
+        if not hasattr(self, "colmap_R"):
+            cm = self.jmap.clone()
+            cm[self.dcol] = -2
+            self.colmap_R = cm.contiguous()
+        check(self.ctx.lib.gs_ecorr_gather(self.ctx.handle, self.C, self.mR, 0, self.ldbp, ptr(self.ecid),
+                                           ptr(self.colmap_R), ptr(self.phm), ptr(TNT_R), tnt_cstride, ptr(d_R),
+                                           d_cstride, ptr(self.Bp), ptr(self.Dg), ptr(self.Ap)), "gs_ecorr_gather")
+
     def _eval(self, x, phiinv_F):
         """lnl / aux / info of every chain at x: one fused likelihood-mode launch when
         available (no model block), else factor + gs_lnlike_marg."""
@@ -365,10 +375,15 @@ class EcorrWhiteChains:
     """
 
     def __init__(self, wm, em: EcorrModel, gw_cols, gwid, rhomin, rhomax, x0, aclength_white,
-                 aclength_ecorr, chain_base=0):
+                 aclength_ecorr, chain_base=0, wmR=None):
         if not em.per_chain:
             raise ValueError("EcorrWhiteChains needs EcorrModel(per_chain=True)")
         self.wm, self.em, self.ctx = wm, em, em.ctx
+        # wmR (white.WhiteNoiseModel over the R columns only): TNT_RR by the batched SYRK and
+        # the epoch rows by segment sums (gs_ecorr_epoch_sums) instead of the full m x m SYRK
+        self.wmR = wmR
+        if wmR is not None:
+            self._epoch_lists()
         dev = self.ctx.device
         C = em.C
         gw = np.asarray(gw_cols, np.int64)
@@ -395,10 +410,35 @@ class EcorrWhiteChains:
                                               ptr(self.xlast) if with_gate else None, ptr(self.gw_cols), None,
                                               ptr(self.phiinv_F), ptr(self.gate)), "gs_pta_gate_phiinv")
 
+    def _epoch_lists(self):
+        """CSR lists (TOA, u) of every epoch column in wm's (backend-grouped) TOA order."""
+        wm, em, dev = self.wm, self.em, self.ctx.device
+        n, m = int(wm.n_toa[0]), em.m
+        Tp = wm.T[:n * m].view(n, m)
+        U = Tp[:, torch.as_tensor(em.ecid_host, device=dev)].cpu().numpy()
+        ptr_, toa, val = [0], [], []
+        for e in range(em.ne):
+            nz = np.nonzero(U[:, e])[0]
+            toa += list(nz)
+            val += list(U[nz, e])
+            ptr_.append(len(toa))
+        self.eptr = _t(np.asarray(ptr_, np.int32), torch.int32, dev)
+        self.etoa = _t(np.asarray(toa, np.int32), torch.int32, dev)
+        self.eu = _t(np.asarray(val, float), torch.float64, dev)
+
     def _operands(self):
         wm, em = self.wm, self.em
-        wm.tnt(self.x, em.n_param)
-        em.gather(wm.TNT, wm.d, wm.tnt_cstride, wm.d_cstride)
+        if self.wmR is None:
+            wm.tnt(self.x, em.n_param)
+            em.gather(wm.TNT, wm.d, wm.tnt_cstride, wm.d_cstride)
+            return
+        wmR = self.wmR
+        wmR.tnt(self.x, em.n_param)
+        em.gather_R(wmR.TNT, wmR.d, wmR.tnt_cstride, wmR.d_cstride)
+        check(self.ctx.lib.gs_ecorr_epoch_sums(
+            self.ctx.handle, em.C, ptr(wm.wdesc), ptr(wm.wcol), ptr(wm.wkind), ptr(wm.wbk), ptr(self.x), em.n_param,
+            ptr(wm.T), em.m, ptr(wm.sigma2), ptr(wm.bk), ptr(wm.r), em.ne, em.ldbp, em.dcol, ptr(em.colmap),
+            ptr(self.eptr), ptr(self.etoa), ptr(self.eu), ptr(em.Bp), ptr(em.Dg)), "gs_ecorr_epoch_sums")
 
     def sweep(self, x_rec=None, b_rec=None, z0=None, z=None, u=None, white_inj=None, ecorr_inj=None):
         em, wm, lib, h = self.em, self.wm, self.ctx.lib, self.ctx.handle
@@ -424,3 +464,24 @@ class EcorrWhiteChains:
         self._phiinv(True)
         em.bdraw(self.x, self.phiinv_F, self.b, z=z, sweep=ii, chain_base=self.chain_base, chain_mask=self.gate)
         self.it += 1
+
+
+def white_ecorr_models(ctx, T, r, sigma, backends, gwid, white_list, ecid, epoch_backend, ecol, emin, emax,
+                       n_param, n_chain, phiinv_fixed=1e-40):
+    """(wm, wmR, em) for EcorrWhiteChains: the white model over the full basis (residuals,
+    white MH), the white model over the R columns (TNT_RR), the per-chain ECORR model."""
+    from .white import WhiteNoiseModel
+    T = np.ascontiguousarray(T, float)
+    m = T.shape[1]
+    gwid = np.asarray(gwid)
+    rc = np.setdiff1d(np.arange(m), np.asarray(ecid))
+    pos = {c: i for i, c in enumerate(rc)}
+    nfix = m - gwid.size
+    wm = WhiteNoiseModel(ctx, [T], [r], [sigma], [backends], [gwid], [np.full(nfix, 1e-40)], [white_list],
+                         n_chain, prefix=False)
+    wmR = WhiteNoiseModel(ctx, [np.ascontiguousarray(T[:, rc])], [r], [sigma], [backends],
+                          [np.array([pos[c] for c in gwid])], [np.full(rc.size - gwid.size, 1e-40)], [white_list],
+                          n_chain, prefix=False)
+    em = EcorrModel(ctx, T, np.asarray(sigma, float) ** 2, r, ecid, epoch_backend, gwid, ecol, emin, emax, n_param,
+                    n_chain, phiinv_fixed=phiinv_fixed, per_chain=True)
+    return wm, wmR, em

@@ -374,10 +374,15 @@ class PulsarBlockGibbs(object):
             raise NotImplementedError("white-noise model is not efac/equad per backend")
         return N0, bk, wl
 
-    def _white_model(self, xs, n_chain):
+    def _white_model(self, xs, n_chain, cols=None):
         params = self.map_params(xs)
         sigma2, bk, wl = self._white_structure(xs)
         T = self.pta.get_basis(params)[0]
+        if cols is not None:   # the R columns of a basis-ECORR model (TNT_RR only)
+            pos = {c: i for i, c in enumerate(cols)}
+            return WhiteNoiseModel(self.ctx, [np.ascontiguousarray(T[:, cols])], [self._residuals],
+                                   [np.sqrt(sigma2)], [bk], [np.array([pos[c] for c in self.gwid])],
+                                   [np.full(len(cols) - len(self.gwid), 1e-40)], [wl], n_chain, prefix=False)
         phiinv = self.pta.get_phiinv(params, logdet=False)[0]
         mask = np.ones(T.shape[1], bool)
         mask[self.gwid] = False
@@ -797,7 +802,8 @@ class PulsarBlockGibbs(object):
                 x0 = self.update_white_params(x0, iters=1000)
                 x0 = self.update_ecorr_params(x0, iters=1000)
             runner = EcorrWhiteChains(self._white_model(xs, nc), em, self.get_gwrho_param_indices(), self.gwid,
-                                      self.rhomin, self.rhomax, x0, self.aclength_white, self.aclength_ecorr)
+                                      self.rhomin, self.rhomax, x0, self.aclength_white, self.aclength_ecorr,
+                                      wmR=self._white_model(xs, nc, cols=em.rc_host))
             runner.aclength = self.aclength_ecorr
             runner.short_chain = None
         else:

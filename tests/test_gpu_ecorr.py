@@ -288,6 +288,33 @@ def test_ecorr_white_blocks_match_reference(ctx):
     assert np.array_equal(x.cpu().numpy(), g["e_out"][sel])
 
 
+def test_ecorr_white_operand_routes_agree(ctx):
+    """Per-chain ECORR operands two ways: the full m x m SYRK (gs_white_tnt) + gs_ecorr_gather,
+    and the R-column SYRK + epoch segment sums (gs_ecorr_epoch_sums) -- equal to 1e-12."""
+    import torch
+    from pulsar_timing_gibbsspec_amd.ecorr import EcorrWhiteChains, white_ecorr_models
+    g = golden("ecorr_white_j1713.npz")
+    X = g["x_like"]
+    C = X.shape[0]
+    _, _, wind, eind = _white_setup(ctx, g, 1)
+    names = list(g["param_names"])
+    wl = [(int(j), 0 if names[j].endswith("efac") else 1, int(names[j].split("_b")[1].split("_")[0]),
+           float(g["pmin"][j]), float(g["pmax"][j])) for j in wind]
+    wm, wmR, em = white_ecorr_models(ctx, g["T"], g["r"], g["sigma"], g["backends"], g["gwid"], wl, g["ecid"],
+                                     g["epoch_backend"], eind, g["pmin"][eind], g["pmax"][eind], len(names), C)
+    run = EcorrWhiteChains(wm, em, _gwind(g), g["gwid"], float(g["rhomin"]), float(g["rhomax"]), X[0], 1, 1,
+                           wmR=wmR)
+    run.x.copy_(_dev(X))
+    run._operands()
+    A = [t.clone().cpu().numpy() for t in (em.Bp, em.Dg, em.Ap)]
+    run.wmR = None
+    run._operands()
+    B = [t.cpu().numpy() for t in (em.Bp, em.Dg, em.Ap)]
+    for a, b in zip(A, B):
+        a, b = a.reshape(C, -1), b.reshape(C, -1)
+        assert normwise_rel(a, b) < 1e-12, normwise_rel(a, b)
+
+
 def test_ecorr_white_sampler_runs(ctx):
     """Philox sampler with both blocks, 256 chains: finite chains, both blocks accept, and
     the per-chain b draw is the exact conditional mean at zero normals."""
