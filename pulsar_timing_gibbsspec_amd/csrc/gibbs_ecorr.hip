@@ -237,35 +237,54 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
     if (l < EC_CH) wb[buf][w][l] = wreg;
   };
   if constexpr (PC) {
-    // per-chain [B | d_E] (white noise sampled: TNT differs per chain): no LDS sharing,
-    // each wavefront streams its own rows; 1/a and the log sums by the c == 0 lanes
+    // per-chain [B | d_E] (white noise sampled: TNT differs per chain): no sharing across
+    // waves; each wavefront stages 16-epoch chunks of its own rows in its slice of the
+    // dynamic LDS (all of a chunk's loads in flight at once), 1/a by lanes 0..15
     if (!live) return;  // no workgroup barriers below
     const double* Bc = A.Bx + (int64_t)ch_id * A.bx_cs;
     const double* Dc = A.Dg + (int64_t)ch_id * A.dg_cs;
-#pragma unroll 2
-    for (int e0 = 0; e0 < ne; e0 += 4) {
-      const int e = e0 + q;
-      const bool ok = e < ne;
+    constexpr int PCH = 16;
+    constexpr int PL = PCH * LDB / 64;  // doubles per lane per chunk
+    double* buf = lds + (int64_t)w * (PCH * LDB + PCH);
+    double* wsl = buf + PCH * LDB;
+    for (int e0 = 0; e0 < ne; e0 += PCH) {
+      double rg[PL];
+#pragma unroll
+      for (int u = 0; u < PL; ++u) {
+        const int idx = l + 64 * u;
+        rg[u] = (e0 + idx / LDB < ne) ? Bc[(int64_t)e0 * LDB + idx] : 0.0;
+      }
       double wv = 0.0;
-      if (ok) {
+      if (l < PCH && e0 + l < ne) {
+        const int e = e0 + l;
         const int kb = A.ebk[e];
         const double a = Dc[e] + sinv[w][kb];
         wv = 1.0 / a;
-        if (c == 0) {
-          sla += log(a);
-          slp += slog[w][kb];
-        }
+        sla += log(a);
+        slp += slog[w][kb];
       }
-      double v[NB];
+      wave_lds_sync();  // previous chunk's LDS reads are done before the overwrite
 #pragma unroll
-      for (int r = 0; r < NB; ++r) v[r] = ok ? Bc[(int64_t)e * LDB + 16 * r + c] : 0.0;
+      for (int u = 0; u < PL; ++u) buf[l + 64 * u] = rg[u];
+      if (l < PCH) wsl[l] = wv;
+      wave_lds_sync();
+      const int nk = min(PCH / 4, (ne - e0 + 3) / 4);
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const double av = v[j] * wv;
+      for (int kk = 0; kk < PCH / 4; ++kk) {
+        if (kk >= nk) break;
+        const double* row = buf + (4 * kk + q) * LDB + c;
+        const double wk = wsl[4 * kk + q];
+        double v[NB];
 #pragma unroll
-        for (int r = j; r < NB; ++r) {
-          const int t = (j == 0) ? r : ts(j, r);
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, v[r], acc[t], 0, 0, 0);
+        for (int r = 0; r < NB; ++r) v[r] = row[16 * r];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const double av = v[j] * wk;
+#pragma unroll
+          for (int r = j; r < NB; ++r) {
+            const int t = (j == 0) ? r : ts(j, r);
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, v[r], acc[t], 0, 0, 0);
+          }
         }
       }
     }
@@ -602,8 +621,9 @@ void launch_schur_nb(hipStream_t s, const EcorrSchurArgs& a) {
 template <int NB, bool LNL, bool PC>
 void launch_prefix_nbp(hipStream_t s, const EcorrPrefixArgs& a) {
   static bool attr = false;
-  const size_t lds = PC ? 0 : (size_t)2 * EC_CH * 16 * NB * sizeof(double);
-  if (!attr && !PC) {
+  const size_t lds = PC ? (size_t)EC_WAVES * (16 * 16 * NB + 16) * sizeof(double)
+                        : (size_t)2 * EC_CH * 16 * NB * sizeof(double);
+  if (!attr) {
     (void)hipFuncSetAttribute((const void*)k_ecorr_prefix<NB, LNL, PC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     attr = true;
