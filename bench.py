@@ -331,6 +331,69 @@ def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, a
                                   "over the HIP-event time of one refresh (SYRK + prefix)"})
 
 
+def ecorr_white_cpu_baseline(seconds=10.0, aclength=10):
+    """The oracle's restatement of the white + ECORR sweep (notebook order: white MH on
+    get_lnlikelihood_white :523-546, TNT recomputed with the new N as the reference's reset
+    forces, ECORR MH on get_lnlikelihood_fullmarg, rho|b, SVD b draw), one chain, 1 thread."""
+    from oracle import gibbs_oracle as O
+    from pulsar_timing_gibbsspec_amd import synthetic
+    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=0, white_vary=True)
+    T, r = pta.get_basis()[0], pta.get_residuals()[0]
+    names = pta.param_names
+    wn = pta.models[0].white[0]
+    ebk = pta.signals["J1713+0747_basis_ecorr"].epoch_backend
+    eind = [i for i, n in enumerate(names) if "ecorr" in n]
+    ef_i = [i for i, n in enumerate(names) if n.endswith("efac")]
+    eq_i = [i for i, n in enumerate(names) if "equad" in n]
+    wind = sorted(ef_i + eq_i)
+    gw = np.array([i for i, n in enumerate(names) if "rho" in n])
+    m, ne = T.shape[1], ebk.size
+    gwid = ne + np.arange(2 * gw.size)
+    lo = np.array([0.1 if i in ef_i else -8.5 for i in range(len(names))])
+    hi = np.array([5.0 if i in ef_i else -5.0 for i in range(len(names))])
+    rng = np.random.default_rng(0)
+    x = np.zeros(len(names))
+    x[ef_i], x[eq_i], x[eind] = 1.0, -7.0, -6.3
+    x[gw] = rng.uniform(-9, -4, gw.size)
+
+    def N_of(xx):
+        return O.ndiag_white(wn.sigma, wn.backends, xx[ef_i], xx[eq_i])
+
+    def phi(xx):
+        ph = np.full(m, 1e40)
+        ph[:ne] = (10.0 ** (2.0 * xx[eind]))[ebk]
+        ph[gwid] = np.repeat(10.0 ** (2.0 * xx[gw]), 2)
+        return ph
+
+    def prior(ind):
+        return lambda xx: 0.0 if np.all((xx[ind] >= lo[ind]) & (xx[ind] <= hi[ind])) else -np.inf
+
+    def steps(ind):
+        return [(rng.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]), rng.choice(ind),
+                 rng.standard_normal(), rng.random()) for _ in range(aclength)]
+    TNT, dd = O.tnt(T, N_of(x), r)
+    b = O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m))
+    it, t0 = 0, time.perf_counter()
+    while True:
+        x = O.white_mh(x, wind, steps(wind), lambda xx: O.lnlike_white(r, T, b, N_of(xx)), prior(wind))
+        N = N_of(x)
+        TNT, dd = O.tnt(T, N, r)
+
+        def lnl(xx):
+            ph = phi(xx)
+            return O.lnlike_fullmarg(r, N, TNT, dd, 1.0 / ph, np.sum(np.log(ph)))
+        x = O.white_mh(x, eind, steps(eind), lnl, prior(eind))
+        x[gw] = 0.5 * np.log10(O.rho_analytic(O.tau_half(b, gwid), rng.random(gw.size), 1e-18, 1e-8))
+        b = O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m))
+        it += 1
+        el = time.perf_counter() - t0
+        if el > seconds:
+            break
+    return dict(value=it / el, unit="iters/s", cores=1, kind="port",
+                sample=f"{it} sweeps of the single-chain white + ECORR loop (m={m}, {ne} epochs, {aclength} white + "
+                       f"{aclength} ECORR MH steps, oracle restatement, numpy/LAPACK, 1 thread) in {el:.1f} s")
+
+
 def ecorr_cpu_baseline(seconds=10.0, aclength=10):
     """The oracle's restatement of the ECORR sweep (notebook order; update_ecorr_params
     :456-484 on get_lnlikelihood_fullmarg :569-610 with TNT recomputed each sweep as the
@@ -663,6 +726,8 @@ def main():
         sec = bench_ecorr_white(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev)
         if rank == 0:
             sec["sharding"] = "chains, weak"
+            if not args.no_cpu_baseline and world == 1:
+                sec["cpu_baseline"] = ecorr_white_cpu_baseline(args.cpu_seconds)
             out["secondary"]["ecorr_white"] = sec
     if args.config5:
         sec = bench_config5(args.c5_chains, args.c5_steps, 1, rank, world, dev)
