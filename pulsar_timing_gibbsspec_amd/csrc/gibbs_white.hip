@@ -9,6 +9,8 @@
 // changes one backend's term.  Each MH step therefore re-sums only that backend's
 // TOAs (n_toa / n_bk of the reference's full recompute, which also redoes T b every
 // step although b is fixed) and the acceptance uses dlnL = -(S_k' - S_k) / 2.
+#include <cstdlib>
+
 #include "gibbs_common.h"
 #include "gibbs_internal.h"
 
@@ -406,6 +408,132 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
   }
 }
 
+
+// Small-m batched SYRK (r-augmented block count NB <= 6: one pulsar's m <= 95): the paired-row
+// workgroup of k_white_syrk would leave 5 of its 8 waves idle, so instead 8 CHAINS of one
+// pulsar share each LDS chunk of [T | r] (32 TOAs x 16 NB) -- T is common to all chains, only
+// N differs -- and each wave accumulates its chain's NB (NB + 1) / 2 lower tiles with the
+// chain's 1/N_t (staged per wave from its white parameters).  grid (ceil(C / 8), n_psr).
+constexpr int MC_WAVES = 8, MC_CH = 32;
+template <int NB>
+__global__ __launch_bounds__(64 * MC_WAVES) void k_white_syrk_mc(WhiteTntArgs A) {
+  extern __shared__ double lds[];
+  __shared__ double wb[2][MC_WAVES][MC_CH];
+  __shared__ double sp[MC_WAVES][3][GS_WHITE_MAX_BK + 1];
+  constexpr int LDB = 16 * NB;
+  constexpr int NT = NB * (NB + 1) / 2;
+  constexpr int LPT = MC_CH * LDB / (64 * MC_WAVES);
+  const int tid = threadIdx.x, l = tid & 63, i = l & 15, k = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int p = blockIdx.y;
+  const int c = blockIdx.x * MC_WAVES + w;
+  const bool live = c < A.n_chain;
+  const gs_tnt_desc D = A.tdesc[p];
+  const gs_white_desc* W = A.wdesc + p;
+  const int m = (int)D.m;
+  const int64_t n = D.n_toa;
+  const int64_t sys = (int64_t)p * A.n_chain + (live ? c : 0);
+  // per-wave (efac^2, t2equad^2, tnequad^2) of every backend of the chain
+  if (l < W->n_bk) {
+    sp[w][0][l] = 1.0;
+    sp[w][1][l] = 0.0;
+    sp[w][2][l] = 0.0;
+  }
+  wave_lds_sync();
+  if (l < W->n_w && live) {
+    const int64_t o = W->w_off + l;
+    const int kb = A.wbk[o], kind = A.wkind[o];
+    double e = 1.0, t = 0.0, q = 0.0;
+    apply_white(kind, A.x[(A.x_per_sys ? sys : (int64_t)c) * A.ldx + A.wcol[o]], e, t, q);
+    if (kind == GS_WHITE_EFAC) sp[w][0][kb] = e;
+    else if (kind == GS_WHITE_TNEQUAD) sp[w][2][kb] = q;
+    else sp[w][1][kb] = t;
+  }
+  __syncthreads();
+  const double* Tp = A.T + D.T_off;
+  const double* rp = A.r + D.toa_off;
+  const double* s2 = A.sigma2 + D.toa_off;
+  const int32_t* bk = A.bk + D.toa_off;
+
+  gs_d4_t acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = gs_d4_t{0.0, 0.0, 0.0, 0.0};
+  double reg[LPT];
+  double wreg = 0.0;
+  auto load = [&](int64_t t0) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int idx = tid + 64 * MC_WAVES * u;
+      const int row = idx / LDB, col = idx % LDB;
+      const int64_t t = t0 + row;
+      double v = 0.0;
+      if (t < n) v = (col < m) ? Tp[t * m + col] : ((col == m) ? rp[t] : 0.0);
+      reg[u] = v;
+    }
+    wreg = 0.0;
+    if (l < MC_CH && live) {
+      const int64_t t = t0 + l;
+      if (t < n) {
+        const int kb = bk[t];
+        wreg = 1.0 / (sp[w][0][kb] * (s2[t] + sp[w][1][kb]) + sp[w][2][kb]);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    double* dst = lds + buf * (MC_CH * LDB);
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) dst[tid + 64 * MC_WAVES * u] = reg[u];
+    if (l < MC_CH) wb[buf][w][l] = wreg;
+  };
+  const int64_t nch = (n + MC_CH - 1) / MC_CH;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int64_t ch = 0; ch < nch; ++ch) {
+    const int cb = (int)(ch & 1);
+    if (ch + 1 < nch) load((ch + 1) * MC_CH);
+    __builtin_amdgcn_sched_barrier(0);
+    const double* cur = lds + cb * (MC_CH * LDB);
+    const int nk = (int)min((int64_t)(MC_CH / 4), (n - ch * MC_CH + 3) / 4);
+#pragma unroll
+    for (int kk = 0; kk < MC_CH / 4; ++kk) {
+      if (kk >= nk) break;
+      const double* row = cur + (4 * kk + k) * LDB + i;
+      const double wv = wb[cb][w][4 * kk + k];
+      double v[NB];
+#pragma unroll
+      for (int r = 0; r < NB; ++r) v[r] = row[16 * r];
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        const double av = v[r] * wv;
+#pragma unroll
+        for (int j = 0; j <= r; ++j)
+          acc[r * (r + 1) / 2 + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, v[j], acc[r * (r + 1) / 2 + j], 0, 0, 0);
+      }
+    }
+    if (ch + 1 < nch) store(cb ^ 1);
+    __syncthreads();
+  }
+  if (!live) return;
+  double* out = A.TNT + D.tnt_off + (int64_t)c * A.tnt_cstride;
+  double* dout = A.d + D.d_off + (int64_t)c * A.d_cstride;
+#pragma unroll
+  for (int r = 0; r < NB; ++r)
+#pragma unroll
+    for (int j = 0; j <= r; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * r + k + 4 * q, col = 16 * j + i;
+        const double v = acc[r * (r + 1) / 2 + j][q];
+        if (row < m && col <= row) {  // lower element only: exact symmetry
+          out[(int64_t)row * m + col] = v;
+          out[(int64_t)col * m + row] = v;
+        } else if (row == m && col < m) {
+          dout[col] = v;
+        }
+      }
+}
+
 // d_c = T^T (r / N_c): grid (n_sys, ceil(m_max / 64)).
 __global__ __launch_bounds__(256) void k_white_tnr(WhiteTntArgs A) {
   __shared__ double red[4][64];
@@ -500,11 +628,34 @@ static void launch_syrk(hipStream_t s, const WhiteTntArgs& a, int64_t n_sys) {
   hipLaunchKernelGGL(k_white_syrk<NB>, dim3((unsigned)(((n_sys + 7) / 8) * 8)), dim3(64 * SY_WAVES), lds, s, a);
 }
 
+template <int NB>
+static void launch_syrk_mc(hipStream_t s, const WhiteTntArgs& a) {
+  static bool attr = false;
+  const size_t lds = (size_t)2 * MC_CH * 16 * NB * sizeof(double);
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_white_syrk_mc<NB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_white_syrk_mc<NB>, dim3((unsigned)((a.n_chain + MC_WAVES - 1) / MC_WAVES), (unsigned)a.n_psr),
+                     dim3(64 * MC_WAVES), lds, s, a);
+}
+
 int launch_white_tnt(hipStream_t s, const WhiteTntArgs& a) {
   const int nb = (a.m_max + 15) / 16;
   const int64_t n_sys = (int64_t)a.n_psr * a.n_chain;
   // one-pass batched SYRK for m + 1 <= 256 (block count of the r-augmented T)
   const int nba = (a.m_max + 1 + 15) / 16;
+  if (nba <= 6 && !getenv("GS_SYRK_PAIRED")) {  // small m: chains share the T chunks
+    switch (nba) {
+      case 1: launch_syrk_mc<1>(s, a); break;
+      case 2: launch_syrk_mc<2>(s, a); break;
+      case 3: launch_syrk_mc<3>(s, a); break;
+      case 4: launch_syrk_mc<4>(s, a); break;
+      case 5: launch_syrk_mc<5>(s, a); break;
+      default: launch_syrk_mc<6>(s, a); break;
+    }
+    return 0;
+  }
   if (nba <= 16) {
     switch (nba) {
       case 1: launch_syrk<1>(s, a, n_sys); break;
