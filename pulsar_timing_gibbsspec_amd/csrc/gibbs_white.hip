@@ -190,6 +190,58 @@ __global__ __launch_bounds__(256) void k_white_resid(WhiteResidArgs A) {
     if (c0 + q < A.n_chain) A.y[(int64_t)(c0 + q) * A.ldy + D.toa_off + i] = r - acc[q];
 }
 
+
+typedef double gs_d4_t __attribute__((ext_vector_type(4)));
+
+// y = r - T b as an fp64 MFMA GEMM: Y (chains x TOAs) = B (chains x m) T^T, one wavefront per
+// 16 x 16 tile (16 chains of a pulsar x 16 TOAs), K = m in v_mfma_f64_16x16x4f64 steps: the A
+// operand is b[c0 + i][j0 + k] (lane i = l & 15, k = l >> 4), the B operand T[t0 + i][j0 + k]
+// from the column-major copy (16 consecutive TOAs per k: coalesced).  Output C layout: register
+// s of lane (i, k) is Y[c0 + 4 s + k][t0 + i].  grid (ceil(n_toa_max / 64), n_psr,
+// ceil(n_chain / 16)), 4 waves per workgroup (consecutive TOA tiles).
+__global__ __launch_bounds__(256) void k_white_resid_mfma(WhiteResidArgs A) {
+  const gs_tnt_desc D = A.tdesc[blockIdx.y];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, k = l >> 4;
+  const int64_t t0 = ((int64_t)blockIdx.x * 4 + w) * 16;
+  if (t0 >= D.n_toa) return;  // wave-uniform, no barriers
+  const int p = blockIdx.y;
+  const int c0 = blockIdx.z * 16;
+  const int m = (int)D.m;
+  const int64_t n = D.n_toa;
+  const double* Tt = A.Tt + D.T_off;
+  const int ca = min(c0 + i, A.n_chain - 1);
+  const double* brow = A.b + ((int64_t)p * A.n_chain + ca) * A.ldb;
+  const int64_t tb = min(t0 + i, n - 1);
+  gs_d4_t acc = {0.0, 0.0, 0.0, 0.0};
+  int j0 = 0;
+  for (; j0 + 16 <= m; j0 += 16) {  // 4 steps per iteration, loads issued together
+    double av[4], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + 4 * u + k;
+      av[u] = brow[j];
+      bv[u] = Tt[(int64_t)j * n + tb];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
+  }
+  for (; j0 < m; j0 += 4) {
+    const int j = j0 + k;
+    const double a = (j < m) ? brow[j] : 0.0;
+    const double b = (j < m) ? Tt[(int64_t)j * n + tb] : 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  const int64_t t = t0 + i;
+  if (t < n) {
+    const double r = A.r[D.toa_off + t];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = c0 + 4 * s + k;
+      if (c < A.n_chain) A.y[(int64_t)c * A.ldy + D.toa_off + t] = r - acc[s];
+    }
+  }
+}
+
 // Per-backend noise values of system (p, c) into LDS (whole workgroup).
 // xrow: the row of x holding this system's white parameters (chain c, or system
 // p * n_chain + c under GS_OPT_X_PER_SYS)
@@ -611,6 +663,11 @@ int launch_white_mh(hipStream_t s, const WhiteMhArgs& a) {
 }
 
 int launch_white_resid(hipStream_t s, const WhiteResidArgs& a) {
+  if (!getenv("GS_RESID_VALU")) {
+    dim3 g((unsigned)((a.n_toa_max + 63) / 64), (unsigned)a.n_psr, (unsigned)((a.n_chain + 15) / 16));
+    hipLaunchKernelGGL(k_white_resid_mfma, g, dim3(256), 0, s, a);
+    return 0;
+  }
   dim3 grid((unsigned)((a.n_toa_max + 255) / 256), (unsigned)a.n_psr,
             (unsigned)((a.n_chain + RES_CT - 1) / RES_CT));
   hipLaunchKernelGGL(k_white_resid, grid, dim3(256), 0, s, a);
