@@ -619,40 +619,63 @@ __global__ __launch_bounds__(256) void k_white_tnr(WhiteTntArgs A) {
 // ECORR operands with white noise sampled (gs_ecorr_epoch_sums): the epoch columns of T
 // are quantisation indicators, so TNT[e, j] = sum over epoch e's TOAs of u_t T[t, j] / N_t
 // -- a segmented sum of a few TOAs per epoch instead of the n_toa x m x m SYRK.  One
-// thread per (chain, epoch, reordered column); column dcol carries d_e = sum u_t r_t / N_t,
-// thread j = 0 also Dg[e] = sum u_t^2 / N_t.
+// workgroup per (16 epochs, chain): the group's u_t / N_t are computed once into LDS, then
+// one thread per (epoch, reordered column); column dcol carries d_e = sum u_t r_t / N_t,
+// j = 0 also Dg[e] = sum u_t^2 / N_t.
+constexpr int ES_EPB = 16;    // epochs per workgroup
+constexpr int ES_MAXQ = 256;  // TOA entries staged per workgroup (larger groups fall back)
 __global__ __launch_bounds__(256) void k_ecorr_epoch_sums(EcorrSumArgs A) {
   __shared__ double sb[3][GS_WHITE_MAX_BK + 1];
+  __shared__ double wq[ES_MAXQ];
+  __shared__ int tq[ES_MAXQ];
   const int c = blockIdx.y;
   const gs_white_desc W = A.w.wdesc[0];
   stage_white(A.w, W, (int64_t)c, sb[0], sb[1], sb[2]);
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)A.ne * A.kb) return;
-  const int e = (int)(i / A.kb), j = (int)(i % A.kb);
-  const int cj = A.colmap[j];
+  const int e_lo = blockIdx.x * ES_EPB;
+  const int e_hi = min(A.ne, e_lo + ES_EPB);
+  const int q_lo = A.eptr[e_lo], q_hi = A.eptr[e_hi];
+  const bool staged = q_hi - q_lo <= ES_MAXQ;
+  // u_t / N_t of the group's TOA entries, once per workgroup
+  auto weight = [&](int q, int& t) {
+    t = A.etoa[q];
+    const int kb = A.w.bk[t];
+    return A.eu[q] / (sb[0][kb] * (A.w.sigma2[t] + sb[1][kb]) + sb[2][kb]);
+  };
+  if (staged)
+    for (int q = q_lo + (int)threadIdx.x; q < q_hi; q += 256) {
+      int t;
+      wq[q - q_lo] = weight(q, t);
+      tq[q - q_lo] = t;
+    }
+  __syncthreads();
   const int m = A.w.m_max;
-  double acc = 0.0, dg = 0.0;
-  if (cj >= 0 || j == A.dcol || j == 0) {
+  for (int idx = threadIdx.x; idx < (e_hi - e_lo) * A.kb; idx += 256) {
+    const int e = e_lo + idx / A.kb, j = idx % A.kb;
+    const int cj = A.colmap[j];
+    double acc = 0.0, dg = 0.0;
     for (int q = A.eptr[e]; q < A.eptr[e + 1]; ++q) {
-      const int t = A.etoa[q];
-      const int kb = A.w.bk[t];
-      const double N = sb[0][kb] * (A.w.sigma2[t] + sb[1][kb]) + sb[2][kb];
-      const double u = A.eu[q];
-      const double wgt = u / N;
+      int t;
+      double wgt;
+      if (staged) {
+        wgt = wq[q - q_lo];
+        t = tq[q - q_lo];
+      } else {
+        wgt = weight(q, t);
+      }
       if (cj >= 0) acc = fma(A.w.T[(int64_t)t * m + cj], wgt, acc);
       else if (j == A.dcol) acc = fma(A.w.r[t], wgt, acc);
-      dg = fma(u, wgt, dg);
+      dg = fma(A.eu[q], wgt, dg);
     }
+    A.Bx[((int64_t)c * A.ne + e) * A.kb + j] = acc;
+    if (j == 0) A.Dg[(int64_t)c * A.ne + e] = dg;
   }
-  A.Bx[(int64_t)c * A.ne * A.kb + i] = acc;
-  if (j == 0) A.Dg[(int64_t)c * A.ne + e] = dg;
 }
 
 }  // namespace
 
 int launch_ecorr_epoch_sums(hipStream_t s, const EcorrSumArgs& a) {
-  const int64_t n = (int64_t)a.ne * a.kb;
-  hipLaunchKernelGGL(k_ecorr_epoch_sums, dim3((unsigned)((n + 255) / 256), (unsigned)a.n_chain), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_ecorr_epoch_sums, dim3((unsigned)((a.ne + ES_EPB - 1) / ES_EPB), (unsigned)a.n_chain),
+                     dim3(256), 0, s, a);
   return 0;
 }
 
