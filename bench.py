@@ -498,8 +498,28 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
         el = float(t.item())
     if int(em.binfo.abs().sum()) or int(em.pinfo.abs().sum()):
         raise RuntimeError("non-PD system in the white + ECORR bench")
+    # dominant kernel: gs_ecorr_prefix in likelihood mode on per-chain operands, timed alone
+    stream = ctx.stream
+    eng._phiinv(False)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    e0.record(stream)
+    for _ in range(reps):
+        em._eval(eng.x, eng.phiinv_F)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    k_ms = e0.elapsed_time(e1) / reps
+    mR, NF, nM = em.mR, em.NF, em.nm
+    flops = C * (ne * (mR + 1) * (mR + 2) + nM * (NF + 1) * (NF + 2) + (NF + 1) ** 3 // 3)
+    tflops = flops / (k_ms * 1e-3) / 1e12
     return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 chains_per_gpu=C, m=m, n_epoch=ne, aclength_white=aclength, aclength_ecorr=aclength,
+                roofline={"bound": "mfma", "kernel": "k_ecorr_prefix<likelihood mode, per-chain operands>",
+                          "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": tflops / FP64_PEAK_TFLOPS, "kernel_avg_ms": k_ms, "alg_flops_per_launch": flops,
+                          "traffic": None,
+                          "note": "as the ecorr line; each chain's [B | d_E] rows stream from HBM (356 MB per "
+                                  "4096-chain launch)"},
                 config="SURVEY 8f-4 with EFAC/EQUAD sampled: J1713-like pulsar, 2 backends, 136 ECORR epochs, "
                        "white MH + per-chain TNT + ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
 
