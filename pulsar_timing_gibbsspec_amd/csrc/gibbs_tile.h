@@ -230,7 +230,7 @@ __device__ __forceinline__ constexpr int tix(int I, int J, int NT) {
 // updated by the same column operation.  Measured on MI355X against an LDS
 // row-broadcast version and a v_permlane32/16_swap broadcast: 1.7x and 1.04x faster.
 template <int KMAX>
-__device__ __forceinline__ void tile_elim(gs_d4& A, gs_d4& B, double& rsd, int q, int c) {
+__device__ __forceinline__ void tile_elim1(gs_d4& A, gs_d4& B, double& rsd, int q, int c) {
   using namespace gtile;
 #pragma unroll
   for (int s = 0; s < 4; ++s) B[s] = (4 * s + q == c) ? 1.0 : 0.0;
@@ -268,6 +268,115 @@ __device__ __forceinline__ void tile_elim(gs_d4& A, gs_d4& B, double& rsd, int q
   double piv = bcast_lane_bp(dg, 16 * (c & 3) + c);
   if (KMAX < 16) piv = (c >= KMAX) ? 1.0 : piv;  // padding (incl. an augmented pivot)
   rsd = rsq_nr(piv);
+}
+
+namespace gtile {
+// fmac_nb with a compile-time choice of the hazard s_nop (n constant after unrolling)
+template <bool NOP>
+__device__ __forceinline__ double fmac_nbx(double acc, double v, double m, int n) {
+#define GS_FMX(N) \
+  case N: return NOP ? fmac_nb_c<N>(acc, v, m) : fmac_nb_c_nn<N>(acc, v, m);
+  switch (n) {
+    GS_FMX(0) GS_FMX(1) GS_FMX(2) GS_FMX(3) GS_FMX(4) GS_FMX(5) GS_FMX(6) GS_FMX(7)
+    GS_FMX(8) GS_FMX(9) GS_FMX(10) GS_FMX(11) GS_FMX(12) GS_FMX(13) GS_FMX(14)
+    default: return NOP ? fmac_nb_c<15>(acc, v, m) : fmac_nb_c_nn<15>(acc, v, m);
+  }
+#undef GS_FMX
+}
+}  // namespace gtile
+
+// Same contract as tile_elim1 (column steps k = 0..KMAX-2, each eliminating row k from
+// every column c > k), but two steps per link of the dependent chain: for columns
+// c > k+1 the 2x2 pivot block P = [[a, b], [c', d]] of rows/columns k, k+1 gives
+// col_c -= g0 col_k + g1 col_{k+1} with P g = (A[k][c], A[k+1][c]); column k+1 takes
+// step k alone (g0 = b/a).  The pivot chain per pair is det -> rcp -> Newton -> scale
+// (both multipliers side by side), so a 16-column tile costs 8 chain links instead of
+// 15.  The two column operations read the ORIGINAL columns k and k+1: column k+1 is
+// applied first (its own multiplier is 0 on lanes k and k+1), then column k.  Same
+// arithmetic as block LDL^T of the tile (the trailing block stays symmetric), equal to
+// tile_elim1 to rounding.
+template <int KMAX>
+__device__ __forceinline__ void tile_elim2(gs_d4& A, gs_d4& B, double& rsd, int q, int c) {
+  using namespace gtile;
+  constexpr int NS = KMAX - 1;  // column steps 0..KMAX-2
+  constexpr int NP = NS > 0 ? NS / 2 : 0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) B[s] = (4 * s + q == c) ? 1.0 : 0.0;
+  double r0 = bcast_group_bp(A[0], 0, c);                 // row 0
+  double r1 = (NP > 0) ? bcast_group_bp(A[0], 1, c) : 0.0;  // row 1
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int k = 2 * p, k1 = k >> 2;
+    const bool nx0 = k + 2 <= NS - 1, nx1 = k + 3 <= NS - 1;
+    // the next pivot rows as before this pair, requested ahead of the pivot chain
+    double n0 = 0.0, n1 = 0.0;
+    if (nx0) n0 = bcast_group_bp(A[(k + 2) >> 2], (k + 2) & 3, c);
+    if (nx1) n1 = bcast_group_bp(A[(k + 3) >> 2], (k + 3) & 3, c);
+    __builtin_amdgcn_sched_barrier(0);
+    const double a = newbcast(r0, k), b = newbcast(r0, k + 1);
+    const double cq = newbcast(r1, k), d = newbcast(r1, k + 1);
+    const bool beyond = c > opq(k + 1);
+    const double r0m = beyond ? r0 : 0.0, r1m = beyond ? r1 : 0.0;
+    const double det = fma(a, d, -(b * cq));
+    const double i0 = __builtin_amdgcn_rcp(det);
+    const double sd = i0 * fma(det, i0, -2.0);  // -1/det (one Newton step)
+    const double ia = __builtin_amdgcn_rcp(a);
+    const double sa = ia * fma(a, ia, -2.0);    // -1/a
+    const double ng1 = fma(a, r1m, -(cq * r0m)) * sd;
+    double ng0 = fma(d, r0m, -(b * r1m)) * sd;
+    ng0 = (c == k + 1) ? b * sa : ng0;
+    // pass 1: original column k+1 (multiplier 0 on lanes <= k+1)
+    if (nx0) n0 = fmac_nbx<false>(n0, n0, ng1, k + 1);
+    if (nx1) n1 = fmac_nbx<false>(n1, n1, ng1, k + 1);
+#pragma unroll
+    for (int s = k1; s < 4; ++s) A[s] = fmac_nbx<false>(A[s], A[s], ng1, k + 1);
+#pragma unroll
+    for (int s = 0; s <= k1; ++s) B[s] = fmac_nbx<false>(B[s], B[s], ng1, k + 1);
+    // pass 2: original column k (unchanged by pass 1); the s_nop covers a DPP read
+    // scheduled right after pass 1's write of the same register
+    if (nx0) n0 = fmac_nbx<true>(n0, n0, ng0, k);
+    if (nx1) n1 = fmac_nbx<true>(n1, n1, ng0, k);
+#pragma unroll
+    for (int s = k1; s < 4; ++s) A[s] = fmac_nbx<true>(A[s], A[s], ng0, k);
+#pragma unroll
+    for (int s = 0; s <= k1; ++s) B[s] = fmac_nbx<true>(B[s], B[s], ng0, k);
+    r0 = n0;
+    r1 = n1;
+  }
+  if constexpr (NS > 0 && (NS & 1)) {
+    // trailing single step k = KMAX-2 (row k is r0)
+    constexpr int k = NS - 1, k1 = k >> 2;
+    __builtin_amdgcn_sched_barrier(0);
+    const double akk = newbcast(r0, k);
+    const double akm = (c > opq(k)) ? r0 : 0.0;
+    const double i0 = __builtin_amdgcn_rcp(akk);
+    const double ng = (akm * i0) * fma(akk, i0, -2.0);
+#pragma unroll
+    for (int s = k1; s < 4; ++s) A[s] = fmac_nbx<true>(A[s], A[s], ng, k);
+#pragma unroll
+    for (int s = 0; s <= k1; ++s) B[s] = fmac_nbx<true>(B[s], B[s], ng, k);
+  }
+  double dg = A[0];
+#pragma unroll
+  for (int s = 1; s < 4; ++s) dg = ((c >> 2) == s) ? A[s] : dg;
+  double piv = bcast_lane_bp(dg, 16 * (c & 3) + c);
+  if (KMAX < 16) piv = (c >= KMAX) ? 1.0 : piv;
+  rsd = rsq_nr(piv);
+}
+
+// Off by default: measured on MI355X (4096 chains, NF = 60) the pair variant is slower,
+// 3.40 vs 3.00 ms per 100-sweep launch -- at 2 waves/SIMD the diag factor is bound by
+// VALU issue (the pair adds det, a second rcp and two more DPP broadcasts per link, and
+// 17 more spilled VGPRs), not by the length of the dependent chain.
+#ifndef GS_TILE_PAIR
+#define GS_TILE_PAIR 0
+#endif
+template <int KMAX>
+__device__ __forceinline__ void tile_elim(gs_d4& A, gs_d4& B, double& rsd, int q, int c) {
+  if constexpr (GS_TILE_PAIR)
+    tile_elim2<KMAX>(A, B, rsd, q, c);
+  else
+    tile_elim1<KMAX>(A, B, rsd, q, c);
 }
 
 // Model block view (see gibbs_bdraw.hip ModelLds): S0 NF x (NF+1), dF, G NMX x (NF+1),
