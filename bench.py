@@ -724,7 +724,7 @@ def main():
                          "alg_flops_per_launch": alg_flops_launch,
                          "executed_tflops": exe, "executed_frac": exe / FP64_PEAK_TFLOPS},
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     for kind in [k for k in args.pta.split(",") if k and k != "none"]:
         mode = "sum" if kind == "curn" else "exact"
@@ -733,7 +733,7 @@ def main():
         if rank == 0:
             sec["config"] = (f"configs[3]: 45-pulsar CURN{' + per-pulsar red' if kind == 'curn_red' else ''} "
                              f"free spectrum, chain-sharded, common draw {mode}")
-            if not args.no_cpu_baseline:
+            if not args.no_cpu_baseline and world == 1:
                 sec["cpu_baseline"] = pta_cpu_baseline(kind, args.cpu_seconds)
             out.setdefault("secondary", {})[kind] = sec
     if args.ecorr:
@@ -754,7 +754,7 @@ def main():
         if rank == 0:
             sec["config"] = ("configs[4]: 200 synthetic pulsars x 10^4 TOAs x 100 frequencies (m=216), "
                              "white-noise MH (20 steps) + per-chain TNT recompute every sweep, chain-sharded")
-            if not args.no_cpu_baseline:
+            if not args.no_cpu_baseline and world == 1:
                 sec["cpu_baseline"] = config5_cpu_baseline(args.cpu_seconds)
             out.setdefault("secondary", {})["config5"] = sec
     if rank == 0:
