@@ -441,11 +441,12 @@ def ecorr_cpu_baseline(seconds=10.0, aclength=10):
                        f"oracle restatement, numpy/LAPACK, 1 thread) in {el:.1f} s")
 
 
-def _ecorr_traffic(C):
+def _ecorr_traffic(C, fname="pmc_traffic_ecorr.json"):
     """HBM bytes per launch of k_ecorr_prefix<likelihood> from the committed PMC passes
-    (tools/gpu_pmc_ecorr.sh -> profiles/pmc_traffic_ecorr.json), same chain count only."""
+    (tools/gpu_pmc_ecorr.sh -> profiles/pmc_traffic_ecorr.json for the shared-operand kernel,
+    profiles/pmc_traffic_ecorr_white.json for the per-chain-operand one), same chain count only."""
     try:
-        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic_ecorr.json")))
+        d = json.load(open(os.path.join(ROOT, "profiles", fname)))
     except (OSError, ValueError):
         return None
     return d.get("bytes_per_launch") if d.get("chains") == C else None
@@ -517,9 +518,10 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
                 roofline={"bound": "mfma", "kernel": "k_ecorr_prefix<likelihood mode, per-chain operands>",
                           "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": tflops / FP64_PEAK_TFLOPS, "kernel_avg_ms": k_ms, "alg_flops_per_launch": flops,
-                          "traffic": None,
-                          "note": "as the ecorr line; each chain's [B | d_E] rows stream from HBM (356 MB per "
-                                  "4096-chain launch)"},
+                          "traffic": _ecorr_traffic(C, "pmc_traffic_ecorr_white.json"),
+                          "note": "as the ecorr line; each chain's [B | d_E] rows stream from HBM (343 MB of "
+                                  "algorithmic reads per 4096-chain launch; traffic = PMC FETCH_SIZE x2 + "
+                                  "WRITE_SIZE, the x2 wide-read correction makes it an upper estimate)"},
                 config="SURVEY 8f-4 with EFAC/EQUAD sampled: J1713-like pulsar, 2 backends, 136 ECORR epochs, "
                        "white MH + per-chain TNT + ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC traffic (FETCH_SIZE, WRITE_SIZE in separate passes) of the ECORR likelihood kernel.
+# PMC traffic (FETCH_SIZE, WRITE_SIZE in separate passes) of the two ECORR likelihood kernels.
 set -u
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/pmc_ecorr
@@ -11,4 +11,6 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_f
 echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $R/bench.py $ARGS > $OUT/write.log 2>&1; rc=$?
 echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
-cd $R && SWEEPS=1 CHAINS=4096 python tools/pmc_traffic.py $OUT "k_ecorr_prefix<5, true>" $OUT/pmc_traffic_ecorr.json
+# both likelihood kernels run in the same passes (bench's ecorr and ecorr_white lines)
+cd $R && SWEEPS=1 CHAINS=4096 python tools/pmc_traffic.py $OUT "k_ecorr_prefix<5, true, false>" $OUT/pmc_traffic_ecorr.json \
+  && SWEEPS=1 CHAINS=4096 python tools/pmc_traffic.py $OUT "k_ecorr_prefix<5, true, true>" $OUT/pmc_traffic_ecorr_white.json
