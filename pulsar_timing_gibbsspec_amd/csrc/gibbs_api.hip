@@ -889,7 +889,7 @@ int gs_ecorr_bdraw_e(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const d
                      int ldb, int64_t bx_cstride, int64_t dg_cstride, int dcol, const int32_t* jmap) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_chain < 0 || mR <= 0 || ne < 0) return fail_arg(2, "n_chain / mR / ne");
-  if (ldbx < mR + 1) return fail_arg(5, "ldbx < mR + 1");
+  if (ldbx < mR + 1 || ldbx > 128) return fail_arg(5, "ldbx must be in [mR + 1, 128]");
   if (dcol < 0 || dcol >= ldbx || !jmap) return fail_arg(26, "dcol / jmap");
   if (bx_cstride < 0 || dg_cstride < 0) return fail_arg(24, "negative per-chain stride");
   if (!Bx || !Dg || !ebk || !xcol) return fail_arg(6, "NULL Bx / Dg / ebk / xcol");

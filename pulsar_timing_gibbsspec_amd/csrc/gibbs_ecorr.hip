@@ -571,29 +571,50 @@ __global__ __launch_bounds__(256) void k_ecorr_accept(EcorrMhArgs A) {
   }
 }
 
-// b_E | b_R (one thread per (chain, epoch)) and the scatter of b_R into b's original
-// column order (threads ne .. ne + mR - 1).
+// b_E | b_R and the scatter of b_R into b's original column order.  Grid (EB_BLK(ne) +
+// ceil(mR / 256), n_chain): the first EB_BLK workgroups hold 64 epochs each, FOUR lanes per
+// epoch splitting the Bx row's columns t = sub, sub + 4, ... (each load instruction touches
+// 16 rows x 32 contiguous bytes instead of 64 rows x 8 bytes with a lane per epoch; the
+// per-chain Bx of the white + ECORR path streams from HBM), partial sums combined over the
+// quad; the remaining workgroups scatter b_R (one thread per column).
+constexpr int EB_EPB = 64;    // epochs per workgroup (4 lanes each)
+constexpr int EB_MAXC = 128;  // Bx columns (16 NB, NB <= 6 -> 96)
+__host__ __device__ constexpr int eb_blk(int ne) { return (ne + EB_EPB - 1) / EB_EPB; }
+
 __global__ __launch_bounds__(256) void k_ecorr_bdraw_e(EcorrBArgs A) {
   const int c = blockIdx.y;
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= A.ne + A.mR) return;
-  if (A.chain_mask && !A.chain_mask[c]) return;  // gate (pulsar_gibbs.py:697-698)
+  if (A.chain_mask && !A.chain_mask[c]) return;  // gate (pulsar_gibbs.py:697-698), uniform
   const double* bR = A.bR + (int64_t)c * A.ldbR;
   double* b = A.b + (int64_t)c * A.ldb;
-  if (j >= A.ne) {
-    b[A.rcol[j - A.ne]] = bR[j - A.ne];
+  const int neb = eb_blk(A.ne);
+  if ((int)blockIdx.x >= neb) {
+    const int j = ((int)blockIdx.x - neb) * 256 + threadIdx.x;
+    if (j < A.mR) b[A.rcol[j]] = bR[j];
     return;
   }
-  const int e = j;
+  // b_R in Bx column order (0 on skipped columns) staged once per workgroup, so the
+  // column loop has one global load per step and no dependent jmap -> b_R gather
+  __shared__ double wb[EB_MAXC];
+  for (int t = threadIdx.x; t < A.ldbx; t += 256) {
+    const int jr = A.jmap[t];
+    wb[t] = (jr >= 0) ? bR[jr] : 0.0;
+  }
+  __syncthreads();
+  const int e = (int)blockIdx.x * EB_EPB + (threadIdx.x >> 2), sub = threadIdx.x & 3;
+  const bool ok = e < A.ne;  // uniform over each quad
+  const double* row = A.Bx + (int64_t)c * A.bx_cs + (int64_t)(ok ? e : 0) * A.ldbx;
+  double s = 0.0;
+  if (ok) {
+#pragma unroll 8
+    for (int t = sub; t < A.ldbx; t += 4) s = fma(-row[t], wb[t], s);
+  }
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  if (!ok || sub != 0) return;
+  s += row[A.dcol];
   double inv, lg;
   ec_phi(A.x[(int64_t)c * A.ldx + A.xcol[A.ebk[e]]], inv, lg);
   const double a = A.Dg[(int64_t)c * A.dg_cs + e] + inv;
-  const double* row = A.Bx + (int64_t)c * A.bx_cs + (int64_t)e * A.ldbx;
-  double s = row[A.dcol];
-  for (int t = 0; t < A.ldbx; ++t) {
-    const int jr = A.jmap[t];
-    if (jr >= 0) s = fma(-row[t], bR[jr], s);
-  }
   double z;
   if (A.z) {
     z = A.z[(int64_t)c * A.m + A.ecid[e]];
@@ -723,7 +744,7 @@ int launch_ecorr_gather(hipStream_t s, const EcorrGatherArgs& a) {
 }
 
 int launch_ecorr_bdraw_e(hipStream_t s, const EcorrBArgs& a) {
-  hipLaunchKernelGGL(k_ecorr_bdraw_e, dim3((unsigned)((a.ne + a.mR + 255) / 256), (unsigned)a.n_chain), dim3(256),
-                     0, s, a);
+  hipLaunchKernelGGL(k_ecorr_bdraw_e, dim3((unsigned)(eb_blk(a.ne) + (a.mR + 255) / 256), (unsigned)a.n_chain),
+                     dim3(256), 0, s, a);
   return 0;
 }
