@@ -619,62 +619,93 @@ __global__ __launch_bounds__(256) void k_white_tnr(WhiteTntArgs A) {
 // ECORR operands with white noise sampled (gs_ecorr_epoch_sums): the epoch columns of T
 // are quantisation indicators, so TNT[e, j] = sum over epoch e's TOAs of u_t T[t, j] / N_t
 // -- a segmented sum of a few TOAs per epoch instead of the n_toa x m x m SYRK.  One
-// workgroup per (16 epochs, chain): the group's u_t / N_t are computed once into LDS, then
-// one thread per (epoch, reordered column); column dcol carries d_e = sum u_t r_t / N_t,
-// j = 0 also Dg[e] = sum u_t^2 / N_t.
+// workgroup per (16 epochs, ES_CH chains): the group's u_t / N_t are computed once per
+// chain into LDS, then one thread per (epoch, reordered column) loads each T[t, j] ONCE
+// for all ES_CH chains (T is shared; only the weights differ per chain); column dcol
+// carries d_e = sum u_t r_t / N_t, j = 0 also Dg[e] = sum u_t^2 / N_t.
 constexpr int ES_EPB = 16;    // epochs per workgroup
 constexpr int ES_MAXQ = 256;  // TOA entries staged per workgroup (larger groups fall back)
+constexpr int ES_CH = 8;      // chains per workgroup
 __global__ __launch_bounds__(256) void k_ecorr_epoch_sums(EcorrSumArgs A) {
-  __shared__ double sb[3][GS_WHITE_MAX_BK + 1];
-  __shared__ double wq[ES_MAXQ];
+  __shared__ double sb[ES_CH][3][GS_WHITE_MAX_BK + 1];
+  __shared__ double wq[ES_CH][ES_MAXQ];
   __shared__ int tq[ES_MAXQ];
-  const int c = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.y * ES_CH;
+  const int nch = min(ES_CH, A.n_chain - c0);
   const gs_white_desc W = A.w.wdesc[0];
-  stage_white(A.w, W, (int64_t)c, sb[0], sb[1], sb[2]);
+  // white parameters of the workgroup's chains (stage_white for ES_CH chains at once)
+  for (int i = tid; i < ES_CH * W.n_bk; i += 256) {
+    const int ci = i / W.n_bk, k = i % W.n_bk;
+    sb[ci][0][k] = 1.0;
+    sb[ci][1][k] = 0.0;
+    sb[ci][2][k] = 0.0;
+  }
+  __syncthreads();
+  for (int i = tid; i < nch * W.n_w; i += 256) {
+    const int ci = i / W.n_w;
+    const int64_t o = W.w_off + i % W.n_w;
+    const int k = A.w.wbk[o], kind = A.w.wkind[o];
+    double e = 1.0, t = 0.0, q = 0.0;
+    apply_white(kind, A.w.x[(int64_t)(c0 + ci) * A.w.ldx + A.w.wcol[o]], e, t, q);
+    if (kind == GS_WHITE_EFAC) sb[ci][0][k] = e;
+    else if (kind == GS_WHITE_TNEQUAD) sb[ci][2][k] = q;
+    else sb[ci][1][k] = t;
+  }
+  __syncthreads();
   const int e_lo = blockIdx.x * ES_EPB;
   const int e_hi = min(A.ne, e_lo + ES_EPB);
   const int q_lo = A.eptr[e_lo], q_hi = A.eptr[e_hi];
   const bool staged = q_hi - q_lo <= ES_MAXQ;
-  // u_t / N_t of the group's TOA entries, once per workgroup
-  auto weight = [&](int q, int& t) {
-    t = A.etoa[q];
+  // u_t / N_t of chain ci for TOA entry q
+  auto weight = [&](int ci, int q, int t) {
     const int kb = A.w.bk[t];
-    return A.eu[q] / (sb[0][kb] * (A.w.sigma2[t] + sb[1][kb]) + sb[2][kb]);
+    return A.eu[q] / (sb[ci][0][kb] * (A.w.sigma2[t] + sb[ci][1][kb]) + sb[ci][2][kb]);
   };
-  if (staged)
-    for (int q = q_lo + (int)threadIdx.x; q < q_hi; q += 256) {
-      int t;
-      wq[q - q_lo] = weight(q, t);
-      tq[q - q_lo] = t;
+  if (staged) {
+    for (int q = q_lo + tid; q < q_hi; q += 256) tq[q - q_lo] = A.etoa[q];
+    __syncthreads();
+    for (int i = tid; i < nch * (q_hi - q_lo); i += 256) {
+      const int ci = i / (q_hi - q_lo), qq = i % (q_hi - q_lo);
+      wq[ci][qq] = weight(ci, q_lo + qq, tq[qq]);
     }
+  }
   __syncthreads();
   const int m = A.w.m_max;
-  for (int idx = threadIdx.x; idx < (e_hi - e_lo) * A.kb; idx += 256) {
+  for (int idx = tid; idx < (e_hi - e_lo) * A.kb; idx += 256) {
     const int e = e_lo + idx / A.kb, j = idx % A.kb;
     const int cj = A.colmap[j];
-    double acc = 0.0, dg = 0.0;
+    double acc[ES_CH], dg[ES_CH];
+#pragma unroll
+    for (int ci = 0; ci < ES_CH; ++ci) acc[ci] = dg[ci] = 0.0;
     for (int q = A.eptr[e]; q < A.eptr[e + 1]; ++q) {
-      int t;
-      double wgt;
-      if (staged) {
-        wgt = wq[q - q_lo];
-        t = tq[q - q_lo];
-      } else {
-        wgt = weight(q, t);
+      const int t = staged ? tq[q - q_lo] : A.etoa[q];
+      const double v = (cj >= 0) ? A.w.T[(int64_t)t * m + cj] : ((j == A.dcol) ? A.w.r[t] : 0.0);
+      const double u = A.eu[q];
+#pragma unroll
+      for (int ci = 0; ci < ES_CH; ++ci) {
+        if (ci < nch) {
+          const double wgt = staged ? wq[ci][q - q_lo] : weight(ci, q, t);
+          acc[ci] = fma(v, wgt, acc[ci]);
+          dg[ci] = fma(u, wgt, dg[ci]);
+        }
       }
-      if (cj >= 0) acc = fma(A.w.T[(int64_t)t * m + cj], wgt, acc);
-      else if (j == A.dcol) acc = fma(A.w.r[t], wgt, acc);
-      dg = fma(A.eu[q], wgt, dg);
     }
-    A.Bx[((int64_t)c * A.ne + e) * A.kb + j] = acc;
-    if (j == 0) A.Dg[(int64_t)c * A.ne + e] = dg;
+#pragma unroll
+    for (int ci = 0; ci < ES_CH; ++ci) {
+      if (ci < nch) {
+        A.Bx[((int64_t)(c0 + ci) * A.ne + e) * A.kb + j] = acc[ci];
+        if (j == 0) A.Dg[(int64_t)(c0 + ci) * A.ne + e] = dg[ci];
+      }
+    }
   }
 }
 
 }  // namespace
 
 int launch_ecorr_epoch_sums(hipStream_t s, const EcorrSumArgs& a) {
-  hipLaunchKernelGGL(k_ecorr_epoch_sums, dim3((unsigned)((a.ne + ES_EPB - 1) / ES_EPB), (unsigned)a.n_chain),
+  hipLaunchKernelGGL(k_ecorr_epoch_sums,
+                     dim3((unsigned)((a.ne + ES_EPB - 1) / ES_EPB), (unsigned)((a.n_chain + ES_CH - 1) / ES_CH)),
                      dim3(256), 0, s, a);
   return 0;
 }
