@@ -459,6 +459,13 @@ int gs_ecorr_propose(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, con
 int gs_ecorr_accept(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, int init, const double* lnl,
                     const int32_t* info, const int32_t* pinfo, const double* aux, const double* prop,
                     const double* xq, double* x, int ldx, double* lnl0, double* q_rec, int32_t* n_acc);
+/* gs_ecorr_accept followed, in the same launch, by gs_ecorr_propose's proposal for step
+ * next_step (< 0: none) from the updated x: one launch per Metropolis step. */
+int gs_ecorr_accept_propose(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, int init, const double* lnl,
+                            const int32_t* info, const int32_t* pinfo, const double* aux, double* prop,
+                            double* xq, double* x, int ldx, double* lnl0, double* q_rec, int32_t* n_acc,
+                            const double* emin, const double* emax, int n_param, int next_step, int64_t sweep,
+                            int64_t chain_base, const double* inj);
 int gs_ecorr_bdraw_e(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const double* Bx, const double* Dg,
                      const int32_t* ebk, const int32_t* xcol, const double* x, int ldx, const double* bR,
                      int ldbR, const int32_t* ecid, const int32_t* rcol, int m, const double* z,

@@ -874,10 +874,35 @@ int gs_ecorr_accept(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, int 
   if (!lnl0) return fail_arg(14, "NULL lnl0");
   if (n_chain == 0) return 0;
   EcorrMhArgs a = {};
+  a.next_step = -1;
   a.n_chain = n_chain; a.n_e = n_e; a.ldx = ldx; a.init = init ? 1 : 0;
   a.ecol = ecol; a.lnl = lnl; a.info = info; a.pinfo = pinfo; a.aux = aux;
   a.prop = const_cast<double*>(prop); a.xq = const_cast<double*>(xq); a.x = x; a.lnl0 = lnl0;
   a.q_rec = q_rec; a.n_acc = n_acc;
+  launch_ecorr_accept(ctx->stream, a);
+  return after_launch("k_ecorr_accept");
+}
+
+int gs_ecorr_accept_propose(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, int init, const double* lnl,
+                            const int32_t* info, const int32_t* pinfo, const double* aux, double* prop,
+                            double* xq, double* x, int ldx, double* lnl0, double* q_rec, int32_t* n_acc,
+                            const double* emin, const double* emax, int n_param, int next_step, int64_t sweep,
+                            int64_t chain_base, const double* inj) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_chain < 0) return fail_arg(2, "n_chain < 0");
+  if (n_e <= 0 || !ecol) return fail_arg(3, "n_e / ecol");
+  if (!lnl || !aux) return fail_arg(6, "NULL lnl / aux");
+  if (!prop || !xq || !x || ldx <= 0) return fail_arg(10, "prop / xq / x / ldx");
+  if (!lnl0) return fail_arg(14, "NULL lnl0");
+  if (next_step >= 0 && (!emin || !emax || n_param <= 0 || n_param > ldx))
+    return fail_arg(17, "emin / emax / n_param");
+  if (n_chain == 0) return 0;
+  EcorrMhArgs a = {};
+  a.n_chain = n_chain; a.n_e = n_e; a.ldx = ldx; a.init = init ? 1 : 0; a.next_step = next_step;
+  a.ecol = ecol; a.lnl = lnl; a.info = info; a.pinfo = pinfo; a.aux = aux;
+  a.prop = prop; a.xq = xq; a.x = x; a.lnl0 = lnl0; a.q_rec = q_rec; a.n_acc = n_acc;
+  a.n_param = n_param; a.emin = emin; a.emax = emax; a.inj = inj;
+  a.sweep = sweep; a.chain_base = chain_base; a.sweep_dev = ctx->sweep_dev; a.key = key_of(ctx);
   launch_ecorr_accept(ctx->stream, a);
   return after_launch("k_ecorr_accept");
 }

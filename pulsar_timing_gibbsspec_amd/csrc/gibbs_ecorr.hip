@@ -511,20 +511,18 @@ __device__ __forceinline__ double ec_scale(double u) {
 // uniformly, q[par] += randn * (0.05 n_e) * scale.  xq = x with the jump applied;
 // prop[c] = {x column, log U, inside prior, proposed value}.  Only the ECORR columns of xq
 // are written (the rest of the row is never read).
-__global__ __launch_bounds__(256) void k_ecorr_propose(EcorrMhArgs A) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= A.n_chain) return;
+__device__ __forceinline__ void ecorr_propose_one(const EcorrMhArgs& A, int c, int step) {
   double sc, z, u;
   int p;
   if (A.inj) {
-    const double* q = A.inj + ((int64_t)A.step * A.n_chain + c) * 4;
+    const double* q = A.inj + ((int64_t)step * A.n_chain + c) * 4;
     sc = q[0];
     p = (int)q[1];
     z = q[2];
     u = q[3];
   } else {
     const long long sw = gs_sweep(A.sweep, A.sweep_dev), gc = A.chain_base + c;
-    const uint32_t s3 = 3u * (uint32_t)A.step;
+    const uint32_t s3 = 3u * (uint32_t)step;
     double u1, u2, v1, v2, u4;
     gs_uniform2(gs_counter(s3, sw, gc, 0, GS_EV_ECORR), A.key, u1, u2);
     gs_uniform2(gs_counter(s3 + 1, sw, gc, 0, GS_EV_ECORR), A.key, v1, v2);
@@ -547,7 +545,13 @@ __global__ __launch_bounds__(256) void k_ecorr_propose(EcorrMhArgs A) {
   pr[3] = qv;
 }
 
-// Metropolis decision (pulsar_gibbs.py:465-472): lnL = lnl_R + (sum d_E^2/a - sum log a -
+__global__ __launch_bounds__(256) void k_ecorr_propose(EcorrMhArgs A) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= A.n_chain) return;
+  ecorr_propose_one(A, c, A.step);
+}
+
+// Metropolis decision (pulsar_gibbs.py:465-472), optionally followed by the next proposal: lnL = lnl_R + (sum d_E^2/a - sum log a -
 // sum log phi_E) / 2 (the chain-independent constants cancel); -inf when a factor was not
 // positive definite or the proposal left the prior.  init: only record lnL0 at x.
 __global__ __launch_bounds__(256) void k_ecorr_accept(EcorrMhArgs A) {
@@ -558,17 +562,20 @@ __global__ __launch_bounds__(256) void k_ecorr_accept(EcorrMhArgs A) {
   const double l1 = pd ? A.lnl[c] + 0.5 * (ax[1] - ax[0] - ax[2]) : -INFINITY;
   if (A.init) {
     A.lnl0[c] = l1;
-    return;
+  } else {
+    const double* pr = A.prop + (int64_t)c * 4;
+    const double diff = (pr[2] != 0.0) ? l1 - A.lnl0[c] : -INFINITY;
+    if (A.q_rec)
+      for (int j = 0; j < A.n_e; ++j) A.q_rec[(int64_t)c * A.n_e + j] = A.xq[(int64_t)c * A.ldx + A.ecol[j]];
+    if (diff > pr[1]) {
+      A.x[(int64_t)c * A.ldx + (int)pr[0]] = pr[3];
+      A.lnl0[c] = l1;
+      if (A.n_acc) A.n_acc[c] += 1;
+    }
   }
-  const double* pr = A.prop + (int64_t)c * 4;
-  const double diff = (pr[2] != 0.0) ? l1 - A.lnl0[c] : -INFINITY;
-  if (A.q_rec)
-    for (int j = 0; j < A.n_e; ++j) A.q_rec[(int64_t)c * A.n_e + j] = A.xq[(int64_t)c * A.ldx + A.ecol[j]];
-  if (diff > pr[1]) {
-    A.x[(int64_t)c * A.ldx + (int)pr[0]] = pr[3];
-    A.lnl0[c] = l1;
-    if (A.n_acc) A.n_acc[c] += 1;
-  }
+  // gs_ecorr_accept_propose: the next step's proposal from the updated state, same thread
+  // (one launch per Metropolis step instead of two)
+  if (A.next_step >= 0) ecorr_propose_one(A, c, A.next_step);
 }
 
 // b_E | b_R and the scatter of b_R into b's original column order.  Grid (EB_BLK(ne) +

@@ -186,6 +186,7 @@ struct EcorrSchurArgs {
 };
 struct EcorrMhArgs {
   int n_chain, n_e, ldx, n_param, step, init;
+  int next_step;  // k_ecorr_accept: propose step next_step afterwards (< 0: no)
   int64_t sweep, chain_base;
   const int64_t* sweep_dev;
   gs_key key;

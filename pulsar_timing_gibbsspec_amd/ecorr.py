@@ -243,19 +243,22 @@ class EcorrModel:
         q_rec (n_steps, C, n_e) proposals or None."""
         lib, h = self.ctx.lib, self.ctx.handle
         ne_p = self.n_bk
+        n_steps = int(n_steps)
         self._eval(x, phiinv_F)
-        check(lib.gs_ecorr_accept(h, self.C, ne_p, ptr(self.ecol), 1, ptr(self.lnl), ptr(self.linfo),
-                                  ptr(self.pinfo), ptr(self.aux), None, None, ptr(x), x.shape[1], ptr(self.lnl0),
-                                  None, None), "gs_ecorr_accept")
-        for s in range(int(n_steps)):
-            check(lib.gs_ecorr_propose(h, self.C, ne_p, ptr(self.ecol), ptr(self.emin), ptr(self.emax), ptr(x),
-                                       x.shape[1], self.n_param, ptr(self.xq), s, sweep, chain_base, ptr(inj),
-                                       ptr(self.prop)), "gs_ecorr_propose")
+
+        # each accept launch also draws the next step's proposal (gs_ecorr_accept_propose):
+        # init + propose(0), then per step likelihood -> accept(s) + propose(s + 1)
+        def accept_propose(init, qr, nxt):
+            check(lib.gs_ecorr_accept_propose(
+                h, self.C, ne_p, ptr(self.ecol), init, ptr(self.lnl), ptr(self.linfo), ptr(self.pinfo),
+                ptr(self.aux), ptr(self.prop), ptr(self.xq), ptr(x), x.shape[1], ptr(self.lnl0), ptr(qr),
+                None if init else ptr(n_acc), ptr(self.emin), ptr(self.emax), self.n_param, nxt, sweep,
+                chain_base, ptr(inj)), "gs_ecorr_accept_propose")
+
+        accept_propose(1, None, 0 if n_steps > 0 else -1)
+        for s in range(n_steps):
             self._eval(self.xq, phiinv_F)
-            qr = q_rec[s] if q_rec is not None else None
-            check(lib.gs_ecorr_accept(h, self.C, ne_p, ptr(self.ecol), 0, ptr(self.lnl), ptr(self.linfo),
-                                      ptr(self.pinfo), ptr(self.aux), ptr(self.prop), ptr(self.xq), ptr(x),
-                                      x.shape[1], ptr(self.lnl0), ptr(qr), ptr(n_acc)), "gs_ecorr_accept")
+            accept_propose(0, q_rec[s] if q_rec is not None else None, s + 1 if s + 1 < n_steps else -1)
 
     def bdraw(self, x, phiinv_F, b, z=None, sweep=0, first=False, chain_base=0, chain_mask=None):
         """b | rho, ECORR of every chain (update_b, pulsar_gibbs.py:489-520): b (C, ldb >= m)
