@@ -610,7 +610,9 @@ def main():
     ap.add_argument("--bcast", type=int, default=None, help="GS_OPT_BCAST (0 readlane, 1 LDS, 2 batched)")
     ap.add_argument("--pta", default="curn_red,curn", help="secondary PTA configs measured in the same run "
                     "(comma list of curn_red, curn; or none). curn uses the sufficient-statistic draw")
-    ap.add_argument("--pta-chains", type=int, default=256)
+    ap.add_argument("--pta-chains", type=int, default=2048,
+                    help="chains per GPU for the PTA lines (measured: 256 -> 1024 -> 2048 -> 4096 chains give "
+                         "CURN + red 3.0e5 -> 3.8e5 -> 3.9e5 -> 4.0e5 chain-it/s: saturated at 2048)")
     ap.add_argument("--pta-steps", type=int, default=20)
     ap.add_argument("--config5", type=int, default=1, help="measure BASELINE configs[4] too (1/0)")
     ap.add_argument("--pta-graph", type=int, default=0, help="time the PTA sweeps as a hipGraph replay (1/0); "
