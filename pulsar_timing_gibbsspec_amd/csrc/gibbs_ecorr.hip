@@ -588,50 +588,71 @@ constexpr int EB_EPB = 64;    // epochs per workgroup (4 lanes each)
 constexpr int EB_MAXC = 128;  // Bx columns (16 NB, NB <= 6 -> 96)
 __host__ __device__ constexpr int eb_blk(int ne) { return (ne + EB_EPB - 1) / EB_EPB; }
 
+// CH chains per workgroup: with a shared Bx (bx_cs = 0) every Bx row load serves CH chains'
+// b_R (CH = 8); per-chain Bx uses CH = 1.
+template <int CH>
 __global__ __launch_bounds__(256) void k_ecorr_bdraw_e(EcorrBArgs A) {
-  const int c = blockIdx.y;
-  if (A.chain_mask && !A.chain_mask[c]) return;  // gate (pulsar_gibbs.py:697-698), uniform
-  const double* bR = A.bR + (int64_t)c * A.ldbR;
-  double* b = A.b + (int64_t)c * A.ldb;
+  const int c0 = blockIdx.y * CH;
+  const int nch = min(CH, A.n_chain - c0);
   const int neb = eb_blk(A.ne);
   if ((int)blockIdx.x >= neb) {
     const int j = ((int)blockIdx.x - neb) * 256 + threadIdx.x;
-    if (j < A.mR) b[A.rcol[j]] = bR[j];
+    for (int ci = 0; ci < nch; ++ci) {
+      const int c = c0 + ci;
+      if (A.chain_mask && !A.chain_mask[c]) continue;  // gate (pulsar_gibbs.py:697-698)
+      if (j < A.mR) A.b[(int64_t)c * A.ldb + A.rcol[j]] = A.bR[(int64_t)c * A.ldbR + j];
+    }
     return;
   }
   // b_R in Bx column order (0 on skipped columns) staged once per workgroup, so the
   // column loop has one global load per step and no dependent jmap -> b_R gather
-  __shared__ double wb[EB_MAXC];
-  for (int t = threadIdx.x; t < A.ldbx; t += 256) {
+  __shared__ double wb[CH][EB_MAXC];
+  for (int i = threadIdx.x; i < nch * A.ldbx; i += 256) {
+    const int ci = i / A.ldbx, t = i % A.ldbx;
     const int jr = A.jmap[t];
-    wb[t] = (jr >= 0) ? bR[jr] : 0.0;
+    wb[ci][t] = (jr >= 0) ? A.bR[(int64_t)(c0 + ci) * A.ldbR + jr] : 0.0;
   }
   __syncthreads();
   const int e = (int)blockIdx.x * EB_EPB + (threadIdx.x >> 2), sub = threadIdx.x & 3;
   const bool ok = e < A.ne;  // uniform over each quad
-  const double* row = A.Bx + (int64_t)c * A.bx_cs + (int64_t)(ok ? e : 0) * A.ldbx;
-  double s = 0.0;
+  const double* row = A.Bx + (int64_t)c0 * A.bx_cs + (int64_t)(ok ? e : 0) * A.ldbx;
+  double s[CH];
+#pragma unroll
+  for (int ci = 0; ci < CH; ++ci) s[ci] = 0.0;
   if (ok) {
-#pragma unroll 8
-    for (int t = sub; t < A.ldbx; t += 4) s = fma(-row[t], wb[t], s);
+#pragma unroll 4
+    for (int t = sub; t < A.ldbx; t += 4) {
+      const double v = row[t];
+#pragma unroll
+      for (int ci = 0; ci < CH; ++ci) s[ci] = fma(-v, wb[ci][t], s[ci]);
+    }
   }
-  s += __shfl_xor(s, 1);
-  s += __shfl_xor(s, 2);
+#pragma unroll
+  for (int ci = 0; ci < CH; ++ci) {
+    s[ci] += __shfl_xor(s[ci], 1);
+    s[ci] += __shfl_xor(s[ci], 2);
+  }
   if (!ok || sub != 0) return;
-  s += row[A.dcol];
-  double inv, lg;
-  ec_phi(A.x[(int64_t)c * A.ldx + A.xcol[A.ebk[e]]], inv, lg);
-  const double a = A.Dg[(int64_t)c * A.dg_cs + e] + inv;
-  double z;
-  if (A.z) {
-    z = A.z[(int64_t)c * A.m + A.ecid[e]];
-  } else {
-    double n1, n2;
-    gs_normal2(gs_counter((uint32_t)(e >> 1), gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, 0, A.event),
-               A.key, n1, n2);
-    z = (e & 1) ? n2 : n1;
+  const double dE = row[A.dcol];
+#pragma unroll
+  for (int ci = 0; ci < CH; ++ci) {
+    const int c = c0 + ci;
+    if (ci >= nch) break;
+    if (A.chain_mask && !A.chain_mask[c]) continue;
+    double inv, lg;
+    ec_phi(A.x[(int64_t)c * A.ldx + A.xcol[A.ebk[e]]], inv, lg);
+    const double a = A.Dg[(int64_t)c * A.dg_cs + e] + inv;
+    double z;
+    if (A.z) {
+      z = A.z[(int64_t)c * A.m + A.ecid[e]];
+    } else {
+      double n1, n2;
+      gs_normal2(gs_counter((uint32_t)(e >> 1), gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, 0, A.event),
+                 A.key, n1, n2);
+      z = (e & 1) ? n2 : n1;
+    }
+    A.b[(int64_t)c * A.ldb + A.ecid[e]] = (dE + s[ci]) / a + z / sqrt(a);
   }
-  b[A.ecid[e]] = s / a + z / sqrt(a);
 }
 
 template <int NB>
@@ -751,7 +772,10 @@ int launch_ecorr_gather(hipStream_t s, const EcorrGatherArgs& a) {
 }
 
 int launch_ecorr_bdraw_e(hipStream_t s, const EcorrBArgs& a) {
-  hipLaunchKernelGGL(k_ecorr_bdraw_e, dim3((unsigned)(eb_blk(a.ne) + (a.mR + 255) / 256), (unsigned)a.n_chain),
-                     dim3(256), 0, s, a);
+  const unsigned gx = (unsigned)(eb_blk(a.ne) + (a.mR + 255) / 256);
+  if (a.bx_cs == 0)  // shared Bx: 8 chains per workgroup
+    hipLaunchKernelGGL(k_ecorr_bdraw_e<8>, dim3(gx, (unsigned)((a.n_chain + 7) / 8)), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_ecorr_bdraw_e<1>, dim3(gx, (unsigned)a.n_chain), dim3(256), 0, s, a);
   return 0;
 }
