@@ -282,17 +282,17 @@ _M32 = np.uint64(0xFFFFFFFF)
 def philox4x32(ctr, key, rounds=10):
     """Philox4x32-10 (Salmon et al. 2011).  ctr: (...,4) uint32, key: (...,2) uint32."""
     c = [np.asarray(ctr[..., i], np.uint64) for i in range(4)]
-    k0 = np.asarray(key[..., 0], np.uint32)
-    k1 = np.asarray(key[..., 1], np.uint32)
+    k0 = np.asarray(key[..., 0], np.uint64)
+    k1 = np.asarray(key[..., 1], np.uint64)
     for r in range(rounds):
-        if r > 0:
-            k0 = (k0 + PHILOX_W0).astype(np.uint32)
-            k1 = (k1 + PHILOX_W1).astype(np.uint32)
+        if r > 0:   # 32-bit wrap-around of the key bumps, in 64-bit arithmetic (no overflow warning)
+            k0 = (k0 + np.uint64(PHILOX_W0)) & _M32
+            k1 = (k1 + np.uint64(PHILOX_W1)) & _M32
         p0 = PHILOX_M0 * c[0]
         p1 = PHILOX_M1 * c[2]
         hi0, lo0 = p0 >> np.uint64(32), p0 & _M32
         hi1, lo1 = p1 >> np.uint64(32), p1 & _M32
-        c = [hi1 ^ c[1] ^ k0.astype(np.uint64), lo1, hi0 ^ c[3] ^ k1.astype(np.uint64), lo0]
+        c = [hi1 ^ c[1] ^ k0, lo1, hi0 ^ c[3] ^ k1, lo0]
     return np.stack([x.astype(np.uint32) for x in c], axis=-1)
 
 

@@ -6,17 +6,41 @@ column order (fixed-prior columns first, then gwid).  For exact-draw parity
 the reference's normals are rotated, z' = L^T U S^-1/2 z, using Sigma along
 the REFERENCE trajectory (tests/golden/single_j1713.npz).
 """
+import os
+
 import numpy as np
 
 from oracle import gibbs_oracle as O
 
+ZC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "single_j1713_zc.npz")
 
-def single_replay(g):
+
+def single_replay(g, committed=True):
+    """single_replay_compute with the rotated normals taken from the committed fixture
+    (tests/golden/make_rotated.py) when ``committed``: the rotation's SVD depends on the
+    host's BLAS in its last bits, the committed values do not."""
+    R = single_replay_compute(g)
+    if committed:
+        zc = np.load(ZC_FILE, allow_pickle=False)["zc"]
+        if zc.shape != R["zc"].shape:
+            raise ValueError(f"{ZC_FILE}: zc {zc.shape} does not match the fixture ({R['zc'].shape})")
+        R["zc"] = zc
+    return R
+
+
+def single_replay_compute(g):
     """-> dict with TNT, d, gwid, order, n_tm, per-draw phiinv and rotated normals.
 
     Draw k of the reference run: k = 0 at x0 (first draw, pulsar_gibbs.py:661-662),
     k = ii + 1 at the state after sweep ii (= chain[ii + 1], or the final state
-    for the last sweep; every gate passes in the analytic branch)."""
+    for the last sweep; every gate passes in the analytic branch).  The rotation
+    runs with single-threaded BLAS whatever the caller's environment."""
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(limits=1):
+        return _single_replay(g)
+
+
+def _single_replay(g):
     TNT, d = O.tnt(g["T"], g["Nvec"], g["r"])
     m = TNT.shape[0]
     gwid = np.asarray(g["gwid"])

@@ -49,6 +49,20 @@ def test_cholesky_draw_with_rotated_normals(single):
     assert np.allclose(np.linalg.norm(R["zc"], axis=1), np.linalg.norm(g["z"], axis=1), rtol=1e-9)
 
 
+@pytest.mark.parametrize("outer_threads", [1, 4])
+def test_committed_rotation_is_host_independent(single, outer_threads):
+    """The committed rotated normals (tests/golden/make_rotated.py) equal a fresh
+    single-threaded rotation, and the fresh rotation stays single-threaded (bit-equal)
+    even when the caller runs BLAS with several threads (the smoke-on-driver failure of
+    round 1: a multi-threaded SVD moved z' by 5e-10)."""
+    from threadpoolctl import threadpool_limits
+    from tests.parity_data import single_replay_compute
+    committed = single_replay(single)["zc"]
+    with threadpool_limits(limits=outer_threads):
+        fresh = single_replay_compute(single)["zc"]
+    assert np.max(np.abs(fresh - committed)) <= 1e-13 * np.max(np.abs(committed))
+
+
 def test_chol_sweep_tracks_reference(single):
     g = single
     R = single_replay(g)
