@@ -58,37 +58,8 @@ def pmc_traffic(S, C):
     return d["bytes_per_launch"]
 
 
-def cpu_baseline(seconds=12.0):
-    """Reference loop (oracle restatement, SVD draw), 1 thread, bounded sample."""
-    from oracle import gibbs_oracle as O
-    from pulsar_timing_gibbsspec_amd import synthetic
-    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0)
-    T, N, r = pta.get_basis()[0], pta.get_ndiag({})[0], pta.get_residuals()[0]
-    gwid = np.arange(60)
-    rng = np.random.default_rng(0)
-    x = rng.uniform(-9, -4, 30)
-    b = np.zeros(T.shape[1])
-    n_tm = T.shape[1] - 60
-    it = 0
-    t0 = time.perf_counter()
-    while True:
-        TNT, d = O.tnt(T, N, r)                    # recomputed every sweep (pulsar_gibbs.py:664-665)
-        if it == 0:                                # first draw from xs (pulsar_gibbs.py:661-662)
-            b = O.bdraw_svd(TNT, d, O.phiinv_single(x, n_tm), rng.standard_normal(T.shape[1]))
-        tau = O.tau_half(b, gwid)
-        x = 0.5 * np.log10(O.rho_analytic(tau, rng.random(30), 1e-18, 1e-8))
-        b = O.bdraw_svd(TNT, d, O.phiinv_single(x, n_tm), rng.standard_normal(T.shape[1]))
-        it += 1
-        el = time.perf_counter() - t0
-        if el > seconds:
-            break
-    return dict(value=it / el, unit="iters/s", cores=1, kind="port",
-                sample=f"{it} sweeps of the J1713 single-chain loop (oracle restatement of "
-                       f"pulsar_gibbs.py:656-698, numpy/OpenBLAS SVD, OPENBLAS_NUM_THREADS=1) in {el:.1f} s")
-
-
 def ess_min_bin(x_rec, elapsed, n_chains_total, max_chains=256):
-    """Min over the 30 bins of the whole-job ESS/s of log10 rho.
+    """Min over the bins of the whole-job ESS/s of log10 rho.
 
     IAT per chain on the post-burn-in rows (first 20 % dropped) of up to
     ``max_chains`` chains; ESS/s = mean ESS per chain x all chains / the time
@@ -102,61 +73,60 @@ def ess_min_bin(x_rec, elapsed, n_chains_total, max_chains=256):
     return float(ess.min() * n_chains_total / (elapsed * n / K))
 
 
-def pta_cpu_baseline(kind, seconds=10.0):
-    """The oracle's restatement of PTABlockGibbs.sample (pta_gibbs.py:664-704), SVD draws,
-    1 thread, bounded sample of the same 45-pulsar model."""
-    from oracle import gibbs_oracle as O
-    from pulsar_timing_gibbsspec_amd import synthetic
-    pta = synthetic.array_pta(kind=kind, seed=0)
-    T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
-    P = len(T)
-    TNT = [O.tnt(T[p], N[p], R[p]) for p in range(P)]
-    names = pta.param_names
-    rind = np.array([i for i, n in enumerate(names) if "rho" in n and "gw" in n])
-    hind = np.array([i for i, n in enumerate(names) if "red" in n and "rho" in n])
-    rng = np.random.default_rng(0)
-    x = rng.uniform(-9, -4, len(names))
-    m = [t.shape[1] for t in T]
-    gw = [np.arange(mm - 60, mm) for mm in m]
-
-    def draw(x):
-        out = []
-        for p in range(P):
-            phi = 10 ** (2 * x[rind]) + (10 ** (2 * x[hind[p * 30:(p + 1) * 30]]) if kind == "curn_red" else 0)
-            ph = np.full(m[p], 1e-40)
-            ph[gw[p]] = 1 / np.repeat(phi, 2)
-            out.append(O.bdraw_svd(TNT[p][0], TNT[p][1], ph, rng.standard_normal(m[p])))
-        return out
-    b = draw(x)
-    it, t0 = 0, time.perf_counter()
-    while True:
-        taus = np.stack([O.tau_full(b[p], gw[p]) for p in range(P)])
-        if kind == "curn_red":
-            rr, _ = O.rho_grid_cdf_red(taus, 10 ** (2 * x[rind]), rng.random((P, 30)), 1e-20, 1e-8)
-            x[hind] = 0.5 * np.log10(rr.ravel())
-        irn = (np.stack([10 ** (2 * x[hind[p * 30:(p + 1) * 30]]) for p in range(P)])
-               if kind == "curn_red" else np.zeros_like(taus))
-        rr, _ = O.rho_grid_cdf_curn(taus, irn, rng.random(30), 1e-18, 1e-8)
-        x[rind] = 0.5 * np.log10(rr)
-        b = draw(x)
-        it += 1
-        el = time.perf_counter() - t0
-        if el > seconds:
-            break
-    return dict(value=it / el, unit="iters/s", cores=1, kind="port",
-                sample=f"{it} sweeps of the 45-pulsar {kind} loop (oracle restatement of "
-                       f"pta_gibbs.py:664-704, numpy SVD, 1 thread) in {el:.1f} s")
+def timed_region(world, dev, fn):
+    """barrier + synchronize, fn(), synchronize + barrier; wall seconds, max over ranks."""
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
 
 
-def bench_pta(kind, C, K, W, rank, world, dev, ctx, curn_mode="exact", graph=True, shard="chain"):
-    """Configs 3/4: PTAChains over the 45 simulated pulsars.  shard='chain': C chains per
+def event_ms(stream, fn, reps):
+    """Average HIP-event time of fn() on ``stream`` (the context stream the C-ABI launches on)."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def grid_peak():
+    """Measured grid-evaluation ceiling (tools/probe/grid_probe.hip -> profiles/grid_probe.json)."""
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", "grid_probe.json")))
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_line(kind, seconds):
+    """cpu_baseline record: the oracle's loop, one single-thread process per host core."""
+    from oracle.cpu_baseline import aggregate
+    return aggregate(kind, seconds)
+
+
+def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain"):
+    """configs[3]: PTAChains over the 45 simulated pulsars.  shard='chain': C chains per
     GPU, no collective (weak).  shard='pulsar' (N > 1): every rank runs the same C chains
     over its pulsar block (balanced by m^3) and exchanges per sweep over RCCL -- the
-    tau-sum all-reduce for CURN (sufficient statistic) or the [tau | x_red] all-gather for
-    CURN + red (strong scaling over pulsars)."""
-    from pulsar_timing_gibbsspec_amd import synthetic
+    tau-sum all-reduce for CURN (sufficient statistic, pta_gibbs.py:181-214) or the
+    [tau | x_red] all-gather for CURN + red (strong scaling over pulsars)."""
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd.array_gibbs import balanced_blocks
     from pulsar_timing_gibbsspec_amd.distributed import PulsarAllGather, TauSumAllReduce
     from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
+    curn_mode = "sum" if kind == "curn" else "exact"
     pta = synthetic.array_pta(kind=kind, seed=0)
     T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
     names = pta.param_names
@@ -167,17 +137,15 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, curn_mode="exact", graph=Tru
     red_col = hind.reshape(len(T), -1) if kind == "curn_red" else None
     sharded = shard == "pulsar" and world > 1
     if sharded:
-        lo, hi = _contiguous_balanced(np.array([t.shape[1] ** 3 for t in T], float), rank, world)
+        blocks = balanced_blocks(np.array([t.shape[1] ** 3 for t in T], float), world)
+        lo, hi = blocks[rank]
         model = DeviceModel(ctx, T[lo:hi], N[lo:hi], R[lo:hi], gwid[lo:hi], fixed[lo:hi])
         x0 = np.random.default_rng(0).uniform(-9, -4, (C, len(names)))
-        bounds = [_contiguous_balanced(np.array([t.shape[1] ** 3 for t in T], float), r, world)
-                  for r in range(world)]
-        assign = [np.arange(a, b) for a, b in bounds]
         ex = dict(allreduce=TauSumAllReduce()) if curn_mode == "sum" else \
-            dict(gather=PulsarAllGather(assign, ((2 if red_col is not None else 1), 30, C), device=dev))
+            dict(gather=PulsarAllGather([np.arange(a, b) for a, b in blocks],
+                                        ((2 if red_col is not None else 1), 30, C), device=dev))
         eng = PTAChains(model, len(names), rind, red_col, (1e-18, 1e-8), (1e-20, 1e-8), C, x0,
                         P_global=len(T), psr_lo=lo, curn_mode=curn_mode, **ex)
-        graph = False
     else:
         model = DeviceModel(ctx, T, N, R, gwid, fixed)
         x0 = np.random.default_rng(rank).uniform(-9, -4, (C, len(names)))
@@ -186,95 +154,144 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, curn_mode="exact", graph=Tru
     rec = torch.empty(K, C, len(names), dtype=torch.float64, device=dev)
     for _ in range(max(1, W)):
         eng.sweep(x_rec=rec[0])
-    if graph:                              # the K timed sweeps as one hipGraph replay
-        eng.capture(K)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    if graph:
-        eng.replay()
-    else:
+
+    def run():
         for i in range(K):
             eng.sweep(x_rec=rec[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = timed_region(world, dev, run)
     if eng.info.cpu().numpy().any():
         raise RuntimeError("non-PD Sigma in the PTA bench")
     total_chains = C if sharded else C * world
-    return dict(value=total_chains * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
-                chains_per_gpu=C, n_psr=len(T), n_param=len(names), hipgraph=bool(graph),
-                sharding=("pulsars over %d GPUs (RCCL %s per sweep), strong" %
-                          (world, "all-reduce" if curn_mode == "sum" else "all-gather")) if sharded
-                else "chains, weak")
+    out = dict(value=total_chains * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+               chains_per_gpu=C, n_psr=len(T), n_param=len(names), n_gpus=world,
+               scaling="strong" if sharded else "weak",
+               sharding=("pulsars over %d GPUs (RCCL %s per sweep)" %
+                         (world, "all-reduce of the tau sums" if curn_mode == "sum" else "all-gather of [tau | x_red]"))
+               if sharded else "chains (no collective)",
+               ess_per_s=ess_min_bin(rec[:, :, rind].cpu().numpy(), el, total_chains))
+    # roofline of the dominant kernels, each HIP-event timed alone on the context stream
+    lib, h, m = ctx.lib, ctx.handle, eng.model
+    st = ctx.stream
+    ms_b = event_ms(st, lambda: eng._bdraw(None, _lib.EV_B, None), 5)
+    mm = m.m.astype(float)
+    bflop = C * float(np.sum(mm ** 3 / 3 + mm ** 2 / 2 + mm / 6 + 3 * mm ** 2))
+    kernels = {"k_bdraw": dict(kernel_avg_ms=ms_b, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
+                               achieved=bflop / (ms_b * 1e-3) / 1e12, alg_per_launch=bflop,
+                               note="b|rho of every (pulsar, chain) system: sum_p m^3/3 + m^2/2 + m/6 + 3 m^2 "
+                                    "flop per chain (SURVEY 8d)")}
+    gp = grid_peak()
+    n_f = eng.n_f
+    if kind == "curn_red":
+        check(lib, lib.gs_phi_from_x(h, C, n_f, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.gw_col),
+                                     _lib.ptr(eng.gwphi)))
+        ms_r = event_ms(st, lambda: check(lib, lib.gs_rho_red(
+            h, eng.P, C, n_f, _lib.ptr(eng.tau), _lib.ptr(eng.gwphi), eng.ngrid, _lib.ptr(eng.grid_red), None,
+            eng.it, eng.chain_base, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.red_col), None)), 5)
+        ev = eng.P * n_f * C * eng.ngrid
+        kernels["k_rho_red"] = dict(kernel_avg_ms=ms_r, bound="valu", unit="Geval/s",
+                                    achieved=ev / (ms_r * 1e-3) / 1e9, alg_per_launch=ev,
+                                    peak=(gp["red_evals_per_s"] / 1e9) if gp else None,
+                                    note="grid-point evaluations ratio*exp(-ratio/2)*ln10 (pta_gibbs.py:265-266): "
+                                         "P x n_f x C x 1000 per launch; peak = the op mix's register-only ceiling "
+                                         "(tools/probe/grid_probe.hip, profiles/grid_probe.json)")
+        if not sharded:
+            check(lib, lib.gs_phi_from_x(h, C, eng.PG * n_f, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.red_col_g),
+                                         _lib.ptr(eng.irn)))
+            ms_c = event_ms(st, lambda: check(lib, lib.gs_rho_curn(
+                h, eng.PG, C, n_f, _lib.ptr(eng.tau_g), _lib.ptr(eng.irn), eng.ngrid, _lib.ptr(eng.grid_gw), None,
+                eng.it, eng.chain_base, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.gw_col), None)), 5)
+            ev = eng.PG * n_f * C * eng.ngrid
+            kernels["k_rho_curn_fast"] = dict(
+                kernel_avg_ms=ms_c, bound="valu", unit="Gterm/s", achieved=ev / (ms_c * 1e-3) / 1e9,
+                alg_per_launch=ev, peak=(gp["curn_pulsar_terms_per_s"] / 1e9) if gp else None,
+                note="(grid point, pulsar) terms of the common pdf product (pta_gibbs.py:192-205): "
+                     "P x n_f x C x 1000 per launch; peak from tools/probe/grid_probe.hip")
+    else:
+        ms_s = event_ms(st, lambda: check(lib, lib.gs_rho_curn_sum(
+            h, eng.PG, C, n_f, _lib.ptr(eng.S), eng.ngrid, _lib.ptr(eng.grid_gw), None, eng.it, eng.chain_base,
+            _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.gw_col), None)), 5)
+        ev = n_f * C * eng.ngrid
+        kernels["k_rho_curn_sum"] = dict(kernel_avg_ms=ms_s, bound="valu", unit="Geval/s",
+                                         achieved=ev / (ms_s * 1e-3) / 1e9, alg_per_launch=ev,
+                                         peak=(gp["red_evals_per_s"] / 1e9) if gp else None,
+                                         note="n_f x C x 1000 grid points of the common pdf from the tau sums "
+                                              "(one exp each); peak: the red op mix's ceiling (an upper bound)")
+    for k in kernels.values():
+        k["frac"] = (k["achieved"] / k["peak"]) if k.get("peak") else None
+    dom = max(kernels, key=lambda k: kernels[k]["kernel_avg_ms"])
+    out["roofline"] = dict(kernel=dom, **kernels[dom])
+    out["kernels"] = kernels
+    return out
 
 
-def _contiguous_balanced(w, rank, world):
-    """Contiguous pulsar block of this rank with ~equal sum of weights (m^3 ~ b|rho cost)."""
-    cw = np.concatenate([[0.0], np.cumsum(w)])
-    cuts = [int(np.searchsorted(cw, cw[-1] * r / world)) for r in range(world + 1)]
-    cuts[0], cuts[-1] = 0, len(w)
-    for r in range(1, world):                     # every rank keeps at least one pulsar
-        cuts[r] = min(max(cuts[r], cuts[r - 1] + 1), len(w) - (world - r))
-    return cuts[rank], cuts[rank + 1]
+def check(lib, rc):
+    if rc != 0:
+        raise RuntimeError(lib.gs_last_error().decode(errors="replace"))
 
 
-def config5_cpu_baseline(seconds=10.0):
-    """The oracle's restatement of one PulsarBlockGibbs sweep with white noise
-    (pulsar_gibbs.py:656-698: TNT, SVD draw, aclength=20 white MH steps each recomputing
-    r - T b and the white likelihood as :523-546 does, analytic rho) on ONE pulsar of the
-    config-5 array (10^4 TOAs, m = 216), 1 thread; reported as array sweeps/s = 1 /
-    (200 x the per-pulsar sweep time)."""
-    from oracle import gibbs_oracle as O
-    from pulsar_timing_gibbsspec_amd import synthetic
-    d = synthetic.config5_array(n_psr=1, seed=1)
-    T, r, sig, bk = d["T"][0], d["r"][0], d["sigma"][0], d["backend"][0]
-    rng = np.random.default_rng(0)
-    x = d["x0"][0].copy()
-    gw = d["gw_cols"]
-    wind = [w[0] for w in d["white"]]
-    nb = len(wind) // 2
-    lo = np.array([w[3] for w in d["white"]])
-    hi = np.array([w[4] for w in d["white"]])
-    m = T.shape[1]
-    n_tm = m - 2 * gw.size
+def bench_indep(C, K, W, S, rank, world, dev):
+    """BASELINE configs[2]: the 45 simulated pulsars, each with its own 30-bin free
+    spectrum (PulsarBlockGibbs per pulsar, pulsar_gibbs.py:620-710), C chains per pulsar,
+    all (pulsar, chain) systems in one fused persistent launch per S sweeps.  N > 1:
+    pulsars sharded over the ranks (contiguous blocks balanced by m^3), no collective;
+    every rank's pulsars keep their global Philox index (bit-identical to N = 1)."""
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd.array_gibbs import shard_pulsars
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel, FreeSpectrumChains
+    ptas = synthetic.pulsar_ptas(synthetic.array_pta(kind="indep", seed=0))
+    lo, hi = shard_pulsars(ptas, rank, world) if world > 1 else (0, len(ptas))
+    mine = ptas[lo:hi]
+    T = [p.get_basis()[0] for p in mine]
+    ctx = _lib.Context(dev.index, seed=20251019)
+    ctx.set_option(_lib.OPT_PSR_BASE, lo)
+    model = DeviceModel(ctx, T, [p.get_ndiag({})[0] for p in mine], [p.get_residuals()[0] for p in mine],
+                        [np.arange(60)] * len(T), [np.full(t.shape[1] - 60, 1e-40) for t in T])
+    P = len(T)
+    x0 = np.random.default_rng(0).uniform(-9, -4, (len(ptas) * C, 30))[lo * C:hi * C]
+    run = FreeSpectrumChains(model, 1e-18, 1e-8, C, x0)
+    x_rec = torch.empty(S, P * C, 30, dtype=torch.float64, device=dev)
+    b_rec = torch.empty(S, P * C, model.ldb, dtype=torch.float64, device=dev)
+    xs = []
+    if W:
+        run.run(min(W, S), x_rec=x_rec[:min(W, S)], b_rec=b_rec[:min(W, S)])
+    launches = []
 
-    def N_of(xx):
-        return O.ndiag_white(sig, bk, xx[[2 * k for k in range(nb)]], xx[[2 * k + 1 for k in range(nb)]])
-    b = np.zeros(m)
-    it, t0 = 0, time.perf_counter()
-    while True:
-        N = N_of(x)
-        TNT, dd = O.tnt(T, N, r)
-        ph = np.full(m, 1e-40)
-        ph[:gw.size * 2] = 1 / np.repeat(10 ** (2 * x[gw]), 2)
-        b = O.bdraw_svd(TNT, dd, ph, rng.standard_normal(m))
-        ll0 = O.lnlike_white(r, T, b, N_of(x))
-        for _ in range(20):
-            q = x.copy()
-            j = rng.integers(len(wind))
-            q[wind[j]] += rng.standard_normal() * 0.05 * len(wind) * rng.choice([0.1, 0.5, 1, 3, 10])
-            if lo[j] <= q[wind[j]] <= hi[j]:
-                ll1 = O.lnlike_white(r, T, b, N_of(q))
-                if ll1 - ll0 > np.log(rng.random()):
-                    x, ll0 = q, ll1
-        tau = O.tau_half(b, np.arange(2 * gw.size))
-        x[gw] = 0.5 * np.log10(O.rho_analytic(tau, rng.random(gw.size), d["rhomin"], d["rhomax"]))
-        it += 1
-        el = time.perf_counter() - t0
-        if el > seconds:
-            break
-    per_psr = el / it
-    return dict(value=1.0 / (200 * per_psr), unit="iters/s", cores=1, kind="port",
-                sample=f"{it} single-pulsar sweeps (10^4 TOAs, m={m}, n_tm={n_tm}, 20 white MH steps) of the "
-                       f"oracle restatement of pulsar_gibbs.py:656-698 + :373-404 in {el:.1f} s, "
-                       f"{per_psr * 1e3:.0f} ms/pulsar, scaled to the 200-pulsar array")
+    def go():
+        done = 0
+        while done < K:
+            n = min(S, K - done)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(ctx.stream)
+            run.run(n, x_rec=x_rec[:n], b_rec=b_rec[:n])
+            e1.record(ctx.stream)
+            launches.append((e0, e1, n))
+            xs.append(x_rec[:n].view(n, P, C, 30)[:, :, :min(C, 4)].clone())
+            done += n
+    el = timed_region(world, dev, go)
+    if run.info.cpu().numpy().any():
+        raise RuntimeError("non-PD Sigma in the configs[2] bench")
+    ms = np.array([a.elapsed_time(b) for a, b, _ in launches])
+    sw = np.array([n for _, _, n in launches])
+    per_sweep = float(np.sum(ms) / 1e3 / np.sum(sw))
+    mm = model.m.astype(float)
+    flops_sweep = C * float(np.sum(mm ** 3 / 3 + mm ** 2 / 2 + mm / 6 + 3 * mm ** 2))
+    ach = flops_sweep / per_sweep / 1e12
+    xh = torch.cat(xs).cpu().numpy()                 # (K, P, <= 4 chains per pulsar, 30)
+    ess = None
+    if K >= 50:                                      # min over (pulsar, bin) of the whole-job ESS/s
+        ess = min(ess_min_bin(xh[:, p], el, C) for p in range(P))
+    return dict(value=C * K / el, unit="array-iters/s", ms_per_step=el / K * 1e3, steps=K,
+                chains_per_pulsar=C, n_psr=len(ptas), n_psr_local=P, m_range=[int(model.m.min()), int(model.m.max())],
+                n_gpus=world, scaling="strong" if world > 1 else "weak",
+                sharding=(f"pulsars over {world} GPUs (no collective)" if world > 1 else "one GPU"),
+                pulsar_iters_per_s=C * K * len(ptas) / el,
+                ess_per_s=ess,
+                roofline={"kernel": "k_sweep_freespec", "bound": "mfma", "unit": "TFLOP/s", "achieved": ach,
+                          "peak": FP64_PEAK_TFLOPS, "frac": ach / FP64_PEAK_TFLOPS,
+                          "kernel_avg_ms": per_sweep * S * 1e3, "sweeps_per_launch": S,
+                          "alg_flops_per_launch": flops_sweep * S, "traffic": None,
+                          "note": "sum over the rank's pulsars of m^3/3 + m^2/2 + m/6 + 3 m^2 flop per chain-sweep "
+                                  "(SURVEY 8d) x C x S over the HIP-event launch time"})
 
 
 def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, aclength=20, reps=5):
@@ -329,116 +346,6 @@ def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, a
                           "alg_flops_per_launch": flops,
                           "note": "per-chain TNT/d of all 200 pulsars (n m (m+1) + 2 n m flop per system) "
                                   "over the HIP-event time of one refresh (SYRK + prefix)"})
-
-
-def ecorr_white_cpu_baseline(seconds=10.0, aclength=10):
-    """The oracle's restatement of the white + ECORR sweep (notebook order: white MH on
-    get_lnlikelihood_white :523-546, TNT recomputed with the new N as the reference's reset
-    forces, ECORR MH on get_lnlikelihood_fullmarg, rho|b, SVD b draw), one chain, 1 thread."""
-    from oracle import gibbs_oracle as O
-    from pulsar_timing_gibbsspec_amd import synthetic
-    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=0, white_vary=True)
-    T, r = pta.get_basis()[0], pta.get_residuals()[0]
-    names = pta.param_names
-    wn = pta.models[0].white[0]
-    ebk = pta.signals["J1713+0747_basis_ecorr"].epoch_backend
-    eind = [i for i, n in enumerate(names) if "ecorr" in n]
-    ef_i = [i for i, n in enumerate(names) if n.endswith("efac")]
-    eq_i = [i for i, n in enumerate(names) if "equad" in n]
-    wind = sorted(ef_i + eq_i)
-    gw = np.array([i for i, n in enumerate(names) if "rho" in n])
-    m, ne = T.shape[1], ebk.size
-    gwid = ne + np.arange(2 * gw.size)
-    lo = np.array([0.1 if i in ef_i else -8.5 for i in range(len(names))])
-    hi = np.array([5.0 if i in ef_i else -5.0 for i in range(len(names))])
-    rng = np.random.default_rng(0)
-    x = np.zeros(len(names))
-    x[ef_i], x[eq_i], x[eind] = 1.0, -7.0, -6.3
-    x[gw] = rng.uniform(-9, -4, gw.size)
-
-    def N_of(xx):
-        return O.ndiag_white(wn.sigma, wn.backends, xx[ef_i], xx[eq_i])
-
-    def phi(xx):
-        ph = np.full(m, 1e40)
-        ph[:ne] = (10.0 ** (2.0 * xx[eind]))[ebk]
-        ph[gwid] = np.repeat(10.0 ** (2.0 * xx[gw]), 2)
-        return ph
-
-    def prior(ind):
-        return lambda xx: 0.0 if np.all((xx[ind] >= lo[ind]) & (xx[ind] <= hi[ind])) else -np.inf
-
-    def steps(ind):
-        return [(rng.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]), rng.choice(ind),
-                 rng.standard_normal(), rng.random()) for _ in range(aclength)]
-    TNT, dd = O.tnt(T, N_of(x), r)
-    b = O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m))
-    it, t0 = 0, time.perf_counter()
-    while True:
-        x = O.white_mh(x, wind, steps(wind), lambda xx: O.lnlike_white(r, T, b, N_of(xx)), prior(wind))
-        N = N_of(x)
-        TNT, dd = O.tnt(T, N, r)
-
-        def lnl(xx):
-            ph = phi(xx)
-            return O.lnlike_fullmarg(r, N, TNT, dd, 1.0 / ph, np.sum(np.log(ph)))
-        x = O.white_mh(x, eind, steps(eind), lnl, prior(eind))
-        x[gw] = 0.5 * np.log10(O.rho_analytic(O.tau_half(b, gwid), rng.random(gw.size), 1e-18, 1e-8))
-        b = O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m))
-        it += 1
-        el = time.perf_counter() - t0
-        if el > seconds:
-            break
-    return dict(value=it / el, unit="iters/s", cores=1, kind="port",
-                sample=f"{it} sweeps of the single-chain white + ECORR loop (m={m}, {ne} epochs, {aclength} white + "
-                       f"{aclength} ECORR MH steps, oracle restatement, numpy/LAPACK, 1 thread) in {el:.1f} s")
-
-
-def ecorr_cpu_baseline(seconds=10.0, aclength=10):
-    """The oracle's restatement of the ECORR sweep (notebook order; update_ecorr_params
-    :456-484 on get_lnlikelihood_fullmarg :569-610 with TNT recomputed each sweep as the
-    reference does, :664-665; SVD b draw :489-520), one chain, 1 thread."""
-    from oracle import gibbs_oracle as O
-    from pulsar_timing_gibbsspec_amd import synthetic
-    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=0)
-    T, r, N = pta.get_basis()[0], pta.get_residuals()[0], pta.get_ndiag()[0]
-    names = pta.param_names
-    sig = pta.signals["J1713+0747_basis_ecorr"]
-    ebk = sig.epoch_backend
-    eind = [i for i, n in enumerate(names) if "ecorr" in n]
-    gw = np.array([i for i, n in enumerate(names) if "rho" in n])
-    m = T.shape[1]
-    ne = ebk.size
-    gwid = ne + np.arange(2 * gw.size)
-    rng = np.random.default_rng(0)
-    x = np.concatenate([[-6.3] * len(eind), rng.uniform(-9, -4, gw.size)])
-
-    def phi(xx):
-        ph = np.full(m, 1e40)
-        ph[:ne] = (10.0 ** (2.0 * xx[eind]))[ebk]
-        ph[gwid] = np.repeat(10.0 ** (2.0 * xx[gw]), 2)
-        return ph
-    TNT, dd = O.tnt(T, N, r)
-    b = O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m))    # first b from xs
-    it, t0 = 0, time.perf_counter()
-    while True:
-        TNT, dd = O.tnt(T, N, r)
-
-        def lnl(xx):
-            ph = phi(xx)
-            return O.lnlike_fullmarg(r, N, TNT, dd, 1.0 / ph, np.sum(np.log(ph)))
-        steps = [(rng.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]), rng.choice(eind),
-                  rng.standard_normal(), rng.random()) for _ in range(aclength)]
-        x = O.white_mh(x, eind, steps, lnl, lambda xx: 0.0 if np.all((xx[eind] >= -8.5) & (xx[eind] <= -5)) else -np.inf)
-        x[gw] = 0.5 * np.log10(O.rho_analytic(O.tau_half(b, gwid), rng.random(gw.size), 1e-18, 1e-8))
-        b = O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m))
-        it += 1
-        el = time.perf_counter() - t0
-        if el > seconds:
-            break
-    return dict(value=it / el, unit="iters/s", cores=1, kind="port",
-                sample=f"{it} sweeps of the single-chain ECORR loop (m={m}, {ne} epochs, {aclength} ECORR MH steps, "
-                       f"oracle restatement, numpy/LAPACK, 1 thread) in {el:.1f} s")
 
 
 def _ecorr_traffic(C, fname="pmc_traffic_ecorr.json"):
@@ -598,6 +505,23 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
                        "spectrum + 16-col TM, ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
 
 
+def launch_ranks(args_list, n):
+    """`bench.py --gpus N` outside a launcher: start N ranks of this script under
+    torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) and return their
+    exit code.  Runs before anything here touches the GPU; the ranks are child
+    processes, nothing is exec'd."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + args_list
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -606,24 +530,30 @@ def main():
     ap.add_argument("--chains", type=int, default=4096, help="chains per GPU")
     ap.add_argument("--sweeps-per-launch", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--bcast", type=int, default=None, help="GS_OPT_BCAST (0 readlane, 1 LDS, 2 batched)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="seconds per CPU-baseline process")
+    ap.add_argument("--bcast", type=int, default=None, help="GS_OPT_BCAST (0 readlane, 1 LDS, 2 batched, 3 tile)")
+    ap.add_argument("--host-stream", type=int, default=1,
+                    help="also time the headline with every recorded row streamed to pinned host memory (1/0)")
+    ap.add_argument("--indep", type=int, default=1, help="measure BASELINE configs[2] (45 independent pulsars)")
+    ap.add_argument("--indep-chains", type=int, default=256, help="chains per pulsar for configs[2]")
+    ap.add_argument("--indep-steps", type=int, default=200)
     ap.add_argument("--pta", default="curn_red,curn", help="secondary PTA configs measured in the same run "
                     "(comma list of curn_red, curn; or none). curn uses the sufficient-statistic draw")
     ap.add_argument("--pta-chains", type=int, default=2048,
                     help="chains per GPU for the PTA lines (measured: 256 -> 1024 -> 2048 -> 4096 chains give "
                          "CURN + red 3.0e5 -> 3.8e5 -> 3.9e5 -> 4.0e5 chain-it/s: saturated at 2048)")
-    ap.add_argument("--pta-steps", type=int, default=20)
+    ap.add_argument("--pta-steps", type=int, default=200)
     ap.add_argument("--config5", type=int, default=1, help="measure BASELINE configs[4] too (1/0)")
-    ap.add_argument("--pta-graph", type=int, default=0, help="time the PTA sweeps as a hipGraph replay (1/0); "
-                    "measured no faster: the sweeps are GPU-bound and eager launches queue ahead")
-    ap.add_argument("--pta-shard", default="chain", help="chain | pulsar: how N > 1 GPUs split the PTA configs")
     ap.add_argument("--ecorr", type=int, default=1, help="measure the basis-ECORR path (SURVEY 8f-4) too (1/0)")
     ap.add_argument("--ecorr-chains", type=int, default=4096)
     ap.add_argument("--ecorr-steps", type=int, default=10)
     ap.add_argument("--c5-chains", type=int, default=16)
     ap.add_argument("--c5-steps", type=int, default=5)
+    ap.add_argument("--dry-run", action="store_true", help="launcher/rendezvous check only: no GPU work")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -631,6 +561,15 @@ def main():
     # one process per GPU over RCCL; GS_DIST_BACKEND=gloo (and more ranks than GPUs, ranks
     # sharing devices round-robin) only to rehearse the multi-rank paths on one GPU
     backend = os.environ.get("GS_DIST_BACKEND", "nccl")
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+            world = dist.get_world_size()
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_requested": args.gpus}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if backend != "nccl":
         local = local % torch.cuda.device_count()
     if world > 1:
@@ -639,11 +578,13 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()          # the ranks the process group actually holds
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    cpu = not args.no_cpu_baseline and world == 1 and rank == 0   # rank 0 at N = 1 only
 
     from pulsar_timing_gibbsspec_amd import _lib, synthetic
-    from pulsar_timing_gibbsspec_amd.engine import DeviceModel, FreeSpectrumChains
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel, FreeSpectrumChains, HistoryStreamer
 
     pta = synthetic.single_pulsar_pta("J1713+0747", seed=0)
     T, N, r = pta.get_basis()[0], pta.get_ndiag({})[0], pta.get_residuals()[0]
@@ -660,37 +601,25 @@ def main():
     x_rec = torch.empty(K, C, 30, dtype=torch.float64, device=dev)
     b_rec = torch.empty(K, C, model.ldb, dtype=torch.float64, device=dev)
 
-    # warmup (untimed)
     done = 0
-    while done < W:
+    while done < W:                                   # warmup (untimed)
         n = min(S, W - done)
         run.run(n, x_rec=x_rec[:n], b_rec=b_rec[:n])
         done += n
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     stream = ctx.stream
     evs = []
-    t0 = time.perf_counter()
-    done = 0
-    while done < K:
-        n = min(S, K - done)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        run.run(n, x_rec=x_rec[done:done + n], b_rec=b_rec[done:done + n])
-        e1.record(stream)
-        evs.append((e0, e1, n))
-        done += n
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+
+    def headline():
+        done = 0
+        while done < K:
+            n = min(S, K - done)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            run.run(n, x_rec=x_rec[done:done + n], b_rec=b_rec[done:done + n])
+            e1.record(stream)
+            evs.append((e0, e1, n))
+            done += n
+    el = timed_region(world, dev, headline)
     info = run.info.cpu().numpy()
     if info.any():
         raise RuntimeError(f"{int((info != 0).sum())} chains hit a non-PD Sigma")
@@ -705,8 +634,31 @@ def main():
     launch_s = per_sweep_s * S
     achieved = alg_flops_launch / launch_s / 1e12
     exe = executed_flops_per_chain_sweep(model.NF, int(model.nm[0])) * C * S / launch_s / 1e12
-    xh = x_rec.cpu().numpy()
-    ess = ess_min_bin(xh, el, total_chains)
+    ess = ess_min_bin(x_rec.cpu().numpy(), el, total_chains)
+
+    host = None
+    if args.host_stream:
+        # the same K sweeps as PulsarBlockGibbs.sample runs them: every block's x and b rows
+        # go to pinned host memory on a side stream while the next block computes
+        streamer = HistoryStreamer(ctx, [(S, C, 30), (S, C, model.ldb)])
+
+        def streamed():
+            done, slot, pending = 0, 0, None
+            while done < K:
+                n = min(S, K - done)
+                xr, br = streamer.buffers(slot, n)
+                run.run(n, x_rec=xr, b_rec=br)
+                streamer.submit(slot, n)
+                if pending is not None:
+                    streamer.fetch(pending)
+                pending, slot, done = slot, slot ^ 1, done + n
+            if pending is not None:
+                streamer.fetch(pending)
+        el_h = timed_region(world, dev, streamed)
+        host = {"value": total_chains * K / el_h, "unit": "chain-iters/s", "ms_per_step": el_h / K * 1e3,
+                "bytes_per_step": C * (30 + model.ldb) * 8,
+                "note": "headline workload with every chain's recorded x and b rows copied to pinned host memory "
+                        "(PCIe), overlapped with the next block's sweeps (engine.HistoryStreamer, as sample())"}
 
     out = None
     if rank == 0:
@@ -719,49 +671,56 @@ def main():
                                    f"{C} independent chains per GPU", "chains_per_gpu": C,
                        "global_chains": total_chains, "m": m, "n_f": 30,
                        "sweeps_per_launch": S, "bcast": ctx.get_option(_lib.OPT_BCAST),
-                       "parallelism": f"chains sharded over {world} GPU(s)"},
+                       "parallelism": f"chains sharded over {world} GPU(s), no collective"},
             "ess_per_s": ess,
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
                          "traffic": pmc_traffic(S, C),
                          "kernel": "k_sweep_freespec", "kernel_avg_ms": launch_s * 1e3,
                          "alg_flops_per_launch": alg_flops_launch,
+                         "note": "achieved = SURVEY 8d's algorithmic flops (dense m=76 potrf + 3 solves); the kernel "
+                                 "executes fewer (executed_*: NF=60 Schur block after the fixed-prior prefix)",
                          "executed_tflops": exe, "executed_frac": exe / FP64_PEAK_TFLOPS},
+            "with_host_stream": host,
         }
-        if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        if cpu:
+            out["cpu_baseline"] = cpu_line("single", args.cpu_seconds)
+    sec = {}
+
+    def add(name, d, kind=None):
+        if rank == 0:
+            if cpu and kind:
+                d["cpu_baseline"] = cpu_line(kind, args.cpu_seconds)
+            sec[name] = d
+
+    if args.indep:
+        d = bench_indep(args.indep_chains, args.indep_steps, 2, 100, rank, world, dev)
+        d["config"] = ("configs[2]: 45 simulated pulsars, each its own 30-bin free spectrum (m 68..77), "
+                       f"{args.indep_chains} chains per pulsar, one fused launch per 100 sweeps")
+        add("indep", d, "indep")
     for kind in [k for k in args.pta.split(",") if k and k != "none"]:
-        mode = "sum" if kind == "curn" else "exact"
-        sec = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, curn_mode=mode,
-                        graph=bool(args.pta_graph), shard=args.pta_shard)
-        if rank == 0:
-            sec["config"] = (f"configs[3]: 45-pulsar CURN{' + per-pulsar red' if kind == 'curn_red' else ''} "
-                             f"free spectrum, chain-sharded, common draw {mode}")
-            if not args.no_cpu_baseline and world == 1:
-                sec["cpu_baseline"] = pta_cpu_baseline(kind, args.cpu_seconds)
-            out.setdefault("secondary", {})[kind] = sec
+        d = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, shard="chain")
+        d["config"] = (f"configs[3]: 45-pulsar CURN{' + per-pulsar red' if kind == 'curn_red' else ''} free "
+                       f"spectrum, common draw {'from the tau sums' if kind == 'curn' else 'exact product'}")
+        add(kind, d, kind)
+        if world > 1:
+            d = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, shard="pulsar")
+            d["config"] = f"configs[3] {kind}, pulsars sharded over the ranks with the per-sweep RCCL exchange"
+            add(kind + "_pulsar_sharded", d)
     if args.ecorr:
-        sec = bench_ecorr(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev)
-        if rank == 0:
-            sec["sharding"] = "chains, weak"
-            if not args.no_cpu_baseline and world == 1:
-                sec["cpu_baseline"] = ecorr_cpu_baseline(args.cpu_seconds)
-            out.setdefault("secondary", {})["ecorr"] = sec
-        sec = bench_ecorr_white(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev)
-        if rank == 0:
-            sec["sharding"] = "chains, weak"
-            if not args.no_cpu_baseline and world == 1:
-                sec["cpu_baseline"] = ecorr_white_cpu_baseline(args.cpu_seconds)
-            out["secondary"]["ecorr_white"] = sec
+        d = bench_ecorr(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev)
+        d["sharding"] = "chains, weak"
+        add("ecorr", d, "ecorr")
+        d = bench_ecorr_white(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev)
+        d["sharding"] = "chains, weak"
+        add("ecorr_white", d, "ecorr_white")
     if args.config5:
-        sec = bench_config5(args.c5_chains, args.c5_steps, 1, rank, world, dev)
-        if rank == 0:
-            sec["config"] = ("configs[4]: 200 synthetic pulsars x 10^4 TOAs x 100 frequencies (m=216), "
-                             "white-noise MH (20 steps) + per-chain TNT recompute every sweep, chain-sharded")
-            if not args.no_cpu_baseline and world == 1:
-                sec["cpu_baseline"] = config5_cpu_baseline(args.cpu_seconds)
-            out.setdefault("secondary", {})["config5"] = sec
+        d = bench_config5(args.c5_chains, args.c5_steps, 1, rank, world, dev)
+        d["config"] = ("configs[4]: 200 synthetic pulsars x 10^4 TOAs x 100 frequencies (m=216), "
+                       "white-noise MH (20 steps) + per-chain TNT recompute every sweep, chain-sharded")
+        add("config5", d, "config5")
     if rank == 0:
+        out["secondary"] = sec
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -1,0 +1,286 @@
+"""CPU baseline loops for bench.py's ``cpu_baseline`` leg -- TEST/MEASUREMENT INFRASTRUCTURE.
+
+Each loop is the oracle's restatement of the reference sampler's per-sweep work for one
+BASELINE configuration (numpy/LAPACK, the reference's own operation order: TNT
+recomputed every sweep as pulsar_gibbs.py:664-665 forces, SVD b draw :505-518, the rho
+draws of :206-236 / pta_gibbs.py:181-276), run single-threaded for a bounded time.
+``aggregate`` runs one such process per host core at once (OPENBLAS_NUM_THREADS=1, the
+way the reference is fastest on a multi-core host: SURVEY.md §6, Appendix A.10) and sums
+their rates: the whole-host CPU throughput the GPU is compared with.
+
+Processes are started as ``python -m oracle.cpu_baseline KIND SECONDS`` so that they
+import numpy only (never torch, never the GPU).  The product path never imports this
+module.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _loop(step, seconds):
+    it, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        it += 1
+        el = time.perf_counter() - t0
+        if el > seconds:
+            return it, el
+
+
+def single(seconds):
+    """configs[0]/[1]: J1713 single chain (PulsarBlockGibbs.sample, pulsar_gibbs.py:656-698)."""
+    import numpy as np
+    from oracle import gibbs_oracle as O
+    from pulsar_timing_gibbsspec_amd import synthetic
+    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0)
+    T, N, r = pta.get_basis()[0], pta.get_ndiag({})[0], pta.get_residuals()[0]
+    gwid = np.arange(60)
+    rng = np.random.default_rng(os.getpid())
+    n_tm = T.shape[1] - 60
+    st = dict(x=rng.uniform(-9, -4, 30), b=None)
+
+    def step():
+        TNT, d = O.tnt(T, N, r)                              # recomputed every sweep (:664-665)
+        if st["b"] is None:                                  # first draw from xs (:661-662)
+            st["b"] = O.bdraw_svd(TNT, d, O.phiinv_single(st["x"], n_tm), rng.standard_normal(T.shape[1]))
+        tau = O.tau_half(st["b"], gwid)
+        st["x"] = 0.5 * np.log10(O.rho_analytic(tau, rng.random(30), 1e-18, 1e-8))
+        st["b"] = O.bdraw_svd(TNT, d, O.phiinv_single(st["x"], n_tm), rng.standard_normal(T.shape[1]))
+    return _loop(step, seconds), "J1713 single-chain sweeps (oracle restatement of pulsar_gibbs.py:656-698)"
+
+
+def indep(seconds):
+    """configs[2]: one sweep of every one of the 45 pulsars' PulsarBlockGibbs loops (each
+    pulsar its own free spectrum, pulsar_gibbs.py:656-698) = one array sweep."""
+    import numpy as np
+    from oracle import gibbs_oracle as O
+    from pulsar_timing_gibbsspec_amd import synthetic
+    ptas = synthetic.pulsar_ptas(synthetic.array_pta(kind="indep", seed=0))
+    data = [(p.get_basis()[0], p.get_ndiag({})[0], p.get_residuals()[0]) for p in ptas]
+    rng = np.random.default_rng(os.getpid())
+    xs = [rng.uniform(-9, -4, 30) for _ in data]
+    bs = [None] * len(data)
+    gwid = np.arange(60)
+
+    def step():
+        for p, (T, N, r) in enumerate(data):
+            m = T.shape[1]
+            TNT, d = O.tnt(T, N, r)
+            if bs[p] is None:
+                bs[p] = O.bdraw_svd(TNT, d, O.phiinv_single(xs[p], m - 60), rng.standard_normal(m))
+            xs[p] = 0.5 * np.log10(O.rho_analytic(O.tau_half(bs[p], gwid), rng.random(30), 1e-18, 1e-8))
+            bs[p] = O.bdraw_svd(TNT, d, O.phiinv_single(xs[p], m - 60), rng.standard_normal(m))
+    return _loop(step, seconds), "45-pulsar array sweeps (each pulsar's PulsarBlockGibbs loop, pulsar_gibbs.py:656-698)"
+
+
+def pta(kind, seconds):
+    """configs[3]: PTABlockGibbs.sample (pta_gibbs.py:664-704), SVD draws, 45 pulsars."""
+    import numpy as np
+    from oracle import gibbs_oracle as O
+    from pulsar_timing_gibbsspec_amd import synthetic
+    p_ = synthetic.array_pta(kind=kind, seed=0)
+    T, N, R = p_.get_basis(), p_.get_ndiag({}), p_.get_residuals()
+    P = len(T)
+    names = p_.param_names
+    rind = np.array([i for i, n in enumerate(names) if "rho" in n and "gw" in n])
+    hind = np.array([i for i, n in enumerate(names) if "red" in n and "rho" in n])
+    rng = np.random.default_rng(os.getpid())
+    st = dict(x=rng.uniform(-9, -4, len(names)))
+    m = [t.shape[1] for t in T]
+    gw = [np.arange(mm - 60, mm) for mm in m]
+
+    def draw(x):
+        out = []
+        for p in range(P):
+            TNT, d = O.tnt(T[p], N[p], R[p])                 # reset + recompute (pta_gibbs.py:672-673)
+            phi = 10 ** (2 * x[rind]) + (10 ** (2 * x[hind[p * 30:(p + 1) * 30]]) if kind == "curn_red" else 0)
+            ph = np.full(m[p], 1e-40)
+            ph[gw[p]] = 1 / np.repeat(phi, 2)
+            out.append(O.bdraw_svd(TNT, d, ph, rng.standard_normal(m[p])))
+        return out
+    st["b"] = draw(st["x"])
+
+    def step():
+        x, b = st["x"], st["b"]
+        taus = np.stack([O.tau_full(b[p], gw[p]) for p in range(P)])
+        if kind == "curn_red":
+            rr, _ = O.rho_grid_cdf_red(taus, 10 ** (2 * x[rind]), rng.random((P, 30)), 1e-20, 1e-8)
+            x[hind] = 0.5 * np.log10(rr.ravel())
+        irn = (np.stack([10 ** (2 * x[hind[p * 30:(p + 1) * 30]]) for p in range(P)])
+               if kind == "curn_red" else np.zeros_like(taus))
+        rr, _ = O.rho_grid_cdf_curn(taus, irn, rng.random(30), 1e-18, 1e-8)
+        x[rind] = 0.5 * np.log10(rr)
+        st["b"] = draw(x)
+    return _loop(step, seconds), f"45-pulsar {kind} sweeps (oracle restatement of pta_gibbs.py:664-704)"
+
+
+def config5(seconds):
+    """configs[4]: one pulsar's sweep (10^4 TOAs, m = 216, 20 white MH steps, each
+    recomputing r - T b and the white likelihood as pulsar_gibbs.py:523-546 does); the
+    rate is reported per 200-pulsar array sweep (x 1/200)."""
+    import numpy as np
+    from oracle import gibbs_oracle as O
+    from pulsar_timing_gibbsspec_amd import synthetic
+    d = synthetic.config5_array(n_psr=1, seed=1)
+    T, r, sig, bk = d["T"][0], d["r"][0], d["sigma"][0], d["backend"][0]
+    rng = np.random.default_rng(os.getpid())
+    st = dict(x=d["x0"][0].copy())
+    gw = d["gw_cols"]
+    wind = [w[0] for w in d["white"]]
+    nb = len(wind) // 2
+    lo = np.array([w[3] for w in d["white"]])
+    hi = np.array([w[4] for w in d["white"]])
+    m = T.shape[1]
+
+    def N_of(xx):
+        return O.ndiag_white(sig, bk, xx[[2 * k for k in range(nb)]], xx[[2 * k + 1 for k in range(nb)]])
+
+    def step():
+        x = st["x"]
+        TNT, dd = O.tnt(T, N_of(x), r)
+        ph = np.full(m, 1e-40)
+        ph[:gw.size * 2] = 1 / np.repeat(10 ** (2 * x[gw]), 2)
+        b = O.bdraw_svd(TNT, dd, ph, rng.standard_normal(m))
+        ll0 = O.lnlike_white(r, T, b, N_of(x))
+        for _ in range(20):
+            q = x.copy()
+            j = rng.integers(len(wind))
+            q[wind[j]] += rng.standard_normal() * 0.05 * len(wind) * rng.choice([0.1, 0.5, 1, 3, 10])
+            if lo[j] <= q[wind[j]] <= hi[j]:
+                ll1 = O.lnlike_white(r, T, b, N_of(q))
+                if ll1 - ll0 > np.log(rng.random()):
+                    x, ll0 = q, ll1
+        x[gw] = 0.5 * np.log10(O.rho_analytic(O.tau_half(b, np.arange(2 * gw.size)), rng.random(gw.size),
+                                              d["rhomin"], d["rhomax"]))
+        st["x"] = x
+    (it, el) = _loop(step, seconds)
+    return (it / 200.0, el), ("single-pulsar sweeps (10^4 TOAs, m=216, 20 white MH steps; pulsar_gibbs.py:656-698 + "
+                              ":373-404) scaled to the 200-pulsar array")
+
+
+def _ecorr(seconds, white, aclength=10):
+    """the ECORR sweep (notebook order), optionally with the white MH block."""
+    import numpy as np
+    from oracle import gibbs_oracle as O
+    from pulsar_timing_gibbsspec_amd import synthetic
+    p_ = synthetic.ecorr_pulsar_pta("J1713+0747", seed=0, white_vary=white)
+    T, r = p_.get_basis()[0], p_.get_residuals()[0]
+    names = p_.param_names
+    ebk = p_.signals["J1713+0747_basis_ecorr"].epoch_backend
+    eind = [i for i, n in enumerate(names) if "ecorr" in n]
+    ef_i = [i for i, n in enumerate(names) if n.endswith("efac")]
+    eq_i = [i for i, n in enumerate(names) if "equad" in n]
+    wind = sorted(ef_i + eq_i)
+    gw = np.array([i for i, n in enumerate(names) if "rho" in n])
+    m, ne = T.shape[1], ebk.size
+    gwid = ne + np.arange(2 * gw.size)
+    lo = np.array([0.1 if i in ef_i else -8.5 for i in range(len(names))])
+    hi = np.array([5.0 if i in ef_i else -5.0 for i in range(len(names))])
+    rng = np.random.default_rng(os.getpid())
+    x = np.zeros(len(names))
+    x[ef_i], x[eq_i], x[eind] = 1.0, -7.0, -6.3
+    x[gw] = rng.uniform(-9, -4, gw.size)
+    N_fixed = None if white else p_.get_ndiag()[0]
+    wn = p_.models[0].white[0]
+
+    def N_of(xx):
+        return O.ndiag_white(wn.sigma, wn.backends, xx[ef_i], xx[eq_i]) if white else N_fixed
+
+    def phi(xx):
+        ph = np.full(m, 1e40)
+        ph[:ne] = (10.0 ** (2.0 * xx[eind]))[ebk]
+        ph[gwid] = np.repeat(10.0 ** (2.0 * xx[gw]), 2)
+        return ph
+
+    def prior(ind):
+        return lambda xx: 0.0 if np.all((xx[ind] >= lo[ind]) & (xx[ind] <= hi[ind])) else -np.inf
+
+    def steps(ind):
+        return [(rng.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]), rng.choice(ind),
+                 rng.standard_normal(), rng.random()) for _ in range(aclength)]
+    TNT, dd = O.tnt(T, N_of(x), r)
+    st = dict(x=x, b=O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m)))
+
+    def step():
+        x, b = st["x"], st["b"]
+        if white:
+            x = O.white_mh(x, wind, steps(wind), lambda xx: O.lnlike_white(r, T, b, N_of(xx)), prior(wind))
+        N = N_of(x)
+        TNT, dd = O.tnt(T, N, r)
+
+        def lnl(xx):
+            ph = phi(xx)
+            return O.lnlike_fullmarg(r, N, TNT, dd, 1.0 / ph, np.sum(np.log(ph)))
+        x = O.white_mh(x, eind, steps(eind), lnl, prior(eind))
+        x[gw] = 0.5 * np.log10(O.rho_analytic(O.tau_half(b, gwid), rng.random(gw.size), 1e-18, 1e-8))
+        st["x"], st["b"] = x, O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m))
+    what = "white + ECORR" if white else "ECORR"
+    return _loop(step, seconds), (f"single-chain {what} sweeps (m={m}, {ne} epochs, {aclength} MH steps per block, "
+                                  "oracle restatement of the notebook sampler)")
+
+
+KINDS = {
+    "single": single,
+    "indep": indep,
+    "curn": lambda s: pta("curn", s),
+    "curn_red": lambda s: pta("curn_red", s),
+    "config5": config5,
+    "ecorr": lambda s: _ecorr(s, False),
+    "ecorr_white": lambda s: _ecorr(s, True),
+}
+
+
+def host_cores():
+    """Cores this process may use: the affinity set, capped by the box's CPU share
+    (GS_CPU_CORES, else OMP_NUM_THREADS when it is > 1 -- gpurun sets 16 -- else all)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("GS_CPU_CORES") or (os.environ.get("OMP_NUM_THREADS")
+                                              if int(os.environ.get("OMP_NUM_THREADS", "1")) > 1 else None)
+    return max(1, min(n, int(cap))) if cap else n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def aggregate(kind, seconds, cores=None):
+    """Run ``cores`` single-thread processes of loop ``kind`` at once; return the
+    cpu_baseline record (value = sum of their rates, iterations/s)."""
+    cores = host_cores() if cores is None else int(cores)
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1", MKL_NUM_THREADS="1",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    procs = [subprocess.Popen([sys.executable, "-m", "oracle.cpu_baseline", kind, str(seconds)], cwd=ROOT, env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for _ in range(cores)]
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=seconds * 10 + 300)
+        if p.returncode != 0:
+            raise RuntimeError(f"cpu baseline {kind} failed: {e[-2000:]}")
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    rates = [o["it"] / o["el"] for o in outs]
+    return dict(value=float(sum(rates)), unit="iters/s", cores=cores, kind="port",
+                per_process=float(sum(rates) / len(rates)), cpu=cpu_model(),
+                sample=f"{cores} concurrent single-thread processes x {seconds:.0f} s of {outs[0]['what']}; "
+                       f"value = sum of their rates (numpy/OpenBLAS, OPENBLAS_NUM_THREADS=1 each)")
+
+
+def main():
+    kind, seconds = sys.argv[1], float(sys.argv[2])
+    (it, el), what = KINDS[kind](seconds)
+    print(json.dumps(dict(it=it, el=el, what=what)))
+
+
+if __name__ == "__main__":
+    main()

@@ -322,6 +322,7 @@ class PTAChains:
         self.info = torch.zeros(P * C, dtype=torch.int32, device=dev)
         self.slab_shape = ((2 if self.red else 1), self.n_f, C)
         self.it = 0
+        self.redraw_b = False      # draw b | x first at the next sweep, as at sweep 0 (resume)
 
     def _bdraw(self, z, event, mask):
         m = self.model
@@ -343,9 +344,10 @@ class PTAChains:
         ii = self.it
         check(lib.gs_pta_record(h, self.C, self.n_param, ptr(self.x), ptr(x_rec), ptr(self.xlast)),
               "gs_pta_record")
-        if ii == 0:                                            # pta_gibbs.py:669-670
+        if ii == 0 or self.redraw_b:                           # pta_gibbs.py:669-670
             self._gate_phiinv(with_gate=False)
             self._bdraw(z0, _lib.EV_B0, None)
+            self.redraw_b = False
         check(lib.gs_tau(h, self.P, self.C, m.NF, m.ldb, ptr(m.fidx), ptr(self.b), 0, ptr(self.tau)),
               "gs_tau")
         if self.red:                                           # pta_gibbs.py:252-276

@@ -22,7 +22,8 @@ import torch
 
 from . import _lib
 from .engine import DeviceModel, PTAChains
-from .pulsar_gibbs import _parse_uniform_bounds
+from .plumbing import basis_layout, expand_names, last_match, matching_indices, power_bounds, vector_to_dict
+from .pulsar_gibbs import resolve_seed
 
 
 class PTABlockGibbs(object):
@@ -35,81 +36,61 @@ class PTABlockGibbs(object):
         self.hypersample = hypersample
         self.redsample = redsample
         self.nchains = int(nchains)
-        if not np.any(["basis_ecorr" in key for key in self.pta._signal_dict.keys()]):
+        # the reference only warns here (pta_gibbs.py:62-66)
+        if not any("basis_ecorr" in key for key in pta._signal_dict):
             print("ERROR: Gibbs outlier analysis must use basis_ecorr, not kernel ecorr")
 
-        self._residuals = self.pta.get_residuals()
-        xs = [p.sample() for p in pta.params]
-        self._b = [np.zeros(self.pta.get_basis(xs)[ii].shape[1]) for ii in range(len(self.pta.pulsars))]
+        self._residuals = pta.get_residuals()
+        T0 = pta.get_basis([p.sample() for p in pta.params])
+        self._b = [np.zeros(T0[i].shape[1]) for i in range(len(pta.pulsars))]
         self.TNT = []
         self.d = []
 
-        ind = None
-        for ct, par in enumerate([p.name for p in self.params]):
-            if "rho" in par and "gw" in par:
-                ind = ct
+        # prior bounds (pta_gibbs.py:83-94): the last 'gw'+'rho' parameter, then the last
+        # 'red'+'rho' one -- which, as in the reference, stays the gw parameter when the
+        # model has no red free spectrum
+        pnames = [p.name for p in self.params]
+        ind = last_match(pnames, lambda n: "rho" in n and "gw" in n)
         if ind is None:
             raise UnboundLocalError("no common 'gw' ... 'rho' parameter in the PTA")
-        lo, hi = _parse_uniform_bounds(self.params[ind].params[0])
-        self.rhomin_gw, self.rhomax_gw = 10 ** (2 * lo), 10 ** (2 * hi)
-        for ct, par in enumerate([p.name for p in self.params]):
-            if "rho" in par and "red" in par:
-                ind = ct
-        lo, hi = _parse_uniform_bounds(self.params[ind].params[0])
-        self.rhomin_red, self.rhomax_red = 10 ** (2 * lo), 10 ** (2 * hi)
+        self.rhomin_gw, self.rhomax_gw = power_bounds(self.params[ind].params[0])
+        red = last_match(pnames, lambda n: "rho" in n and "red" in n)
+        self.rhomin_red, self.rhomax_red = power_bounds(self.params[ind if red is None else red].params[0])
 
-        # per-pulsar GW basis indices (pta_gibbs.py:96-109)
-        self.gwid = []
-        for pname in self.pta.pulsars:
-            ct = 0
-            psigs = [sig for sig in self.pta.signals.keys() if pname in sig]
-            for sig in psigs:
-                Fmat = self.pta.signals[sig].get_basis()
-                if "gw" in self.pta.signals[sig].name:
-                    self.gwid.append(ct + np.arange(0, Fmat.shape[1]))
-                if Fmat is not None and "red" not in sig:
-                    ct += Fmat.shape[1]
+        # per-pulsar gw columns, each pulsar's signals walked alone (pta_gibbs.py:96-109)
+        self.gwid = [basis_layout(pta.signals, [k for k in pta.signals if pname in k])[0]
+                     for pname in pta.pulsars]
 
-        self.red_sig = []
-        self.gw_sig = None
-        for sig in self.pta.signals:
-            if "red" in self.pta.signals[sig].name:
-                self.red_sig.append(self.pta.signals[sig])
-            if "gw" in self.pta.signals[sig].name:
-                self.gw_sig = self.pta.signals[sig]
+        sigs = [pta.signals[k] for k in pta.signals]
+        self.red_sig = [s for s in sigs if "red" in s.name]
+        self.gw_sig = next((s for s in reversed(sigs) if "gw" in s.name), None)
 
-        self.ctx = _lib.Context(device, seed=np.random.SeedSequence(seed).generate_state(1, np.uint64)[0]
-                                if seed is not None else 0)
+        self.seed, self._key = resolve_seed(seed)
+        self._device = device
+        self._ctx = None
         self._device_model = None
         self._engine = None
+
+    @property
+    def ctx(self):
+        if self._ctx is None:
+            self._ctx = _lib.Context(self._device, seed=self._key)
+        return self._ctx
 
     # ------------------------------------------------------------ plumbing
     @property
     def params(self):
-        return [p for p in self.pta.params]
+        return list(self.pta.params)
 
     @property
     def param_names(self):
-        ret = []
-        for p in self.params:
-            if p.size:
-                for ii in range(0, p.size):
-                    ret.append(p.name + "_{}".format(ii))
-            else:
-                ret.append(p.name)
-        return ret
+        return expand_names(self.params)
 
     def map_params(self, xs):
-        ret = {}
-        ct = 0
-        for p in self.params:
-            n = p.size if p.size else 1
-            ret[p.name] = xs[ct: ct + n] if n > 1 else float(xs[ct])
-            ct += n
-        return ret
+        return vector_to_dict(self.params, xs)
 
     def _indices(self, pred):
-        return np.array([ct for ct, par in enumerate(self.param_names) if pred(par)])
+        return matching_indices(self.param_names, pred)
 
     def get_rho_param_indices(self):
         return self._indices(lambda par: "rho" in par and "gw" in par)
@@ -223,6 +204,23 @@ class PTABlockGibbs(object):
         eng.it += 1
         return eng.x[0].cpu().numpy()
 
+    # ------------------------------------------------------------ resume state
+    @staticmethod
+    def _save_state(outdir, rows, eng):
+        """gibbs_state.npz next to chain.txt: every chain's x and every (pulsar, chain)
+        b BEFORE sweep ``rows`` -- what resume needs to continue bit for bit (the reference
+        keeps no b on disk, pta_gibbs.py:707-712)."""
+        np.savez(f"{outdir}/gibbs_state.npz", rows=rows, x=eng.x.cpu().numpy(), b=eng.b.cpu().numpy())
+
+    def _load_state(self, outdir, rows, npar):
+        f = f"{outdir}/gibbs_state.npz"
+        if not os.path.exists(f):
+            return None
+        st = np.load(f, allow_pickle=False)
+        if int(st["rows"]) != rows or st["x"].shape != (self.nchains, npar):
+            return None
+        return st
+
     # ------------------------------------------------------------ loop
     def sample(self, xs, outdir="./", niter=10000, resume=False, save_every=100, *, flush_final=False):
         """PTABlockGibbs.sample (pta_gibbs.py:631-713): chain row ii = state before sweep ii;
@@ -240,22 +238,37 @@ class PTABlockGibbs(object):
         self.iter = 0
         start = 0
         x0 = np.asarray(xs, float)
+        state = None
         if resume and os.path.exists(f"{outdir}/chain.txt"):
             print("Resuming from previous run...")
             prev = np.atleast_2d(np.loadtxt(f"{outdir}/chain.txt"))
             start = prev.shape[0]
             self.chain[:start] = prev
             x0 = prev[-1]
+            state = self._load_state(outdir, start, npar)
+            if nc > 1 and os.path.exists(f"{outdir}/chains.npy"):
+                prevc = np.load(f"{outdir}/chains.npy")
+                if prevc.shape[0] == nc and prevc.shape[1] >= start:
+                    self.chains[:, :start] = prevc[:, :start]
         eng = self._new_engine(x0)
         self._engine = eng
         dev = self.ctx.device
         buf = torch.empty(save_every + 1, nc, npar, dtype=torch.float64, device=dev)
         tstart = time.time()
         ii = start
-        if start > 0:                      # resume: redo sweep start-1 from its recorded state
-            eng.it = start - 1
-            eng.sweep()
-            ii = start
+        if start > 0:
+            eng.it = start
+            if state is not None:
+                # the device state saved with these rows (gibbs_state.npz): the run continues
+                # exactly where the uninterrupted one would be
+                eng.x.copy_(torch.as_tensor(state["x"], device=dev))
+                eng.b.copy_(torch.as_tensor(state["b"], device=dev))
+            else:
+                # only chain.txt (e.g. written by the reference): as pta_gibbs.py:642-661,
+                # restart from the last row, which the next sweep records again -- but draw
+                # b | x first (the reference keeps b = 0 there, which makes tau = 0 and the
+                # grid CDF 0/0)
+                eng.redraw_b = True
         while ii < niter:
             nxt = min(niter, (ii // save_every + 1) * save_every + 1)
             for j in range(nxt - ii):
@@ -274,10 +287,12 @@ class PTABlockGibbs(object):
                 np.savetxt(f"{outdir}/chain.txt", self.chain[:last + 1, :])
                 if nc > 1:
                     np.save(f"{outdir}/chains.npy", self.chains[:, :last + 1])
+                self._save_state(outdir, last + 1, eng)
         if flush_final:
             np.savetxt(f"{outdir}/chain.txt", self.chain[:self.iter + 1, :])
             if nc > 1:
                 np.save(f"{outdir}/chains.npy", self.chains[:, :self.iter + 1])
+            self._save_state(outdir, self.iter + 1, eng)
         b = eng.b.cpu().numpy()
         self._b = [b[p * eng.C, :eng.model.m[p]] for p in range(eng.P)]
         if eng.info.cpu().numpy().any():

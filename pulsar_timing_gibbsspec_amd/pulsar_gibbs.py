@@ -40,6 +40,8 @@ from . import _lib
 from .diagnostics import white_aclength
 from .ecorr import EcorrFreeSpectrumChains, EcorrModel, EcorrWhiteChains
 from .engine import DeviceModel, FreeSpectrumChains, HistoryStreamer, grid3
+from .plumbing import (basis_layout, expand_names, last_match, matching_indices, power_bounds,
+                       uniform_bounds, vector_to_dict)
 from .rednoise import (DE_BUFFER, RED_STEPS, RedJumps, RedNoiseChains, powerlaw_loglinear,
                        warmup as red_warmup)
 from .white import MAX_W, WhiteFreeSpectrumChains, WhiteNoiseModel, white_kind
@@ -47,8 +49,123 @@ from .white import MAX_W, WhiteFreeSpectrumChains, WhiteNoiseModel, white_kind
 
 def _parse_uniform_bounds(param):
     """'name:Uniform(pmin=a, pmax=b)[n]' -> (a, b)  (pulsar_gibbs.py:84-87)."""
-    s = str(param).split("(")[1].split(")")[0].split(", ")
-    return float(s[0].split("=")[1]), float(s[1].split("=")[1])
+    return uniform_bounds(param)
+
+
+def resolve_seed(seed):
+    """(seed, Philox key) of a sampler.  seed=None draws fresh OS entropy, as the reference's
+    unseeded global np.random does, so independent jobs never repeat each other's chains; the
+    drawn seed is kept on the sampler (``.seed``) so a run can be reproduced."""
+    if seed is None:
+        seed = int(np.random.SeedSequence().entropy % (1 << 63))
+    return int(seed), int(np.random.SeedSequence(int(seed)).generate_state(1, np.uint64)[0])
+
+
+def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_every, psr_base=0):
+    """The free-spectrum sample loop (PulsarBlockGibbs.sample, pulsar_gibbs.py:620-710) for
+    one or many pulsars at once: pulsar p of ``model`` is ``samplers[p]``'s PTA, its chains
+    are systems p*nchains .. p*nchains + nchains - 1 of one FreeSpectrumChains run (the
+    fused sweep kernel), and its files go to ``outdirs[p]``.
+
+    Per pulsar, exactly the reference's layout: chain row ii = state BEFORE sweep ii (row 0
+    = xs, bchain[0] = 0); chain.npy / bchain.npy rewritten with rows [:ii+1] at ii % 100 == 0,
+    ii > 0 (pulsar_gibbs.py:701-710); with nchains > 1 also chains.npy / bchains.npy.
+    Resume continues from the shortest saved chain of the pulsars: the recorded (x, b) of
+    row start-1 are restored and sweep start-1 re-run with its own Philox counters, so a
+    resumed run reproduces the uninterrupted one bit for bit."""
+    P = len(samplers)
+    nc = samplers[0].nchains
+    ctx = model.ctx
+    dev = ctx.device
+    rhomin, rhomax = samplers[0].rhomin, samplers[0].rhomax
+    m = [int(v) for v in model.m]
+    n_f = model.NF // 2
+    for s in samplers:
+        s.chain = np.zeros((niter, n_f))
+        s.bchain = np.zeros((niter, len(s._b)))
+        s.chains = np.zeros((nc, niter, n_f)) if nc > 1 else None
+        s.bchains = np.zeros((nc, niter, len(s._b))) if nc > 1 else None
+        s.iter = 0
+    start = 0
+    if resume and all(os.path.exists(f"{o}/chain.npy") for o in outdirs):
+        print("Resuming from previous run...")
+        prev = [(np.load(f"{o}/chain.npy"), np.load(f"{o}/bchain.npy")) for o in outdirs]
+        start = min(min(c.shape[0], b.shape[0]) for c, b in prev)
+        for s, (c0, b0) in zip(samplers, prev):
+            s.chain[:start] = c0[:start]
+            s.bchain[:start] = b0[:start]
+        # every chain's rows when the multi-chain files hold them (else all chains restart
+        # from chain 0's recorded state)
+        multi = nc > 1 and all(os.path.exists(f"{o}/chains.npy") and os.path.exists(f"{o}/bchains.npy")
+                               for o in outdirs)
+        if multi:
+            prevc = [(np.load(f"{o}/chains.npy"), np.load(f"{o}/bchains.npy")) for o in outdirs]
+            multi = all(c.shape[0] == nc and min(c.shape[1], b.shape[1]) >= start for c, b in prevc)
+        if multi:
+            for s, (c0, b0) in zip(samplers, prevc):
+                s.chains[:, :start] = c0[:, :start]
+                s.bchains[:, :start] = b0[:, :start]
+    x0 = np.concatenate([np.broadcast_to(np.asarray(x, float), (nc, n_f)) for x in xs_list])
+    ctx.set_option(_lib.OPT_PSR_BASE, int(psr_base))
+    runner = FreeSpectrumChains(model, rhomin, rhomax, nc, x0)
+    if start > 0:
+        for p, s in enumerate(samplers):
+            rows = slice(p * nc, (p + 1) * nc)
+            if multi:
+                runner.x[rows] = torch.as_tensor(s.chains[:, start - 1], device=dev)
+                runner.b[rows, :m[p]] = torch.as_tensor(s.bchains[:, start - 1], device=dev)
+            else:
+                runner.x[rows] = torch.as_tensor(s.chain[start - 1], device=dev)
+                runner.b[rows, :m[p]] = torch.as_tensor(s.bchain[start - 1], device=dev)
+        runner.it = start - 1
+        runner.run(1, record=False)        # re-run sweep start-1: row start-1's successor
+    runner.it = max(runner.it, start)
+    blk = max(1, save_every) + 1
+    # block k+1's sweeps run while block k's rows stream to pinned host memory
+    streamer = HistoryStreamer(ctx, [(blk, P * nc, n_f), (blk, P * nc, model.ldb)])
+
+    def consume(slot, ii, nxt):
+        xh, bh = (t.numpy() for t in streamer.fetch(slot))
+        last = nxt - 1
+        save = last % save_every == 0 and last > 0
+        for p, (s, o) in enumerate(zip(samplers, outdirs)):
+            xp = xh[:, p * nc:(p + 1) * nc]
+            bp = bh[:, p * nc:(p + 1) * nc, :m[p]]
+            s.chain[ii:nxt] = xp[:, 0]
+            s.bchain[ii:nxt] = bp[:, 0]
+            if nc > 1:
+                s.chains[:, ii:nxt] = np.moveaxis(xp, 1, 0)
+                s.bchains[:, ii:nxt] = np.moveaxis(bp, 1, 0)
+            s.iter = last
+            if save:
+                np.save(f"{o}/chain.npy", s.chain[:last + 1, :])
+                np.save(f"{o}/bchain.npy", s.bchain[:last + 1, :])
+                if nc > 1:
+                    np.save(f"{o}/chains.npy", s.chains[:, :last + 1])
+                    np.save(f"{o}/bchains.npy", s.bchains[:, :last + 1])
+
+    ii, slot, pending = start, 0, None
+    while ii < niter:
+        nxt = min(niter, (ii // save_every + 1) * save_every + 1)
+        n = nxt - ii
+        xr, br = streamer.buffers(slot, n)
+        runner.run(n, x_rec=xr, b_rec=br)
+        streamer.submit(slot, n)
+        if pending is not None:
+            consume(*pending)
+        pending = (slot, ii, nxt)
+        slot ^= 1
+        ii = nxt
+    if pending is not None:
+        consume(*pending)
+    info = runner.info.cpu().numpy()
+    if info.any():
+        print(f"WARNING: {int((info != 0).sum())} chains hit a non-positive-definite Sigma")
+    b_end = runner.b.cpu().numpy()
+    for p, s in enumerate(samplers):
+        s._b = b_end[p * nc, :m[p]].copy()
+        s._runner = runner
+    return runner
 
 
 class PulsarBlockGibbs(object):
@@ -59,107 +176,75 @@ class PulsarBlockGibbs(object):
     """
 
     def __init__(self, pta, hypersample="conditional", ecorrsample="mh", psr=None, *,
-                 nchains=1, device=0, seed=None):
+                 nchains=1, device=0, seed=None, ctx=None):
         self.pta = pta
         self.pulsar_name = pta.pulsars[0]
         self.hypersample = hypersample
         self.ecorrsample = ecorrsample
         self.nchains = int(nchains)
 
-        signal_names = [pta.signals[sc].__class__.__name__ for sc in pta.signals]
-        if np.any(["EcorrKernelNoise" in sc for sc in signal_names]):
+        # kernel ECORR is not a Gibbs block (pulsar_gibbs.py:65-68)
+        if any("EcorrKernelNoise" in type(pta.signals[k]).__name__ for k in pta.signals):
             raise TypeError("Gibbs outlier analysis must use basis_ecorr, not kernel ecorr")
 
-        self._residuals = self.pta.get_residuals()[0]
-        xs = [p.sample() for p in pta.params]
-        self._b = np.zeros(self.pta.get_basis(xs)[0].shape[1])
-
+        self._residuals = pta.get_residuals()[0]
+        self._b = np.zeros(pta.get_basis([p.sample() for p in pta.params])[0].shape[1])
         self.TNT = None
         self.d = None
 
-        # prior bounds of the free-spectrum powers (pulsar_gibbs.py:82-87)
-        ind = None
-        for ct, par in enumerate([p.name for p in self.params]):
-            if "rho" in par and "gw" in par:
-                ind = ct
+        # free-spectrum prior: the last 'gw' + 'rho' parameter (pulsar_gibbs.py:82-87)
+        ind = last_match([p.name for p in self.params], lambda n: "rho" in n and "gw" in n)
         if ind is None:
             raise UnboundLocalError("no gw free-spectrum ('gw' ... 'rho') parameter in the PTA")
-        lo, hi = _parse_uniform_bounds(self.params[ind].params[0])
-        self.rhomin, self.rhomax = 10 ** (2 * lo), 10 ** (2 * hi)
+        self.rhomin, self.rhomax = power_bounds(self.params[ind].params[0])
 
-        # basis indices of the GW (and ECORR) processes (pulsar_gibbs.py:89-109)
-        ct = 0
-        self.b_param_names = []
-        self.gwid = None
-        self.ecid = None
-        for sig in self.pta.signals:
-            Fmat = self.pta.signals[sig].get_basis()
-            if "gw" in self.pta.signals[sig].name:
-                self.gwid = ct + np.arange(0, Fmat.shape[1])
-            if "ecorr" in self.pta.signals[sig].name:
-                self.ecid = ct + np.arange(0, Fmat.shape[1])
-            if Fmat is not None and "red" not in sig:
-                ct += Fmat.shape[1]
-                self.b_param_names += [sig + "_" + str(ii) for ii in range(Fmat.shape[1])]
-        if ct == self.pta.get_basis()[0].shape[1]:
-            print("Basis count is good")
-        else:
-            print("WARNING: Miscounted basis entries. Maybe red noise and GW do not share a design matrix.")
+        # columns of the gw (and ECORR) blocks in T (pulsar_gibbs.py:89-109)
+        self.gwid, self.ecid, self.b_param_names, ncol = basis_layout(pta.signals)
+        print("Basis count is good" if ncol == pta.get_basis()[0].shape[1] else
+              "WARNING: Miscounted basis entries. Maybe red noise and GW do not share a design matrix.")
 
         if self.ecid is not None:
-            # prior bounds of the ECORR parameters (pulsar_gibbs.py:111-118)
-            ind = None
-            for ct, par in enumerate([p.name for p in self.params]):
-                if "ecorr" in par:
-                    ind = ct
-            lo, hi = _parse_uniform_bounds(self.params[ind].params[0])
-            self.ecorrmin, self.ecorrmax = 10 ** (2 * lo), 10 ** (2 * hi)
+            # ECORR prior: the last 'ecorr' parameter (pulsar_gibbs.py:111-118)
+            ind = last_match([p.name for p in self.params], lambda n: "ecorr" in n)
+            self.ecorrmin, self.ecorrmax = power_bounds(self.params[ind].params[0])
             if self.ecorrsample == "conditional":
                 # the reference's epoch selection needs enterprise's selections.by_backend
                 # (:121-127) and its conditional draw is commented out ('NEEDS TO BE FIXED')
                 raise NotImplementedError("ecorrsample='conditional' is not implemented in the reference")
 
-        self.red_sig = None
-        self.gw_sig = None
-        for sig in self.pta.signals:
-            if "red" in self.pta.signals[sig].name:
-                self.red_sig = self.pta.signals[sig]
-            if "gw" in self.pta.signals[sig].name:
-                self.gw_sig = self.pta.signals[sig]
+        # the last signal named 'red' / 'gw' (pulsar_gibbs.py:130-136)
+        sigs = [pta.signals[k] for k in pta.signals]
+        self.red_sig = next((s for s in reversed(sigs) if "red" in s.name), None)
+        self.gw_sig = next((s for s in reversed(sigs) if "gw" in s.name), None)
 
-        # ---- device side
-        self.ctx = _lib.Context(device, seed=np.random.SeedSequence(seed).generate_state(1, np.uint64)[0]
-                                if seed is not None else 0)
+        # ---- device side (the context is created on first use: the plumbing above
+        # needs no GPU)
+        self.seed, self._key = resolve_seed(seed)
+        self._device = device
+        self._ctx = ctx
         self._ndraw = 0
         self._device_model = None
+
+    @property
+    def ctx(self):
+        if self._ctx is None:
+            self._ctx = _lib.Context(self._device, seed=self._key)
+        return self._ctx
 
     # ------------------------------------------------------------ plumbing
     @property
     def params(self):
-        return [p for p in self.pta.params]
+        return list(self.pta.params)
 
     @property
     def param_names(self):
-        ret = []
-        for p in self.params:
-            if p.size:
-                for ii in range(0, p.size):
-                    ret.append(p.name + "_{}".format(ii))
-            else:
-                ret.append(p.name)
-        return ret
+        return expand_names(self.params)
 
     def map_params(self, xs):
-        ret = {}
-        ct = 0
-        for p in self.params:
-            n = p.size if p.size else 1
-            ret[p.name] = xs[ct: ct + n] if n > 1 else float(xs[ct])
-            ct += n
-        return ret
+        return vector_to_dict(self.params, xs)
 
     def _indices(self, pred):
-        return np.array([ct for ct, par in enumerate(self.param_names) if pred(par)])
+        return matching_indices(self.param_names, pred)
 
     def get_gwrho_param_indices(self):
         return self._indices(lambda par: "rho" in par)
@@ -620,72 +705,7 @@ class PulsarBlockGibbs(object):
             if flush_final:
                 self._flush(outdir)
             return out
-        model = self._model(xs)
-        nc = self.nchains
-        self.chain = np.zeros((niter, len(xs)))
-        self.bchain = np.zeros((niter, len(self._b)))
-        self.chains = np.zeros((nc, niter, len(xs))) if nc > 1 else None
-        self.bchains = np.zeros((nc, niter, len(self._b))) if nc > 1 else None
-        self.iter = 0
-        start = 0
-        x0 = np.asarray(xs, float)
-        if resume and os.path.exists(f"{outdir}/chain.npy"):
-            print("Resuming from previous run...")
-            c0 = np.load(f"{outdir}/chain.npy")
-            b0 = np.load(f"{outdir}/bchain.npy")
-            start = min(c0.shape[0], b0.shape[0])
-            self.chain[:start] = c0[:start]
-            self.bchain[:start] = b0[:start]
-        runner = FreeSpectrumChains(model, self.rhomin, self.rhomax, nc, x0)
-        if start > 0:
-            runner.x.copy_(torch.as_tensor(self.chain[start - 1][None, :], device=self.ctx.device)
-                           .expand(nc, -1))
-            runner.b[:, :model.m[0]] = torch.as_tensor(self.bchain[start - 1], device=self.ctx.device)
-            runner.it = start - 1
-            # re-run sweep start-1 so row start-1's successor state is regenerated
-            runner.run(1, record=False)
-        runner.it = max(runner.it, start)
-        m = int(model.m[0])
-        blk = max(1, save_every) + 1
-        # block k+1's sweeps run while block k's rows stream to pinned host memory
-        streamer = HistoryStreamer(self.ctx, [(blk, nc, runner.n_f), (blk, nc, model.ldb)])
-
-        def consume(slot, ii, nxt):
-            xh, bh = (t.numpy() for t in streamer.fetch(slot))
-            bh = bh[:, :, :m]
-            self.chain[ii:nxt] = xh[:, 0]
-            self.bchain[ii:nxt] = bh[:, 0]
-            if nc > 1:
-                self.chains[:, ii:nxt] = np.moveaxis(xh, 1, 0)
-                self.bchains[:, ii:nxt] = np.moveaxis(bh, 1, 0)
-            self.iter = nxt - 1
-            last = nxt - 1
-            if last % save_every == 0 and last > 0:
-                np.save(f"{outdir}/chain.npy", self.chain[:last + 1, :])
-                np.save(f"{outdir}/bchain.npy", self.bchain[:last + 1, :])
-                if nc > 1:
-                    np.save(f"{outdir}/chains.npy", self.chains[:, :last + 1])
-                    np.save(f"{outdir}/bchains.npy", self.bchains[:, :last + 1])
-
-        ii, slot, pending = start, 0, None
-        while ii < niter:
-            nxt = min(niter, (ii // save_every + 1) * save_every + 1)
-            n = nxt - ii
-            xr, br = streamer.buffers(slot, n)
-            runner.run(n, x_rec=xr, b_rec=br)
-            streamer.submit(slot, n)
-            if pending is not None:
-                consume(*pending)
-            pending = (slot, ii, nxt)
-            slot ^= 1
-            ii = nxt
-        if pending is not None:
-            consume(*pending)
-        info = runner.info.cpu().numpy()
-        if info.any():
-            print(f"WARNING: {int((info != 0).sum())} chains hit a non-positive-definite Sigma")
-        self._b = runner.b[0, :m].cpu().numpy()
-        self._runner = runner
+        sample_free_spectrum([self], self._model(xs), [xs], [outdir], niter, resume, save_every)
         if flush_final:
             self._flush(outdir)
         return self.chain

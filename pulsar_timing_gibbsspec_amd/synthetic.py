@@ -442,14 +442,21 @@ def ecorr_pulsar_pta(psr="J1713+0747", n_epoch=160, n_sub=(1, 6), n_backends=2, 
     return PTA([PulsarModel(psr, toas, r, [white, ecorr, gw, tm])])
 
 
-def array_pta(kind="curn_red",n_f=30, n_psr=None, gw_prior=(-9.0, -4.0), red_prior=(-10.0, -4.0),
+def array_pta(kind="curn_red", n_f=30, n_psr=None, gw_prior=(-9.0, -4.0), red_prior=(-10.0, -4.0),
               log10_A=np.log10(2e-15), gamma=13.0 / 3.0, seed=0):
     """Config 3/4 models over the simulated array (model_definition.py:184-234 order: TM, CRN, red, white).
 
     kind = 'curn'      common 'gw_crn' free spectrum only,
-           'curn_red'  + per-pulsar 'red_noise' free spectrum on the same basis.
-    Common Tspan = the array's span (model_utils.get_tspan).
+           'curn_red'  + per-pulsar 'red_noise' free spectrum on the same basis,
+           'indep'     BASELINE configs[2]: no common process; every pulsar carries its
+                       own 'gw' free spectrum ``{psr}_gw_log10_rho`` on its own T_span
+                       (config 1's model for each of the 45 pulsars: signals white, gw,
+                       TM -> T = [F | M]); ``pulsar_ptas`` splits it into the single-pulsar
+                       PTAs that PulsarBlockGibbs takes.
+    Common Tspan = the array's span (model_utils.get_tspan) for the CURN kinds.
     """
+    if kind == "indep":
+        return _indep_array(n_f, n_psr, gw_prior, log10_A, gamma, seed)
     rng = np.random.default_rng(seed)
     data = load_simulated_array()
     names = sorted(data)[: n_psr or len(data)]
@@ -474,6 +481,30 @@ def array_pta(kind="curn_red",n_f=30, n_psr=None, gw_prior=(-9.0, -4.0), red_pri
                                 log10_A, gamma, red=(-14.5, 3.0) if kind == "curn_red" else None)
         models.append(PulsarModel(n, toas, r, sigs))
     return PTA(models)
+
+
+def _indep_array(n_f, n_psr, gw_prior, log10_A, gamma, seed):
+    rng = np.random.default_rng(seed)
+    data = load_simulated_array()
+    names = sorted(data)[: n_psr or len(data)]
+    models = []
+    for n in names:
+        d = data[n]
+        toas = d["mjd"] * DAY
+        err = d["err_us"] * 1e-6
+        Tspan = toas.max() - toas.min()                      # the pulsar's own span
+        rho = Uniform(f"{n}_gw_log10_rho", gw_prior[0], gw_prior[1], size=n_f)
+        gw = FourierGP(n, "gw", toas, Tspan, n_f, "spectrum", [rho])
+        tm = TimingModelGP(n, synthetic_design_matrix(toas, d["nfit"] + 1, d["pb_days"]), use_svd=True)
+        r = _simulate_residuals(rng, gw.get_basis(), gw.freqs, Tspan, tm.get_basis(), err, log10_A, gamma)
+        models.append(PulsarModel(n, toas, r, [MeasurementNoise(n, err), gw, tm]))
+    return PTA(models)
+
+
+def pulsar_ptas(pta):
+    """One single-pulsar PTA per pulsar of ``pta`` (what PulsarBlockGibbs takes, one
+    pulsar's signals and parameters each)."""
+    return [PTA([m]) for m in pta.models]
 
 
 def config5_array(n_psr=200, n_toa=10_000, n_f=100, n_tm=16, n_bk=4, span_yr=15.0, seed=0,

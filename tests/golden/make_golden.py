@@ -489,10 +489,41 @@ def ecorr_white_mh(ref, out, nsweep=5, acl_w=12, acl_e=12, nlike=6):
     print("ecorr+white:", out, len(log))
 
 
+def indep_runs(ref, out, niter=60, picks=("B1937+21", "J1455-3330", "J1909-3744")):
+    """BASELINE configs[2]: 45 independent pulsars, each its own PulsarBlockGibbs
+    (pulsar_gibbs.py:620-710) on its own free spectrum.  The reference has no array
+    sampler, so a user runs PulsarBlockGibbs per pulsar; this fixture runs the reference
+    on three of them (the smallest, a middle and the largest m: 68, 74, 77) with every
+    draw captured."""
+    pta = synthetic.array_pta(kind="indep", seed=0)
+    ptas = synthetic.pulsar_ptas(pta)
+    names = [p.pulsars[0] for p in ptas]
+    rec = dict(pulsars=np.array(names), picks=np.array([names.index(n) for n in picks]))
+    for k, n in enumerate(picks):
+        pp = ptas[names.index(n)]
+        np.random.seed(100 + k)
+        g = _quiet(ref.PulsarBlockGibbs, pp)
+        x0 = np.concatenate([p.sample().flatten() for p in g.params])
+        with tempfile.TemporaryDirectory() as d, Capture() as cap:
+            np.random.seed(200 + k)
+            _quiet(g.sample, x0, outdir=d, niter=niter)
+        rec.update({f"p{k}_T": pp.get_basis()[0], f"p{k}_Nvec": pp.get_ndiag({})[0],
+                    f"p{k}_r": pp.get_residuals()[0], f"p{k}_x0": x0, f"p{k}_z": np.stack(cap.take("randn")),
+                    f"p{k}_U": np.stack(cap.take("uniform")), f"p{k}_chain": g.chain,
+                    f"p{k}_bchain": g.bchain, f"p{k}_b_final": g._b, f"p{k}_gwid": np.asarray(g.gwid),
+                    f"p{k}_rhomin": g.rhomin, f"p{k}_rhomax": g.rhomax,
+                    f"p{k}_param_names": np.array(g.param_names)})
+    np.savez_compressed(out, niter=niter, **rec)
+    print("indep:", out, [rec[f"p{k}_z"].shape for k in range(len(picks))])
+
+
 def main(root):
     mods = load_reference(root)
     PB = mods["pulsar_gibbs"]
     PT = mods["pta_gibbs"]
+    if "--only-indep" in sys.argv:
+        indep_runs(PB, os.path.join(HERE, "indep_array.npz"))
+        return
     if "--only-ecorr-white" in sys.argv:
         ecorr_white_mh(PB, os.path.join(HERE, "ecorr_white_j1713.npz"))
         return
@@ -514,6 +545,7 @@ def main(root):
     red_likelihood(PB, os.path.join(HERE, "red_lnlike_j1713.npz"))
     ecorr_mh(PB, os.path.join(HERE, "ecorr_mh_j1713.npz"))
     ecorr_white_mh(PB, os.path.join(HERE, "ecorr_white_j1713.npz"))
+    indep_runs(PB, os.path.join(HERE, "indep_array.npz"))
     if "--long" in sys.argv:
         single_pulsar_long(PB, os.path.join(HERE, "long_j1713.npz"))
         ecorr_long(PB, os.path.join(HERE, "ecorr_long_j1713.npz"))

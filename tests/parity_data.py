@@ -12,20 +12,29 @@ import numpy as np
 
 from oracle import gibbs_oracle as O
 
-ZC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "single_j1713_zc.npz")
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+ZC_FILE = os.path.join(GOLDEN, "single_j1713_zc.npz")
+INDEP_ZC_FILE = os.path.join(GOLDEN, "indep_array_zc.npz")
 
 
-def single_replay(g, committed=True):
+def single_replay(g, committed=True, zc_file=ZC_FILE, key="zc"):
     """single_replay_compute with the rotated normals taken from the committed fixture
     (tests/golden/make_rotated.py) when ``committed``: the rotation's SVD depends on the
     host's BLAS in its last bits, the committed values do not."""
     R = single_replay_compute(g)
     if committed:
-        zc = np.load(ZC_FILE, allow_pickle=False)["zc"]
+        zc = np.load(zc_file, allow_pickle=False)[key]
         if zc.shape != R["zc"].shape:
-            raise ValueError(f"{ZC_FILE}: zc {zc.shape} does not match the fixture ({R['zc'].shape})")
+            raise ValueError(f"{zc_file}: {key} {zc.shape} does not match the fixture ({R['zc'].shape})")
         R["zc"] = zc
     return R
+
+
+def indep_pick(g, k):
+    """Pulsar k of the configs[2] fixture (tests/golden/indep_array.npz) as a
+    single-pulsar fixture dict (the keys of single_j1713.npz)."""
+    pre = f"p{k}_"
+    return {n[len(pre):]: g[n] for n in g.files if n.startswith(pre)}
 
 
 def single_replay_compute(g):
@@ -176,12 +185,23 @@ def exact_chol_draw(T, Nvec, r, phiinv, zc, order):
     'exact' value for systems so ill-conditioned (cond(S) ~ 5e7) that any two fp64
     implementations (numpy, the device, the reference's SVD) already differ by
     ~5e-10 relative and a chain's rho feedback amplifies that."""
+    return exact_chol_draw_pre(exact_tnt(T, Nvec, r), phiinv, zc, order)
+
+
+def exact_tnt(T, Nvec, r):
+    """(TNT, d) in x87 long double (for exact_chol_draw_pre: computed once per pulsar)."""
     L_ = np.longdouble
     Tl = np.asarray(T, dtype=L_)
     w = 1 / np.asarray(Nvec, dtype=L_)
-    A = Tl.T @ (Tl * w[:, None])
+    return Tl.T @ (Tl * w[:, None]), Tl.T @ (np.asarray(r, dtype=L_) * w)
+
+
+def exact_chol_draw_pre(tnt_l, phiinv, zc, order):
+    """exact_chol_draw from a long-double (TNT, d) pair."""
+    L_ = np.longdouble
+    A = tnt_l[0].copy()
+    dv = tnt_l[1]
     A[np.diag_indices_from(A)] += np.asarray(phiinv, dtype=L_)
-    dv = Tl.T @ (np.asarray(r, dtype=L_) * w)
     A = A[np.ix_(order, order)]
     m = A.shape[0]
     L = np.zeros_like(A)

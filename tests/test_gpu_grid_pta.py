@@ -186,6 +186,37 @@ def test_pta_block_gibbs_surface(tmp_path):
     assert len(b) == 6 and all(np.all(np.isfinite(bb)) for bb in b)
 
 
+def test_pta_resume(tmp_path):
+    """PTABlockGibbs resume (pta_gibbs.py:642-661): with the device state saved next to
+    chain.txt the resumed run equals the uninterrupted one bit for bit (every chain); from
+    chain.txt alone (the reference's own files) b is redrawn from the last row first, so the
+    resumed rows stay finite and inside the prior instead of the reference's b = 0 ->
+    tau = 0 -> 0/0 CDF -> every common rho pinned to the top grid point."""
+    import os
+    from pulsar_timing_gibbsspec_amd import PTABlockGibbs, synthetic
+    pta = synthetic.array_pta(kind="curn_red", n_psr=5, seed=3)
+
+    def new():
+        return PTABlockGibbs(pta, hypersample="conditional", redsample="conditional", nchains=4, seed=9)
+    x0 = np.concatenate([p.sample().flatten() for p in new().params])
+    full = new()
+    full.sample(x0, outdir=str(tmp_path / "a"), niter=230)
+    part = new()
+    part.sample(x0, outdir=str(tmp_path / "b"), niter=150)            # saves rows [:101] + state
+    res = new()
+    chain = res.sample(x0, outdir=str(tmp_path / "b"), niter=230, resume=True)
+    assert np.array_equal(chain, full.chain)
+    assert np.array_equal(res.chains, full.chains)
+    os.remove(tmp_path / "b" / "gibbs_state.npz")
+    np.savetxt(tmp_path / "b" / "chain.txt", full.chain[:101])
+    cold = new()
+    c2 = cold.sample(x0, outdir=str(tmp_path / "b"), niter=160, resume=True)
+    assert np.array_equal(c2[101], c2[100])                            # the reference's repeated row
+    gw = c2[102:, cold.get_rho_param_indices()]
+    assert np.all(np.isfinite(gw)) and gw.min() >= -9.0 and gw.max() <= -4.0
+    assert not np.all(gw == gw.max())                                  # not pinned to rho_max
+
+
 @pytest.mark.parametrize("kind", ["curn", "curn_red"])
 def test_pulsar_sharded_engine_bit_identical(kind):
     """Two pulsar shards (own context, own DeviceModel) exchanging [tau | x_red] slabs

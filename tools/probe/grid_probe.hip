@@ -1,0 +1,103 @@
+// Ceiling of the free-spectrum grid conditionals (pta_gibbs.py:189-212, 254-274) on gfx950:
+// how many grid-point evaluations per second the chip sustains for the per-point op mix
+// of the device kernels, with no memory traffic at all (operands in registers, every CU
+// busy, 8 waves per SIMD).  This is the "peak" the bench prices the grid kernels against
+// (MI355X_MICROARCH.md has no fp64 transcendental rate).
+//
+//   red  : ratio = tau * rcp(gw + rho_g) (+ 2 Newton steps); cdf += ratio * exp(-ratio/2) * ln10
+//          -- k_rho_red's per-point work (one fp64 exp per point)
+//   curn : a = irn + rho_g; sr += tau * rcp(a) (+ 2 Newton); prod *= a
+//          -- k_rho_curn_fast's per-(point, pulsar) work (no transcendental)
+//
+// Build: hipcc --offload-arch=gfx950 -O3 tools/probe/grid_probe.hip -o tools/probe/grid_probe
+// Run:   tools/probe/grid_probe  -> one JSON line
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+constexpr double LN10 = 2.302585092994045684017991454684364208;
+
+__device__ __forceinline__ double rcp_nr(double a) {
+  double r = __builtin_amdgcn_rcp(a);
+  r = fma(r, fma(-a, r, 1.0), r);
+  return fma(r, fma(-a, r, 1.0), r);
+}
+
+// each thread: 8 independent rows x npts grid points
+__global__ __launch_bounds__(256) void k_red(int npts, double q, double* out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  double tau[8], cum[8];
+  for (int j = 0; j < 8; ++j) {
+    tau[j] = 1e-14 * (1.0 + 0.01 * ((t + j) & 255));
+    cum[j] = 0.0;
+  }
+  double rg = 1e-20;
+  const double gw = 3e-15;
+  for (int g = 0; g < npts; ++g) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double ratio = tau[j] * rcp_nr(gw + rg);
+      cum[j] += ratio * exp(-ratio / 2) * LN10;
+    }
+    rg *= q;
+  }
+  double s = 0.0;
+  for (int j = 0; j < 8; ++j) s += cum[j];
+  if (s == 1.2345) out[t] = s;  // keep the work alive
+}
+
+__global__ __launch_bounds__(256) void k_curn(int npts, double q, double* out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  double sr[8], prod[8], rg[8];
+  for (int j = 0; j < 8; ++j) {
+    sr[j] = 0.0;
+    prod[j] = 1.0;
+    rg[j] = 1e-18 * (1.0 + j);
+  }
+  const double tau = 1e-14 * (1.0 + 0.01 * (t & 255));
+  for (int p = 0; p < npts; ++p) {
+    const double irn = 1e-15 * (1.0 + 1e-3 * p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double a = irn + rg[j];
+      sr[j] = fma(tau, rcp_nr(a), sr[j]);
+      prod[j] *= a;
+    }
+    if ((p & 7) == 7)
+      for (int j = 0; j < 8; ++j) prod[j] = __builtin_amdgcn_frexp_mant(prod[j]);
+  }
+  double s = 0.0;
+  for (int j = 0; j < 8; ++j) s += sr[j] + prod[j];
+  if (s == 1.2345) out[t] = s;
+}
+
+int main() {
+  int dev = 0, ncu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int blocks = ncu * 8;  // 8 x 256 threads per CU = 8 waves per SIMD
+  const int npts = 4000;
+  double* out;
+  (void)hipMalloc(&out, sizeof(double) * blocks * 256);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  double rates[2];
+  for (int kind = 0; kind < 2; ++kind) {
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; ++rep) {
+      (void)hipEventRecord(e0, 0);
+      if (kind == 0)
+        hipLaunchKernelGGL(k_red, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
+      else
+        hipLaunchKernelGGL(k_curn, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
+      (void)hipEventRecord(e1, 0);
+      (void)hipEventSynchronize(e1);
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (rep > 0 && ms < best) best = ms;
+    }
+    rates[kind] = (double)blocks * 256 * 8 * npts / (best * 1e-3);
+  }
+  printf("{\"cus\": %d, \"red_evals_per_s\": %.6e, \"curn_pulsar_terms_per_s\": %.6e}\n", ncu, rates[0], rates[1]);
+  return 0;
+}
