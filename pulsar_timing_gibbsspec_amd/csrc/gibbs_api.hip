@@ -239,7 +239,8 @@ __global__ void k_philox(int64_t n, const uint32_t* ctr, uint32_t* out, gs_key k
   out[4 * i + 3] = w.w;
 }
 
-bool nf_supported(int NF) { return NF == 20 || NF == 40 || NF == 60; }
+// register-tile b draw / fused sweep / likelihood: any even NF <= 64 (one lane per column)
+bool nf_supported(int NF) { return NF > 0 && NF <= 64 && (NF % 2) == 0; }
 
 }  // namespace
 
@@ -366,7 +367,7 @@ int gs_prefix_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const gs
   if (n_psr < 0) return fail_arg(2, "n_psr < 0");
   if (n_chain < 0) return fail_arg(3, "n_chain < 0");
   if (NF <= 0 || NF > 254 || (NF & 1)) return fail_arg(4, "NF must be even and <= 254");
-  if (NMX <= 0 || NMX > 64) return fail_arg(5, "NMX must be in 1..64");
+  if (NMX < 0 || NMX > 64) return fail_arg(5, "NMX must be in 0..64");
   if (!desc) return fail_arg(6, "desc is NULL");
   if (tnt_cstride < 0) return fail_arg(7, "tnt_cstride < 0");
   if (d_cstride < 0) return fail_arg(8, "d_cstride < 0");
@@ -388,7 +389,7 @@ int gs_prefix(gs_ctx* ctx, int n_psr, int NF, int NMX, const gs_prefix_desc* des
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_psr < 0) return fail_arg(2, "n_psr < 0");
   if (NF <= 0 || NF > 254 || (NF & 1)) return fail_arg(3, "NF must be even and <= 254");
-  if (NMX <= 0 || NMX > 64) return fail_arg(4, "NMX must be in 1..64");
+  if (NMX < 0 || NMX > 64) return fail_arg(4, "NMX must be in 0..64");
   if (!desc || !TNT || !d || !fidx || !midx || !phiinv_fixed || !model)
     return fail_arg(5, "NULL array");
   return gs_prefix_sys(ctx, n_psr, 1, NF, NMX, desc, 0, 0, TNT, d, fidx, midx, phiinv_fixed, model, info);
@@ -401,8 +402,8 @@ static int bdraw_impl(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
   const bool big = big_nf_supported(NF);
-  if (!nf_supported(NF) && !big) return fail_arg(4, "NF must be 20, 40, 60 or even in 66..254");
-  if (NMX <= 0 || NMX > 64) return fail_arg(5, "NMX must be in 1..64");
+  if (!nf_supported(NF) && !big) return fail_arg(4, "NF must be even and <= 254");
+  if (NMX < 0 || NMX > 64) return fail_arg(5, "NMX must be in 0..64");
   if (ldb < NF + 1) return fail_arg(6, "ldb too small");
   if (!model || !fidx || !midx || !nm || !phiinv_F || !b) return fail_arg(7, "NULL array");
   if (n_psr == 0 || n_chain == 0) return 0;
@@ -498,8 +499,8 @@ int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
                       const double* u_inj, int32_t* info) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
-  if (!nf_supported(NF)) return fail_arg(4, "NF must be one of 20, 40, 60");
-  if (NMX <= 0 || NMX > 64) return fail_arg(5, "NMX must be in 1..64");
+  if (!nf_supported(NF)) return fail_arg(4, "NF must be even and <= 64");
+  if (NMX < 0 || NMX > 64) return fail_arg(5, "NMX must be in 0..64");
   if (ldb < NF + 1) return fail_arg(6, "ldb too small");
   if (!model || !fidx || !midx || !nm) return fail_arg(7, "NULL model array");
   if (!(rhomin > 0.0) || !(rhomax > rhomin)) return fail_arg(11, "need 0 < rhomin < rhomax");
@@ -563,8 +564,8 @@ int gs_lnlike_marg(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const d
                    int model_per_sys, const int32_t* nm, const double* phiinv_F, double* lnl, int32_t* info) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
-  if (!nf_supported(NF)) return fail_arg(4, "NF must be 20, 40 or 60");
-  if (NMX <= 0 || NMX > 64) return fail_arg(5, "NMX must be in 1..64");
+  if (!nf_supported(NF)) return fail_arg(4, "NF must be even and <= 64");
+  if (NMX < 0 || NMX > 64) return fail_arg(5, "NMX must be in 0..64");
   if (!model || !nm || !phiinv_F || !lnl) return fail_arg(6, "NULL array");
   if (n_psr == 0 || n_chain == 0) return 0;
   LnlArgs a;

@@ -175,14 +175,18 @@ __device__ __forceinline__ int bdraw_wave(const ModelLds& M, int NMX, int nM, in
   return fail;
 }
 
-// One b|rho draw with the variant BC (tile MFMA or lane-row broadcast).
-template <int NF, int BC>
+// One b|rho draw with the variant BC (tile MFMA or lane-row broadcast).  NFC > 0: the
+// fixed-NF instantiations (20 / 40 / 60, every variant); NFC == 0: any even NF < 16 NTC at
+// run time (tile variant only).
+template <int NFC, int NTC, int BC>
 __device__ __forceinline__ int bdraw_sys(const ModelLds& M, int NMX, int nM, int lane, double phinv,
-                                         double zF, double zM, double& bF, double& bM, double* scr) {
-  if constexpr (BC == GS_BCAST_TILE)
-    return bdraw_tile<NF>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
+                                         double zF, double zM, double& bF, double& bM, double* scr, int NF) {
+  if constexpr (NFC == 0)
+    return bdraw_tile_n<NTC>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
+  else if constexpr (BC == GS_BCAST_TILE)
+    return bdraw_tile<NFC>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
   else
-    return bdraw_wave<NF, BC>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
+    return bdraw_wave<NFC, BC>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
 }
 
 // Copy a pulsar's model block into LDS (whole workgroup).
@@ -192,9 +196,10 @@ __device__ __forceinline__ void stage_model(double* lds, const double* g, int64_
 }
 
 // ------------------------------------------------------------ batched b draw
-template <int NF, int WPB, int BC>
+template <int NFC, int NTC, int WPB, int BC>
 __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
   extern __shared__ double lds[];
+  const int NF = NFC ? NFC : A.NF;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nb = (A.n_chain + WPB - 1) / WPB;
   const int p = blockIdx.x / nb;
@@ -220,7 +225,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
   }
   double bF = 0.0, bM = 0.0;
   double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * GS_SCR_DOUBLES(BC);
-  const int fail = bdraw_sys<NF, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
+  const int fail = bdraw_sys<NFC, NTC, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
   if (lane < NF) A.b[sys * A.ldb + fi] = bF;
   if (lane < nM) A.b[sys * A.ldb + mi] = bM;
   if (A.info && lane == 0) A.info[sys] = fail;
@@ -232,9 +237,10 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
 // with the prefix: d^T Sigma^-1 d = |e|^2 + |y|^2, log det Sigma = 2 sum log diag L_M +
 // log det S; |y|^2 and log det S come out of the augmented tile factorisation.  The
 // model constants -1/2 (log det N + r^T N^-1 r) - 1/2 sum_M log phi_M are the caller's.
-template <int NF, int WPB>
+template <int NFC, int NTC, int WPB>
 __global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
   extern __shared__ double lds[];
+  const int NF = NFC ? NFC : A.NF;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nb = (A.n_chain + WPB - 1) / WPB;
   const int p = blockIdx.x / nb;
@@ -247,7 +253,11 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
   const double phinv = lane < NF ? A.phiinv_F[sys * NF + lane] : 1.0;
   double yy = 0.0, ldS = 0.0;
   double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * GS_TILE_SCR;
-  const int fail = bdraw_tile<NF, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr);
+  int fail;
+  if constexpr (NFC == 0)
+    fail = bdraw_tile_n<NTC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr, NF);
+  else
+    fail = bdraw_tile<NFC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr);
   double lph = lane < NF ? log(phinv) : 0.0;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) lph += __shfl_xor(lph, o);
@@ -260,10 +270,11 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
 }
 
 // ------------------------------------------------------------ fused sweep
-template <int NF, int WPB, int BC>
+template <int NFC, int NTC, int WPB, int BC>
 __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepArgs A) {
   extern __shared__ double lds[];
-  constexpr int NFR = NF / 2;
+  const int NF = NFC ? NFC : A.NF;
+  const int NFR = NF / 2;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nb = (A.n_chain + WPB - 1) / WPB;
   const int p = blockIdx.x / nb;
@@ -356,7 +367,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
       }
       if (pass == 0) phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;  // first draw from xs
       GS_PH(7)
-      const int f = bdraw_sys<NF, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
+      const int f = bdraw_sys<NFC, NTC, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
       if (!fail) fail = f;
     }
   }
@@ -403,21 +414,34 @@ extern "C" int gs_debug_phase_cycles(unsigned long long* out, int reset) {
 }
 #endif
 
-#define GS_NF_CASES(KERNEL, ARGS)                                                            \
-  switch (NF * 4 + bc) {                                                                     \
-    case 80: hipLaunchKernelGGL((KERNEL<20, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 81: hipLaunchKernelGGL((KERNEL<20, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 82: hipLaunchKernelGGL((KERNEL<20, WPB, 2>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 83: hipLaunchKernelGGL((KERNEL<20, WPB, 3>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 160: hipLaunchKernelGGL((KERNEL<40, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 161: hipLaunchKernelGGL((KERNEL<40, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 162: hipLaunchKernelGGL((KERNEL<40, WPB, 2>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 163: hipLaunchKernelGGL((KERNEL<40, WPB, 3>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 240: hipLaunchKernelGGL((KERNEL<60, WPB, 0>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 241: hipLaunchKernelGGL((KERNEL<60, WPB, 1>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 242: hipLaunchKernelGGL((KERNEL<60, WPB, 2>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    case 243: hipLaunchKernelGGL((KERNEL<60, WPB, 3>), grid, dim3(64 * WPB), lds, s, ARGS); return 0; \
-    default: return 1;                                                                       \
+// Fixed NF in {20, 40, 60}: every broadcast variant; any other even NF <= 64: the tile
+// variant with NF at run time, one instantiation per tile count NT = NF / 16 + 1.
+#define GS_LAUNCH(KERNEL, NFC, NTC, BC, ARGS) \
+  hipLaunchKernelGGL((KERNEL<NFC, NTC, WPB, BC>), grid, dim3(64 * WPB), lds, s, ARGS); \
+  return 0;
+#define GS_NF_CASES(KERNEL, ARGS)                                                       \
+  switch (NF * 4 + bc) {                                                                \
+    case 80: GS_LAUNCH(KERNEL, 20, 0, 0, ARGS)                                          \
+    case 81: GS_LAUNCH(KERNEL, 20, 0, 1, ARGS)                                          \
+    case 82: GS_LAUNCH(KERNEL, 20, 0, 2, ARGS)                                          \
+    case 83: GS_LAUNCH(KERNEL, 20, 0, 3, ARGS)                                          \
+    case 160: GS_LAUNCH(KERNEL, 40, 0, 0, ARGS)                                         \
+    case 161: GS_LAUNCH(KERNEL, 40, 0, 1, ARGS)                                         \
+    case 162: GS_LAUNCH(KERNEL, 40, 0, 2, ARGS)                                         \
+    case 163: GS_LAUNCH(KERNEL, 40, 0, 3, ARGS)                                         \
+    case 240: GS_LAUNCH(KERNEL, 60, 0, 0, ARGS)                                         \
+    case 241: GS_LAUNCH(KERNEL, 60, 0, 1, ARGS)                                         \
+    case 242: GS_LAUNCH(KERNEL, 60, 0, 2, ARGS)                                         \
+    case 243: GS_LAUNCH(KERNEL, 60, 0, 3, ARGS)                                         \
+    default: break;                                                                     \
+  }                                                                                     \
+  if (NF <= 0 || NF > 64 || (NF & 1)) return 1;                                         \
+  switch (NF / 16 + 1) {                                                                \
+    case 1: GS_LAUNCH(KERNEL, 0, 1, 3, ARGS)                                            \
+    case 2: GS_LAUNCH(KERNEL, 0, 2, 3, ARGS)                                            \
+    case 3: GS_LAUNCH(KERNEL, 0, 3, 3, ARGS)                                            \
+    case 4: GS_LAUNCH(KERNEL, 0, 4, 3, ARGS)                                            \
+    default: GS_LAUNCH(KERNEL, 0, 5, 3, ARGS)                                           \
   }
 
 template <int WPB>
@@ -438,24 +462,36 @@ int launch_lnlike_marg(hipStream_t s, const LnlArgs& a) {
   dim3 grid((unsigned)(a.n_psr * nb));
   const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) + GS_TILE_SCR * WPB) * sizeof(double);
   switch (a.NF) {
-    case 20: hipLaunchKernelGGL((k_lnlike_marg<20, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    case 40: hipLaunchKernelGGL((k_lnlike_marg<40, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    case 60: hipLaunchKernelGGL((k_lnlike_marg<60, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    default: return 1;
+    case 20: hipLaunchKernelGGL((k_lnlike_marg<20, 0, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 40: hipLaunchKernelGGL((k_lnlike_marg<40, 0, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 60: hipLaunchKernelGGL((k_lnlike_marg<60, 0, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    default: break;
+  }
+  if (a.NF <= 0 || a.NF > 64 || (a.NF & 1)) return 1;
+  switch (a.NF / 16 + 1) {
+    case 1: hipLaunchKernelGGL((k_lnlike_marg<0, 1, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 2: hipLaunchKernelGGL((k_lnlike_marg<0, 2, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 3: hipLaunchKernelGGL((k_lnlike_marg<0, 3, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 4: hipLaunchKernelGGL((k_lnlike_marg<0, 4, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    default: hipLaunchKernelGGL((k_lnlike_marg<0, 5, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
   }
 }
 
 int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
-  const size_t lds = ((size_t)a.mstride + GS_SCR_DOUBLES(a.bcast) * GS_SWEEP_WPB) * sizeof(double);
+  const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
+  const size_t lds = ((size_t)a.mstride + (fixed ? GS_SCR_DOUBLES(a.bcast) : GS_TILE_SCR) * GS_SWEEP_WPB) *
+                     sizeof(double);
   return dispatch_nf_sweep<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
 
 int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
-  const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) + GS_SCR_DOUBLES(a.bcast) * GS_SWEEP_WPB) * sizeof(double);
+  const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
+  const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) +
+                      (fixed ? GS_SCR_DOUBLES(a.bcast) : GS_TILE_SCR) * GS_SWEEP_WPB) * sizeof(double);
   return dispatch_nf_bdraw<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
 

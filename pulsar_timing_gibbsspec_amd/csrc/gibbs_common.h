@@ -6,11 +6,11 @@
 #define GS_WAVE 64
 
 // per-wave LDS scratch (doubles) of the tile b-draw (gibbs_tile.h): 272 transpose /
-// factor rows + 64 vector + 64 output
+// factor rows + 64 vector + 80 output (16 per tile row, up to 5 tile rows)
 #ifdef GS_PHASE_PROF
-#define GS_TILE_SCR 408
+#define GS_TILE_SCR 424
 #else
-#define GS_TILE_SCR 400
+#define GS_TILE_SCR 416
 #endif
 
 // ---------------------------------------------------------------- intra-wave LDS sync

@@ -31,8 +31,8 @@ typedef double gs_d4 __attribute__((ext_vector_type(4)));
 // waves, read back with gs_debug_phase_cycles.
 #ifdef GS_PHASE_PROF
 static __device__ unsigned long long gs_phase_cyc[8];
-// per-wave accumulators in the wave's LDS scratch (doubles 400..407), flushed once
-#define GS_PH_ACC(scr) reinterpret_cast<unsigned long long*>((scr) + 400)
+// per-wave accumulators in the wave's LDS scratch (doubles 416..423), flushed once
+#define GS_PH_ACC(scr) reinterpret_cast<unsigned long long*>((scr) + 416)
 #define GS_PH_INIT(scr) \
   if ((threadIdx.x & 63) < 8) GS_PH_ACC(scr)[threadIdx.x & 63] = 0ull;
 #define GS_PH_FLUSH(scr) \
@@ -379,24 +379,54 @@ __device__ __forceinline__ void tile_elim(gs_d4& A, gs_d4& B, double& rsd, int q
     tile_elim1<KMAX>(A, B, rsd, q, c);
 }
 
+// tile_elim with a runtime KMAX (0..16): one instantiation per value, a uniform switch
+// that folds away when kmax is a compile-time constant after inlining.
+__device__ __forceinline__ void tile_elim_rt(int kmax, gs_d4& A, gs_d4& B, double& rsd, int q, int c) {
+  switch (kmax) {
+#define GS_TE(K) \
+  case K: tile_elim<K>(A, B, rsd, q, c); return;
+    GS_TE(0) GS_TE(1) GS_TE(2) GS_TE(3) GS_TE(4) GS_TE(5) GS_TE(6) GS_TE(7)
+    GS_TE(8) GS_TE(9) GS_TE(10) GS_TE(11) GS_TE(12) GS_TE(13) GS_TE(14) GS_TE(15)
+#undef GS_TE
+    default: tile_elim<16>(A, B, rsd, q, c); return;
+  }
+}
+
+namespace gtile {
+// register i (runtime, 0..3) of a C-layout tile without a dynamically indexed vector
+__device__ __forceinline__ double d4_get(const gs_d4 v, int i) {
+  double r = v[0];
+  r = (i == 1) ? v[1] : r;
+  r = (i == 2) ? v[2] : r;
+  r = (i == 3) ? v[3] : r;
+  return r;
+}
+}  // namespace gtile
+
 // Model block view (see gibbs_bdraw.hip ModelLds): S0 NF x (NF+1), dF, G NMX x (NF+1),
 // h, R NMX x NMX.  Same interface and outputs as bdraw_wave.
 // LNL = true (the marginalised likelihood, gs_lnlike_marg): stop after the factorisation
 // and return, wave-uniform, bF = |y|^2 = dF^T S^-1 dF and bM = log det S (sum of the log
 // pivots of the real columns).
-template <int NF, bool LNL = false, typename ModelT>
-__device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int lane, double phinv,
-                                          double zF, double zM, double& bF, double& bM,
-                                          double* __restrict__ scr) {
+//
+// NT tile rows with NF < 16 NT, so the augmented row/column always fits in the last tile
+// (CP = NF - 16 (NT - 1) <= 15).  NF is a function argument: the fixed-NF entry point
+// bdraw_tile<NF> passes a constant (everything folds as before); bdraw_tile_n<NT> serves
+// any even NF < 16 NT with one instantiation per tile count.
+template <int NT, int CPC, bool LNL, typename ModelT>
+__device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM, int lane, double phinv,
+                                               double zF, double zM, double& bF, double& bM,
+                                               double* __restrict__ scr, const int nf_rt) {
   using namespace gtile;
-  constexpr int NT = (NF + 15) / 16;
-  constexpr int LD = NF + 1;
+  // CPC >= 0: NF = 16 (NT - 1) + CPC fixed at compile time; CPC < 0: NF = nf_rt
+  const int NF = CPC >= 0 ? 16 * (NT - 1) + CPC : nf_rt;
+  const int LD = NF + 1;
   constexpr int NTILE = NT * (NT + 1) / 2;
   const int q = lane >> 4, c = lane & 15;
   GS_PH_BEGIN
   double* tb = scr;        // 272
   double* vb = scr + 272;  // 64
-  double* ob = scr + 336;  // 64
+  double* ob = scr + 336;  // 80
 
   // phinv_F and z_F (lane-row) -> column layout per tile row
   lds_fence();
@@ -421,8 +451,8 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
   // [[S, dF], [dF^T, 1]] yields y = U^-T dF on the way (column CP of U_I,last for
   // I < last; row CP of the eliminated last diagonal tile scaled by the pivots^-1/2):
   // no forward solve.  S0 stores dF in its padding column NF (gs_prefix).
-  constexpr bool AUG = (NF % 16) != 0;
-  constexpr int CP = NF - 16 * (NT - 1);  // local index of the augmented column
+  constexpr bool AUG = true;
+  const int CP = NF - 16 * (NT - 1);  // local index of the augmented column (0..15)
   gs_d4 t[NTILE];
 #pragma unroll
   for (int I = 0; I < NT; ++I) {
@@ -464,13 +494,17 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
     // from row group k&3 (permlane swaps): no LDS, no transpose.
     gs_d4 A = t[tix(K, K, NT)], B;
     double rsd;
-    if (K == NT - 1)
-      tile_elim<NF - 16 * (NT - 1)>(A, B, rsd, q, c);
-    else
+    if (K == NT - 1) {
+      if constexpr (CPC >= 0)
+        tile_elim<CPC>(A, B, rsd, q, c);
+      else
+        tile_elim_rt(CP, A, B, rsd, q, c);
+    } else {
       tile_elim<16>(A, B, rsd, q, c);
+    }
     if (AUG && K == NT - 1) {
       // y_last[k] = (row CP of the eliminated tile)[k] * pivot_k^-1/2, k < CP
-      const double yl = bcast_group_bp(A[CP >> 2], CP & 3, c);
+      const double yl = bcast_group_bp(CPC >= 0 ? A[(CPC >= 0 ? CPC : 0) >> 2] : d4_get(A, CP >> 2), CP & 3, c);
       ylast = (c < CP) ? yl * rsd : 0.0;
     }
     GS_PH(1)
@@ -518,7 +552,9 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
   if constexpr (AUG) {
     // y_K = column CP of U_K,last = row CP of the stored U_K,last^T (row group CP&3)
 #pragma unroll
-    for (int K = 0; K + 1 < NT; ++K) ycol[K] = bcast_group_bp(t[tix(K, NT - 1, NT)][CP >> 2], CP & 3, c);
+    for (int K = 0; K + 1 < NT; ++K)
+      ycol[K] = bcast_group_bp(CPC >= 0 ? t[tix(K, NT - 1, NT)][(CPC >= 0 ? CPC : 0) >> 2]
+                                        : d4_get(t[tix(K, NT - 1, NT)], CP >> 2), CP & 3, c);
     ycol[NT - 1] = ylast;
   } else
 #pragma unroll
@@ -616,4 +652,21 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
   lds_fence();
   GS_PH(5)
   return fail;
+}
+
+// Fixed NF (the tuned 20 / 40 / 60 instantiations); NF % 16 != 0.
+template <int NF, bool LNL = false, typename ModelT>
+__device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int lane, double phinv,
+                                          double zF, double zM, double& bF, double& bM,
+                                          double* __restrict__ scr) {
+  static_assert(NF % 16 != 0, "the augmented column needs a free slot in the last tile");
+  return bdraw_tile_core<(NF + 15) / 16, NF % 16, LNL>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
+}
+
+// Any even NF with NF / 16 + 1 == NT (NF <= 64: one lane per free-spectrum column).
+template <int NT, bool LNL = false, typename ModelT>
+__device__ __forceinline__ int bdraw_tile_n(const ModelT& M, int NMX, int nM, int lane, double phinv,
+                                            double zF, double zM, double& bF, double& bM,
+                                            double* __restrict__ scr, int NF) {
+  return bdraw_tile_core<NT, -1, LNL>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
 }

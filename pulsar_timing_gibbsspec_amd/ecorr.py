@@ -25,7 +25,7 @@ import torch
 
 from . import _lib
 from ._lib import check, ptr
-from .engine import SUPPORTED_NF, _t
+from .engine import TUNED_NF, _t
 
 
 class EcorrModel:
@@ -49,8 +49,8 @@ class EcorrModel:
         ecid = np.asarray(ecid, np.int64)
         gwid = np.asarray(gwid, np.int64)
         NF = gwid.size
-        if NF not in SUPPORTED_NF:
-            raise NotImplementedError(f"ECORR path needs NF in {SUPPORTED_NF}, got {NF}")
+        if NF not in TUNED_NF:
+            raise NotImplementedError(f"ECORR path needs NF in {TUNED_NF}, got {NF}")
         self.m, self.ne, self.NF = m, ecid.size, NF
         self.C = int(n_chain)
         self.n_param = int(n_param)

@@ -15,13 +15,15 @@ import torch
 from . import _lib
 from ._lib import check, ptr
 
-SUPPORTED_NF = (20, 40, 60)      # register-tile b-draw and the fused sweep kernel
+TUNED_NF = (20, 40, 60)          # fixed-NF instantiations (every broadcast variant)
+FUSED_NF_MAX = 64                # register-tile b-draw and the fused sweep: any even NF <= 64
 BIG_NF = (66, 254)               # even NF in this range: workspace-tile b-draw (config 5)
+NMX_MAX = 64                     # fixed-prior (timing-model) columns per pulsar
 
 
 def nf_supported(NF):
-    """NF = 2 n_f the b-draw handles (gs_bdraw, gs_bdraw_sys)."""
-    return NF in SUPPORTED_NF or (BIG_NF[0] <= NF <= BIG_NF[1] and NF % 2 == 0)
+    """NF = 2 n_f the b-draw handles (gs_bdraw, gs_bdraw_sys): any even NF <= 254."""
+    return 0 < NF <= BIG_NF[1] and NF % 2 == 0
 
 
 def _t(a, dtype, device):
@@ -47,20 +49,22 @@ class DeviceModel:
         if any(len(f) != NF for f in fidx_list):
             raise ValueError("every pulsar must have the same number of free-spectrum columns")
         if not nf_supported(NF):
-            raise NotImplementedError(f"NF = 2*n_f = {NF}; supported: {SUPPORTED_NF} or even {BIG_NF}")
+            raise NotImplementedError(f"NF = 2*n_f = {NF}; supported: even NF <= {BIG_NF[1]}")
         self.P, self.NF = P, NF
         self.m = np.array([t.shape[1] for t in T_list], np.int64)
         self.n_toa = np.array([t.shape[0] for t in T_list], np.int64)
         self.nm = (self.m - NF).astype(np.int32)
-        if (self.nm <= 0).any() or (self.nm > 64).any():
-            raise NotImplementedError("need 1..64 fixed-prior columns per pulsar")
+        if (self.nm < 0).any() or (self.nm > NMX_MAX).any():
+            raise NotImplementedError(f"need 0..{NMX_MAX} fixed-prior (timing-model) columns per pulsar")
         self.NMX = int(self.nm.max())
-        self.ldb = int(self.m.max())
+        self.ldb = max(int(self.m.max()), NF + 1)    # the C-ABI wants ldb > NF (nm = 0 models)
         self.fidx_host = [np.asarray(f, np.int64) for f in fidx_list]
         self.midx_host = []
         fidx = np.zeros((P, NF), np.int32)
-        midx = np.zeros((P, self.NMX), np.int32)
-        phfix = np.ones((P, self.NMX))
+        # nm = 0 (MarginalizingTimingModel: no timing-model columns in T): the arrays keep
+        # one (unused) column so their device pointers are not NULL
+        midx = np.zeros((P, max(1, self.NMX)), np.int32)
+        phfix = np.ones((P, max(1, self.NMX)))
         for p in range(P):
             mask = np.ones(self.m[p], bool)
             mask[self.fidx_host[p]] = False
@@ -166,9 +170,7 @@ class FreeSpectrumChains:
     """
 
     def __init__(self, model: DeviceModel, rhomin, rhomax, n_chain, x0, chain_base=0):
-        if model.NF not in SUPPORTED_NF:
-            raise NotImplementedError(f"the fused sweep needs NF in {SUPPORTED_NF}; "
-                                      f"NF = {model.NF} runs through gs_bdraw + gs_rho_analytic")
+        self.fused = model.NF <= FUSED_NF_MAX
         self.model = model
         self.ctx = model.ctx
         self.n_chain = int(n_chain)
@@ -182,6 +184,11 @@ class FreeSpectrumChains:
         self.b = torch.zeros(n_sys, model.ldb, dtype=torch.float64, device=dev)
         self.info = torch.zeros(n_sys, dtype=torch.int32, device=dev)
         self.it = 0
+        if not self.fused:
+            self.xlast = torch.empty(n_sys, dtype=torch.float64, device=dev)
+            self.gate = torch.ones(n_sys, dtype=torch.int32, device=dev)
+            self.phiinv_F = torch.empty(n_sys, model.NF, dtype=torch.float64, device=dev)
+            self.gw_col = torch.arange(self.n_f, dtype=torch.int32, device=dev)
 
     @property
     def n_sys(self):
@@ -195,6 +202,9 @@ class FreeSpectrumChains:
             x_rec = torch.empty(n_sweeps, self.n_sys, self.n_f, dtype=torch.float64, device=dev)
         if record and record_b and b_rec is None:
             b_rec = torch.empty(n_sweeps, self.n_sys, m.ldb, dtype=torch.float64, device=dev)
+        if not self.fused:
+            self._run_sequence(n_sweeps, x_rec, b_rec if record_b else None, z0_inj, z_inj, u_inj)
+            return x_rec, b_rec
         check(self.ctx.lib.gs_sweep_freespec(
             self.ctx.handle, m.P, self.n_chain, m.NF, m.NMX, m.ldb, ptr(m.model), ptr(m.fidx),
             ptr(m.midx), ptr(m.nm_dev), self.rhomin, self.rhomax, self.chain_base, ptr(self.x),
@@ -202,6 +212,47 @@ class FreeSpectrumChains:
             ptr(u_inj), ptr(self.info)), "gs_sweep_freespec")
         self.it += int(n_sweeps)
         return x_rec, b_rec
+
+    def _gate_phiinv(self, with_gate):
+        check(self.ctx.lib.gs_pta_gate_phiinv(
+            self.ctx.handle, 1, self.n_sys, self.n_f, self.n_f, ptr(self.x),
+            ptr(self.xlast) if with_gate else None, ptr(self.gw_col), None, ptr(self.phiinv_F),
+            ptr(self.gate)), "gs_pta_gate_phiinv")
+
+    def _bdraw(self, z, event, mask):
+        """gs_bdraw of every (pulsar, chain) system with the gate indexed by system."""
+        m, lib, h = self.model, self.ctx.lib, self.ctx.handle
+        per_sys = self.ctx.get_option(_lib.OPT_X_PER_SYS)
+        self.ctx.set_option(_lib.OPT_X_PER_SYS, 1)
+        inf = torch.zeros(self.n_sys, dtype=torch.int32, device=self.ctx.device)
+        try:
+            check(lib.gs_bdraw(h, m.P, self.n_chain, m.NF, m.NMX, m.ldb, ptr(m.model), ptr(m.fidx), ptr(m.midx),
+                               ptr(m.nm_dev), ptr(self.phiinv_F), ptr(z), self.it, event, self.chain_base,
+                               ptr(mask), ptr(self.b), ptr(inf)), "gs_bdraw")
+        finally:
+            self.ctx.set_option(_lib.OPT_X_PER_SYS, per_sys)
+        torch.where(self.info == 0, inf, self.info, out=self.info)
+
+    def _run_sequence(self, n_sweeps, x_rec, b_rec, z0_inj, z_inj, u_inj):
+        """NF > 64 (workspace-tile b draw): the same loop body as the fused kernel as a launch
+        sequence per sweep -- record, [first draw], analytic rho|b (gs_rho_analytic), gate +
+        phiinv, gated b|rho (gs_bdraw) -- with the same Philox counters per draw."""
+        m, lib, h = self.model, self.ctx.lib, self.ctx.handle
+        for i in range(int(n_sweeps)):
+            ii = self.it
+            check(lib.gs_pta_record(h, self.n_sys, self.n_f, ptr(self.x), ptr(x_rec[i]) if x_rec is not None
+                                    else None, ptr(self.xlast)), "gs_pta_record")   # pulsar_gibbs.py:658
+            if b_rec is not None:
+                b_rec[i].copy_(self.b)                                               # :659
+            if ii == 0:                                                              # :661-662
+                self._gate_phiinv(with_gate=False)
+                self._bdraw(z0_inj, _lib.EV_B0, None)
+            check(lib.gs_rho_analytic(h, m.P, self.n_chain, m.NF, m.ldb, ptr(m.fidx), ptr(self.b),
+                                      ptr(u_inj[i]) if u_inj is not None else None, ii, self.chain_base,
+                                      self.rhomin, self.rhomax, ptr(self.x), self.n_f), "gs_rho_analytic")
+            self._gate_phiinv(with_gate=True)                                        # :697
+            self._bdraw(z_inj[i] if z_inj is not None else None, _lib.EV_B, self.gate)   # :698
+            self.it += 1
 
 
 class HistoryStreamer:

@@ -398,11 +398,15 @@ def single_pulsar_pta(psr="J1713+0747", n_f=30, rho_prior=(-9.0, -4.0), log10_A=
         la = Uniform("red_log10_A", -20.0, -11.0)
         ga = Uniform("red_gamma", 0.0, 7.0)
         sigs.append(FourierGP(psr, "red", toas, Tspan, n_f, "powerlaw", [la, ga]))
-    M = synthetic_design_matrix(toas, ncol, pb)
-    tm = TimingModelGP(psr, M, use_svd=tm_svd)
-    sigs.append(tm)
-    r = _simulate_residuals(rng, gw.get_basis(), gw.freqs, Tspan, tm.get_basis(), err,
-                            log10_A, gamma)
+    if ncol > 0:
+        tm = TimingModelGP(psr, synthetic_design_matrix(toas, ncol, pb), use_svd=tm_svd)
+        sigs.append(tm)
+        Mb = tm.get_basis()
+    else:
+        # tm_cols = 0: the timing model is marginalised analytically outside T
+        # (model_definition.py:185-186, MarginalizingTimingModel) -- no basis columns
+        Mb = np.zeros((toas.size, 0))
+    r = _simulate_residuals(rng, gw.get_basis(), gw.freqs, Tspan, Mb, err, log10_A, gamma)
     return PTA([PulsarModel(psr, toas, r, sigs)])
 
 

@@ -25,7 +25,7 @@ import torch
 from . import _lib
 from ._lib import check, ptr
 from .diagnostics import white_aclength
-from .engine import BIG_NF, SUPPORTED_NF, _t, nf_supported
+from .engine import BIG_NF, _t, nf_supported
 
 MAX_BK = 15
 MAX_W = 32
@@ -67,7 +67,7 @@ class WhiteNoiseModel:
         if any(len(f) != NF for f in fidx_list):
             raise ValueError("every pulsar must have the same number of free-spectrum columns")
         if not nf_supported(NF):
-            raise NotImplementedError(f"NF = 2*n_f = {NF}; supported: {SUPPORTED_NF} or even {BIG_NF}")
+            raise NotImplementedError(f"NF = 2*n_f = {NF}; supported: even NF <= {BIG_NF[1]}")
         self.P, self.C, self.NF = P, C, NF
         self.m = np.array([t.shape[1] for t in T_list], np.int64)
         self.n_toa = np.array([t.shape[0] for t in T_list], np.int64)
@@ -75,13 +75,13 @@ class WhiteNoiseModel:
         # prefix=False: per-chain TNT / d, residuals and the white MH only (the basis-ECORR
         # path factors its own Schur systems, ecorr.EcorrModel(per_chain=True))
         self.prefix = bool(prefix)
-        if self.prefix and ((self.nm <= 0).any() or (self.nm > 64).any()):
-            raise NotImplementedError("need 1..64 fixed-prior columns per pulsar")
+        if self.prefix and ((self.nm < 0).any() or (self.nm > 64).any()):
+            raise NotImplementedError("need 0..64 fixed-prior columns per pulsar")
         self.NMX = int(self.nm.max())
-        self.ldb = int(self.m.max())
+        self.ldb = max(int(self.m.max()), NF + 1)    # the C-ABI wants ldb > NF (nm = 0 models)
         fidx = np.zeros((P, NF), np.int32)
-        midx = np.zeros((P, self.NMX), np.int32)
-        phfix = np.ones((P, self.NMX))
+        midx = np.zeros((P, max(1, self.NMX)), np.int32)      # one unused column when nm = 0
+        phfix = np.ones((P, max(1, self.NMX)))
         self.perm = []
         Ts, Tts, rs, s2s, bks = [], [], [], [], []
         wdesc = np.zeros(P, WHITE_DESC)

@@ -1,0 +1,121 @@
+"""Any number of free-spectrum bins and timing-model columns (model_definition.py:21, 66,
+207: ``common_components`` is any n_f; :185-189: ``tm_marg`` gives no timing-model
+columns in T).
+
+The register-tile b draw and the fused sweep take any even NF = 2 n_f <= 64 (one
+instantiation per tile count, NF at run time; 20 / 40 / 60 keep their tuned fixed-NF
+builds); NF > 64 runs the workspace-tile draw in a per-sweep launch sequence with the same
+Philox counters.  nm = 0 (no fixed-prior block) and up to 64 timing-model columns.
+
+Oracles: the exact long-double Cholesky draw with the same normals (1e-9 normwise), the
+oracle's Cholesky sweep loop on the same injected normals / uniforms (1e-9), and the
+marginalised likelihood of pulsar_gibbs.py:569-610 (1e-10 relative)."""
+import numpy as np
+import pytest
+
+from oracle import gibbs_oracle as O
+from tests.parity_data import exact_chol_draw_pre, exact_tnt, normwise_rel
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from pulsar_timing_gibbsspec_amd import _lib
+    return _lib.Context(0, seed=99)
+
+
+def _pulsar(n_f, nm):
+    from pulsar_timing_gibbsspec_amd import synthetic
+    pta = synthetic.single_pulsar_pta("J1713+0747", n_f=n_f, tm_cols=nm, seed=2)
+    return pta.get_basis()[0], pta.get_ndiag({})[0], pta.get_residuals()[0]
+
+
+def _model(ctx, n_f, nm):
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel
+    T, N, r = _pulsar(n_f, nm)
+    return DeviceModel(ctx, [T], [N], [r], [np.arange(2 * n_f)], [np.full(nm, 1e-40)]), T, N, r
+
+
+def dev(a):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64).cuda()
+
+
+@pytest.mark.parametrize("n_f,nm", [(1, 16), (7, 0), (7, 16), (15, 16), (16, 8), (23, 0), (31, 16), (32, 16),
+                                    (40, 16)])
+def test_bdraw_any_nf_matches_exact_draw(ctx, n_f, nm):
+    model, T, N, r = _model(ctx, n_f, nm)
+    m = T.shape[1]
+    rng = np.random.default_rng(n_f + 100 * nm)
+    C = 4
+    logrho = rng.uniform(-8.5, -5.0, (C, n_f))
+    ph = 1.0 / np.repeat(10 ** (2 * logrho), 2, axis=1)
+    z = np.zeros((C, model.ldb))
+    z[:, :m] = rng.standard_normal((C, m))
+    b, info = model.bdraw(dev(ph), C, z=dev(z))
+    b = b.cpu().numpy()
+    assert not info.cpu().numpy().any()
+    tl = exact_tnt(T, N, r)
+    order = O.chol_order(m, np.arange(2 * n_f))
+    for c in range(C):
+        phi = np.concatenate([ph[c], np.full(nm, 1e-40)])
+        bx = exact_chol_draw_pre(tl, phi, z[c, :m], order)
+        assert normwise_rel(b[c, :m], bx) < 1e-9, (n_f, nm, c, normwise_rel(b[c, :m], bx))
+
+
+@pytest.mark.parametrize("n_f,nm", [(7, 16), (15, 0), (15, 16), (32, 16), (40, 16)])
+def test_sweep_any_nf_matches_oracle_loop(ctx, n_f, nm):
+    """FreeSpectrumChains (fused for NF <= 64, launch sequence above) == the oracle's
+    PulsarBlockGibbs loop (pulsar_gibbs.py:656-698) with the Cholesky draw on the same draws."""
+    from pulsar_timing_gibbsspec_amd.engine import FreeSpectrumChains
+    model, T, N, r = _model(ctx, n_f, nm)
+    m = T.shape[1]
+    n, C = 20, 3
+    rng = np.random.default_rng(7 * n_f + nm)
+    x0 = rng.uniform(-9, -4, (C, n_f))
+    z = np.zeros((n + 1, C, model.ldb))
+    z[:, :, :m] = rng.standard_normal((n + 1, C, m))
+    U = rng.random((n, C, n_f))
+    run = FreeSpectrumChains(model, 1e-18, 1e-8, C, x0)
+    assert run.fused == (2 * n_f <= 64)
+    xr, br = run.run(n, z0_inj=dev(z[0]), z_inj=dev(z[1:]), u_inj=dev(U))
+    xr, br = xr.cpu().numpy(), br.cpu().numpy()
+    assert not run.info.cpu().numpy().any()
+    TNT, d = O.tnt(T, N, r)
+    order = O.chol_order(m, np.arange(2 * n_f))
+    for c in range(C):
+        want_x, want_b, _ = O.sweep_single(TNT, d, np.arange(2 * n_f), x0[c], 1e-18, 1e-8, z[:, c, :m], U[:, c], n,
+                                           lambda x: O.phiinv_single(x, nm), draw="chol", order=order)
+        assert normwise_rel(xr[:, c], want_x) < 1e-9, (n_f, nm, c)
+        assert normwise_rel(br[1:, c, :m], want_b[1:]) < 1e-9, (n_f, nm, c)
+
+
+@pytest.mark.parametrize("n_f,nm", [(7, 16), (15, 0), (32, 16)])
+def test_lnlike_marg_any_nf(ctx, n_f, nm):
+    model, T, N, r = _model(ctx, n_f, nm)
+    rng = np.random.default_rng(n_f)
+    C = 3
+    logrho = rng.uniform(-8.5, -5.0, (C, n_f))
+    ph = 1.0 / np.repeat(10 ** (2 * logrho), 2, axis=1)
+    lnl, info = model.lnlike_marg(dev(ph), C)
+    lnl = lnl.cpu().numpy()
+    assert not info.cpu().numpy().any()
+    TNT, d = O.tnt(T, N, r)
+    for c in range(C):
+        phi = np.concatenate([1.0 / ph[c], np.full(nm, 1e40)])
+        want = O.lnlike_fullmarg(r, N, TNT, d, 1.0 / phi, np.sum(np.log(phi)))
+        assert abs(lnl[c] - want) <= 1e-10 * abs(want), (n_f, nm, c, lnl[c], want)
+
+
+def test_pulsar_block_gibbs_with_15_bins_and_no_timing_model(tmp_path):
+    """The drop-in with common_components = 15 and a marginalised timing model (nm = 0)."""
+    from pulsar_timing_gibbsspec_amd import PulsarBlockGibbs, synthetic
+    pta = synthetic.single_pulsar_pta("J1713+0747", n_f=15, tm_cols=0, seed=4)
+    gb = PulsarBlockGibbs(pta, seed=3, nchains=8)
+    x0 = np.random.default_rng(0).uniform(-9, -4, 15)
+    chain = gb.sample(x0, outdir=str(tmp_path), niter=150)
+    assert chain.shape == (150, 15) and gb.bchain.shape == (150, 30)
+    assert np.all(np.isfinite(gb.chains)) and gb.chains.min() >= -9 and gb.chains.max() <= -4
+    assert np.load(tmp_path / "chain.npy").shape == (101, 15)
