@@ -195,6 +195,48 @@ __device__ __forceinline__ void stage_model(double* lds, const double* g, int64_
   __syncthreads();
 }
 
+// ------------------------------------------------------------ batched b draw, wide timing model
+// 64 < nM <= 128 fixed-prior columns (NF <= 64): the model block (R alone is up to 128 KB) is
+// read from global memory / L2, z_M rows 64.. come from Philox slot 64 + lane (or injected),
+// and rows >= 64 of x_M are stored by the factorisation routine itself.
+template <int NTC, int WPB>
+__global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
+  extern __shared__ double lds[];
+  const int NF = A.NF;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nb = (A.n_chain + WPB - 1) / WPB;
+  const int p = blockIdx.x / nb;
+  const int c = (blockIdx.x % nb) * WPB + wave;
+  if (c >= A.n_chain) return;
+  const int64_t sys = (int64_t)p * A.n_chain + c;
+  if (A.chain_mask && A.chain_mask[A.mask_per_sys ? sys : (int64_t)c] == 0) return;
+  const ModelLds M = model_view(A.model + (A.model_per_sys ? sys : (int64_t)p) * A.mstride, NF, A.NMX);
+  const int nM = A.nm[p];
+  const int32_t* mrow = A.midx + (int64_t)p * A.NMX;
+  const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
+  const int mi = lane < nM ? mrow[lane] : 0;
+  const int mia = 64 + lane < nM ? mrow[64 + lane] : 0;
+  const double phinv = lane < NF ? A.phiinv_F[sys * NF + lane] : 0.0;
+  double zF = 0.0, zM = 0.0, zMa = 0.0;
+  if (A.z) {
+    zF = lane < NF ? A.z[sys * A.ldb + fi] : 0.0;
+    zM = lane < nM ? A.z[sys * A.ldb + mi] : 0.0;
+    zMa = 64 + lane < nM ? A.z[sys * A.ldb + mia] : 0.0;
+  } else {
+    const long long sw = gs_sweep(A.sweep, A.sweep_dev);
+    gs_normal2(gs_counter(lane, sw, A.chain_base + c, p + A.psr_base, A.event), A.key, zF, zM);
+    double unused;
+    gs_normal2(gs_counter(64 + lane, sw, A.chain_base + c, p + A.psr_base, A.event), A.key, zMa, unused);
+  }
+  double bF = 0.0, bM = 0.0;
+  double* scr = lds + wave * GS_TILE_SCR;
+  double* brow = A.b + sys * A.ldb;
+  const int fail = bdraw_tile_wide<NTC>(M, A.NMX, nM, lane, phinv, zF, zM, zMa, bF, bM, scr, NF, brow, mrow);
+  if (lane < NF) brow[fi] = bF;
+  if (lane < nM) brow[mi] = bM;
+  if (A.info && lane == 0) A.info[sys] = fail;
+}
+
 // ------------------------------------------------------------ batched b draw
 template <int NFC, int NTC, int WPB, int BC>
 __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
@@ -245,14 +287,15 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
   const int nb = (A.n_chain + WPB - 1) / WPB;
   const int p = blockIdx.x / nb;
   const int c = (blockIdx.x % nb) * WPB + wave;
-  if (!A.model_per_sys) stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+  const bool in_lds = !A.model_per_sys && !A.model_global;
+  if (in_lds) stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
   if (c >= A.n_chain) return;
   const int64_t sys = (int64_t)p * A.n_chain + c;
-  const double* mb = A.model_per_sys ? A.model + sys * A.mstride : lds;
+  const double* mb = in_lds ? lds : A.model + (A.model_per_sys ? sys : (int64_t)p) * A.mstride;
   const ModelLds M = model_view(mb, NF, A.NMX);
   const double phinv = lane < NF ? A.phiinv_F[sys * NF + lane] : 1.0;
   double yy = 0.0, ldS = 0.0;
-  double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * GS_TILE_SCR;
+  double* scr = lds + (in_lds ? A.mstride : 0) + wave * GS_TILE_SCR;
   int fail;
   if constexpr (NFC == 0)
     fail = bdraw_tile_n<NTC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr, NF);
@@ -460,7 +503,8 @@ int launch_lnlike_marg(hipStream_t s, const LnlArgs& a) {
   constexpr int WPB = GS_SWEEP_WPB;
   const int nb = (a.n_chain + WPB - 1) / WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
-  const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) + GS_TILE_SCR * WPB) * sizeof(double);
+  const size_t lds = ((size_t)(a.model_per_sys || a.model_global ? 0 : a.mstride) + GS_TILE_SCR * WPB) *
+                     sizeof(double);
   switch (a.NF) {
     case 20: hipLaunchKernelGGL((k_lnlike_marg<20, 0, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
     case 40: hipLaunchKernelGGL((k_lnlike_marg<40, 0, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
@@ -489,6 +533,18 @@ int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
 int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
+  if (a.NMX > 64) {
+    constexpr int WPB = GS_SWEEP_WPB;
+    const size_t lds = (size_t)GS_TILE_SCR * WPB * sizeof(double);
+    if (a.NF <= 0 || a.NF > 64 || (a.NF & 1)) return 1;
+    switch (a.NF / 16 + 1) {
+      case 1: hipLaunchKernelGGL((k_bdraw_wide<1, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+      case 2: hipLaunchKernelGGL((k_bdraw_wide<2, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+      case 3: hipLaunchKernelGGL((k_bdraw_wide<3, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+      case 4: hipLaunchKernelGGL((k_bdraw_wide<4, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+      default: hipLaunchKernelGGL((k_bdraw_wide<5, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    }
+  }
   const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
   const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) +
                       (fixed ? GS_SCR_DOUBLES(a.bcast) : GS_TILE_SCR) * GS_SWEEP_WPB) * sizeof(double);

@@ -12,6 +12,10 @@
 #define GS_SWEEP_WPB 4
 #endif
 
+// fixed-prior (timing-model) columns per pulsar: up to 64 everywhere (lane per row), up to
+// GS_NMX_WIDE in gs_prefix / gs_bdraw with NF <= 64 (k_prefix_wide: L_M in LDS, 128 KB)
+#define GS_NMX_WIDE 128
+
 // model block: S0 | dF | G | h | R | aux[2] (aux: sum log diag L_M, |L_M^-1 d_M|^2)
 __host__ __device__ inline int64_t model_aux_offset(int NF, int NMX) {
   return (int64_t)NF * (NF + 1) + NF + (int64_t)NMX * (NF + 1) + NMX + (int64_t)NMX * NMX;
@@ -23,6 +27,7 @@ __host__ __device__ inline int64_t model_stride_doubles(int NF, int NMX) {
 
 struct LnlArgs {
   int n_psr, n_chain, NF, NMX, model_per_sys;
+  int model_global;  // shared model block read from global memory (too large for LDS)
   int64_t mstride;
   const double* model;
   const int32_t* nm;

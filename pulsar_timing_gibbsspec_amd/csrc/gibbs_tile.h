@@ -413,10 +413,16 @@ __device__ __forceinline__ double d4_get(const gs_d4 v, int i) {
 // (CP = NF - 16 (NT - 1) <= 15).  NF is a function argument: the fixed-NF entry point
 // bdraw_tile<NF> passes a constant (everything folds as before); bdraw_tile_n<NT> serves
 // any even NF < 16 NT with one instantiation per tile count.
-template <int NT, int CPC, bool LNL, typename ModelT>
+//
+// WIDE (64 < nM <= 128 timing-model columns, gs_bdraw only): z_M rows 64..127 arrive in zMa
+// (lane l holds row 64 + l), the R z_M operand is staged in tb, and rows >= 64 of x_M are
+// stored straight to bext[mrow[row]] (rows < 64 still return in bM, one per lane).
+template <int NT, int CPC, bool LNL, bool WIDE = false, typename ModelT>
 __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM, int lane, double phinv,
                                                double zF, double zM, double& bF, double& bM,
-                                               double* __restrict__ scr, const int nf_rt) {
+                                               double* __restrict__ scr, const int nf_rt, double zMa = 0.0,
+                                               double* __restrict__ bext = nullptr,
+                                               const int32_t* __restrict__ mrow = nullptr) {
   using namespace gtile;
   // CPC >= 0: NF = 16 (NT - 1) + CPC fixed at compile time; CPC < 0: NF = nf_rt
   const int NF = CPC >= 0 ? 16 * (NT - 1) + CPC : nf_rt;
@@ -622,7 +628,9 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
 
   GS_PH(4)
   // ---- fixed-prior block: x_M = h + R z_M - G x_F, 16 rows per chunk
-  vb[lane] = (lane < nM) ? zM : 0.0;
+  double* zb = WIDE ? tb : vb;  // z_M staging (tb is free after the factorisation)
+  zb[lane] = (lane < nM) ? zM : 0.0;
+  if constexpr (WIDE) zb[64 + lane] = (64 + lane < nM) ? zMa : 0.0;
   lds_fence();
   const int nP = (nM + 15) >> 4;
   for (int P = 0; P < nP; ++P) {
@@ -642,10 +650,14 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
       for (int s = 0; s < 4; ++s) {
         const int mm = 16 * Q + 4 * s + q;
         const double rv = (rok && mm < nM) ? M.R[row * NMX + mm + z0] : 0.0;
-        p = fma(rv, vb[mm], p);
+        p = fma(rv, zb[mm], p);
       }
     p = qsum(p);
-    ob[row] = rok ? M.h[row + z0] + p : 0.0;
+    const double xm = rok ? M.h[row + z0] + p : 0.0;
+    if (!WIDE || P < 4)
+      ob[row] = xm;
+    else if (rok && q == 0)
+      bext[mrow[row]] = xm;
   }
   lds_fence();
   bM = (lane < nM) ? ob[lane] : 0.0;
@@ -669,4 +681,13 @@ __device__ __forceinline__ int bdraw_tile_n(const ModelT& M, int NMX, int nM, in
                                             double zF, double zM, double& bF, double& bM,
                                             double* __restrict__ scr, int NF) {
   return bdraw_tile_core<NT, -1, LNL>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
+}
+
+// Same with up to 128 timing-model columns (see bdraw_tile_core, WIDE).
+template <int NT, typename ModelT>
+__device__ __forceinline__ int bdraw_tile_wide(const ModelT& M, int NMX, int nM, int lane, double phinv,
+                                               double zF, double zM, double zMa, double& bF, double& bM,
+                                               double* __restrict__ scr, int NF, double* bext,
+                                               const int32_t* mrow) {
+  return bdraw_tile_core<NT, -1, false, true>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF, zMa, bext, mrow);
 }

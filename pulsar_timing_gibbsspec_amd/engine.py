@@ -18,7 +18,8 @@ from ._lib import check, ptr
 TUNED_NF = (20, 40, 60)          # fixed-NF instantiations (every broadcast variant)
 FUSED_NF_MAX = 64                # register-tile b-draw and the fused sweep: any even NF <= 64
 BIG_NF = (66, 254)               # even NF in this range: workspace-tile b-draw (config 5)
-NMX_MAX = 64                     # fixed-prior (timing-model) columns per pulsar
+NMX_MAX = 128                    # fixed-prior (timing-model) columns per pulsar (> 64: NF <= 64,
+NMX_FUSED = 64                   # gs_bdraw's wide kernel; the fused sweep keeps <= 64)
 
 
 def nf_supported(NF):
@@ -57,6 +58,8 @@ class DeviceModel:
         if (self.nm < 0).any() or (self.nm > NMX_MAX).any():
             raise NotImplementedError(f"need 0..{NMX_MAX} fixed-prior (timing-model) columns per pulsar")
         self.NMX = int(self.nm.max())
+        if self.NMX > NMX_FUSED and NF > FUSED_NF_MAX:
+            raise NotImplementedError(f"more than {NMX_FUSED} timing-model columns with NF > {FUSED_NF_MAX}")
         self.ldb = max(int(self.m.max()), NF + 1)    # the C-ABI wants ldb > NF (nm = 0 models)
         self.fidx_host = [np.asarray(f, np.int64) for f in fidx_list]
         self.midx_host = []
@@ -170,7 +173,7 @@ class FreeSpectrumChains:
     """
 
     def __init__(self, model: DeviceModel, rhomin, rhomax, n_chain, x0, chain_base=0):
-        self.fused = model.NF <= FUSED_NF_MAX
+        self.fused = model.NF <= FUSED_NF_MAX and model.NMX <= NMX_FUSED
         self.model = model
         self.ctx = model.ctx
         self.n_chain = int(n_chain)

@@ -352,7 +352,14 @@ def synthetic_design_matrix(toas_s, n_cols, pb_days=0.0):
             tn * np.sin(wb * t), tn * np.cos(wb * t), tn ** 3,
             np.sin(3 * wb * t), np.cos(3 * wb * t), tn ** 4, np.sin(3 * wy * t)]
     if n_cols > len(cols):
-        raise ValueError(f"at most {len(cols)} synthetic timing-model columns")
+        # DMX-like columns beyond the 20 smooth ones: indicators of consecutive windows with
+        # equal TOA counts (window 0 left out: the windows would otherwise sum to the offset)
+        n_win = n_cols - len(cols) + 1
+        rank = np.argsort(np.argsort(toas_s, kind="stable"), kind="stable")
+        win = (rank * n_win) // toas_s.size
+        if n_win > toas_s.size // 2:
+            raise ValueError("too many DMX-like windows for the TOAs")
+        cols = cols + [(win == k).astype(float) for k in range(1, n_win)]
     return np.stack(cols[:n_cols], axis=1)
 
 
