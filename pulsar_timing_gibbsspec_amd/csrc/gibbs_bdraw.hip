@@ -335,6 +335,10 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
   const int mi = actm ? A.midx[p * A.NMX + lane] : 0;
   double* scr = lds + A.mstride + wave * GS_SCR_DOUBLES(BC);
   GS_PH_INIT(scr)
+#ifdef GS_STATIC_PRIO
+  // A/B knob: half of the workgroups (one of the two co-resident waves of a SIMD) at priority 1
+  if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
+#endif
 
   // state: x replicated on the (sin, cos) lane pair, b split over F/M lanes
   double x = act ? A.x_state[sys * NFR + kf] : 0.0;
@@ -363,6 +367,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
       double phinv = 0.0;
       int64_t zrow = sys;
       if (pass == 1) {
+        if constexpr (GS_RHO_PRIO > 0) __builtin_amdgcn_s_setprio(GS_RHO_PRIO);
         // rho|b analytic (pulsar_gibbs.py:208-216, 236)
         const double partner = __shfl_xor(bF, 1);
         const double be = (lane & 1) ? partner : bF, bo = (lane & 1) ? bF : partner;
@@ -395,6 +400,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
         const bool same = act && (xnew == xlast);
         const bool gate = __ballot(same) == 0ull;
         x = xnew;
+        if constexpr (GS_RHO_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
         if (!gate) break;
         zinj = A.z_inj;
         ev = GS_EV_B;

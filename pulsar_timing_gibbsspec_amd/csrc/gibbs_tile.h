@@ -229,9 +229,36 @@ __device__ __forceinline__ constexpr int tix(int I, int J, int NT) {
 // step.  Row k+1 (as before step k) is requested ahead of the pivot chain and
 // updated by the same column operation.  Measured on MI355X against an LDS
 // row-broadcast version and a v_permlane32/16_swap broadcast: 1.7x and 1.04x faster.
+// Issue priority (s_setprio) per phase.  Two independent waves share each SIMD; VALU issue is
+// arbitrated by priority, then age (MI355X_MICROARCH.md, co-resident waves items 2 and 4).
+// Raising the wave that runs the latency-bound dependent chains -- the diagonal-tile
+// elimination (GS_DIAG_PRIO) and the backward solve (GS_SOLVE_PRIO) -- lets its next link
+// issue as soon as it is ready while the partner fills the gaps with MFMAs and independent
+// VALU.  Measured on MI355X (4096 chains, NF = 60, 100-sweep launches; tools/gpu_ab_lib.sh):
+// 2.96-3.09 ms -> 2.77-2.92 ms per launch with DIAG 2 / SOLVE 1; raising the update,
+// fixed-block or rho phases as well, or DIAG 3, was no better.
+#ifndef GS_DIAG_PRIO
+#define GS_DIAG_PRIO 2
+#endif
+#ifndef GS_BASE_PRIO
+#define GS_BASE_PRIO 0
+#endif
+#ifndef GS_UPD_PRIO  // ... while it runs the TRSM / trailing-update MFMAs
+#define GS_UPD_PRIO 0
+#endif
+#ifndef GS_SOLVE_PRIO  // ... while it runs the backward solve
+#define GS_SOLVE_PRIO 1
+#endif
+#ifndef GS_FIX_PRIO  // ... while it runs the fixed-prior block
+#define GS_FIX_PRIO 0
+#endif
+#ifndef GS_RHO_PRIO  // ... while it runs the sweep's rho|b draw and gate (k_sweep_freespec)
+#define GS_RHO_PRIO 0
+#endif
 template <int KMAX>
 __device__ __forceinline__ void tile_elim1(gs_d4& A, gs_d4& B, double& rsd, int q, int c) {
   using namespace gtile;
+  if constexpr (GS_DIAG_PRIO > 0) __builtin_amdgcn_s_setprio(GS_DIAG_PRIO);
 #pragma unroll
   for (int s = 0; s < 4; ++s) B[s] = (4 * s + q == c) ? 1.0 : 0.0;
   double akc = bcast_group_bp(A[0], 0, c);  // row 0
@@ -268,6 +295,7 @@ __device__ __forceinline__ void tile_elim1(gs_d4& A, gs_d4& B, double& rsd, int 
   double piv = bcast_lane_bp(dg, 16 * (c & 3) + c);
   if (KMAX < 16) piv = (c >= KMAX) ? 1.0 : piv;  // padding (incl. an augmented pivot)
   rsd = rsq_nr(piv);
+  if constexpr (GS_DIAG_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
 }
 
 namespace gtile {
@@ -522,6 +550,7 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
 #pragma unroll
     for (int s = 0; s < 4; ++s) V[s] = B[s] * rsd;
     t[tix(K, K, NT)] = V;
+    if constexpr (GS_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(GS_UPD_PRIO);
     // TRSM: U_KJ = U_KK^-T T_KJ
 #pragma unroll
     for (int J = K + 1; J < NT; ++J) {
@@ -551,6 +580,7 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
 #pragma unroll
       for (int J = K + 1; J < NT; ++J) t[tix(K, J, NT)] = transpose(t[tix(K, J, NT)], tb, q, c);
     }
+    if constexpr (GS_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
     GS_PH(2)
   }
 
@@ -598,6 +628,7 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
     bM = lp;
     return fail;
   }
+  if constexpr (GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_SOLVE_PRIO);
   // ---- backward: U x = y + zF   (x_K = U_KK^-1 (w_K - sum_{J>K} U_KJ x_J))
   double xcol[NT];
   gs_d4 xrow[NT];
@@ -626,7 +657,9 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
   bF = (lane < NF) ? ob[lane] : 0.0;
   lds_fence();
 
+  if constexpr (GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
   GS_PH(4)
+  if constexpr (GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_FIX_PRIO);
   // ---- fixed-prior block: x_M = h + R z_M - G x_F, 16 rows per chunk
   double* zb = WIDE ? tb : vb;  // z_M staging (tb is free after the factorisation)
   zb[lane] = (lane < nM) ? zM : 0.0;
@@ -662,6 +695,7 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
   lds_fence();
   bM = (lane < nM) ? ob[lane] : 0.0;
   lds_fence();
+  if constexpr (GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
   GS_PH(5)
   return fail;
 }
