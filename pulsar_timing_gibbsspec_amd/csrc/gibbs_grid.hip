@@ -333,9 +333,12 @@ __global__ void k_rho_red(GridArgs A) {
   const int ch = (A.ngrid + GS_RED_NCH - 1) / GS_RED_NCH;
   double ck[GS_RED_NCH];
   double cum = 0.0;
+  // The grid is wave-uniform (scalar loads): unrolled by 8 so a group's loads are issued
+  // together instead of one load + wait per point; the running sum stays sequential.
 #pragma unroll
   for (int j = 0; j < GS_RED_NCH; ++j) {
     const int g1 = min(A.ngrid, (j + 1) * ch);
+#pragma unroll 8
     for (int g = j * ch; g < g1; ++g) {
       const double ratio = red_ratio<EXACT>(tau, gw + A.grid3[g]);
       cum += ratio * exp(-ratio / 2) * LN10;
@@ -343,12 +346,16 @@ __global__ void k_rho_red(GridArgs A) {
     ck[j] = cum;
   }
   const double total = cum;
+  // cdf < u as numpy computes it, cumsum / max < u (EXACT); otherwise cumsum < u * max,
+  // which differs only when u falls within an ulp of a cdf value (no divisions)
+  const double ut = u * total;
+  auto below = [&](double cs) { return EXACT ? (cs / total < u) : (cs < ut); };
   // first chunk whose end crosses u; everything before it counts
   int jx = GS_RED_NCH;
   double entry = 0.0;
 #pragma unroll
   for (int j = GS_RED_NCH - 1; j >= 0; --j) {
-    if (!(ck[j] / total < u)) {
+    if (!below(ck[j])) {
       jx = j;
       entry = j > 0 ? ck[j - 1] : 0.0;
     }
@@ -360,10 +367,11 @@ __global__ void k_rho_red(GridArgs A) {
     cnt = jx * ch;
     double cc = entry;
     const int g1 = min(A.ngrid, (jx + 1) * ch);
+#pragma unroll 4
     for (int g = jx * ch; g < g1; ++g) {
       const double ratio = red_ratio<EXACT>(tau, gw + A.grid3[g]);
       cc += ratio * exp(-ratio / 2) * LN10;
-      cnt += (cc / total < u) ? 1 : 0;
+      cnt += below(cc) ? 1 : 0;
     }
   }
   int idx = cnt - 1;
