@@ -23,7 +23,7 @@ import torch
 from . import _lib
 from .engine import DeviceModel, PTAChains
 from .plumbing import basis_layout, expand_names, last_match, matching_indices, power_bounds, vector_to_dict
-from .pulsar_gibbs import resolve_seed
+from .pulsar_gibbs import HOST_CHAIN, resolve_seed
 
 
 class PTABlockGibbs(object):
@@ -142,19 +142,22 @@ class PTABlockGibbs(object):
             self.d.append(b)
         return self._device_model
 
-    def _new_engine(self, xs):
+    def _new_engine(self, xs, chain_base=0):
         self._check_supported()
         model = self._model(xs)
         hind = self.get_hyper_param_indices()
         red_col = hind.reshape(len(self.pta.pulsars), -1) if hind.size else None
         return PTAChains(model, len(self.param_names), self.get_rho_param_indices(), red_col,
                          (self.rhomin_gw, self.rhomax_gw), (self.rhomin_red, self.rhomax_red),
-                         self.nchains, np.asarray(xs, float))
+                         self.nchains, np.asarray(xs, float), chain_base=chain_base)
 
     # ------------------------------------------------------------ conditionals (single-call API)
     def _engine_at(self, xs):
-        eng = self._engine or self._new_engine(xs)
-        self._engine = eng
+        """The single-call API's own engine: chain ids from HOST_CHAIN, so its Philox draws
+        never repeat those of a sample() run (chains 0 .. nchains - 1)."""
+        eng = self._api_engine if getattr(self, "_api_engine", None) is not None else \
+            self._new_engine(xs, chain_base=HOST_CHAIN)
+        self._api_engine = eng
         eng.x.copy_(torch.as_tensor(np.asarray(xs, float), device=self.ctx.device).expand_as(eng.x))
         b = np.zeros((len(self._b), eng.model.ldb))
         for p, bb in enumerate(self._b):
@@ -181,7 +184,7 @@ class PTABlockGibbs(object):
             _lib.check(lib.gs_phi_from_x(h, eng.C, eng.P * eng.n_f, _lib.ptr(eng.x), eng.n_param,
                                          _lib.ptr(eng.red_col), _lib.ptr(eng.irn)), "gs_phi_from_x")
         _lib.check(lib.gs_rho_curn(h, eng.P, eng.C, eng.n_f, _lib.ptr(eng.tau), _lib.ptr(eng.irn),
-                                   eng.ngrid, _lib.ptr(eng.grid_gw), None, eng.it, 0, _lib.ptr(eng.x),
+                                   eng.ngrid, _lib.ptr(eng.grid_gw), None, eng.it, eng.chain_base, _lib.ptr(eng.x),
                                    eng.n_param, _lib.ptr(eng.gw_col), None), "gs_rho_curn")
         eng.it += 1
         return eng.x[0].cpu().numpy()
@@ -199,7 +202,7 @@ class PTABlockGibbs(object):
         _lib.check(lib.gs_phi_from_x(h, eng.C, eng.n_f, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.gw_col),
                                      _lib.ptr(eng.gwphi)), "gs_phi_from_x")
         _lib.check(lib.gs_rho_red(h, eng.P, eng.C, eng.n_f, _lib.ptr(eng.tau), _lib.ptr(eng.gwphi), eng.ngrid,
-                                  _lib.ptr(eng.grid_red), None, eng.it, 0, _lib.ptr(eng.x), eng.n_param,
+                                  _lib.ptr(eng.grid_red), None, eng.it, eng.chain_base, _lib.ptr(eng.x), eng.n_param,
                                   _lib.ptr(eng.red_col), None), "gs_rho_red")
         eng.it += 1
         return eng.x[0].cpu().numpy()

@@ -52,6 +52,13 @@ def _parse_uniform_bounds(param):
     return uniform_bounds(param)
 
 
+# Global chain id base of the single-call API (update_b, update_white_params, ...): its
+# Philox counters (slot, sweep, chain, pulsar/event) then never coincide with those of a
+# sample() run, whose chains are 0 .. nchains - 1 (the warm-up's draws were
+# being reused by chain 0's first sweeps).
+HOST_CHAIN = 1 << 31
+
+
 def resolve_seed(seed):
     """(seed, Philox key) of a sampler.  seed=None draws fresh OS entropy, as the reference's
     unseeded global np.random does, so independent jobs never repeat each other's chains; the
@@ -394,7 +401,7 @@ class PulsarBlockGibbs(object):
         n = int(iters) if iters is not None else int(self.aclength_ecorr)
         q_rec = torch.empty(n, 1, em.n_bk, dtype=torch.float64, device=dev) if iters is not None else None
         it = None if inj is None else torch.as_tensor(np.asarray(inj, float).reshape(n, 1, 4), device=dev)
-        em.mh(x, ph, n, sweep=self._ndraw, inj=it, q_rec=q_rec)
+        em.mh(x, ph, n, sweep=self._ndraw, chain_base=HOST_CHAIN, inj=it, q_rec=q_rec)
         self._ndraw += 1
         if iters is not None:
             short_chain = q_rec[:, 0].cpu().numpy()
@@ -494,7 +501,7 @@ class PulsarBlockGibbs(object):
         n = int(iters) if iters is not None else int(self.aclength_white)
         q_rec = torch.empty(n, 1, MAX_W, dtype=torch.float64, device=dev) if iters is not None else None
         it = None if inj is None else torch.as_tensor(np.asarray(inj, float).reshape(n, 1, 4), device=dev)
-        wm.mh(x, x.shape[1], n, self._ndraw, inj=it, q_rec=q_rec)
+        wm.mh(x, x.shape[1], n, self._ndraw, chain_base=HOST_CHAIN, inj=it, q_rec=q_rec)
         self._ndraw += 1
         if iters is not None:
             short_chain = q_rec[:, 0, :wind.size].cpu().numpy()
@@ -518,7 +525,7 @@ class PulsarBlockGibbs(object):
             ph = torch.as_tensor(np.ascontiguousarray(self._ecorr_phiinv_F(xs))[None], device=dev)
             zt = None if z is None else torch.as_tensor(np.asarray(z, float)[None, :em.m], device=dev).contiguous()
             b = torch.zeros(1, em.m, dtype=torch.float64, device=dev)
-            em.bdraw(x, ph, b, z=zt, sweep=self._ndraw, first=False)
+            em.bdraw(x, ph, b, z=zt, sweep=self._ndraw, first=False, chain_base=HOST_CHAIN)
             self._ndraw += 1
             if int(em.binfo[0]) != 0:
                 raise np.linalg.LinAlgError(f"Sigma not positive definite (leading minor {int(em.binfo[0])})")
@@ -529,7 +536,7 @@ class PulsarBlockGibbs(object):
         ph = torch.as_tensor(self._phiinv_F(xs)[None, :], dtype=torch.float64, device=dev)
         zt = None if z is None else torch.as_tensor(np.asarray(z, float)[None, :model.ldb],
                                                     dtype=torch.float64, device=dev)
-        b, info = model.bdraw(ph, 1, z=zt, sweep=self._ndraw, event=_lib.EV_USER)
+        b, info = model.bdraw(ph, 1, z=zt, sweep=self._ndraw, event=_lib.EV_USER, chain_base=HOST_CHAIN)
         self._ndraw += 1
         if int(info[0]) != 0:
             raise np.linalg.LinAlgError(f"Sigma not positive definite (leading minor {int(info[0])})")
@@ -560,7 +567,7 @@ class PulsarBlockGibbs(object):
             cols = torch.arange(n_f, dtype=torch.int32, device=dev)
             grid = grid3(self.rhomin, self.rhomax, device=dev)
             _lib.check(self.ctx.lib.gs_rho_gumbel(self.ctx.handle, 1, n_f, _lib.ptr(tau), _lib.ptr(irt), 1000,
-                                                  _lib.ptr(grid), _lib.ptr(ut), self._ndraw, 0, _lib.ptr(x),
+                                                  _lib.ptr(grid), _lib.ptr(ut), self._ndraw, HOST_CHAIN, _lib.ptr(x),
                                                   n_f, _lib.ptr(cols), None), "gs_rho_gumbel")
             self._ndraw += 1
             xnew[gwind] = x[0].cpu().numpy()
@@ -569,7 +576,7 @@ class PulsarBlockGibbs(object):
                                                     device=dev)
         x = torch.empty(1, n_f, dtype=torch.float64, device=dev)
         _lib.check(self.ctx.lib.gs_rho_analytic(self.ctx.handle, 1, 1, 2 * n_f, b.shape[1], _lib.ptr(fidx),
-                                                _lib.ptr(b), _lib.ptr(ut), self._ndraw, 0, self.rhomin,
+                                                _lib.ptr(b), _lib.ptr(ut), self._ndraw, HOST_CHAIN, self.rhomin,
                                                 self.rhomax, _lib.ptr(x), n_f), "gs_rho_analytic")
         self._ndraw += 1
         xnew[gwind] = x[0].cpu().numpy()
@@ -608,13 +615,14 @@ class PulsarBlockGibbs(object):
             hi += [b] * (p.size or 1)
         return np.array(lo), np.array(hi)
 
-    def _red_engine(self, xs, n_chain, jumps=None, x_first=None):
+    def _red_engine(self, xs, n_chain, jumps=None, x_first=None, chain_base=0):
         ia, ig, lnphi, bounds = self._red_setup(xs)
         if jumps is None:
             jumps = getattr(self, "_red_jumps", None) or RedJumps(np.eye(2) * 0.01, np.zeros((0, 2)), bounds,
                                                                   self.ctx.device)
         return RedNoiseChains(self._model(xs), len(xs), self.get_gwrho_param_indices(),
-                              (ia, ig), lnphi, jumps, self.rhomin, self.rhomax, n_chain, xs, x_first=x_first)
+                              (ia, ig), lnphi, jumps, self.rhomin, self.rhomax, n_chain, xs, x_first=x_first,
+                              chain_base=chain_base)
 
     def get_lnlikelihood_red(self, xs):
         """get_lnlikelihood_red (pulsar_gibbs.py:549-566) on the device at (xs, self._b)."""
@@ -645,7 +653,7 @@ class PulsarBlockGibbs(object):
             return x1
         if rind.size == 0:
             return xnew
-        eng = self._red_engine(xnew, 1)
+        eng = self._red_engine(xnew, 1, chain_base=HOST_CHAIN)
         eng.b[0, :len(self._b)] = torch.as_tensor(self._b, device=self.ctx.device)
         eng.it = self._ndraw
         eng._tau()

@@ -384,3 +384,30 @@ def test_pulsar_block_gibbs_ecorr_white_surface(ctx, tmp_path):
     chain = gb.sample(g["x0"], outdir=str(tmp_path), niter=8, save_every=4)
     assert chain.shape == (8, len(g["param_names"])) and np.isfinite(chain).all()
     assert gb.chains.shape[0] == 32 and gb.aclength_white >= 1 and gb.aclength_ecorr >= 1
+
+
+def test_ecorr_bdraw_chain_mask_mixed(ctx):
+    """the 8-chain shared-Bx b_E kernel (k_ecorr_bdraw_e<8>) with a mixed 0/1
+    chain_mask and n_chain not a multiple of 8: masked chains keep their b untouched (both
+    the b_R draw and the b_E scatter), unmasked chains equal the same draw run unmasked."""
+    import torch
+    g = golden("ecorr_mh_j1713.npz")
+    m = g["T"].shape[1]
+    C = 13
+    em = _model(ctx, g, C)
+    rng = np.random.default_rng(5)
+    X = np.broadcast_to(g["x0"], (C, g["x0"].size)).copy()
+    X[:, _gwind(g)] += rng.uniform(-0.3, 0.3, (C, len(_gwind(g))))
+    Z = rng.standard_normal((C, m))
+    ref = torch.zeros(C, m, dtype=torch.float64, device="cuda")
+    em.bdraw(_dev(X), _dev(_phiinv_F(g, X)), ref, z=_dev(Z))
+    mask = np.array([1, 0, 1, 1, 0, 0, 1, 0, 1, 1, 1, 0, 1], np.int32)
+    sentinel = 123.25
+    b = torch.full((C, m), sentinel, dtype=torch.float64, device="cuda")
+    em.bdraw(_dev(X), _dev(_phiinv_F(g, X)), b, z=_dev(Z), chain_mask=torch.as_tensor(mask, device="cuda"))
+    B, R = b.cpu().numpy(), ref.cpu().numpy()
+    for c in range(C):
+        if mask[c]:
+            assert np.array_equal(B[c], R[c]), c
+        else:
+            assert np.all(B[c] == sentinel), c

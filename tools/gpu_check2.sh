@@ -1,0 +1,9 @@
+#!/bin/bash
+# Full GPU tests + the PTA bench lines (per-kernel times).
+set -u
+O=gpurun_out
+mkdir -p $O
+export GS_PARITY_REPORT=$O/parity
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
+echo "pytest rc=$?"; tail -2 $O/pytest_gpu.log; grep -E "^E  |FAILED" $O/pytest_gpu.log | head -10
+bash tools/gpu_pta_check.sh | tail -3
