@@ -91,7 +91,7 @@ class PulsarArrayGibbs(object):
             fixed.append(ph[mask])
         return DeviceModel(self.ctx, T, N, R, [s.gwid for s in self.samplers], fixed)
 
-    def sample(self, xs_list, outdir="./", niter=10000, resume=False, save_every=100):
+    def sample(self, xs_list, outdir="./", niter=10000, resume=False, save_every=100, record_bchains=None):
         """Every pulsar's PulsarBlockGibbs.sample (pulsar_gibbs.py:620-710) at once.
         xs_list[p]: pulsar p's initial parameter vector.  Pulsar p writes to
         ``outdir/<pulsar name>/``.  Returns the list of chain-0 chains."""
@@ -105,5 +105,5 @@ class PulsarArrayGibbs(object):
             np.savetxt(f"{o}/pars_bchain.txt", s.b_param_names, fmt="%s")
         model = self._model(xs_list)
         self._runner = sample_free_spectrum(self.samplers, model, xs_list, outdirs, niter, resume, save_every,
-                                            psr_base=self.psr_base)
+                                            psr_base=self.psr_base, record_bchains=record_bchains)
         return [s.chain for s in self.samplers]

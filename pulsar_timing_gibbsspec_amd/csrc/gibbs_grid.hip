@@ -198,9 +198,9 @@ __global__ __launch_bounds__(256) void k_rho_curn_sum(GridArgs A) {
 // The same draw as k_rho_curn without numpy's operation order (GS_OPT_GRID_EXACT = 0,
 // the default): log pdf_g = -sum_p log(irn_p + rho_g) - 1/2 sum_p tau_p / (irn_p + rho_g)
 // + const (sum_p log tau_p and P log ln10 cancel in cdf / max).  Per (grid point, pulsar):
-// one add, one v_rcp_f64 + Newton step, one FMA into the ratio sum and one multiply into
-// the product of (irn + rho), renormalised by frexp every 8 pulsars -- instead of a
-// division and an exp; one log and one exp per grid point.  pdf rounding differs from
+// one add, two multiplies and one FMA (the ratio sum kept as a fraction N / D over the
+// product D of (irn + rho), renormalised by frexp every 8 pulsars) -- instead of a
+// division and an exp; one log, one division and one exp per grid point.  pdf rounding differs from
 // numpy's by ~1e-15 relative, so the index can only differ when u falls that close to a
 // cdf value (tested equal to the reference on every fixture sweep).  One wavefront per
 // row, lane l owns grid points [l G, (l+1) G), wave scan of the lane sums.
@@ -214,14 +214,17 @@ __global__ __launch_bounds__(256) void k_rho_curn_fast(GridArgs A) {
   const int c = (int)(r % A.n_chain), k = (int)(r / A.n_chain);
   const int G = (A.ngrid + 63) / 64;
   const int g0 = lane * G;
-  double rg[CF_MAXG], prod[CF_MAXG], sr[CF_MAXG];
+  // Per grid point: D = prod_p (irn_p + rho), N / D = sum_p tau_p / (irn_p + rho) kept as one
+  // fraction (N <- N a + tau D, D <- D a: three multiplies and an FMA per (point, pulsar),
+  // no division); D and N are rescaled together by D's binary exponent every 8 pulsars.
+  double rg[CF_MAXG], dd[CF_MAXG], nn[CF_MAXG];
   int ex[CF_MAXG];
 #pragma unroll
   for (int j = 0; j < CF_MAXG; ++j) {
     const int g = min(g0 + j, A.ngrid - 1);
     rg[j] = A.grid3[g];
-    prod[j] = 1.0;
-    sr[j] = 0.0;
+    dd[j] = 1.0;
+    nn[j] = 0.0;
     ex[j] = 0;
   }
   const int P = A.n_psr;
@@ -231,17 +234,16 @@ __global__ __launch_bounds__(256) void k_rho_curn_fast(GridArgs A) {
 #pragma unroll
     for (int j = 0; j < CF_MAXG; ++j) {
       const double a = irn + rg[j];
-      double ra = __builtin_amdgcn_rcp(a);
-      ra = fma(ra, fma(-a, ra, 1.0), ra);
-      ra = fma(ra, fma(-a, ra, 1.0), ra);
-      sr[j] = fma(tau, ra, sr[j]);
-      prod[j] *= a;
+      nn[j] = fma(nn[j], a, tau * dd[j]);
+      dd[j] *= a;
     }
     if ((p & 7) == 7 || p == P - 1) {
 #pragma unroll
       for (int j = 0; j < CF_MAXG; ++j) {
-        ex[j] += __builtin_amdgcn_frexp_exp(prod[j]);
-        prod[j] = __builtin_amdgcn_frexp_mant(prod[j]);
+        const int e = __builtin_amdgcn_frexp_exp(dd[j]);
+        ex[j] += e;
+        dd[j] = __builtin_amdgcn_frexp_mant(dd[j]);
+        nn[j] = ldexp(nn[j], -e);
       }
     }
   }
@@ -252,7 +254,7 @@ __global__ __launch_bounds__(256) void k_rho_curn_fast(GridArgs A) {
   for (int j = 0; j < CF_MAXG; ++j) {
     lp[j] = -__builtin_inf();
     if (j < G && g0 + j < A.ngrid) {
-      lp[j] = -(log(prod[j]) + ex[j] * LN2) - 0.5 * sr[j];
+      lp[j] = -(log(dd[j]) + ex[j] * LN2) - 0.5 * (nn[j] / dd[j]);
       mx = fmax(mx, lp[j]);
     }
   }

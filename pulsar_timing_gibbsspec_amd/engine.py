@@ -267,11 +267,17 @@ class HistoryStreamer:
     the copy engine while the next block's sweeps run.  ``fetch`` waits for a slot's
     copy and returns the pinned host tensors.  A slot is reused only after its fetch."""
 
-    def __init__(self, ctx, shapes, dtype=torch.float64):
+    def __init__(self, ctx, shapes, dtype=torch.float64, views=None):
+        """shapes: device record buffers (rows first); views[i] (optional): the part of a
+        block of buffer i that goes to the host, e.g. ``lambda t: t[:, ::nc]`` for chain 0
+        of every pulsar -- the rest stays in HBM and never crosses PCIe."""
         dev = ctx.device
         self.ctx = ctx
+        self.views = list(views) if views is not None else [None] * len(shapes)
+        self.views = [v if v is not None else (lambda t: t) for v in self.views]
+        hshapes = [tuple(v(torch.empty(s, device="meta")).shape) for s, v in zip(shapes, self.views)]
         self.dev_bufs = [[torch.empty(s, dtype=dtype, device=dev) for s in shapes] for _ in range(2)]
-        self.host_bufs = [[torch.empty(s, dtype=dtype, pin_memory=True) for s in shapes] for _ in range(2)]
+        self.host_bufs = [[torch.empty(s, dtype=dtype, pin_memory=True) for s in hshapes] for _ in range(2)]
         self.side = torch.cuda.Stream(device=dev)
         self.done = [torch.cuda.Event(), torch.cuda.Event()]
         self.rows = [0, 0]
@@ -284,8 +290,8 @@ class HistoryStreamer:
         ready.record(self.ctx.stream)
         with torch.cuda.stream(self.side):
             self.side.wait_event(ready)
-            for d, h in zip(self.dev_bufs[slot], self.host_bufs[slot]):
-                h[:n].copy_(d[:n], non_blocking=True)
+            for d, h, v in zip(self.dev_bufs[slot], self.host_bufs[slot], self.views):
+                h[:n].copy_(v(d[:n]), non_blocking=True)
             self.done[slot].record(self.side)
         self.rows[slot] = n
 

@@ -68,7 +68,8 @@ def resolve_seed(seed):
     return int(seed), int(np.random.SeedSequence(int(seed)).generate_state(1, np.uint64)[0])
 
 
-def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_every, psr_base=0):
+def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_every, psr_base=0,
+                         record_bchains=None):
     """The free-spectrum sample loop (PulsarBlockGibbs.sample, pulsar_gibbs.py:620-710) for
     one or many pulsars at once: pulsar p of ``model`` is ``samplers[p]``'s PTA, its chains
     are systems p*nchains .. p*nchains + nchains - 1 of one FreeSpectrumChains run (the
@@ -79,7 +80,12 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
     ii > 0 (pulsar_gibbs.py:701-710); with nchains > 1 also chains.npy / bchains.npy.
     Resume continues from the shortest saved chain of the pulsars: the recorded (x, b) of
     row start-1 are restored and sweep start-1 re-run with its own Philox counters, so a
-    resumed run reproduces the uninterrupted one bit for bit."""
+    resumed run reproduces the uninterrupted one bit for bit.
+
+    record_bchains: keep every chain's b history on the host (``bchains``, bchains.npy);
+    default only for nchains <= 16 -- 4096 chains x 10^4 sweeps of b are 25 GB, and chain 0's
+    b (the reference's bchain) is what the reference layout needs.  Without it only chain 0's
+    b rows cross PCIe (the rest are recorded in HBM only)."""
     P = len(samplers)
     nc = samplers[0].nchains
     ctx = model.ctx
@@ -87,11 +93,14 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
     rhomin, rhomax = samplers[0].rhomin, samplers[0].rhomax
     m = [int(v) for v in model.m]
     n_f = model.NF // 2
+    if record_bchains is None:
+        record_bchains = nc <= 16
+    allb = nc > 1 and bool(record_bchains)
     for s in samplers:
         s.chain = np.zeros((niter, n_f))
         s.bchain = np.zeros((niter, len(s._b)))
         s.chains = np.zeros((nc, niter, n_f)) if nc > 1 else None
-        s.bchains = np.zeros((nc, niter, len(s._b))) if nc > 1 else None
+        s.bchains = np.zeros((nc, niter, len(s._b))) if allb else None
         s.iter = 0
     start = 0
     if resume and all(os.path.exists(f"{o}/chain.npy") for o in outdirs):
@@ -103,8 +112,8 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
             s.bchain[:start] = b0[:start]
         # every chain's rows when the multi-chain files hold them (else all chains restart
         # from chain 0's recorded state)
-        multi = nc > 1 and all(os.path.exists(f"{o}/chains.npy") and os.path.exists(f"{o}/bchains.npy")
-                               for o in outdirs)
+        multi = allb and all(os.path.exists(f"{o}/chains.npy") and os.path.exists(f"{o}/bchains.npy")
+                             for o in outdirs)
         if multi:
             prevc = [(np.load(f"{o}/chains.npy"), np.load(f"{o}/bchains.npy")) for o in outdirs]
             multi = all(c.shape[0] == nc and min(c.shape[1], b.shape[1]) >= start for c, b in prevc)
@@ -129,7 +138,9 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
     runner.it = max(runner.it, start)
     blk = max(1, save_every) + 1
     # block k+1's sweeps run while block k's rows stream to pinned host memory
-    streamer = HistoryStreamer(ctx, [(blk, P * nc, n_f), (blk, P * nc, model.ldb)])
+    bview = None if (allb or nc == 1) else (lambda t: t[:, ::nc])      # chain 0 of every pulsar
+    streamer = HistoryStreamer(ctx, [(blk, P * nc, n_f), (blk, P * nc, model.ldb)], views=[None, bview])
+    bstride = 1 if bview is not None else nc
 
     def consume(slot, ii, nxt):
         xh, bh = (t.numpy() for t in streamer.fetch(slot))
@@ -137,11 +148,12 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
         save = last % save_every == 0 and last > 0
         for p, (s, o) in enumerate(zip(samplers, outdirs)):
             xp = xh[:, p * nc:(p + 1) * nc]
-            bp = bh[:, p * nc:(p + 1) * nc, :m[p]]
+            bp = bh[:, p * bstride:(p + 1) * bstride, :m[p]]
             s.chain[ii:nxt] = xp[:, 0]
             s.bchain[ii:nxt] = bp[:, 0]
             if nc > 1:
                 s.chains[:, ii:nxt] = np.moveaxis(xp, 1, 0)
+            if allb:
                 s.bchains[:, ii:nxt] = np.moveaxis(bp, 1, 0)
             s.iter = last
             if save:
@@ -149,6 +161,7 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
                 np.save(f"{o}/bchain.npy", s.bchain[:last + 1, :])
                 if nc > 1:
                     np.save(f"{o}/chains.npy", s.chains[:, :last + 1])
+                if allb:
                     np.save(f"{o}/bchains.npy", s.bchains[:, :last + 1])
 
     ii, slot, pending = start, 0, None
@@ -685,7 +698,8 @@ class PulsarBlockGibbs(object):
         if not self._white_loop() and not np.array_equal(gwind, np.arange(len(self.gwid) // 2)):
             raise NotImplementedError("gw rho parameters must be the whole parameter vector")
 
-    def sample(self, xs, outdir="./", niter=10000, resume=False, save_every=100, *, flush_final=False):
+    def sample(self, xs, outdir="./", niter=10000, resume=False, save_every=100, *, flush_final=False,
+               record_bchains=None):
         """PulsarBlockGibbs.sample (pulsar_gibbs.py:620-710) as persistent device sweeps.
 
         Chain row ii holds the state BEFORE sweep ii (row 0 = xs, bchain[0] = 0).
@@ -713,7 +727,8 @@ class PulsarBlockGibbs(object):
             if flush_final:
                 self._flush(outdir)
             return out
-        sample_free_spectrum([self], self._model(xs), [xs], [outdir], niter, resume, save_every)
+        sample_free_spectrum([self], self._model(xs), [xs], [outdir], niter, resume, save_every,
+                             record_bchains=record_bchains)
         if flush_final:
             self._flush(outdir)
         return self.chain
@@ -726,6 +741,7 @@ class PulsarBlockGibbs(object):
         np.save(f"{outdir}/bchain.npy", self.bchain[:n, :])
         if self.chains is not None:
             np.save(f"{outdir}/chains.npy", self.chains[:, :n])
+        if getattr(self, "bchains", None) is not None:
             np.save(f"{outdir}/bchains.npy", self.bchains[:, :n])
 
     def _sample_white(self, xs, outdir, niter, resume, save_every):

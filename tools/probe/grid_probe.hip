@@ -6,8 +6,8 @@
 //
 //   red  : ratio = tau * rcp(gw + rho_g) (+ 2 Newton steps); cdf += ratio * exp(-ratio/2) * ln10
 //          -- k_rho_red's per-point work (one fp64 exp per point)
-//   curn : a = irn + rho_g; sr += tau * rcp(a) (+ 2 Newton); prod *= a
-//          -- k_rho_curn_fast's per-(point, pulsar) work (no transcendental)
+//   curn : a = irn + rho_g; N = N a + tau D; D *= a (rescaled every 8 pulsars)
+//          -- k_rho_curn_fast's per-(point, pulsar) work (no transcendental, no division)
 //
 // Build: hipcc --offload-arch=gfx950 -O3 tools/probe/grid_probe.hip -o tools/probe/grid_probe
 // Run:   tools/probe/grid_probe  -> one JSON line
@@ -47,10 +47,10 @@ __global__ __launch_bounds__(256) void k_red(int npts, double q, double* out) {
 
 __global__ __launch_bounds__(256) void k_curn(int npts, double q, double* out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  double sr[8], prod[8], rg[8];
+  double nn[8], dd[8], rg[8];
   for (int j = 0; j < 8; ++j) {
-    sr[j] = 0.0;
-    prod[j] = 1.0;
+    nn[j] = 0.0;
+    dd[j] = 1.0;
     rg[j] = 1e-18 * (1.0 + j);
   }
   const double tau = 1e-14 * (1.0 + 0.01 * (t & 255));
@@ -59,14 +59,18 @@ __global__ __launch_bounds__(256) void k_curn(int npts, double q, double* out) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const double a = irn + rg[j];
-      sr[j] = fma(tau, rcp_nr(a), sr[j]);
-      prod[j] *= a;
+      nn[j] = fma(nn[j], a, tau * dd[j]);
+      dd[j] *= a;
     }
     if ((p & 7) == 7)
-      for (int j = 0; j < 8; ++j) prod[j] = __builtin_amdgcn_frexp_mant(prod[j]);
+      for (int j = 0; j < 8; ++j) {
+        const int e = __builtin_amdgcn_frexp_exp(dd[j]);
+        dd[j] = __builtin_amdgcn_frexp_mant(dd[j]);
+        nn[j] = ldexp(nn[j], -e);
+      }
   }
   double s = 0.0;
-  for (int j = 0; j < 8; ++j) s += sr[j] + prod[j];
+  for (int j = 0; j < 8; ++j) s += nn[j] + dd[j];
   if (s == 1.2345) out[t] = s;
 }
 
