@@ -178,13 +178,13 @@ __device__ __forceinline__ int bdraw_wave(const ModelLds& M, int NMX, int nM, in
 // One b|rho draw with the variant BC (tile MFMA or lane-row broadcast).  NFC > 0: the
 // fixed-NF instantiations (20 / 40 / 60, every variant); NFC == 0: any even NF < 16 NTC at
 // run time (tile variant only).
-template <int NFC, int NTC, int BC>
+template <int NFC, int NTC, int BC, bool PR = false>
 __device__ __forceinline__ int bdraw_sys(const ModelLds& M, int NMX, int nM, int lane, double phinv,
                                          double zF, double zM, double& bF, double& bM, double* scr, int NF) {
   if constexpr (NFC == 0)
-    return bdraw_tile_n<NTC>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
+    return bdraw_tile_n<NTC, false, PR>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
   else if constexpr (BC == GS_BCAST_TILE)
-    return bdraw_tile<NFC>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
+    return bdraw_tile<NFC, false, PR>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
   else
     return bdraw_wave<NFC, BC>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
 }
@@ -247,7 +247,9 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
   const int p = blockIdx.x / nb;
   const int c = (blockIdx.x % nb) * WPB + wave;
   // shared pulsar model: staged once per workgroup; per-system models (white-noise
-  // runs, TNT differs per chain) are read from global memory (L2) directly
+  // runs, TNT differs per chain) are read from global memory (L2) directly.  (Looping a
+  // workgroup over several chain groups to stage less often measured slower: the loop
+  // raised the kernel from 164 to 231 VGPRs, 3 -> 2 waves/SIMD.)
   if (!A.model_per_sys) stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
   if (c >= A.n_chain) return;
   const int64_t sys = (int64_t)p * A.n_chain + c;
@@ -416,7 +418,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
       }
       if (pass == 0) phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;  // first draw from xs
       GS_PH(7)
-      const int f = bdraw_sys<NFC, NTC, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
+      const int f = bdraw_sys<NFC, NTC, BC, true>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
       if (!fail) fail = f;
     }
   }

@@ -255,10 +255,10 @@ __device__ __forceinline__ constexpr int tix(int I, int J, int NT) {
 #ifndef GS_RHO_PRIO  // ... while it runs the sweep's rho|b draw and gate (k_sweep_freespec)
 #define GS_RHO_PRIO 0
 #endif
-template <int KMAX>
+template <int KMAX, bool PR = false>
 __device__ __forceinline__ void tile_elim1(gs_d4& A, gs_d4& B, double& rsd, int q, int c) {
   using namespace gtile;
-  if constexpr (GS_DIAG_PRIO > 0) __builtin_amdgcn_s_setprio(GS_DIAG_PRIO);
+  if constexpr (PR && GS_DIAG_PRIO > 0) __builtin_amdgcn_s_setprio(GS_DIAG_PRIO);
 #pragma unroll
   for (int s = 0; s < 4; ++s) B[s] = (4 * s + q == c) ? 1.0 : 0.0;
   double akc = bcast_group_bp(A[0], 0, c);  // row 0
@@ -295,7 +295,7 @@ __device__ __forceinline__ void tile_elim1(gs_d4& A, gs_d4& B, double& rsd, int 
   double piv = bcast_lane_bp(dg, 16 * (c & 3) + c);
   if (KMAX < 16) piv = (c >= KMAX) ? 1.0 : piv;  // padding (incl. an augmented pivot)
   rsd = rsq_nr(piv);
-  if constexpr (GS_DIAG_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+  if constexpr (PR && GS_DIAG_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
 }
 
 namespace gtile {
@@ -399,24 +399,25 @@ __device__ __forceinline__ void tile_elim2(gs_d4& A, gs_d4& B, double& rsd, int 
 #ifndef GS_TILE_PAIR
 #define GS_TILE_PAIR 0
 #endif
-template <int KMAX>
+template <int KMAX, bool PR = false>
 __device__ __forceinline__ void tile_elim(gs_d4& A, gs_d4& B, double& rsd, int q, int c) {
   if constexpr (GS_TILE_PAIR)
     tile_elim2<KMAX>(A, B, rsd, q, c);
   else
-    tile_elim1<KMAX>(A, B, rsd, q, c);
+    tile_elim1<KMAX, PR>(A, B, rsd, q, c);
 }
 
 // tile_elim with a runtime KMAX (0..16): one instantiation per value, a uniform switch
 // that folds away when kmax is a compile-time constant after inlining.
+template <bool PR = false>
 __device__ __forceinline__ void tile_elim_rt(int kmax, gs_d4& A, gs_d4& B, double& rsd, int q, int c) {
   switch (kmax) {
 #define GS_TE(K) \
-  case K: tile_elim<K>(A, B, rsd, q, c); return;
+  case K: tile_elim<K, PR>(A, B, rsd, q, c); return;
     GS_TE(0) GS_TE(1) GS_TE(2) GS_TE(3) GS_TE(4) GS_TE(5) GS_TE(6) GS_TE(7)
     GS_TE(8) GS_TE(9) GS_TE(10) GS_TE(11) GS_TE(12) GS_TE(13) GS_TE(14) GS_TE(15)
 #undef GS_TE
-    default: tile_elim<16>(A, B, rsd, q, c); return;
+    default: tile_elim<16, PR>(A, B, rsd, q, c); return;
   }
 }
 
@@ -445,7 +446,9 @@ __device__ __forceinline__ double d4_get(const gs_d4 v, int i) {
 // WIDE (64 < nM <= 128 timing-model columns, gs_bdraw only): z_M rows 64..127 arrive in zMa
 // (lane l holds row 64 + l), the R z_M operand is staged in tb, and rows >= 64 of x_M are
 // stored straight to bext[mrow[row]] (rows < 64 still return in bM, one per lane).
-template <int NT, int CPC, bool LNL, bool WIDE = false, typename ModelT>
+// PR: the issue-priority raises of GS_DIAG_PRIO / GS_SOLVE_PRIO (the persistent fused sweep
+// only: in the short-lived k_bdraw waves at 3 waves/SIMD they cost 25 %).
+template <int NT, int CPC, bool LNL, bool WIDE = false, bool PR = false, typename ModelT>
 __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM, int lane, double phinv,
                                                double zF, double zM, double& bF, double& bM,
                                                double* __restrict__ scr, const int nf_rt, double zMa = 0.0,
@@ -530,11 +533,11 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
     double rsd;
     if (K == NT - 1) {
       if constexpr (CPC >= 0)
-        tile_elim<CPC>(A, B, rsd, q, c);
+        tile_elim<CPC, PR>(A, B, rsd, q, c);
       else
-        tile_elim_rt(CP, A, B, rsd, q, c);
+        tile_elim_rt<PR>(CP, A, B, rsd, q, c);
     } else {
-      tile_elim<16>(A, B, rsd, q, c);
+      tile_elim<16, PR>(A, B, rsd, q, c);
     }
     if (AUG && K == NT - 1) {
       // y_last[k] = (row CP of the eliminated tile)[k] * pivot_k^-1/2, k < CP
@@ -550,7 +553,7 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
 #pragma unroll
     for (int s = 0; s < 4; ++s) V[s] = B[s] * rsd;
     t[tix(K, K, NT)] = V;
-    if constexpr (GS_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(GS_UPD_PRIO);
+    if constexpr (PR && GS_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(GS_UPD_PRIO);
     // TRSM: U_KJ = U_KK^-T T_KJ
 #pragma unroll
     for (int J = K + 1; J < NT; ++J) {
@@ -580,7 +583,7 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
 #pragma unroll
       for (int J = K + 1; J < NT; ++J) t[tix(K, J, NT)] = transpose(t[tix(K, J, NT)], tb, q, c);
     }
-    if constexpr (GS_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+    if constexpr (PR && GS_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
     GS_PH(2)
   }
 
@@ -628,7 +631,7 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
     bM = lp;
     return fail;
   }
-  if constexpr (GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_SOLVE_PRIO);
+  if constexpr (PR && GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_SOLVE_PRIO);
   // ---- backward: U x = y + zF   (x_K = U_KK^-1 (w_K - sum_{J>K} U_KJ x_J))
   double xcol[NT];
   gs_d4 xrow[NT];
@@ -657,9 +660,9 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
   bF = (lane < NF) ? ob[lane] : 0.0;
   lds_fence();
 
-  if constexpr (GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+  if constexpr (PR && GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
   GS_PH(4)
-  if constexpr (GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_FIX_PRIO);
+  if constexpr (PR && GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_FIX_PRIO);
   // ---- fixed-prior block: x_M = h + R z_M - G x_F, 16 rows per chunk
   double* zb = WIDE ? tb : vb;  // z_M staging (tb is free after the factorisation)
   zb[lane] = (lane < nM) ? zM : 0.0;
@@ -695,26 +698,27 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
   lds_fence();
   bM = (lane < nM) ? ob[lane] : 0.0;
   lds_fence();
-  if constexpr (GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+  if constexpr (PR && GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
   GS_PH(5)
   return fail;
 }
 
 // Fixed NF (the tuned 20 / 40 / 60 instantiations); NF % 16 != 0.
-template <int NF, bool LNL = false, typename ModelT>
+template <int NF, bool LNL = false, bool PR = false, typename ModelT>
 __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int lane, double phinv,
                                           double zF, double zM, double& bF, double& bM,
                                           double* __restrict__ scr) {
   static_assert(NF % 16 != 0, "the augmented column needs a free slot in the last tile");
-  return bdraw_tile_core<(NF + 15) / 16, NF % 16, LNL>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
+  return bdraw_tile_core<(NF + 15) / 16, NF % 16, LNL, false, PR>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr,
+                                                                  NF);
 }
 
 // Any even NF with NF / 16 + 1 == NT (NF <= 64: one lane per free-spectrum column).
-template <int NT, bool LNL = false, typename ModelT>
+template <int NT, bool LNL = false, bool PR = false, typename ModelT>
 __device__ __forceinline__ int bdraw_tile_n(const ModelT& M, int NMX, int nM, int lane, double phinv,
                                             double zF, double zM, double& bF, double& bM,
                                             double* __restrict__ scr, int NF) {
-  return bdraw_tile_core<NT, -1, LNL>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
+  return bdraw_tile_core<NT, -1, LNL, false, PR>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
 }
 
 // Same with up to 128 timing-model columns (see bdraw_tile_core, WIDE).
