@@ -39,7 +39,7 @@
 #define GS_MINW(bc) ((bc) == GS_BCAST_TILE ? GS_TILE_MINW : GS_SWEEP_MINW)
 
 // per-wave LDS scratch (doubles) of each factorisation variant
-#define GS_SCR_DOUBLES(bc) ((bc) == GS_BCAST_TILE ? GS_TILE_SCR : 64)
+#define GS_SCR_DOUBLES(bc, nf) ((bc) == GS_BCAST_TILE ? gs_tile_scr(nf) : 64)
 
 #ifndef GS_BCAST_CHUNK
 #define GS_BCAST_CHUNK 8
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
     gs_normal2(gs_counter(64 + lane, sw, A.chain_base + c, p + A.psr_base, A.event), A.key, zMa, unused);
   }
   double bF = 0.0, bM = 0.0;
-  double* scr = lds + wave * GS_TILE_SCR;
+  double* scr = lds + wave * gs_tile_scr(NF);
   double* brow = A.b + sys * A.ldb;
   const int fail = bdraw_tile_wide<NTC>(M, A.NMX, nM, lane, phinv, zF, zM, zMa, bF, bM, scr, NF, brow, mrow);
   if (lane < NF) brow[fi] = bF;
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
     gs_normal2(gs_counter(lane, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, p + A.psr_base, A.event), A.key, zF, zM);
   }
   double bF = 0.0, bM = 0.0;
-  double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * GS_SCR_DOUBLES(BC);
+  double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * GS_SCR_DOUBLES(BC, NF);
   const int fail = bdraw_sys<NFC, NTC, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
   if (lane < NF) A.b[sys * A.ldb + fi] = bF;
   if (lane < nM) A.b[sys * A.ldb + mi] = bM;
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
   const ModelLds M = model_view(mb, NF, A.NMX);
   const double phinv = lane < NF ? A.phiinv_F[sys * NF + lane] : 1.0;
   double yy = 0.0, ldS = 0.0;
-  double* scr = lds + (in_lds ? A.mstride : 0) + wave * GS_TILE_SCR;
+  double* scr = lds + (in_lds ? A.mstride : 0) + wave * gs_tile_scr(NF);
   int fail;
   if constexpr (NFC == 0)
     fail = bdraw_tile_n<NTC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr, NF);
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
   const int kf = act ? (lane >> 1) : 0;  // frequency of this lane
   const int fi = act ? A.fidx[p * NF + lane] : 0;
   const int mi = actm ? A.midx[p * A.NMX + lane] : 0;
-  double* scr = lds + A.mstride + wave * GS_SCR_DOUBLES(BC);
+  double* scr = lds + A.mstride + wave * GS_SCR_DOUBLES(BC, NF);
   GS_PH_INIT(scr)
 #ifdef GS_STATIC_PRIO
   // A/B knob: half of the workgroups (one of the two co-resident waves of a SIMD) at priority 1
@@ -511,7 +511,7 @@ int launch_lnlike_marg(hipStream_t s, const LnlArgs& a) {
   constexpr int WPB = GS_SWEEP_WPB;
   const int nb = (a.n_chain + WPB - 1) / WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
-  const size_t lds = ((size_t)(a.model_per_sys || a.model_global ? 0 : a.mstride) + GS_TILE_SCR * WPB) *
+  const size_t lds = ((size_t)(a.model_per_sys || a.model_global ? 0 : a.mstride) + gs_tile_scr(a.NF) * WPB) *
                      sizeof(double);
   switch (a.NF) {
     case 20: hipLaunchKernelGGL((k_lnlike_marg<20, 0, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
@@ -533,7 +533,7 @@ int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
   const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
-  const size_t lds = ((size_t)a.mstride + (fixed ? GS_SCR_DOUBLES(a.bcast) : GS_TILE_SCR) * GS_SWEEP_WPB) *
+  const size_t lds = ((size_t)a.mstride + (fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) * GS_SWEEP_WPB) *
                      sizeof(double);
   return dispatch_nf_sweep<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
@@ -543,7 +543,7 @@ int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
   dim3 grid((unsigned)(a.n_psr * nb));
   if (a.NMX > 64) {
     constexpr int WPB = GS_SWEEP_WPB;
-    const size_t lds = (size_t)GS_TILE_SCR * WPB * sizeof(double);
+    const size_t lds = (size_t)gs_tile_scr(a.NF) * WPB * sizeof(double);
     if (a.NF <= 0 || a.NF > 64 || (a.NF & 1)) return 1;
     switch (a.NF / 16 + 1) {
       case 1: hipLaunchKernelGGL((k_bdraw_wide<1, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
@@ -555,7 +555,7 @@ int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
   }
   const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
   const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) +
-                      (fixed ? GS_SCR_DOUBLES(a.bcast) : GS_TILE_SCR) * GS_SWEEP_WPB) * sizeof(double);
+                      (fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) * GS_SWEEP_WPB) * sizeof(double);
   return dispatch_nf_bdraw<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
 

@@ -6,12 +6,19 @@
 #define GS_WAVE 64
 
 // per-wave LDS scratch (doubles) of the tile b-draw (gibbs_tile.h): 272 transpose /
-// factor rows + 64 vector + 80 output (16 per tile row, up to 5 tile rows)
+// factor rows + 64 vector + max(64, 16 NT) output (NT = NF / 16 + 1 <= 5).  Sized per NF,
+// not at the 5-tile maximum: the LDS of a k_bdraw workgroup (model block + 4 scratches) sits
+// at the 3-workgroups-per-CU edge for the simulated array (NF = 60, NMX = 17: 53320 B at 400
+// doubles per wave vs 53832 B at 416), and dropping to 2 workgroups per CU cost 25 %
+// (0.665 -> 0.835 ms per launch measured on MI355X).
+#define GS_TILE_SCR_MAX 416
+__host__ __device__ constexpr int gs_tile_scr(int NF) {
 #ifdef GS_PHASE_PROF
-#define GS_TILE_SCR 424
+  return GS_TILE_SCR_MAX + 8;  // + the phase-profile accumulators at 416..423
 #else
-#define GS_TILE_SCR 416
+  return 336 + (NF / 16 + 1 > 4 ? 16 * (NF / 16 + 1) : 64);  // output: max(64 lanes, 16 NT)
 #endif
+}
 
 // ---------------------------------------------------------------- intra-wave LDS sync
 // Lanes of one wavefront exchanging data through LDS: wavefront-scope release/acquire
