@@ -31,8 +31,10 @@
 #define GS_BCAST_BATCH 2
 #define GS_BCAST_TILE 3
 
-// min workgroups per CU (launch bounds): the tile variant fits 3 x 4 waves of
-// <= 168 VGPRs and 3 x 52.5 KB of LDS per CU
+// min workgroups per CU (launch bounds) of the tile variant: 2 (256 VGPRs).  Measured on
+// MI355X against 3 (<= 168 VGPRs, 3 waves/SIMD; NF = 60, 4096 chains, one box, interleaved):
+// 3.05 vs 2.85 ms per launch -- the 35 spilled VGPRs and the tighter schedule of the
+// latency-bound factorisation cost more than the extra wave hides (tools/gpu_ab_variants.sh).
 #ifndef GS_TILE_MINW
 #define GS_TILE_MINW 2
 #endif
@@ -467,8 +469,15 @@ extern "C" int gs_debug_phase_cycles(unsigned long long* out, int reset) {
 
 // Fixed NF in {20, 40, 60}: every broadcast variant; any other even NF <= 64: the tile
 // variant with NF at run time, one instantiation per tile count NT = NF / 16 + 1.
-#define GS_LAUNCH(KERNEL, NFC, NTC, BC, ARGS) \
-  hipLaunchKernelGGL((KERNEL<NFC, NTC, WPB, BC>), grid, dim3(64 * WPB), lds, s, ARGS); \
+// dynamic LDS above 64 KB (nm up to 64: model blocks up to 95 KB) needs the kernel attribute
+template <typename K>
+int set_lds(K kernel, size_t lds) {
+  return hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+         hipSuccess;
+}
+#define GS_LAUNCH(KERNEL, NFC, NTC, BC, ARGS)                                              \
+  if (lds > 65536 && set_lds(KERNEL<NFC, NTC, WPB, BC>, lds)) return 2;                     \
+  hipLaunchKernelGGL((KERNEL<NFC, NTC, WPB, BC>), grid, dim3(64 * WPB), lds, s, ARGS);     \
   return 0;
 #define GS_NF_CASES(KERNEL, ARGS)                                                       \
   switch (NF * 4 + bc) {                                                                \
