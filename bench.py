@@ -642,8 +642,8 @@ def main():
         # to pinned host memory on a side stream while the next block computes.  sample()'s
         # default for 4096 chains streams x of every chain and b of chain 0 (the reference's
         # bchain); with record_bchains=True every chain's b too.
-        def streamed_rate(views):
-            streamer = HistoryStreamer(ctx, [(S, C, 30), (S, C, model.ldb)], views=views)
+        def streamed_rate(views, direct):
+            streamer = HistoryStreamer(ctx, [(S, C, 30), (S, C, model.ldb)], views=views, direct=direct)
 
             def go():
                 done, slot, pending = 0, 0, None
@@ -659,13 +659,14 @@ def main():
                     streamer.fetch(pending)
             el_h = timed_region(world, dev, go)
             return total_chains * K / el_h, el_h / K * 1e3
-        v0, ms0 = streamed_rate([None, lambda t: t[:, :1]])
-        v1, ms1 = streamed_rate(None)
+        v0, ms0 = streamed_rate([None, lambda t: t[:, :1]], [True, False])
+        v1, ms1 = streamed_rate(None, [True, False])
         host = {"value": v0, "unit": "chain-iters/s", "ms_per_step": ms0, "bytes_per_step": C * 30 * 8 + model.ldb * 8,
-                "note": "sample()'s default: x of every chain + b of chain 0 copied to pinned host memory (PCIe), "
-                        "overlapped with the next block's sweeps (engine.HistoryStreamer)",
+                "note": "sample()'s default: the kernel writes x of every chain straight into pinned host memory "
+                        "(zero-copy over PCIe); b of chain 0 copied after each block, overlapped with the next "
+                        "block's sweeps (engine.HistoryStreamer)",
                 "all_b": {"value": v1, "ms_per_step": ms1, "bytes_per_step": C * (30 + model.ldb) * 8,
-                          "note": "record_bchains=True: every chain's b as well"}}
+                          "note": "record_bchains=True: every chain's b as well (HBM, then the copy engine)"}}
 
     out = None
     if rank == 0:

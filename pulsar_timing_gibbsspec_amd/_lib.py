@@ -115,11 +115,12 @@ def check(rc, what):
 
 
 def ptr(t):
-    """Device pointer of a tensor (or None -> NULL)."""
+    """Device-accessible pointer of a tensor (or None -> NULL): device memory, or pinned
+    (page-locked, device-mapped) host memory, which kernels read and write over PCIe."""
     if t is None:
         return None
-    if not t.is_cuda:
-        raise GibbsLibError("expected a device tensor")
+    if not t.is_cuda and not t.is_pinned():
+        raise GibbsLibError("expected a device tensor (or pinned host memory)")
     if not t.is_contiguous():
         raise GibbsLibError("expected a contiguous tensor")
     return C.c_void_p(t.data_ptr())

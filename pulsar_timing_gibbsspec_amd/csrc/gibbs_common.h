@@ -95,13 +95,95 @@ __device__ __forceinline__ void gs_uniform2(gs_u4 c, gs_key k, double& u1, doubl
   u2 = gs_u53(w.z, w.w);
 }
 
+// ---------------------------------------------------------------- short f64 math
+// The hot kernels are VALU-issue bound (k_sweep_freespec: ~1.9k VALU instructions per
+// draw), and the libm forms carry double-double corrections for correct rounding that the
+// samplers do not need: the draws are compared with the reference at 1e-9.  These are
+// within ~2 ulp (tools/probe/fastmath_probe.hip measures them against long double).
+// GS_FAST_MATH=0 restores log / sincospi.
+#ifndef GS_FAST_MATH
+#define GS_FAST_MATH 1
+#endif
+
+// 1/x by v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient)
+__device__ __forceinline__ double rcp_nr2(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+
+// log(x) for positive normal x (fdlibm's e_log.c reduction and Lg1..Lg7 polynomial, no
+// special cases): x = 2^e m, m in [sqrt(1/2), sqrt(2)), f = m - 1 (exact),
+// s = f / (2 + f) by v_rcp_f64 + one Newton step (s only enters the O(f^3) correction),
+// log x = e ln2_hi - ((hfsq - (s (hfsq + R) + e ln2_lo)) - f).  ~35 VALU vs ~90.
+__device__ __forceinline__ double gs_log_pos(double x) {
+#if GS_FAST_MATH
+  double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
+  int e = __builtin_amdgcn_frexp_exp(x);
+  const bool lo = m < 0.70710678118654752440;
+  m = lo ? m + m : m;
+  e = lo ? e - 1 : e;
+  const double f = m - 1.0;
+  const double den = 2.0 + f;
+  double rd = __builtin_amdgcn_rcp(den);
+  rd = fma(rd, fma(-den, rd, 1.0), rd);
+  const double s = f * rd, z = s * s, w = z * z;
+  const double t1 = w * fma(w, fma(w, 0x1.39a09d078c69fp-3, 0x1.c71c51d8e78afp-3), 0x1.999999997fa04p-2);
+  const double t2 =
+      z * fma(w, fma(w, fma(w, 0x1.2f112df3e5244p-3, 0x1.7466496cb03dep-3), 0x1.2492494229359p-2),
+              0x1.5555555555593p-1);
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)e;
+  return fma(dk, 0x1.62e42feep-1, -((hfsq - fma(s, hfsq + R, dk * 0x1.a39ef35793c76p-33)) - f));
+#else
+  return log(x);
+#endif
+}
+
+// sin(2 pi u), cos(2 pi u) for u in [0, 1): q = rint(4u), r = u - q/4 in [-1/8, 1/8]
+// (exact), Taylor polynomials of sin / cos (2 pi r) in r^2 through r^17 / r^16 (truncation
+// < 0.6 ulp), quadrant by swap and sign.  ~30 VALU vs ~60 for sincospi.
+__device__ __forceinline__ void gs_sincos2pi(double u, double& sn, double& cs) {
+#if GS_FAST_MATH
+  const double q = __builtin_rint(4.0 * u);
+  const double r = fma(q, -0.25, u);
+  const double z = r * r;
+  double ps = 0x1.aaec32af93359p-4;
+  ps = fma(ps, z, -0x1.6fadb9f155744p-1);
+  ps = fma(ps, z, 0x1.e8f434d018d63p+1);
+  ps = fma(ps, z, -0x1.e3074fde8871fp+3);
+  ps = fma(ps, z, 0x1.50783487ee782p+5);
+  ps = fma(ps, z, -0x1.32d2cce62bd86p+6);
+  ps = fma(ps, z, 0x1.466bc6775aae2p+6);
+  ps = fma(ps, z, -0x1.4abbce625be53p+5);
+  ps = fma(ps, z, 0x1.921fb54442d18p+2);
+  const double s0 = ps * r;
+  double pc = 0x1.20c62c2f2d7f5p-2;
+  pc = fma(pc, z, -0x1.b6e24f44b128fp+0);
+  pc = fma(pc, z, 0x1.f9d38a3763cc3p+2);
+  pc = fma(pc, z, -0x1.a6d1f2a204a8cp+4);
+  pc = fma(pc, z, 0x1.e1f506891babbp+5);
+  pc = fma(pc, z, -0x1.55d3c7e3cbffap+6);
+  pc = fma(pc, z, 0x1.03c1f081b5ac4p+6);
+  pc = fma(pc, z, -0x1.3bd3cc9be45dep+4);
+  const double c0 = fma(pc, z, 1.0);
+  const int qi = (int)q & 3;  // angle = 2 pi r + q pi / 2
+  const double a = (qi & 1) ? c0 : s0, b = (qi & 1) ? s0 : c0;
+  sn = (qi & 2) ? -a : a;                   // q = 2, 3
+  cs = ((qi + 1) & 2) ? -b : b;             // q = 1, 2
+#else
+  sincospi(2.0 * u, &sn, &cs);
+#endif
+}
+
 // Two independent standard normals (Box-Muller) for one counter.
 __device__ __forceinline__ void gs_normal2(gs_u4 c, gs_key k, double& n1, double& n2) {
   double u1, u2;
   gs_uniform2(c, k, u1, u2);
-  const double r = sqrt(-2.0 * log(1.0 - u1));
+  const double r = sqrt(-2.0 * gs_log_pos(1.0 - u1));
   double s, co;
-  sincospi(2.0 * u2, &s, &co);
+  gs_sincos2pi(u2, s, co);
   n1 = r * co;
   n2 = r * s;
 }

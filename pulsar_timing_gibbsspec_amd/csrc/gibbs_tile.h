@@ -192,6 +192,36 @@ __device__ __forceinline__ double fmac_nb(double acc, double v, double m, int n)
   }
 }
 
+// v with the lanes of columns c = lane & 15 <= K zeroed: exec set by two SALU moves of a
+// literal around ONE v_mov_b64, then back to all lanes (instead of v_cmp + two v_cndmask_b32
+// per elimination step).  The tile routines run on full waves only (their DPP and
+// ds_bpermute exchanges read every lane), so exec is all ones on entry; restoring -1
+// instead of a saved copy needs no SGPR pair (the sweep kernel's SGPRs are at their limit:
+// 15 saved pairs spilled 26 more SGPRs into VGPR lanes, +164 v_readlane).  No DPP reads
+// inside the block (a VALU exec write needs wait states before a DPP op; SALU ones do not).
+template <int K>
+__device__ __forceinline__ double zero_cols_le_c(double v) {
+  constexpr unsigned P16 = (2u << K) - 1u;
+  constexpr unsigned P32 = P16 | (P16 << 16);
+  asm("s_mov_b32 exec_lo, %1\n\t"
+      "s_mov_b32 exec_hi, %1\n\t"
+      "v_mov_b64 %0, 0\n\t"
+      "s_mov_b64 exec, -1"
+      : "+v"(v)
+      : "n"(P32));
+  return v;
+}
+__device__ __forceinline__ double zero_cols_le(double v, int k) {
+#define GS_ZC(N) \
+  case N: return zero_cols_le_c<N>(v);
+  switch (k) {  // k constant after unrolling
+    GS_ZC(0) GS_ZC(1) GS_ZC(2) GS_ZC(3) GS_ZC(4) GS_ZC(5) GS_ZC(6) GS_ZC(7)
+    GS_ZC(8) GS_ZC(9) GS_ZC(10) GS_ZC(11) GS_ZC(12) GS_ZC(13) GS_ZC(14)
+    default: return zero_cols_le_c<15>(v);
+  }
+#undef GS_ZC
+}
+
 // x^-1/2: v_rsq_f64 + two Newton steps (x > 0 normal; NaN/inf/<= 0 propagate to a
 // non-finite or non-positive result, caught by the pivot ballot)
 __device__ __forceinline__ double rsq_nr(double x) {
@@ -255,6 +285,9 @@ __device__ __forceinline__ constexpr int tix(int I, int J, int NT) {
 #ifndef GS_RHO_PRIO  // ... while it runs the sweep's rho|b draw and gate (k_sweep_freespec)
 #define GS_RHO_PRIO 0
 #endif
+#ifndef GS_EXEC_MASK
+#define GS_EXEC_MASK 1
+#endif
 template <int KMAX, bool PR = false>
 __device__ __forceinline__ void tile_elim1(gs_d4& A, gs_d4& B, double& rsd, int q, int c) {
   using namespace gtile;
@@ -275,7 +308,11 @@ __device__ __forceinline__ void tile_elim1(gs_d4& A, gs_d4& B, double& rsd, int 
       // lane mask c > k from an opaque k: one v_cmp per step instead of loop-invariant
       // 64-bit masks held in (spilled) SGPRs across the caller's sweep loop; applied to
       // the row before the pivot arrives, so it is off the critical path
+#if GS_EXEC_MASK
+      const double akm = zero_cols_le(akc, k);
+#else
       const double akm = (c > opq(k)) ? akc : 0.0;
+#endif
       // -A[k][c]/A[k][k] = akm i0 (akk i0 - 2) (one Newton step on v_rcp_f64): the two
       // products run side by side, 4 dependent ops from pivot to multiplier
       const double i0 = __builtin_amdgcn_rcp(akk);

@@ -139,7 +139,10 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
     blk = max(1, save_every) + 1
     # block k+1's sweeps run while block k's rows stream to pinned host memory
     bview = None if (allb or nc == 1) else (lambda t: t[:, ::nc])      # chain 0 of every pulsar
-    streamer = HistoryStreamer(ctx, [(blk, P * nc, n_f), (blk, P * nc, model.ldb)], views=[None, bview])
+    # x rows (and b rows when they all go to the host and are few) are written by the kernel
+    # straight into pinned host memory; every chain's b goes through HBM + the copy engine
+    streamer = HistoryStreamer(ctx, [(blk, P * nc, n_f), (blk, P * nc, model.ldb)], views=[None, bview],
+                               direct=[True, bview is None and not allb])
     bstride = 1 if bview is not None else nc
 
     def consume(slot, ii, nxt):
