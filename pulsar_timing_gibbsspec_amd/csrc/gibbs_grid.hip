@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void k_rho_curn_sum(GridArgs A) {
 #pragma unroll
   for (int j = 0; j < CS_MAXG; ++j) {
     if (j < G) {
-      loc += exp(lp[j] - mx);  // exp(-inf) = 0 past the grid
+      loc += gs_exp_neg(lp[j] - mx);  // -inf past the grid -> 0
       lp[j] = loc;
     }
   }
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256) void k_rho_curn_fast(GridArgs A) {
   for (int j = 0; j < CF_MAXG; ++j) {
     lp[j] = -__builtin_inf();
     if (j < G && g0 + j < A.ngrid) {
-      lp[j] = -(log(dd[j]) + ex[j] * LN2) - 0.5 * (nn[j] / dd[j]);
+      lp[j] = -(gs_log_pos(dd[j]) + ex[j] * LN2) - 0.5 * (nn[j] * rcp_nr2(dd[j]));
       mx = fmax(mx, lp[j]);
     }
   }
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void k_rho_curn_fast(GridArgs A) {
 #pragma unroll
   for (int j = 0; j < CF_MAXG; ++j) {
     if (j < G) {
-      loc += exp(lp[j] - mx);
+      loc += gs_exp_neg(lp[j] - mx);
       lp[j] = loc;
     }
   }
@@ -315,6 +315,14 @@ __device__ __forceinline__ double red_ratio(double tau, double a) {
   return tau * ra;
 }
 
+// one grid point's pdf: ratio * exp(-ratio/2) * ln10 (pta_gibbs.py:265-266); the default
+// mode uses the short exp (gibbs_common.h, <= 2 ulp), EXACT the device library's
+template <bool EXACT>
+__device__ __forceinline__ double red_pdf(double tau, double a) {
+  const double ratio = red_ratio<EXACT>(tau, a);
+  return ratio * (EXACT ? exp(-ratio / 2) : gs_exp_neg(-0.5 * ratio)) * LN10;
+}
+
 template <bool EXACT>
 __global__ void k_rho_red(GridArgs A) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -341,10 +349,7 @@ __global__ void k_rho_red(GridArgs A) {
   for (int j = 0; j < GS_RED_NCH; ++j) {
     const int g1 = min(A.ngrid, (j + 1) * ch);
 #pragma unroll 8
-    for (int g = j * ch; g < g1; ++g) {
-      const double ratio = red_ratio<EXACT>(tau, gw + A.grid3[g]);
-      cum += ratio * exp(-ratio / 2) * LN10;
-    }
+    for (int g = j * ch; g < g1; ++g) cum += red_pdf<EXACT>(tau, gw + A.grid3[g]);
     ck[j] = cum;
   }
   const double total = cum;
@@ -371,8 +376,7 @@ __global__ void k_rho_red(GridArgs A) {
     const int g1 = min(A.ngrid, (jx + 1) * ch);
 #pragma unroll 4
     for (int g = jx * ch; g < g1; ++g) {
-      const double ratio = red_ratio<EXACT>(tau, gw + A.grid3[g]);
-      cc += ratio * exp(-ratio / 2) * LN10;
+      cc += red_pdf<EXACT>(tau, gw + A.grid3[g]);
       cnt += below(cc) ? 1 : 0;
     }
   }
@@ -380,6 +384,84 @@ __global__ void k_rho_red(GridArgs A) {
   if (idx < 0) idx += A.ngrid;
   if (A.idx_out) A.idx_out[r] = idx;
   A.x[(int64_t)c * A.ldx + A.xcol[p * A.n_f + k]] = A.grid3[2 * A.ngrid + idx];
+}
+
+// ------------------------------------------------------------ a7 fast: red CDF, wave per row
+// The default (non-exact) mode.  A wave takes 64 consecutive rows (one per lane for the loads
+// and the Philox uniform) and then walks them one at a time with all 64 lanes on the grid:
+// lane l owns grid points [16 l, 16 l + 16) (held in registers for the whole wave), sums
+// its pdf values sequentially, and a wave scan of the lane sums gives every point's cdf.
+// Against the lane-per-row kernel: no second pass over the crossing chunk, no wave-count
+// tail (43k one-row-per-lane waves at configs[3] sizes are 5.3 rounds of the chip), and
+// every grid point is evaluated once.  Per point: h = (tau/2) / (gw + rho_g) (rcp + two
+// Newton steps), pdf' = h exp(-h) with the short exp -- the reference's
+// ratio exp(-ratio/2) ln10 (pta_gibbs.py:265-266) up to the constant 2 ln10, which cancels
+// in cdf / max.  Sums differ from np.cumsum's sequential order by rounding (~1e-16 relative),
+// so an index can only differ when u falls that close to a cdf value.
+constexpr int RW_G = 16;  // grid points per lane (ngrid <= 1024)
+
+__global__ __launch_bounds__(256) void k_rho_red_wave(GridArgs A) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t nrow = (int64_t)A.n_psr * A.n_f * A.n_chain;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
+  if (r0 >= nrow) return;
+  const int64_t r = r0 + lane;
+  const bool rok = r < nrow;
+  const int64_t rr = rok ? r : r0;
+  const int c = (int)(rr % A.n_chain);
+  const int k = (int)((rr / A.n_chain) % A.n_f);
+  const int p = (int)(rr / ((int64_t)A.n_chain * A.n_f));
+  double u;
+  if (A.u) {
+    u = A.u[((int64_t)c * A.n_psr + p) * A.n_f + k];
+  } else {
+    double u2;
+    gs_uniform2(gs_counter(k, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, p + A.psr_base, GS_EV_RED), A.key, u, u2);
+  }
+  const double th = 0.5 * A.tau[rr];
+  const double gw = A.irn[(int64_t)k * A.n_chain + c];
+  // this lane's grid points; past the grid a huge rho_g makes the pdf ~1e-300 (and those
+  // points are never counted)
+  double rg[RW_G];
+#pragma unroll
+  for (int j = 0; j < RW_G; ++j) {
+    const int g = RW_G * lane + j;
+    rg[j] = g < A.ngrid ? A.grid3[g] : 1e300;
+  }
+  unsigned long long valid[RW_G];  // lanes whose point j is on the grid (wave-uniform)
+#pragma unroll
+  for (int j = 0; j < RW_G; ++j) valid[j] = __ballot(RW_G * lane + j < A.ngrid);
+  const int nr = (int)min((int64_t)64, nrow - r0);
+  int myidx = 0;
+  for (int i = 0; i < nr; ++i) {
+    const double thi = rdlane(th, i), gwi = rdlane(gw, i), ui = rdlane(u, i);
+    double cum[RW_G];
+    double loc = 0.0;
+#pragma unroll
+    for (int j = 0; j < RW_G; ++j) {
+      const double h = thi * rcp_nr2(gwi + rg[j]);
+      loc = fma(h, gs_exp_neg(-h), loc);
+      cum[j] = loc;
+    }
+    double incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    const double total = rdlane(incl, 63);
+    const double thr = ui * total - (incl - loc);  // cum_j + (exclusive lane prefix) < u * total
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < RW_G; ++j) cnt += __popcll(__ballot(cum[j] < thr) & valid[j]);
+    int idx = cnt - 1;
+    if (idx < 0) idx += A.ngrid;
+    myidx = (lane == i) ? idx : myidx;
+  }
+  if (rok) {
+    if (A.idx_out) A.idx_out[r] = myidx;
+    A.x[(int64_t)c * A.ldx + A.xcol[p * A.n_f + k]] = A.grid3[2 * A.ngrid + myidx];
+  }
 }
 
 // ------------------------------------------------------------ a4: Gumbel-max
@@ -509,6 +591,8 @@ int launch_rho_red(hipStream_t s, const GridArgs& a) {
   if (n == 0) return 0;
   if (a.exact)
     hipLaunchKernelGGL(k_rho_red<true>, grid1(n, 64), dim3(64), 0, s, a);
+  else if (a.ngrid <= 64 * RW_G)
+    hipLaunchKernelGGL(k_rho_red_wave, grid1(n, 256), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(k_rho_red<false>, grid1(n, 64), dim3(64), 0, s, a);
   return 0;

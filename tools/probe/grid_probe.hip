@@ -5,14 +5,17 @@
 // (MI355X_MICROARCH.md has no fp64 transcendental rate).
 //
 //   red  : ratio = tau * rcp(gw + rho_g) (+ 2 Newton steps); cdf += ratio * exp(-ratio/2) * ln10
-//          -- k_rho_red's per-point work (one fp64 exp per point)
+//          -- k_rho_red's per-point work (one fp64 exp per point: gs_exp_neg, the short exp of
+//          gibbs_common.h, as the kernel; red_libm_evals_per_s: the device library's exp)
 //   curn : a = irn + rho_g; N = N a + tau D; D *= a (rescaled every 8 pulsars)
 //          -- k_rho_curn_fast's per-(point, pulsar) work (no transcendental, no division)
 //
-// Build: hipcc --offload-arch=gfx950 -O3 tools/probe/grid_probe.hip -o tools/probe/grid_probe
+// Build: hipcc --offload-arch=gfx950 -O3 -I pulsar_timing_gibbsspec_amd/csrc tools/probe/grid_probe.hip -o tools/probe/grid_probe
 // Run:   tools/probe/grid_probe  -> one JSON line
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+
+#include "gibbs_common.h"
 
 constexpr double LN10 = 2.302585092994045684017991454684364208;
 
@@ -23,6 +26,7 @@ __device__ __forceinline__ double rcp_nr(double a) {
 }
 
 // each thread: 8 independent rows x npts grid points
+template <bool LIBM>
 __global__ __launch_bounds__(256) void k_red(int npts, double q, double* out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   double tau[8], cum[8];
@@ -36,7 +40,7 @@ __global__ __launch_bounds__(256) void k_red(int npts, double q, double* out) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const double ratio = tau[j] * rcp_nr(gw + rg);
-      cum[j] += ratio * exp(-ratio / 2) * LN10;
+      cum[j] += ratio * (LIBM ? exp(-ratio / 2) : gs_exp_neg(-0.5 * ratio)) * LN10;
     }
     rg *= q;
   }
@@ -85,13 +89,15 @@ int main() {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  double rates[2];
-  for (int kind = 0; kind < 2; ++kind) {
+  double rates[3];
+  for (int kind = 0; kind < 3; ++kind) {
     float best = 1e30f;
     for (int rep = 0; rep < 5; ++rep) {
       (void)hipEventRecord(e0, 0);
       if (kind == 0)
-        hipLaunchKernelGGL(k_red, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
+        hipLaunchKernelGGL(k_red<false>, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
+      else if (kind == 2)
+        hipLaunchKernelGGL(k_red<true>, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
       else
         hipLaunchKernelGGL(k_curn, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
       (void)hipEventRecord(e1, 0);
@@ -102,6 +108,7 @@ int main() {
     }
     rates[kind] = (double)blocks * 256 * 8 * npts / (best * 1e-3);
   }
-  printf("{\"cus\": %d, \"red_evals_per_s\": %.6e, \"curn_pulsar_terms_per_s\": %.6e}\n", ncu, rates[0], rates[1]);
+  printf("{\"cus\": %d, \"red_evals_per_s\": %.6e, \"curn_pulsar_terms_per_s\": %.6e, \"red_libm_evals_per_s\": %.6e}\n",
+         ncu, rates[0], rates[1], rates[2]);
   return 0;
 }
