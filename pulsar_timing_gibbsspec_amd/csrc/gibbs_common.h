@@ -145,8 +145,34 @@ __device__ __forceinline__ double gs_log_pos(double x) {
 // n = rint(x log2 e), r = x - n ln2 (two-term Cody-Waite), the degree-11 minimax polynomial
 // of the device library's exp on |r| <= ln2/2, ldexp.  No overflow / special-case branches
 // (x <= 0 by contract, clamped at -800 where exp is 0): ~17 VALU vs ~29.
+#ifndef GS_EXP_MAGIC
+#define GS_EXP_MAGIC 1
+#endif
 __device__ __forceinline__ double gs_exp_neg(double x) {
-#if GS_FAST_MATH
+#if GS_FAST_MATH && GS_EXP_MAGIC
+  // n by the round-to-integer constant 1.5 2^52 (n sits in the low word of t), 2^n built in
+  // the exponent field: no v_rndne / v_cvt / v_ldexp.  x is clamped at -708 so 2^n stays
+  // normal: exp(x) < 3.4e-308 below that is returned as exp(-708) -- in the grid pdfs those
+  // points are ~1e-308 of the row maximum, below every comparison the draws make.
+  x = fmax(x, -708.0);
+  const double t = fma(x, 0x1.71547652b82fep+0, 0x1.8p52);
+  const double n = t - 0x1.8p52;
+  double r = fma(n, -0x1.62e42fefa39efp-1, x);
+  r = fma(n, -0x1.abc9e3b39803fp-56, r);
+  double p = fma(r, 0x1.ade156a5dcb37p-26, 0x1.28af3fca7ab0cp-22);
+  p = fma(r, p, 0x1.71dee623fde64p-19);
+  p = fma(r, p, 0x1.a01997c89e6b0p-16);
+  p = fma(r, p, 0x1.a01a014761f6ep-13);
+  p = fma(r, p, 0x1.6c16c1852b7b0p-10);
+  p = fma(r, p, 0x1.1111111122322p-7);
+  p = fma(r, p, 0x1.55555555502a1p-5);
+  p = fma(r, p, 0x1.5555555555511p-3);
+  p = fma(r, p, 0x1.000000000000bp-1);
+  p = fma(r, p, 1.0);
+  p = fma(r, p, 1.0);
+  const int ni = (int)(unsigned)__double_as_longlong(t);  // n (low word of 1.5 2^52 + n)
+  return p * __hiloint2double((ni + 1023) << 20, 0);
+#elif GS_FAST_MATH
   x = fmax(x, -800.0);
   const double n = __builtin_rint(x * 0x1.71547652b82fep+0);
   double r = fma(n, -0x1.62e42fefa39efp-1, x);

@@ -14,6 +14,7 @@
 // (grid3 = [rho | log rho | 0.5 log10 rho]), bit-identical to the reference's.
 #include "gibbs_common.h"
 #include "gibbs_internal.h"
+#include "gibbs_gridpt.h"
 
 namespace {
 
@@ -228,22 +229,30 @@ __global__ __launch_bounds__(256) void k_rho_curn_fast(GridArgs A) {
     ex[j] = 0;
   }
   const int P = A.n_psr;
-  for (int p = 0; p < P; ++p) {
-    const double tau = A.tau[p * nrow + r];
-    const double irn = A.irn ? A.irn[p * nrow + r] : 0.0;
-#pragma unroll
-    for (int j = 0; j < CF_MAXG; ++j) {
-      const double a = irn + rg[j];
-      nn[j] = fma(nn[j], a, tau * dd[j]);
-      dd[j] *= a;
-    }
-    if ((p & 7) == 7 || p == P - 1) {
+  // the row's (tau_p, irn_p) for up to 64 pulsars at a time: lane p loads pulsar p0 + p once
+  // (instead of two loads + a full memory-latency wait per pulsar inside the product loop),
+  // the loop reads them back by v_readlane
+  for (int p0 = 0; p0 < P; p0 += 64) {
+    const int np = min(64, P - p0);
+    const double tl = lane < np ? A.tau[(int64_t)(p0 + lane) * nrow + r] : 0.0;
+    const double il = (lane < np && A.irn) ? A.irn[(int64_t)(p0 + lane) * nrow + r] : 0.0;
+    for (int q = 0; q < np; ++q) {
+      const int p = p0 + q;
+      const double tau = rdlane(tl, q), irn = rdlane(il, q);
 #pragma unroll
       for (int j = 0; j < CF_MAXG; ++j) {
-        const int e = __builtin_amdgcn_frexp_exp(dd[j]);
-        ex[j] += e;
-        dd[j] = __builtin_amdgcn_frexp_mant(dd[j]);
-        nn[j] = ldexp(nn[j], -e);
+        const double a = irn + rg[j];
+        nn[j] = fma(nn[j], a, tau * dd[j]);
+        dd[j] *= a;
+      }
+      if ((p & 7) == 7 || p == P - 1) {
+#pragma unroll
+        for (int j = 0; j < CF_MAXG; ++j) {
+          const int e = __builtin_amdgcn_frexp_exp(dd[j]);
+          ex[j] += e;
+          dd[j] = __builtin_amdgcn_frexp_mant(dd[j]);
+          nn[j] = ldexp(nn[j], -e);
+        }
       }
     }
   }
@@ -401,7 +410,10 @@ __global__ void k_rho_red(GridArgs A) {
 constexpr int RW_G = 16;  // grid points per lane (ngrid <= 1024)
 
 __global__ __launch_bounds__(256) void k_rho_red_wave(GridArgs A) {
+  __shared__ double tb[64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
+  __syncthreads();
   const int64_t nrow = (int64_t)A.n_psr * A.n_f * A.n_chain;
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
   if (r0 >= nrow) return;
@@ -420,13 +432,13 @@ __global__ __launch_bounds__(256) void k_rho_red_wave(GridArgs A) {
   }
   const double th = 0.5 * A.tau[rr];
   const double gw = A.irn[(int64_t)k * A.n_chain + c];
-  // this lane's grid points; past the grid a huge rho_g makes the pdf ~1e-300 (and those
+  // this lane's grid points; past the grid a huge rho_g makes the pdf ~tau 1e-60 (and those
   // points are never counted)
   double rg[RW_G];
 #pragma unroll
   for (int j = 0; j < RW_G; ++j) {
     const int g = RW_G * lane + j;
-    rg[j] = g < A.ngrid ? A.grid3[g] : 1e300;
+    rg[j] = g < A.ngrid ? A.grid3[g] : 1e60;  // a^4 stays finite
   }
   unsigned long long valid[RW_G];  // lanes whose point j is on the grid (wave-uniform)
 #pragma unroll
@@ -436,13 +448,7 @@ __global__ __launch_bounds__(256) void k_rho_red_wave(GridArgs A) {
   for (int i = 0; i < nr; ++i) {
     const double thi = rdlane(th, i), gwi = rdlane(gw, i), ui = rdlane(u, i);
     double cum[RW_G];
-    double loc = 0.0;
-#pragma unroll
-    for (int j = 0; j < RW_G; ++j) {
-      const double h = thi * rcp_nr2(gwi + rg[j]);
-      loc = fma(h, gs_exp_neg(-h), loc);
-      cum[j] = loc;
-    }
+    const double loc = red_lane_cumsum<RW_G>(thi, gwi, rg, tb, cum);
     double incl = loc;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {

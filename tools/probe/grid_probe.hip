@@ -4,9 +4,11 @@
 // busy, 8 waves per SIMD).  This is the "peak" the bench prices the grid kernels against
 // (MI355X_MICROARCH.md has no fp64 transcendental rate).
 //
-//   red  : ratio = tau * rcp(gw + rho_g) (+ 2 Newton steps); cdf += ratio * exp(-ratio/2) * ln10
-//          -- k_rho_red's per-point work (one fp64 exp per point: gs_exp_neg, the short exp of
-//          gibbs_common.h, as the kernel; red_libm_evals_per_s: the device library's exp)
+//   red  : red_lane_cumsum (gibbs_gridpt.h) -- k_rho_red_wave's per-point work: h = (tau/2) /
+//          (gw + rho_g) with one reciprocal per four points, pdf' = h exp(-h) by the LDS-table
+//          exp, the lane's running sum; 16 points per lane, (tau, gw) changing every row as in
+//          the kernel.  red_libm_evals_per_s: the first kernel's op mix (ratio by rcp + two
+//          Newton steps per point, the device library's exp), for reference.
 //   curn : a = irn + rho_g; N = N a + tau D; D *= a (rescaled every 8 pulsars)
 //          -- k_rho_curn_fast's per-(point, pulsar) work (no transcendental, no division)
 //
@@ -16,6 +18,7 @@
 #include <stdio.h>
 
 #include "gibbs_common.h"
+#include "gibbs_gridpt.h"
 
 constexpr double LN10 = 2.302585092994045684017991454684364208;
 
@@ -25,9 +28,29 @@ __device__ __forceinline__ double rcp_nr(double a) {
   return fma(r, fma(-a, r, 1.0), r);
 }
 
-// each thread: 8 independent rows x npts grid points
-template <bool LIBM>
+// each lane: 16 grid points in registers, npts/16 rows of (tau, gw) (the kernel's loop)
 __global__ __launch_bounds__(256) void k_red(int npts, double q, double* out) {
+  __shared__ double tb[64];
+  if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
+  __syncthreads();
+  double rg[16], cum[16];
+  double r0 = 1e-20 * (1.0 + 1e-3 * (threadIdx.x & 63));
+  for (int j = 0; j < 16; ++j) {
+    rg[j] = r0;
+    r0 *= q;
+  }
+  double th = 0.5e-14 * (1.0 + 0.01 * (threadIdx.x & 255)), gw = 3e-15, acc = 0.0;
+  for (int row = 0; row < npts / 16; ++row) {
+    acc += red_lane_cumsum<16>(th, gw, rg, tb, cum);
+    th *= 1.0001;
+    gw *= 0.9999;
+  }
+  for (int j = 0; j < 16; ++j) acc += cum[j];
+  if (acc == 1.2345) out[blockIdx.x * blockDim.x + threadIdx.x] = acc;  // keep the work alive
+}
+
+// the first red kernel's op mix: 8 independent rows per thread, one division + libm exp per point
+__global__ __launch_bounds__(256) void k_red_libm(int npts, double q, double* out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   double tau[8], cum[8];
   for (int j = 0; j < 8; ++j) {
@@ -40,13 +63,13 @@ __global__ __launch_bounds__(256) void k_red(int npts, double q, double* out) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const double ratio = tau[j] * rcp_nr(gw + rg);
-      cum[j] += ratio * (LIBM ? exp(-ratio / 2) : gs_exp_neg(-0.5 * ratio)) * LN10;
+      cum[j] += ratio * exp(-ratio / 2) * LN10;
     }
     rg *= q;
   }
   double s = 0.0;
   for (int j = 0; j < 8; ++j) s += cum[j];
-  if (s == 1.2345) out[t] = s;  // keep the work alive
+  if (s == 1.2345) out[t] = s;
 }
 
 __global__ __launch_bounds__(256) void k_curn(int npts, double q, double* out) {
@@ -95,9 +118,9 @@ int main() {
     for (int rep = 0; rep < 5; ++rep) {
       (void)hipEventRecord(e0, 0);
       if (kind == 0)
-        hipLaunchKernelGGL(k_red<false>, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
+        hipLaunchKernelGGL(k_red, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
       else if (kind == 2)
-        hipLaunchKernelGGL(k_red<true>, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
+        hipLaunchKernelGGL(k_red_libm, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
       else
         hipLaunchKernelGGL(k_curn, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
       (void)hipEventRecord(e1, 0);
@@ -106,7 +129,7 @@ int main() {
       (void)hipEventElapsedTime(&ms, e0, e1);
       if (rep > 0 && ms < best) best = ms;
     }
-    rates[kind] = (double)blocks * 256 * 8 * npts / (best * 1e-3);
+    rates[kind] = (double)blocks * 256 * (kind == 0 ? 1 : 8) * npts / (best * 1e-3);  // k_red: npts per lane
   }
   printf("{\"cus\": %d, \"red_evals_per_s\": %.6e, \"curn_pulsar_terms_per_s\": %.6e, \"red_libm_evals_per_s\": %.6e}\n",
          ncu, rates[0], rates[1], rates[2]);
