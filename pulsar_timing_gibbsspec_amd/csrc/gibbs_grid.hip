@@ -195,6 +195,84 @@ __global__ __launch_bounds__(256) void k_rho_curn_sum(GridArgs A) {
   }
 }
 
+// k_rho_curn_sum over 64 rows per wave (ngrid <= 1024): the lane-per-row loads and Philox
+// uniform as k_rho_red_wave, each lane's 16 grid points prepared once per wave as
+// c_g = -P log rho_g and w_g = 1 / (2 rho_g), so a row costs one FMA (log pdf = c_g - S w_g),
+// the wave maximum, the LDS-table exp and the scan / count per point.
+constexpr int CSW_G = 16;
+
+__global__ __launch_bounds__(256) void k_rho_curn_sum_wave(GridArgs A) {
+  __shared__ double tb[64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
+  __syncthreads();
+  const int64_t nrow = (int64_t)A.n_f * A.n_chain;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
+  if (r0 >= nrow) return;
+  const int64_t r = r0 + lane;
+  const bool rok = r < nrow;
+  const int64_t rr = rok ? r : r0;
+  const int c = (int)(rr % A.n_chain), k = (int)(rr / A.n_chain);
+  double u;
+  if (A.u) {
+    u = A.u[(int64_t)c * A.n_f + k];
+  } else {
+    double u2;
+    gs_uniform2(gs_counter(k, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, 0, GS_EV_CURN), A.key, u, u2);
+  }
+  const double S = A.tau[rr];
+  const double P = (double)A.n_psr;
+  double cg[CSW_G], wg[CSW_G];
+#pragma unroll
+  for (int j = 0; j < CSW_G; ++j) {
+    const int g = CSW_G * lane + j;
+    const bool ok = g < A.ngrid;
+    cg[j] = ok ? -P * A.grid3[A.ngrid + g] : -1e300;  // past the grid: exp -> ~0, never counted
+    wg[j] = ok ? 0.5 / A.grid3[g] : 0.0;
+  }
+  unsigned long long valid[CSW_G];
+#pragma unroll
+  for (int j = 0; j < CSW_G; ++j) valid[j] = __ballot(CSW_G * lane + j < A.ngrid);
+  const int nr = (int)min((int64_t)64, nrow - r0);
+  int myidx = 0;
+  for (int i = 0; i < nr; ++i) {
+    const double nS = -rdlane(S, i), ui = rdlane(u, i);
+    double lp[CSW_G];
+    double mx = -__builtin_inf();
+#pragma unroll
+    for (int j = 0; j < CSW_G; ++j) {
+      lp[j] = fma(nS, wg[j], cg[j]);
+      mx = fmax(mx, lp[j]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+    double loc = 0.0;
+#pragma unroll
+    for (int j = 0; j < CSW_G; ++j) {
+      loc += exp_neg_t64(lp[j] - mx, tb);
+      lp[j] = loc;
+    }
+    double incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    const double total = rdlane(incl, 63);
+    const double thr = ui * total - (incl - loc);
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < CSW_G; ++j) cnt += __popcll(__ballot(lp[j] < thr) & valid[j]);
+    int idx = cnt - 1;
+    if (idx < 0) idx += A.ngrid;
+    myidx = (lane == i) ? idx : myidx;
+  }
+  if (rok) {
+    if (A.idx_out) A.idx_out[r] = myidx;
+    A.x[(int64_t)c * A.ldx + A.xcol[k]] = A.grid3[2 * A.ngrid + myidx];
+  }
+}
+
 // ------------------------------------------------------------ a6 fast: CURN product in log space
 // The same draw as k_rho_curn without numpy's operation order (GS_OPT_GRID_EXACT = 0,
 // the default): log pdf_g = -sum_p log(irn_p + rho_g) - 1/2 sum_p tau_p / (irn_p + rho_g)
@@ -588,7 +666,10 @@ int launch_tau_sum(hipStream_t s, int n_psr, int64_t nrow, const double* tau, do
 int launch_rho_curn_sum(hipStream_t s, const GridArgs& a) {
   const int64_t n = (int64_t)a.n_f * a.n_chain;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(k_rho_curn_sum, grid1(n, 4), dim3(256), 0, s, a);
+  if (a.ngrid <= 64 * CSW_G)
+    hipLaunchKernelGGL(k_rho_curn_sum_wave, grid1(n, 256), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_rho_curn_sum, grid1(n, 4), dim3(256), 0, s, a);
   return 0;
 }
 
