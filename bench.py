@@ -213,9 +213,11 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain"):
         ev = n_f * C * eng.ngrid
         kernels["k_rho_curn_sum"] = dict(kernel_avg_ms=ms_s, bound="valu", unit="Geval/s",
                                          achieved=ev / (ms_s * 1e-3) / 1e9, alg_per_launch=ev,
-                                         peak=(gp["red_evals_per_s"] / 1e9) if gp else None,
+                                         peak=(gp.get("curn_sum_evals_per_s", gp["red_evals_per_s"]) / 1e9)
+                                         if gp else None,
                                          note="n_f x C x 1000 grid points of the common pdf from the tau sums "
-                                              "(one exp each); peak: the red op mix's ceiling (an upper bound)")
+                                              "(one FMA + one exp each); peak = that op mix's register-only "
+                                              "ceiling (tools/probe/grid_probe.hip k_curn_sum)")
     for k in kernels.values():
         k["frac"] = (k["achieved"] / k["peak"]) if k.get("peak") else None
     dom = max(kernels, key=lambda k: kernels[k]["kernel_avg_ms"])
@@ -642,15 +644,15 @@ def main():
         # to pinned host memory on a side stream while the next block computes.  sample()'s
         # default for 4096 chains streams x of every chain and b of chain 0 (the reference's
         # bchain); with record_bchains=True every chain's b too.
-        def streamed_rate(views, direct):
-            streamer = HistoryStreamer(ctx, [(S, C, 30), (S, C, model.ldb)], views=views, direct=direct)
+        def streamed_rate(bk, direct):
+            streamer = HistoryStreamer(ctx, [(S, C, 30), (S, bk, model.ldb)], direct=direct)
 
             def go():
                 done, slot, pending = 0, 0, None
                 while done < K:
                     n = min(S, K - done)
                     xr, br = streamer.buffers(slot, n)
-                    run.run(n, x_rec=xr, b_rec=br)
+                    run.run(n, x_rec=xr, b_rec=br, record_b_chains=bk)
                     streamer.submit(slot, n)
                     if pending is not None:
                         streamer.fetch(pending)
@@ -659,12 +661,12 @@ def main():
                     streamer.fetch(pending)
             el_h = timed_region(world, dev, go)
             return total_chains * K / el_h, el_h / K * 1e3
-        v0, ms0 = streamed_rate([None, lambda t: t[:, :1]], [True, False])
-        v1, ms1 = streamed_rate(None, [True, False])
+        v0, ms0 = streamed_rate(1, [True, True])
+        v1, ms1 = streamed_rate(C, [True, False])
         host = {"value": v0, "unit": "chain-iters/s", "ms_per_step": ms0, "bytes_per_step": C * 30 * 8 + model.ldb * 8,
-                "note": "sample()'s default: the kernel writes x of every chain straight into pinned host memory "
-                        "(zero-copy over PCIe); b of chain 0 copied after each block, overlapped with the next "
-                        "block's sweeps (engine.HistoryStreamer)",
+                "note": "sample()'s default: the kernel writes x of every chain and b of chain 0 (the reference's "
+                        "bchain, GS_OPT_BREC_CHAINS = 1) straight into pinned host memory (zero-copy over PCIe), "
+                        "read while the next block runs (engine.HistoryStreamer)",
                 "all_b": {"value": v1, "ms_per_step": ms1, "bytes_per_step": C * (30 + model.ldb) * 8,
                           "note": "record_bchains=True: every chain's b as well (HBM, then the copy engine)"}}
 

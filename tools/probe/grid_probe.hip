@@ -101,6 +101,42 @@ __global__ __launch_bounds__(256) void k_curn(int npts, double q, double* out) {
   if (s == 1.2345) out[t] = s;
 }
 
+// k_rho_curn_sum_wave's per-point work: log pdf = c_g - S w_g (one FMA), the wave maximum,
+// the LDS-table exp, the lane's running sum (16 points per lane, S changing every row)
+__global__ __launch_bounds__(256) void k_curn_sum(int npts, double q, double* out) {
+  __shared__ double tb[64];
+  if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
+  __syncthreads();
+  double cg[16], wg[16], lp[16];
+  double r0 = 1e-18 * (1.0 + 1e-3 * (threadIdx.x & 63));
+  for (int j = 0; j < 16; ++j) {
+    cg[j] = -45.0 * log(r0);
+    wg[j] = 0.5 / r0;
+    r0 *= q;
+  }
+  double nS = -1e-14 * (1.0 + 0.01 * (threadIdx.x & 255)), acc = 0.0;
+  for (int row = 0; row < npts / 16; ++row) {
+    double mx = -__builtin_inf();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      lp[j] = fma(nS, wg[j], cg[j]);
+      mx = fmax(mx, lp[j]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+    double loc = 0.0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      loc += exp_neg_t64(lp[j] - mx, tb);
+      lp[j] = loc;
+    }
+    acc += loc;
+    nS *= 1.0001;
+  }
+  for (int j = 0; j < 16; ++j) acc += lp[j];
+  if (acc == 1.2345) out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
 int main() {
   int dev = 0, ncu = 0;
   (void)hipGetDevice(&dev);
@@ -112,8 +148,8 @@ int main() {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  double rates[3];
-  for (int kind = 0; kind < 3; ++kind) {
+  double rates[4];
+  for (int kind = 0; kind < 4; ++kind) {
     float best = 1e30f;
     for (int rep = 0; rep < 5; ++rep) {
       (void)hipEventRecord(e0, 0);
@@ -121,6 +157,8 @@ int main() {
         hipLaunchKernelGGL(k_red, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
       else if (kind == 2)
         hipLaunchKernelGGL(k_red_libm, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
+      else if (kind == 3)
+        hipLaunchKernelGGL(k_curn_sum, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
       else
         hipLaunchKernelGGL(k_curn, dim3(blocks), dim3(256), 0, 0, npts, 1.0277, out);
       (void)hipEventRecord(e1, 0);
@@ -129,9 +167,10 @@ int main() {
       (void)hipEventElapsedTime(&ms, e0, e1);
       if (rep > 0 && ms < best) best = ms;
     }
-    rates[kind] = (double)blocks * 256 * (kind == 0 ? 1 : 8) * npts / (best * 1e-3);  // k_red: npts per lane
+    rates[kind] = (double)blocks * 256 * ((kind == 0 || kind == 3) ? 1 : 8) * npts / (best * 1e-3);  // wave kernels: npts per lane
   }
-  printf("{\"cus\": %d, \"red_evals_per_s\": %.6e, \"curn_pulsar_terms_per_s\": %.6e, \"red_libm_evals_per_s\": %.6e}\n",
-         ncu, rates[0], rates[1], rates[2]);
+  printf("{\"cus\": %d, \"red_evals_per_s\": %.6e, \"curn_pulsar_terms_per_s\": %.6e, \"red_libm_evals_per_s\": %.6e, "
+         "\"curn_sum_evals_per_s\": %.6e}\n",
+         ncu, rates[0], rates[1], rates[2], rates[3]);
   return 0;
 }
