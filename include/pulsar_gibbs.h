@@ -65,10 +65,15 @@ enum {
                          PulsarBlockGibbs, config 5).  Read by gs_white_mh, gs_white_tnt;
                          with 1, gs_bdraw*'s chain_mask and gs_white_mh's nsteps_chain
                          are indexed by system too. */
-  GS_OPT_GRID_EXACT = 4 /* gs_rho_curn: 1 = numpy's operation order (sequential product of
+  GS_OPT_GRID_EXACT = 4, /* gs_rho_curn: 1 = numpy's operation order (sequential product of
                          per-pulsar pdfs, sequential cumsum: bit-identical pdfs); 0 (default)
                          = log-space product (one log + one exp per grid point, rcp for the
                          ratios), equal pdfs to ~1e-15 relative */
+  GS_OPT_BREC_CHAINS = 5 /* gs_sweep_freespec b_rec: 0 (default) = every system, row
+                         sweep * n_psr * n_chain + p * n_chain + c; K > 0 = chains c < K of
+                         each pulsar only, compact rows (sweep * n_psr + p) * K + c (the
+                         reference's bchain is chain 0: K = 1 puts n_psr rows per sweep on
+                         the host instead of staging every chain's b in HBM) */
 };
 
 typedef struct gs_ctx gs_ctx;
@@ -188,6 +193,8 @@ int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
                       double* x_state, double* b_state, int64_t it0, int n_sweeps,
                       double* x_rec, double* b_rec, const double* z0_inj, const double* z_inj,
                       const double* u_inj, int32_t* info);
+/* (x_rec / b_rec may be pinned host memory: the kernel then writes the history straight to
+   the host over PCIe, readable after the call's work completes.) */
 
 /*
  * tau[p][k][c] = b_sin^2 + b_cos^2 over fidx (pta_gibbs.py:194-195, 259-260), or

@@ -14,6 +14,7 @@ struct gs_ctx {
   int psr_base;  // GS_OPT_PSR_BASE: global index of this shard's pulsar 0 (RNG counters)
   int x_per_sys = 0;  // GS_OPT_X_PER_SYS
   int grid_exact = 0;  // GS_OPT_GRID_EXACT
+  int brec_nc = 0;     // GS_OPT_BREC_CHAINS
   const int64_t* sweep_dev = nullptr;  // gs_ctx_set_sweep_counter
   double* ws = nullptr;  // tile workspace of the large-NF b-draw (grown on demand)
   size_t ws_bytes = 0;
@@ -427,6 +428,10 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
       if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_GRID_EXACT must be 0 or 1");
       ctx->grid_exact = value;
       return 0;
+    case GS_OPT_BREC_CHAINS:
+      if (value < 0) return fail_arg(3, "GS_OPT_BREC_CHAINS must be >= 0");
+      ctx->brec_nc = value;
+      return 0;
     case GS_OPT_X_PER_SYS:
       if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_X_PER_SYS must be 0 or 1");
       ctx->x_per_sys = value;
@@ -442,6 +447,7 @@ int gs_ctx_get_option(gs_ctx* ctx, int option) {
   if (option == GS_OPT_PSR_BASE) return ctx->psr_base;
   if (option == GS_OPT_X_PER_SYS) return ctx->x_per_sys;
   if (option == GS_OPT_GRID_EXACT) return ctx->grid_exact;
+  if (option == GS_OPT_BREC_CHAINS) return ctx->brec_nc;
   return -1;
 }
 
@@ -653,6 +659,7 @@ int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.x_state = x_state; a.b_state = b_state; a.x_rec = x_rec; a.b_rec = b_rec;
   a.z0_inj = z0_inj; a.z_inj = z_inj; a.u_inj = u_inj; a.info = info; a.key = key_of(ctx);
   a.bcast = ctx->bcast; a.psr_base = ctx->psr_base;
+  a.brec_nc = ctx->brec_nc < n_chain ? ctx->brec_nc : 0;
   if (launch_sweep_freespec(ctx->stream, a)) return fail_arg(4, "unsupported NF");
   return after_launch("k_sweep_freespec");
 }

@@ -359,9 +359,11 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
     GS_PH_BEGIN
     // record-before-update (pulsar_gibbs.py:658-659)
     if (A.x_rec && act && !(lane & 1)) A.x_rec[rec * NFR + kf] = x;
-    if (A.b_rec) {
-      if (act) A.b_rec[rec * A.ldb + fi] = bF;
-      if (actm) A.b_rec[rec * A.ldb + mi] = bM;
+    if (A.b_rec && (A.brec_nc == 0 || c < A.brec_nc)) {
+      // every system (row rec), or the first brec_nc chains of each pulsar, compact
+      const int64_t brow = A.brec_nc == 0 ? rec : ((int64_t)sw * A.n_psr + p) * A.brec_nc + c;
+      if (act) A.b_rec[brow * A.ldb + fi] = bF;
+      if (actm) A.b_rec[brow * A.ldb + mi] = bM;
     }
     // pass 0: first b draw from xs at global sweep 0 (pulsar_gibbs.py:661-662);
     // pass 1: rho|b then the gated b draw.  One bdraw_wave call site.

@@ -198,21 +198,30 @@ class FreeSpectrumChains:
         return self.model.P * self.n_chain
 
     def run(self, n_sweeps, record=True, record_b=True, z0_inj=None, z_inj=None, u_inj=None,
-            x_rec=None, b_rec=None):
+            x_rec=None, b_rec=None, record_b_chains=None):
+        """record_b_chains=K (< n_chain): b_rec holds only chains c < K of each pulsar, row
+        sweep * P * K + p * K + c (GS_OPT_BREC_CHAINS) -- the reference's bchain is chain 0."""
         m = self.model
         dev = self.ctx.device
+        bk = self.n_chain if record_b_chains is None else min(int(record_b_chains), self.n_chain)
         if record and x_rec is None:
             x_rec = torch.empty(n_sweeps, self.n_sys, self.n_f, dtype=torch.float64, device=dev)
         if record and record_b and b_rec is None:
-            b_rec = torch.empty(n_sweeps, self.n_sys, m.ldb, dtype=torch.float64, device=dev)
+            b_rec = torch.empty(n_sweeps, m.P * bk, m.ldb, dtype=torch.float64, device=dev)
         if not self.fused:
-            self._run_sequence(n_sweeps, x_rec, b_rec if record_b else None, z0_inj, z_inj, u_inj)
+            self._run_sequence(n_sweeps, x_rec, b_rec if record_b else None, z0_inj, z_inj, u_inj, bk)
             return x_rec, b_rec
-        check(self.ctx.lib.gs_sweep_freespec(
-            self.ctx.handle, m.P, self.n_chain, m.NF, m.NMX, m.ldb, ptr(m.model), ptr(m.fidx),
-            ptr(m.midx), ptr(m.nm_dev), self.rhomin, self.rhomax, self.chain_base, ptr(self.x),
-            ptr(self.b), self.it, int(n_sweeps), ptr(x_rec), ptr(b_rec), ptr(z0_inj), ptr(z_inj),
-            ptr(u_inj), ptr(self.info)), "gs_sweep_freespec")
+        lib, h = self.ctx.lib, self.ctx.handle
+        prev = self.ctx.get_option(_lib.OPT_BREC_CHAINS)
+        self.ctx.set_option(_lib.OPT_BREC_CHAINS, bk if bk < self.n_chain else 0)
+        try:
+            check(lib.gs_sweep_freespec(
+                h, m.P, self.n_chain, m.NF, m.NMX, m.ldb, ptr(m.model), ptr(m.fidx),
+                ptr(m.midx), ptr(m.nm_dev), self.rhomin, self.rhomax, self.chain_base, ptr(self.x),
+                ptr(self.b), self.it, int(n_sweeps), ptr(x_rec), ptr(b_rec), ptr(z0_inj), ptr(z_inj),
+                ptr(u_inj), ptr(self.info)), "gs_sweep_freespec")
+        finally:
+            self.ctx.set_option(_lib.OPT_BREC_CHAINS, prev)
         self.it += int(n_sweeps)
         return x_rec, b_rec
 
@@ -236,7 +245,7 @@ class FreeSpectrumChains:
             self.ctx.set_option(_lib.OPT_X_PER_SYS, per_sys)
         torch.where(self.info == 0, inf, self.info, out=self.info)
 
-    def _run_sequence(self, n_sweeps, x_rec, b_rec, z0_inj, z_inj, u_inj):
+    def _run_sequence(self, n_sweeps, x_rec, b_rec, z0_inj, z_inj, u_inj, bk=None):
         """NF > 64 (workspace-tile b draw): the same loop body as the fused kernel as a launch
         sequence per sweep -- record, [first draw], analytic rho|b (gs_rho_analytic), gate +
         phiinv, gated b|rho (gs_bdraw) -- with the same Philox counters per draw."""
@@ -245,8 +254,11 @@ class FreeSpectrumChains:
             ii = self.it
             check(lib.gs_pta_record(h, self.n_sys, self.n_f, ptr(self.x), ptr(x_rec[i]) if x_rec is not None
                                     else None, ptr(self.xlast)), "gs_pta_record")   # pulsar_gibbs.py:658
-            if b_rec is not None:
-                b_rec[i].copy_(self.b)                                               # :659
+            if b_rec is not None:                                                    # :659
+                if bk is None or bk >= self.n_chain:
+                    b_rec[i].copy_(self.b)
+                else:
+                    b_rec[i].copy_(self.b.view(m.P, self.n_chain, m.ldb)[:, :bk].reshape(m.P * bk, m.ldb))
             if ii == 0:                                                              # :661-662
                 self._gate_phiinv(with_gate=False)
                 self._bdraw(z0_inj, _lib.EV_B0, None)

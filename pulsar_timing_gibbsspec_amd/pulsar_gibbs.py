@@ -137,13 +137,13 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
         runner.run(1, record=False)        # re-run sweep start-1: row start-1's successor
     runner.it = max(runner.it, start)
     blk = max(1, save_every) + 1
-    # block k+1's sweeps run while block k's rows stream to pinned host memory
-    bview = None if (allb or nc == 1) else (lambda t: t[:, ::nc])      # chain 0 of every pulsar
-    # x rows (and b rows when they all go to the host and are few) are written by the kernel
-    # straight into pinned host memory; every chain's b goes through HBM + the copy engine
-    streamer = HistoryStreamer(ctx, [(blk, P * nc, n_f), (blk, P * nc, model.ldb)], views=[None, bview],
-                               direct=[True, bview is None and not allb])
-    bstride = 1 if bview is not None else nc
+    # block k+1's sweeps run while block k's rows reach pinned host memory: the kernel writes
+    # every chain's x rows and chain 0's b rows (GS_OPT_BREC_CHAINS = 1; the reference's bchain)
+    # straight into the pinned slots; every chain's b (record_bchains) goes through HBM and the
+    # copy engine
+    bk = nc if (allb or nc == 1) else 1
+    streamer = HistoryStreamer(ctx, [(blk, P * nc, n_f), (blk, P * bk, model.ldb)], direct=[True, not allb])
+    bstride = bk
 
     def consume(slot, ii, nxt):
         xh, bh = (t.numpy() for t in streamer.fetch(slot))
@@ -172,7 +172,7 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
         nxt = min(niter, (ii // save_every + 1) * save_every + 1)
         n = nxt - ii
         xr, br = streamer.buffers(slot, n)
-        runner.run(n, x_rec=xr, b_rec=br)
+        runner.run(n, x_rec=xr, b_rec=br, record_b_chains=bk)
         streamer.submit(slot, n)
         if pending is not None:
             consume(*pending)

@@ -214,3 +214,24 @@ def test_sample_flush_final_and_resume(tmp_path):
     res = PulsarBlockGibbs(pta, seed=8).sample(g["x0"], outdir=str(tmp_path / "b"), niter=260, resume=True,
                                                 flush_final=True)
     assert np.array_equal(res, full)
+
+
+def test_history_straight_to_pinned_host(model, replay):
+    """Zero-copy history (sample()'s default): x rows and the first K chains' b rows written
+    by the kernel into pinned host memory (GS_OPT_BREC_CHAINS) equal the HBM rows of the same
+    sweeps, bit for bit; the option is restored after the call."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import FreeSpectrumChains
+    C, n, K = 8, 30, 2
+    x0 = golden("single_j1713.npz")["x0"]
+    ra = FreeSpectrumChains(model, replay["rhomin"], replay["rhomax"], C, x0)
+    xa, ba = ra.run(n)
+    rb = FreeSpectrumChains(model, replay["rhomin"], replay["rhomax"], C, x0)
+    xh = torch.empty(n, C, 30, dtype=torch.float64, pin_memory=True)
+    bh = torch.empty(n, K, model.ldb, dtype=torch.float64, pin_memory=True)
+    rb.run(n, x_rec=xh, b_rec=bh, record_b_chains=K)
+    torch.cuda.synchronize()
+    assert model.ctx.get_option(_lib.OPT_BREC_CHAINS) == 0
+    assert torch.equal(xh, xa.cpu())
+    assert torch.equal(bh, ba.cpu()[:, :K])
+    assert torch.equal(rb.b, ra.b)
