@@ -352,19 +352,28 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
 
   const double rhomin = A.rhomin, rhomax = A.rhomax;
   const double irhomin = 1.0 / rhomin, irhomax = 1.0 / rhomax;
+  // record pointers of this lane, advanced by one sweep's rows per iteration (no per-sweep
+  // 64-bit index products, and the SweepArgs pointers are dead inside the loop): x rows of every
+  // system; b rows of every system, or of the first brec_nc chains of each pulsar, compact
+  double* xrp = (A.x_rec && act && !(lane & 1)) ? A.x_rec + sys * NFR + kf : nullptr;
+  const int64_t xr_step = n_sys * NFR;
+  const bool brec = A.b_rec && (A.brec_nc == 0 || c < A.brec_nc);
+  const int64_t brow0 = A.brec_nc == 0 ? sys : (int64_t)p * A.brec_nc + c;
+  double* bFp = (brec && act) ? A.b_rec + brow0 * A.ldb + fi : nullptr;
+  double* bMp = (brec && actm) ? A.b_rec + brow0 * A.ldb + mi : nullptr;
+  const int64_t br_step = (A.brec_nc == 0 ? n_sys : (int64_t)A.n_psr * A.brec_nc) * A.ldb;
 #pragma unroll 1
   for (int sw = 0; sw < A.n_sweeps; ++sw) {
     const long long ii = A.it0 + sw;
     const int64_t rec = (int64_t)sw * n_sys + sys;
     GS_PH_BEGIN
     // record-before-update (pulsar_gibbs.py:658-659)
-    if (A.x_rec && act && !(lane & 1)) A.x_rec[rec * NFR + kf] = x;
-    if (A.b_rec && (A.brec_nc == 0 || c < A.brec_nc)) {
-      // every system (row rec), or the first brec_nc chains of each pulsar, compact
-      const int64_t brow = A.brec_nc == 0 ? rec : ((int64_t)sw * A.n_psr + p) * A.brec_nc + c;
-      if (act) A.b_rec[brow * A.ldb + fi] = bF;
-      if (actm) A.b_rec[brow * A.ldb + mi] = bM;
-    }
+    if (xrp) *xrp = x;
+    if (bFp) *bFp = bF;
+    if (bMp) *bMp = bM;
+    xrp = xrp ? xrp + xr_step : nullptr;
+    bFp = bFp ? bFp + br_step : nullptr;
+    bMp = bMp ? bMp + br_step : nullptr;
     // pass 0: first b draw from xs at global sweep 0 (pulsar_gibbs.py:661-662);
     // pass 1: rho|b then the gated b draw.  One bdraw_wave call site.
 #pragma unroll 1
