@@ -573,10 +573,10 @@ int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
 }
 
 int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
-  const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
-  dim3 grid((unsigned)(a.n_psr * nb));
   if (a.NMX > 64) {
     constexpr int WPB = GS_SWEEP_WPB;
+    const int nb = (a.n_chain + WPB - 1) / WPB;
+    dim3 grid((unsigned)(a.n_psr * nb));
     const size_t lds = (size_t)gs_tile_scr(a.NF) * WPB * sizeof(double);
     if (a.NF <= 0 || a.NF > 64 || (a.NF & 1)) return 1;
     switch (a.NF / 16 + 1) {
@@ -587,10 +587,13 @@ int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
       default: hipLaunchKernelGGL((k_bdraw_wide<5, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
     }
   }
+  constexpr int WPB = GS_BDRAW_WPB;
+  const int nb = (a.n_chain + WPB - 1) / WPB;
+  dim3 grid((unsigned)(a.n_psr * nb));
   const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
   const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) +
-                      (fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) * GS_SWEEP_WPB) * sizeof(double);
-  return dispatch_nf_bdraw<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);
+                      (fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) * WPB) * sizeof(double);
+  return dispatch_nf_bdraw<WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
 
 int launch_rho_analytic(hipStream_t s, const RhoArgs& a) {

@@ -11,6 +11,11 @@
 #ifndef GS_SWEEP_WPB
 #define GS_SWEEP_WPB 4
 #endif
+// ... of the one-draw-per-launch b|rho kernel (k_bdraw: every PTA sweep stages each pulsar's
+// model block once per workgroup)
+#ifndef GS_BDRAW_WPB
+#define GS_BDRAW_WPB 4
+#endif
 
 // fixed-prior (timing-model) columns per pulsar: up to 64 everywhere (lane per row), up to
 // GS_NMX_WIDE in gs_prefix / gs_bdraw with NF <= 64 (k_prefix_wide: L_M in LDS, 128 KB)

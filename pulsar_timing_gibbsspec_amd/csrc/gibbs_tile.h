@@ -709,27 +709,24 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
   for (int P = 0; P < nP; ++P) {
     const int row = 16 * P + c;
     const bool rok = row < nM;
-    // padding rows read row nM - 1 (written by the prefix, finite) and are discarded below; R
-    // columns past nM read column nM - 1 against a staged z of 0: no exec-masked loads, no zero
-    // fills (a ragged batch's rows / columns nM..NMX-1 are never written, so never read)
-    const int rowc = min(row, nM - 1);
     double p = 0.0;
 #pragma unroll
     for (int J = 0; J < NT; ++J)
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int f = 16 * J + 4 * s + q;
-        const double g = M.G[rowc * LD + min(f, NF - 1) + z0];
-        p = fma(f < NF ? -g : 0.0, xrow[J][s], p);
+        const double g = (rok && f < NF) ? M.G[row * LD + f + z0] : 0.0;
+        p = fma(-g, xrow[J][s], p);
       }
     for (int Q = P; Q < nP; ++Q)
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int mm = 16 * Q + 4 * s + q;
-        p = fma(M.R[rowc * NMX + min(mm, nM - 1) + z0], zb[mm], p);
+        const double rv = (rok && mm < nM) ? M.R[row * NMX + mm + z0] : 0.0;
+        p = fma(rv, zb[mm], p);
       }
     p = qsum(p);
-    const double xm = rok ? M.h[rowc + z0] + p : 0.0;
+    const double xm = rok ? M.h[row + z0] + p : 0.0;
     if (!WIDE || P < 4)
       ob[row] = xm;
     else if (rok && q == 0)

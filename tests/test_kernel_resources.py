@@ -1,0 +1,49 @@
+"""Occupancy guard for the hot kernels (CPU: reads the built library's code-object metadata).
+
+The tile b-draw and the fused sweep are f64-issue bound at a fixed number of waves per SIMD;
+a change that pushes a kernel past a VGPR boundary silently costs 25-30 % (k_bdraw at NF = 60:
+164 -> 170 VGPRs, 3 -> 2 waves/SIMD, CURN sweep 0.71 -> 0.89 ms on MI355X, round 2).
+"""
+import os
+
+import pytest
+
+from tools.kernel_resources import kernel_resources, waves_per_simd
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "pulsar_timing_gibbsspec_amd",
+                   "libpulsar_gibbs.so")
+
+
+@pytest.fixture(scope="module")
+def res():
+    if not os.path.exists(LIB):
+        pytest.skip("library not built")
+    return kernel_resources(LIB)
+
+
+def one(res, frag):
+    hits = [r for n, r in res.items() if frag in n]
+    assert len(hits) == 1, (frag, [n for n in res if frag in n])
+    return hits[0]
+
+
+# (mangled-name fragment, minimum waves per SIMD, VGPR spills allowed)
+HOT = [
+    ("k_bdrawILi60ELi0ELi4ELi3E", 3, 0),           # PTA / CURN b|rho (configs[3])
+    ("k_sweep_freespecILi60ELi0ELi4ELi3E", 2, 0),  # headline fused sweep (configs[1], [2])
+    ("k_rho_red_waveE", 4, 0),                     # CURN + red grid CDF
+    ("k_rho_curn_fastE", 2, 0),
+    ("k_rho_curn_sum_waveE", 2, 0),
+]
+
+
+@pytest.mark.parametrize("frag,min_waves,spills", HOT)
+def test_hot_kernel_occupancy(res, frag, min_waves, spills):
+    r = one(res, frag)
+    assert waves_per_simd(r["vgpr_count"]) >= min_waves, (frag, r)
+    assert r.get("vgpr_spill_count", 0) <= spills, (frag, r)
+
+
+def test_every_kernel_has_metadata(res):
+    assert len(res) > 50
+    assert all("vgpr_count" in r for r in res.values())
