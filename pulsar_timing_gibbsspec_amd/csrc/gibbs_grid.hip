@@ -613,15 +613,41 @@ __global__ void k_pta_gate_phiinv(PtaGateArgs A) {
   for (int j = lane; j < A.n_param; j += 64) same |= (xc[j] == xl);
   const bool gate = __ballot(same) == 0ull;
   if (lane == 0) A.gate[c] = A.xlast ? (gate ? 1 : 0) : 1;
-  for (int t = lane; t < A.n_psr * A.n_f; t += 64) {
-    const int p = t / A.n_f, k = t % A.n_f;
-    double phi = pow(10.0, 2.0 * xc[A.gw_col[k]]);
-    if (A.red_col) phi = phi + pow(10.0, 2.0 * xc[A.red_col[p * A.n_f + k]]);
-    if (A.irn) phi = phi + A.irn[(int64_t)k * A.n_chain + c];
-    const double pinv = 1.0 / phi;
-    double* o = A.phiinv_F + ((int64_t)p * A.n_chain + c) * (2 * A.n_f);
-    o[2 * k] = pinv;
-    o[2 * k + 1] = pinv;
+  if (A.n_f <= 64) {
+    // the common part once per frequency (lane k), shared by every pulsar through a lane
+    // shuffle: phi_gw (+ irn) and, without per-pulsar red noise, its reciprocal (the CURN
+    // sweep's phiinv is the same for all pulsars: n_f instead of n_psr n_f pows per chain)
+    __shared__ double phg_s[64], ping_s[64];  // one wave per workgroup
+    const int kk = lane < A.n_f ? lane : 0;
+    double phg = pow(10.0, 2.0 * xc[A.gw_col[kk]]);
+    if (A.irn) phg = phg + A.irn[(int64_t)kk * A.n_chain + c];
+    phg_s[lane] = phg;
+    ping_s[lane] = 1.0 / phg;
+    wave_lds_sync();
+    for (int t = lane; t < A.n_psr * A.n_f; t += 64) {
+      const int p = t / A.n_f, k = t % A.n_f;
+      double pinv;
+      if (A.red_col) {
+        const double phi = phg_s[k] + pow(10.0, 2.0 * xc[A.red_col[p * A.n_f + k]]);
+        pinv = 1.0 / phi;
+      } else {
+        pinv = ping_s[k];
+      }
+      double* o = A.phiinv_F + ((int64_t)p * A.n_chain + c) * (2 * A.n_f);
+      o[2 * k] = pinv;
+      o[2 * k + 1] = pinv;
+    }
+  } else {
+    for (int t = lane; t < A.n_psr * A.n_f; t += 64) {
+      const int p = t / A.n_f, k = t % A.n_f;
+      double phi = pow(10.0, 2.0 * xc[A.gw_col[k]]);
+      if (A.red_col) phi = phi + pow(10.0, 2.0 * xc[A.red_col[p * A.n_f + k]]);
+      if (A.irn) phi = phi + A.irn[(int64_t)k * A.n_chain + c];
+      const double pinv = 1.0 / phi;
+      double* o = A.phiinv_F + ((int64_t)p * A.n_chain + c) * (2 * A.n_f);
+      o[2 * k] = pinv;
+      o[2 * k + 1] = pinv;
+    }
   }
 }
 
