@@ -191,9 +191,14 @@ __device__ __forceinline__ int bdraw_sys(const ModelLds& M, int NMX, int nM, int
     return bdraw_wave<NFC, BC>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
 }
 
-// Copy a pulsar's model block into LDS (whole workgroup).
+// Copy a pulsar's model block into LDS (whole workgroup), 16 bytes per lane and access: model
+// blocks are a 16-byte multiple of doubles (model_stride_doubles) at 16-byte aligned offsets.
 __device__ __forceinline__ void stage_model(double* lds, const double* g, int64_t n) {
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) lds[i] = g[i];
+  const double2* __restrict__ g2 = reinterpret_cast<const double2*>(g);
+  double2* l2 = reinterpret_cast<double2*>(lds);
+  const int n2 = (int)(n >> 1);
+#pragma unroll 4
+  for (int i = threadIdx.x; i < n2; i += blockDim.x) l2[i] = g2[i];
   __syncthreads();
 }
 
