@@ -193,12 +193,27 @@ __device__ __forceinline__ int bdraw_sys(const ModelLds& M, int NMX, int nM, int
 
 // Copy a pulsar's model block into LDS (whole workgroup), 16 bytes per lane and access: model
 // blocks are a 16-byte multiple of doubles (model_stride_doubles) at 16-byte aligned offsets.
+// GS_STAGE_GLDS: by LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no ds_write), each
+// wave-instruction filling 1 KB of the block lane-linearly.
+#ifndef GS_STAGE_GLDS
+#define GS_STAGE_GLDS 1
+#endif
+typedef __attribute__((address_space(3))) void* gs_lds_vptr;
 __device__ __forceinline__ void stage_model(double* lds, const double* g, int64_t n) {
+  const int n2 = (int)(n >> 1);
+#if GS_STAGE_GLDS
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  for (int base = wave * 64; base < n2; base += nw * 64) {
+    if (base + lane < n2)
+      __builtin_amdgcn_global_load_lds((const void*)(g + 2 * (base + lane)), (gs_lds_vptr)(lds + 2 * base), 16, 0,
+                                       0);
+  }
+#else
   const double2* __restrict__ g2 = reinterpret_cast<const double2*>(g);
   double2* l2 = reinterpret_cast<double2*>(lds);
-  const int n2 = (int)(n >> 1);
 #pragma unroll 4
   for (int i = threadIdx.x; i < n2; i += blockDim.x) l2[i] = g2[i];
+#endif
   __syncthreads();
 }
 
