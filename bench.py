@@ -538,7 +538,7 @@ def main():
                     help="also time the headline with every recorded row streamed to pinned host memory (1/0)")
     ap.add_argument("--indep", type=int, default=1, help="measure BASELINE configs[2] (45 independent pulsars)")
     ap.add_argument("--indep-chains", type=int, default=256, help="chains per pulsar for configs[2]")
-    ap.add_argument("--indep-steps", type=int, default=200)
+    ap.add_argument("--indep-steps", type=int, default=500)
     ap.add_argument("--pta", default="curn_red,curn", help="secondary PTA configs measured in the same run "
                     "(comma list of curn_red, curn; or none). curn uses the sufficient-statistic draw")
     ap.add_argument("--pta-chains", type=int, default=2048,
