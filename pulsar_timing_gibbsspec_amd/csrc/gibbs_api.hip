@@ -47,13 +47,24 @@ gs_key key_of(const gs_ctx* c) {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------ TNT (a2)
-// grid (n_psr, nb*nb), nb = ceil(m_max/16); 4 wavefronts split the TOAs.
+// Blocked compensated accumulation: each MFMA chain sums one block of 64 TOAs from zero, and
+// the block sums enter a two-sum (hi, lo) pair, so the rounding error grows with the block
+// length rather than with n_toa (n_toa = 10^4 in configs[4]: a plain running sum was ~5x
+// less accurate than numpy's blocked dgemm).  Once per model: accuracy over speed.
+__device__ __forceinline__ void two_sum_acc(double& hi, double& lo, double x) {
+  const double s = hi + x;
+  const double bb = s - hi;
+  lo += (hi - (s - bb)) + (x - bb);
+  hi = s;
+}
+
+// grid (n_psr, nb*nb), nb = ceil(m_max/16); 4 wavefronts take alternate 64-TOA blocks.
 // D[i][j] += sum_t (T[t][I0+i] / N[t]) T[t][J0+j] with v_mfma_f64_16x16x4f64:
 // A lane l holds A[l&15][l>>4], B lane l holds B[l>>4][l&15];
 // C/D lane l reg r holds D[(l>>4) + 4r][l&15].
 __global__ __launch_bounds__(256) void k_tnt(const gs_tnt_desc* desc, int nb, const double* T,
                                              const double* Nv, const double* r, double* TNT) {
-  __shared__ double red[3][4][64];
+  __shared__ double red[3][8][64];
   const gs_tnt_desc D = desc[blockIdx.x];
   const int bi = blockIdx.y / nb, bj = blockIdx.y % nb;
   const int m = (int)D.m;
@@ -64,45 +75,77 @@ __global__ __launch_bounds__(256) void k_tnt(const gs_tnt_desc* desc, int nb, co
   const double* Tp = T + D.T_off;
   const double* Np = Nv + D.toa_off;
   const int64_t n = D.n_toa;
-  d4 acc = {0.0, 0.0, 0.0, 0.0};
-  for (int64_t t0 = (int64_t)w * 4; t0 < n; t0 += 16) {
-    const int64_t t = t0 + k;
-    const bool ok = t < n;
-    const double invN = ok ? 1.0 / Np[t] : 0.0;
-    const double a = (ok && ci < m) ? Tp[t * m + ci] * invN : 0.0;
-    const double b = (ok && cj < m) ? Tp[t * m + cj] : 0.0;
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  d4 hi = {0.0, 0.0, 0.0, 0.0}, lo = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t tb = (int64_t)w * 64; tb < n; tb += 256) {
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int s = 0; s < 16; ++s) {
+      const int64_t t = tb + s * 4 + k;
+      const bool ok = t < n;
+      const double a = (ok && ci < m) ? Tp[t * m + ci] / Np[t] : 0.0;
+      const double b = (ok && cj < m) ? Tp[t * m + cj] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+    for (int q = 0; q < 4; ++q) {
+      double h = hi[q], e = lo[q];
+      two_sum_acc(h, e, acc[q]);
+      hi[q] = h;
+      lo[q] = e;
+    }
   }
   if (w > 0) {
-    for (int q = 0; q < 4; ++q) red[w - 1][q][l] = acc[q];
+    for (int q = 0; q < 4; ++q) {
+      red[w - 1][q][l] = hi[q];
+      red[w - 1][4 + q][l] = lo[q];
+    }
   }
   __syncthreads();
   if (w == 0) {
     for (int q = 0; q < 4; ++q) {
-      const double v = acc[q] + red[0][q][l] + red[1][q][l] + red[2][q][l];
+      double h = hi[q], e = lo[q];
+      for (int u = 0; u < 3; ++u) {
+        two_sum_acc(h, e, red[u][q][l]);
+        e += red[u][4 + q][l];
+      }
       const int row = bi * 16 + (l >> 4) + 4 * q, col = bj * 16 + (l & 15);
-      if (row < m && col < m) TNT[D.tnt_off + (int64_t)row * m + col] = v;
+      if (row < m && col < m) TNT[D.tnt_off + (int64_t)row * m + col] = h + e;
     }
   }
   (void)r;
 }
 
-// d = T^T (r / N): grid (n_psr, ceil(m_max/64)), 4 wavefronts split the TOAs.
+// d = T^T (r / N): grid (n_psr, ceil(m_max/64)), 4 wavefronts take alternate 64-TOA blocks,
+// block sums compensated as in k_tnt.
 __global__ __launch_bounds__(256) void k_tnr(const gs_tnt_desc* desc, const double* T,
                                              const double* Nv, const double* r, double* d) {
-  __shared__ double red[4][64];
+  __shared__ double red[2][4][64];
   const gs_tnt_desc D = desc[blockIdx.x];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int m = (int)D.m;
   const int j = blockIdx.y * 64 + l;
-  double s = 0.0;
+  double hi = 0.0, lo = 0.0;
   if (j < m) {
     const double* Tp = T + D.T_off;
-    for (int64_t t = w; t < D.n_toa; t += 4) s = fma(Tp[t * m + j], r[D.toa_off + t] / Nv[D.toa_off + t], s);
+    const double* rp = r + D.toa_off;
+    const double* Np = Nv + D.toa_off;
+    for (int64_t tb = (int64_t)w * 64; tb < D.n_toa; tb += 256) {
+      const int64_t te = tb + 64 < D.n_toa ? tb + 64 : D.n_toa;
+      double s = 0.0;
+      for (int64_t t = tb; t < te; ++t) s = fma(Tp[t * m + j], rp[t] / Np[t], s);
+      two_sum_acc(hi, lo, s);
+    }
   }
-  red[w][l] = s;
+  red[0][w][l] = hi;
+  red[1][w][l] = lo;
   __syncthreads();
-  if (w == 0 && j < m) d[D.d_off + j] = red[0][l] + red[1][l] + red[2][l] + red[3][l];
+  if (w == 0 && j < m) {
+    double h = red[0][0][l], e = red[1][0][l];
+    for (int u = 1; u < 4; ++u) {
+      two_sum_acc(h, e, red[0][u][l]);
+      e += red[1][u][l];
+    }
+    d[D.d_off + j] = h + e;
+  }
 }
 
 // ------------------------------------------------------------------ prefix, wide timing model

@@ -182,3 +182,57 @@ def test_array_engine_philox_runs(ctx):
     assert int(eng.info.abs().sum()) == 0
     gw = d["gw_cols"]
     assert (x[:, gw] >= -9.0).all() and (x[:, gw] <= -4.0).all()
+
+
+def test_full_size_config4_pulsar(ctx):
+    """One pulsar of BASELINE configs[4] at its full size (10^4 TOAs, 4 backends, n_f = 100,
+    m = 216): the per-chain batched SYRK against numpy's TNT/d and the b draw against the
+    exact long-double Cholesky draw with the same normals (the bench runs 200 of these)."""
+    import torch
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel
+    from pulsar_timing_gibbsspec_amd.white import WhiteNoiseModel
+    d = synthetic.config5_array(n_psr=1, n_toa=10000, n_f=100, seed=21)
+    T, r = d["T"][0], d["r"][0]
+    assert T.shape == (10000, 216)
+    C = 2
+    c2 = _lib.Context(0, seed=2)
+    c2.set_option(_lib.OPT_X_PER_SYS, 1)
+    wm = WhiteNoiseModel(c2, d["T"], d["r"], d["sigma"], d["backend"], [d["fidx"]], [d["phiinv_fixed"]],
+                         [d["white"]], C)
+    rng = np.random.default_rng(22)
+    x = np.repeat(d["x0"], C, axis=0)
+    for col, kind, k, lo, hi in d["white"]:
+        x[:, col] = rng.uniform(lo, hi, C)
+    wm.refresh(torch.as_tensor(x, device=c2.device), d["n_param"])
+    for c in range(C):
+        TNT, dd = O.tnt(T, _white_N(d, 0, x[c]), r)
+        TNTd, ddd = wm.tnt_host(0, c)
+        assert np.max(np.abs(TNTd - TNT)) <= 1e-12 * np.max(np.abs(TNT))
+        assert normwise_rel(ddd, dd) < 1e-12
+    # b draw at the full size, fixed white noise (sigma^2), injected normals
+    N = d["sigma"][0] ** 2
+    model = DeviceModel(ctx, [T], [N], [r], [d["fidx"]], [d["phiinv_fixed"]])
+    m = T.shape[1]
+    logrho = rng.uniform(-8.5, -5.0, (1, 100))
+    ph = 1.0 / np.repeat(10 ** (2 * logrho), 2, axis=1)
+    z = np.zeros((1, model.ldb))
+    z[:, :m] = rng.standard_normal((1, m))
+    dev = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=ctx.device)  # noqa: E731
+    b, info = model.bdraw(dev(ph), 1, z=dev(z))
+    assert not info.cpu().numpy().any()
+    phi = np.full(m, 1e-40)
+    phi[d["fidx"]] = ph[0]
+    order = O.chol_order(m, d["fidx"])
+    bx = exact_chol_draw(T, N, r, phi, z[0, :m], order)
+    # fp64 noise floor of this system (cond(S) ~ 1e11 at 10^4 TOAs): numpy's own fp64 draw
+    # (blocked dgemm TNT, LAPACK Cholesky, the same normals) against the exact draw
+    import scipy.linalg as sl
+    S = (T.T @ (T / N[:, None]) + np.diag(phi))[np.ix_(order, order)]
+    L = np.linalg.cholesky(S)
+    y = sl.solve_triangular(L, (T.T @ (r / N))[order], lower=True) + z[0, order]
+    bn = np.empty(m)
+    bn[order] = sl.solve_triangular(L.T, y, lower=False)
+    floor = normwise_rel(bn, bx)
+    err = normwise_rel(b.cpu().numpy()[0, :m], bx)
+    assert err < max(1e-9, 4 * floor), (err, floor)

@@ -92,13 +92,16 @@ def test_indep_array_matches_reference_and_oracle(ctx, arr):
             # The reference's own fp64 SVD draw is 6e-10 from the exact (long-double) draw for
             # J1909-3744 (m = 77, cond ~1e9), and over 60 fed-back sweeps a CPU fp64 Cholesky
             # replay of the same draws already departs from the reference chain by 1.7e-9 in b.
-            # Tolerance: 1e-9 (north_star), or twice what that CPU replay shows when larger.
+            # Tolerance: 1e-9 (north_star), or a few times what that CPU replay shows when
+            # larger (x: 2x; b: 4x, as for the oracle pulsars below -- J1909-3744's b trajectory
+            # sat at 0.88 of a 2x bound in round 2a and moves with any last-bit change of TNT,
+            # e.g. the compensated k_tnt sum, while each of its draws stays 2e-10 from exact).
             R = single_replay(f, zc_file=INDEP_ZC_FILE, key=f"zc{picks[p]}")
             cx, cb, _ = O.sweep_single(R["TNT"], R["d"], R["gwid"], f["x0"], R["rhomin"], R["rhomax"], R["zc"],
                                        f["U"], n, lambda x: O.phiinv_single(x, R["n_tm"]), draw="chol",
                                        order=R["order"])
             tol_x = max(1e-9, 2 * normwise_rel(cx, want_x))
-            tol_b = max(1e-9, 2 * normwise_rel(cb[1:], want_b[1:]))
+            tol_b = max(1e-9, 4 * normwise_rel(cb[1:], want_b[1:]))
             tl = exact_tnt(f["T"], f["Nvec"], f["r"])
             order = O.chol_order(m, arr["gwid"][p])
             floor = max(normwise_rel(want_b[j], exact_chol_draw_pre(tl, O.phiinv_single(want_x[j], m - 60),
@@ -135,14 +138,23 @@ def test_indep_array_matches_reference_and_oracle(ctx, arr):
         m = int(model.m[p])
         tl = exact_tnt(arr["T"][p], arr["N"][p], arr["R"][p])
         order = O.chol_order(m, arr["gwid"][p])
-        worst = 0.0
+        TNT, d = O.tnt(arr["T"][p], arr["N"][p], arr["R"][p])
+        worst = worst_np = 0.0
         for ii in range(1, n - 1, 3):
             ph = O.phiinv_single(xr[ii + 1, p], m - 60)
             want = exact_chol_draw_pre(tl, ph, z[ii + 1, p, :m], order)
             worst = max(worst, normwise_rel(br[ii + 1, p, :m], want))
+            worst_np = max(worst_np, normwise_rel(O.bdraw_chol(TNT, d, ph, z[ii + 1, p, :m], order), want))
         report[p]["b_vs_exact"] = worst
-        assert worst < max(1e-9, 2 * report[p]["fp64_floor"]), (p, report[p])
+        report[p]["numpy_vs_exact"] = worst_np
     _report("indep_parity", report)
+    # bound: 1e-9, or twice the fp64 floor -- the oracle trajectory's, or numpy's own fp64
+    # Cholesky draw at the SAME states (the device chain may visit states worse conditioned
+    # than the oracle's first sweeps: pulsar 32 reaches cond ~1e10, where numpy's draw is
+    # 1.7e-9 from exact and the device's 1.3e-9)
+    for p in range(P):
+        r = report[p]
+        assert r["b_vs_exact"] < max(1e-9, 2 * r["fp64_floor"], 2 * r["numpy_vs_exact"]), (p, r)
 
 
 def _report(name, rep):

@@ -1,0 +1,60 @@
+"""Where does the full-size configs[4] b draw lose accuracy (GPU diagnostic)?
+Compares, against the exact long-double draw: numpy fp64 on numpy's TNT, numpy fp64 on the
+device's TNT, the device draw on the device's TNT, and the device draw on the exact TNT."""
+import sys, os
+import numpy as np
+import scipy.linalg as sl
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pulsar_timing_gibbsspec_amd import _lib, synthetic
+from pulsar_timing_gibbsspec_amd.engine import DeviceModel
+from pulsar_timing_gibbsspec_amd._lib import ptr, check
+from oracle import gibbs_oracle as O
+from tests.parity_data import exact_chol_draw_pre, exact_tnt, normwise_rel
+
+d = synthetic.config5_array(n_psr=1, n_toa=int(sys.argv[1]) if len(sys.argv) > 1 else 10000, n_f=100, seed=21)
+T, r = d["T"][0], d["r"][0]
+N = d["sigma"][0] ** 2
+m = T.shape[1]
+rng = np.random.default_rng(5)
+logrho = rng.uniform(-8.5, -5.0, 100)
+ph = 1.0 / np.repeat(10 ** (2 * logrho), 2)
+z = rng.standard_normal(m)
+phi = np.full(m, 1e-40); phi[d["fidx"]] = ph
+order = O.chol_order(m, d["fidx"])
+tl = exact_tnt(T, N, r)
+bx = exact_chol_draw_pre(tl, phi, z, order)
+
+
+def np_draw(TNT, dv):
+    S = (TNT + np.diag(phi))[np.ix_(order, order)]
+    L = np.linalg.cholesky(S)
+    y = sl.solve_triangular(L, dv[order], lower=True) + z[order]
+    xx = sl.solve_triangular(L.T, y, lower=False)
+    b = np.empty(m); b[order] = xx
+    return b
+
+
+ctx = _lib.Context(0, seed=1)
+model = DeviceModel(ctx, [T], [N], [r], [d["fidx"]], [d["phiinv_fixed"]])
+TNTd, dd = model.tnt_host(0)
+TNTn = T.T @ (T / N[:, None]); dn = T.T @ (r / N)
+TNTx = np.asarray(tl[0], np.float64); dx = np.asarray(tl[1], np.float64)
+out = {"numpy_draw_numpy_tnt": normwise_rel(np_draw(TNTn, dn), bx),
+       "numpy_draw_device_tnt": normwise_rel(np_draw(TNTd, dd), bx),
+       "numpy_draw_exact_tnt": normwise_rel(np_draw(TNTx, dx), bx),
+       "device_tnt_rel_err": float(np.max(np.abs(TNTd - TNTx)) / np.max(np.abs(TNTx))),
+       "numpy_tnt_rel_err": float(np.max(np.abs(TNTn - TNTx)) / np.max(np.abs(TNTx)))}
+dev = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=ctx.device)
+zz = np.zeros((1, model.ldb)); zz[0, :m] = z
+b, info = model.bdraw(dev(ph[None]), 1, z=dev(zz))
+out["device_draw_device_tnt"] = normwise_rel(b.cpu().numpy()[0, :m], bx)
+# device draw from the exact (fp64-rounded) TNT: overwrite TNT/d, redo the prefix only
+model.TNT.copy_(torch.as_tensor(TNTx.ravel(), device=ctx.device))
+model.d.copy_(torch.as_tensor(dx, device=ctx.device))
+lib, h = ctx.lib, ctx.handle
+check(lib.gs_prefix(h, model.P, model.NF, model.NMX, ptr(model.prefix_desc), ptr(model.TNT), ptr(model.d),
+                    ptr(model.fidx), ptr(model.midx), ptr(model.phfix), ptr(model.model), ptr(model.info)), "prefix")
+b2, _ = model.bdraw(dev(ph[None]), 1, z=dev(zz))
+out["device_draw_exact_tnt"] = normwise_rel(b2.cpu().numpy()[0, :m], bx)
+print({k: float("%.3g" % v) for k, v in out.items()})
