@@ -337,6 +337,9 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
 }
 
 // ------------------------------------------------------------ fused sweep
+#ifndef GS_RHO_EXP
+#define GS_RHO_EXP 0
+#endif
 template <int NFC, int NTC, int WPB, int BC>
 __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepArgs A) {
   extern __shared__ double lds[];
@@ -428,7 +431,11 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
         // 1 - exp(arg) rounds to exactly 1 for arg < -37.5: skip the exp when every
         // lane is there (the usual case, tau >> rhomin)
         double hi = 1.0;
+#if GS_FAST_MATH && GS_RHO_EXP
+        if (__ballot(act && !(arg < -40.0))) hi = 1 - gs_exp_neg(arg);  // arg <= 0 (rhomin < rhomax)
+#else
         if (__ballot(act && !(arg < -40.0))) hi = 1 - exp(arg);
+#endif
         const double eta = 0.0 + hi * U;
 #if GS_FAST_MATH
         const double den = t1 - gs_log_pos(1 - eta);

@@ -285,6 +285,9 @@ __device__ __forceinline__ constexpr int tix(int I, int J, int NT) {
 #ifndef GS_RHO_PRIO  // ... while it runs the sweep's rho|b draw and gate (k_sweep_freespec)
 #define GS_RHO_PRIO 0
 #endif
+#ifndef GS_PIV_NR2
+#define GS_PIV_NR2 0
+#endif
 #ifndef GS_EXEC_MASK
 #define GS_EXEC_MASK 1
 #endif
@@ -316,7 +319,13 @@ __device__ __forceinline__ void tile_elim1(gs_d4& A, gs_d4& B, double& rsd, int 
       // -A[k][c]/A[k][k] = akm i0 (akk i0 - 2) (one Newton step on v_rcp_f64): the two
       // products run side by side, 4 dependent ops from pivot to multiplier
       const double i0 = __builtin_amdgcn_rcp(akk);
+#if GS_PIV_NR2
+      // two Newton steps: -1/akk to ~1 ulp instead of ~2^-50 relative
+      const double n1 = i0 * fma(akk, i0, -2.0);           // -1/akk, one step
+      const double ng = (akm * n1) * fma(akk, n1, 2.0);
+#else
       const double ng = (akm * i0) * fma(akk, i0, -2.0);
+#endif
       akc = fmac_nb(rn, rn, ng, k);                        // row k+1 after step k
 #pragma unroll
       for (int s = k1; s < 4; ++s) A[s] = fmac_nb(A[s], A[s], ng, k);
