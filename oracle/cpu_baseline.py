@@ -48,10 +48,10 @@ def single(seconds):
     def step():
         TNT, d = O.tnt(T, N, r)                              # recomputed every sweep (:664-665)
         if st["b"] is None:                                  # first draw from xs (:661-662)
-            st["b"] = O.bdraw_svd(TNT, d, O.phiinv_single(st["x"], n_tm), rng.standard_normal(T.shape[1]))
+            st["b"] = O.bdraw_svd(TNT, d, O.phiinv_single(st["x"], n_tm), rng.standard_normal(T.shape[1]), fallback=True)
         tau = O.tau_half(st["b"], gwid)
         st["x"] = 0.5 * np.log10(O.rho_analytic(tau, rng.random(30), 1e-18, 1e-8))
-        st["b"] = O.bdraw_svd(TNT, d, O.phiinv_single(st["x"], n_tm), rng.standard_normal(T.shape[1]))
+        st["b"] = O.bdraw_svd(TNT, d, O.phiinv_single(st["x"], n_tm), rng.standard_normal(T.shape[1]), fallback=True)
     return _loop(step, seconds), "J1713 single-chain sweeps (oracle restatement of pulsar_gibbs.py:656-698)"
 
 
@@ -73,9 +73,9 @@ def indep(seconds):
             m = T.shape[1]
             TNT, d = O.tnt(T, N, r)
             if bs[p] is None:
-                bs[p] = O.bdraw_svd(TNT, d, O.phiinv_single(xs[p], m - 60), rng.standard_normal(m))
+                bs[p] = O.bdraw_svd(TNT, d, O.phiinv_single(xs[p], m - 60), rng.standard_normal(m), fallback=True)
             xs[p] = 0.5 * np.log10(O.rho_analytic(O.tau_half(bs[p], gwid), rng.random(30), 1e-18, 1e-8))
-            bs[p] = O.bdraw_svd(TNT, d, O.phiinv_single(xs[p], m - 60), rng.standard_normal(m))
+            bs[p] = O.bdraw_svd(TNT, d, O.phiinv_single(xs[p], m - 60), rng.standard_normal(m), fallback=True)
     return _loop(step, seconds), "45-pulsar array sweeps (each pulsar's PulsarBlockGibbs loop, pulsar_gibbs.py:656-698)"
 
 
@@ -102,7 +102,7 @@ def pta(kind, seconds):
             phi = 10 ** (2 * x[rind]) + (10 ** (2 * x[hind[p * 30:(p + 1) * 30]]) if kind == "curn_red" else 0)
             ph = np.full(m[p], 1e-40)
             ph[gw[p]] = 1 / np.repeat(phi, 2)
-            out.append(O.bdraw_svd(TNT, d, ph, rng.standard_normal(m[p])))
+            out.append(O.bdraw_svd(TNT, d, ph, rng.standard_normal(m[p]), fallback=True))
         return out
     st["b"] = draw(st["x"])
 
@@ -146,7 +146,7 @@ def config5(seconds):
         TNT, dd = O.tnt(T, N_of(x), r)
         ph = np.full(m, 1e-40)
         ph[:gw.size * 2] = 1 / np.repeat(10 ** (2 * x[gw]), 2)
-        b = O.bdraw_svd(TNT, dd, ph, rng.standard_normal(m))
+        b = O.bdraw_svd(TNT, dd, ph, rng.standard_normal(m), fallback=True)
         ll0 = O.lnlike_white(r, T, b, N_of(x))
         for _ in range(20):
             q = x.copy()
@@ -205,7 +205,7 @@ def _ecorr(seconds, white, aclength=10):
         return [(rng.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]), rng.choice(ind),
                  rng.standard_normal(), rng.random()) for _ in range(aclength)]
     TNT, dd = O.tnt(T, N_of(x), r)
-    st = dict(x=x, b=O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m)))
+    st = dict(x=x, b=O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m), fallback=True))
 
     def step():
         x, b = st["x"], st["b"]
@@ -219,7 +219,7 @@ def _ecorr(seconds, white, aclength=10):
             return O.lnlike_fullmarg(r, N, TNT, dd, 1.0 / ph, np.sum(np.log(ph)))
         x = O.white_mh(x, eind, steps(eind), lnl, prior(eind))
         x[gw] = 0.5 * np.log10(O.rho_analytic(O.tau_half(b, gwid), rng.random(gw.size), 1e-18, 1e-8))
-        st["x"], st["b"] = x, O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m))
+        st["x"], st["b"] = x, O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m), fallback=True)
     what = "white + ECORR" if white else "ECORR"
     return _loop(step, seconds), (f"single-chain {what} sweeps (m={m}, {ne} epochs, {aclength} MH steps per block, "
                                   "oracle restatement of the notebook sampler)")

@@ -33,12 +33,23 @@ def tnt(T, Nvec, r):
 
 
 # ============================================================== b | rho (a1, a5)
-def bdraw_svd(TNT, d, phiinv, z):
+def bdraw_svd(TNT, d, phiinv, z, fallback=False):
     """Reference draw: Sigma = TNT + diag(phiinv); SVD; b = mn + U S^-1/2 z
     (pulsar_gibbs.py:505-518; pta_gibbs.py:533-546).  The LinAlgError QR branch
-    (:511-516) draws with the wrong covariance and is deliberately not restated."""
+    (:511-516) draws with the wrong covariance and is not restated for parity; with
+    fallback=True (the CPU baseline's timing loop only, so a rare LAPACK non-convergence
+    costs what it costs the reference instead of ending the run) it is followed as written:
+    Sigi = R^-1 Q^T, mn = Sigi d, Li = U(Sigi) s(Sigi)^-1/2."""
     Sigma = TNT + np.diag(phiinv)
-    u, s, _ = sl.svd(Sigma)
+    try:
+        u, s, _ = sl.svd(Sigma)
+    except np.linalg.LinAlgError:
+        if not fallback:
+            raise
+        Q, R = sl.qr(Sigma)
+        Sigi = sl.solve(R, Q.T)
+        u, s, _ = sl.svd(Sigi)
+        return np.dot(Sigi, d) + np.dot(u * np.sqrt(1 / s), z)
     mn = np.dot(u, np.dot(u.T, d) / s)
     Li = u * np.sqrt(1 / s)
     return mn + np.dot(Li, z)

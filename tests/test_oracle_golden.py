@@ -445,3 +445,28 @@ def test_ecorr_block_draw_distribution():
         z[j] = 1.0
         G[:, j] = O.bdraw_ecorr(TNT, d, ecid, ph, z[:rc.size], z[rc.size:]) - mean
     assert np.abs(G.T @ Sig @ G - np.eye(m)).max() < 1e-6
+
+
+def test_bdraw_svd_fallback_follows_reference_qr_branch(monkeypatch):
+    """fallback=True (CPU baseline only) takes pulsar_gibbs.py:511-516 when the SVD of Sigma
+    does not converge; the parity path (default) still raises."""
+    import scipy.linalg as sl
+    rng = np.random.default_rng(3)
+    A = rng.standard_normal((8, 8))
+    TNT, d, ph, z = A @ A.T, rng.standard_normal(8), np.full(8, 0.5), rng.standard_normal(8)
+    Sigma = TNT + np.diag(ph)
+    real_svd = sl.svd
+
+    def svd(M, *a, **k):
+        if M is not None and np.array_equal(M, Sigma):
+            raise np.linalg.LinAlgError("SVD did not converge")
+        return real_svd(M, *a, **k)
+
+    monkeypatch.setattr(O.sl, "svd", svd)
+    with pytest.raises(np.linalg.LinAlgError):
+        O.bdraw_svd(TNT, d, ph, z)
+    b = O.bdraw_svd(TNT, d, ph, z, fallback=True)
+    Q, R = np.linalg.qr(Sigma)
+    Sigi = np.linalg.solve(R, Q.T)
+    u, s, _ = real_svd(Sigi)
+    np.testing.assert_allclose(b, Sigi @ d + (u * np.sqrt(1 / s)) @ z, rtol=1e-10)
