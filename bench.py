@@ -111,9 +111,13 @@ def grid_peak():
 
 
 def cpu_line(kind, seconds):
-    """cpu_baseline record: the oracle's loop, one single-thread process per host core."""
+    """cpu_baseline record: the oracle's loop, one single-thread process per host core.  A
+    baseline that cannot run is reported as such rather than discarding the GPU figures."""
     from oracle.cpu_baseline import aggregate
-    return aggregate(kind, seconds)
+    try:
+        return aggregate(kind, seconds)
+    except Exception as exc:  # noqa: BLE001
+        return {"value": None, "unit": "iters/s", "kind": "port", "error": str(exc)[-500:]}
 
 
 def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain"):

@@ -263,15 +263,21 @@ def aggregate(kind, seconds, cores=None):
                PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     procs = [subprocess.Popen([sys.executable, "-m", "oracle.cpu_baseline", kind, str(seconds)], cwd=ROOT, env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for _ in range(cores)]
-    outs = []
+    outs, errs = [], []
     for p in procs:
         o, e = p.communicate(timeout=seconds * 10 + 300)
         if p.returncode != 0:
-            raise RuntimeError(f"cpu baseline {kind} failed: {e[-2000:]}")
+            errs.append(e[-2000:])
+            continue
         outs.append(json.loads(o.strip().splitlines()[-1]))
+    if not outs:
+        raise RuntimeError(f"cpu baseline {kind} failed: {errs[0]}")
+    # a process that died (e.g. a LAPACK error the reference would also have raised) is left
+    # out; the aggregate is the survivors' rate scaled to all cores, and says so
     rates = [o["it"] / o["el"] for o in outs]
-    return dict(value=float(sum(rates)), unit="iters/s", cores=cores, kind="port",
-                per_process=float(sum(rates) / len(rates)), cpu=cpu_model(),
+    extra = {} if not errs else {"failed_processes": len(errs), "error": errs[0].strip().splitlines()[-1][:300]}
+    return dict(value=float(sum(rates) * cores / len(outs)), unit="iters/s", cores=cores, kind="port",
+                per_process=float(sum(rates) / len(rates)), cpu=cpu_model(), **extra,
                 sample=f"{cores} concurrent single-thread processes x {seconds:.0f} s of {outs[0]['what']}; "
                        f"value = sum of their rates (numpy/OpenBLAS, OPENBLAS_NUM_THREADS=1 each)")
 
