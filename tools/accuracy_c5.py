@@ -48,7 +48,16 @@ out = {"numpy_draw_numpy_tnt": normwise_rel(np_draw(TNTn, dn), bx),
 dev = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=ctx.device)
 zz = np.zeros((1, model.ldb)); zz[0, :m] = z
 b, info = model.bdraw(dev(ph[None]), 1, z=dev(zz))
-out["device_draw_device_tnt"] = normwise_rel(b.cpu().numpy()[0, :m], bx)
+bd = b.cpu().numpy()[0, :m]
+out["device_draw_device_tnt"] = normwise_rel(bd, bx)
+fi = np.asarray(d["fidx"]); mi = np.setdiff1d(np.arange(m), fi); sc = np.max(np.abs(bx))
+bn = np_draw(TNTn, dn)
+out["device_F_part"] = float(np.max(np.abs(bd[fi] - bx[fi])) / sc)
+out["device_M_part"] = float(np.max(np.abs(bd[mi] - bx[mi])) / sc)
+out["numpy_F_part"] = float(np.max(np.abs(bn[fi] - bx[fi])) / sc)
+out["numpy_M_part"] = float(np.max(np.abs(bn[mi] - bx[mi])) / sc)
+out["F_rel_own_scale_device"] = float(np.max(np.abs(bd[fi] - bx[fi])) / np.max(np.abs(bx[fi])))
+out["F_rel_own_scale_numpy"] = float(np.max(np.abs(bn[fi] - bx[fi])) / np.max(np.abs(bx[fi])))
 # device draw from the exact (fp64-rounded) TNT: overwrite TNT/d, redo the prefix only
 model.TNT.copy_(torch.as_tensor(TNTx.ravel(), device=ctx.device))
 model.d.copy_(torch.as_tensor(dx, device=ctx.device))
