@@ -34,6 +34,8 @@ HOT = [
     ("k_rho_red_waveE", 4, 0),                     # CURN + red grid CDF
     ("k_rho_curn_fastE", 2, 0),
     ("k_rho_curn_sum_waveE", 2, 0),
+    ("k_white_syrkILi14EE", 2, 0),                 # configs[4] per-chain TNT (m = 216)
+    ("k_tntEPK", 4, 0),                            # TNT / d, compensated block sums
 ]
 
 
