@@ -67,7 +67,7 @@ check(lib.gs_prefix(h, model.P, model.NF, model.NMX, ptr(model.prefix_desc), ptr
 b2, _ = model.bdraw(dev(ph[None]), 1, z=dev(zz))
 out["device_draw_exact_tnt"] = normwise_rel(b2.cpu().numpy()[0, :m], bx)
 print({k: float("%.3g" % v) for k, v in out.items()})
-# mean only (z = 0) and noise only (dF's contribution removed: exact draw with d = 0)
+# mean only (z = 0), the device on the exact TNT (set above); numpy on its own and on the exact TNT
 z0 = np.zeros((1, model.ldb))
 model.TNT.copy_(torch.as_tensor(np.asarray(model.tnt_host(0)[0]).ravel(), device=ctx.device))
 b0, _ = model.bdraw(dev(ph[None]), 1, z=dev(z0))
@@ -80,4 +80,8 @@ zsave = z.copy(); z[:] = 0.0
 bn0 = np_draw(TNTn, dn); z[:] = zsave
 res["numpy_mean_only_F"] = float(np.max(np.abs(bn0[fi] - bx0[fi])) / sc)
 res["numpy_mean_only_M"] = float(np.max(np.abs(bn0[mi] - bx0[mi])) / sc)
+z[:] = 0.0
+bnx = np_draw(TNTx, dx); z[:] = zsave           # numpy on the exact TNT (as the device run above)
+res["numpy_exact_tnt_mean_only_F"] = float(np.max(np.abs(bnx[fi] - bx0[fi])) / sc)
+res["numpy_exact_tnt_mean_only_M"] = float(np.max(np.abs(bnx[mi] - bx0[mi])) / sc)
 print({k: float("%.3g" % v) for k, v in res.items()})
