@@ -392,7 +392,7 @@ int gs_bdraw_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,
  * The ne epoch columns E (ecid) of a basis-ECORR signal have a diagonal TNT block, so the
  * ECORR state enters only through a_e = TNT_ee + 1/phi_e, phi_e = 10**(2 x[c][xcol[ebk[e]]]).
  * R = the other mR columns in increasing order (rcol).  Caller-built, chain-independent:
- *   Bx [ne x ldbx] rows [TNT[e, R] | d_e | 0 ...], ldbx = 16 ceil((mR + 1) / 16) <= 96;
+ *   Bx [ne x ldbx] rows [TNT[e, R] | d_e | 0 ...], ldbx = 16 ceil((mR + 1) / 16) <= 128;
  *   Dg [ne] = TNT_ee;  A [mR x mR] = TNT_RR;  dR [mR] = d_R;  ebk [ne] backend of each epoch;
  *   xcol [n_bk] x column of each backend's log10_ecorr (n_bk <= GS_WHITE_MAX_BK).
  * gs_ecorr_schur: per chain TNT [c][mR x mR] = A - B^T diag(1/a) B, d [c][mR] = dR - B^T (d_E/a),

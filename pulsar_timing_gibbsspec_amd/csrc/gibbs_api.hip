@@ -947,7 +947,7 @@ int gs_ecorr_schur(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const dou
   if (mR <= 0) return fail_arg(3, "mR <= 0");
   if (ne < 0) return fail_arg(4, "ne < 0");
   if (ldbx % 16 || ldbx < mR + 1 || !ecorr_nb_supported(ldbx / 16) || ldbx > 16 * ((mR + 1 + 15) / 16))
-    return fail_arg(5, "ldbx must be 16 ceil((mR + 1) / 16) <= 96");
+    return fail_arg(5, "ldbx must be 16 ceil((mR + 1) / 16) <= 128");
   if (!Bx || !Dg || !ebk) return fail_arg(6, "NULL Bx / Dg / ebk");
   if (n_bk <= 0 || n_bk > GS_WHITE_MAX_BK) return fail_arg(9, "n_bk must be in 1..15");
   if (!xcol || !x || ldx <= 0) return fail_arg(10, "xcol / x / ldx");

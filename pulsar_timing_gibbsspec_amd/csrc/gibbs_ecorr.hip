@@ -45,7 +45,10 @@ __device__ __forceinline__ void ec_phi(double x, double& inv, double& lg) {
 // [B | d_E]^T diag(1/a) [B | d_E]: rows < mR give B^T W B, row mR gives B^T W d_E and
 // (mR, mR) gives sum d_E^2 / a.  Roofline: fp64 MFMA, 2 ne (16 NB)^2 / 2 flop per chain,
 // Bx read once per workgroup from L2.
-template <int NB>
+// NP > 1 (NB >= 7, m_R > 96): the NT accumulator tiles (4 f64 registers each: 36 tiles at
+// NB = 8 would need 288 VGPRs and spilled ~1.8k) are split over NP launches, launch PART
+// keeping tiles t with t % NP == PART; each launch streams Bx again.
+template <int NB, int NP = 1, int PART = 0>
 __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A) {
   extern __shared__ double lds[];
   __shared__ double wb[2][EC_WAVES][EC_CH];
@@ -65,9 +68,10 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
   }
   __syncthreads();
 
-  gs_d4_t acc[NT];
+  constexpr int NTP = (NT - PART + NP - 1) / NP;  // tiles of this part
+  gs_d4_t acc[NTP];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = gs_d4_t{0.0, 0.0, 0.0, 0.0};
+  for (int t = 0; t < NTP; ++t) acc[t] = gs_d4_t{0.0, 0.0, 0.0, 0.0};
   double sla = 0.0, slp = 0.0;
 
   constexpr int LPT = EC_CH * LDB / (64 * EC_WAVES);  // chunk elements per thread
@@ -121,8 +125,10 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
       for (int r = 0; r < NB; ++r) {
         const double av = v[r] * wv;
 #pragma unroll
-        for (int j = 0; j <= r; ++j)
-          acc[r * (r + 1) / 2 + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, v[j], acc[r * (r + 1) / 2 + j], 0, 0, 0);
+        for (int j = 0; j <= r; ++j) {
+          const int t = r * (r + 1) / 2 + j;
+          if (t % NP == PART) acc[t / NP] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, v[j], acc[t / NP], 0, 0, 0);
+        }
       }
     }
     if (ch + 1 < nch) store(cb ^ 1);
@@ -138,7 +144,8 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
   for (int r = 0; r < NB; ++r) {
 #pragma unroll
     for (int j = 0; j <= r; ++j) {
-      const gs_d4_t v4 = acc[r * (r + 1) / 2 + j];
+      if ((r * (r + 1) / 2 + j) % NP != PART) continue;
+      const gs_d4_t v4 = acc[(r * (r + 1) / 2 + j) / NP];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = 16 * r + k + 4 * q, col = 16 * j + i;
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
       }
     }
   }
-  if (l == 0) {
+  if (PART == 0 && l == 0) {
     A.aux[(int64_t)c * 4 + 0] = sla;
     A.aux[(int64_t)c * 4 + 2] = slp;
     A.aux[(int64_t)c * 4 + 3] = 0.0;
@@ -655,16 +662,27 @@ __global__ __launch_bounds__(256) void k_ecorr_bdraw_e(EcorrBArgs A) {
   }
 }
 
-template <int NB>
-void launch_schur_nb(hipStream_t s, const EcorrSchurArgs& a) {
+template <int NB, int NP, int PART>
+void launch_schur_part(hipStream_t s, const EcorrSchurArgs& a) {
   static bool attr = false;
   const size_t lds = (size_t)2 * EC_CH * 16 * NB * sizeof(double);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_ecorr_schur<NB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_ecorr_schur<NB, NP, PART>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL(k_ecorr_schur<NB>, dim3((unsigned)((a.n_chain + EC_WAVES - 1) / EC_WAVES)),
+  hipLaunchKernelGGL((k_ecorr_schur<NB, NP, PART>), dim3((unsigned)((a.n_chain + EC_WAVES - 1) / EC_WAVES)),
                      dim3(64 * EC_WAVES), lds, s, a);
+}
+
+template <int NB>
+void launch_schur_nb(hipStream_t s, const EcorrSchurArgs& a) {
+  if constexpr (NB >= 7) {
+    launch_schur_part<NB, 2, 0>(s, a);
+    launch_schur_part<NB, 2, 1>(s, a);
+  } else {
+    launch_schur_part<NB, 1, 0>(s, a);
+  }
 }
 
 template <int NB, bool LNL, bool PC>
@@ -737,7 +755,7 @@ int launch_ecorr_prefix(hipStream_t s, const EcorrPrefixArgs& a) {
   return 0;
 }
 
-bool ecorr_nb_supported(int nb) { return nb >= 1 && nb <= 6; }  // NB 7, 8 spill
+bool ecorr_nb_supported(int nb) { return nb >= 1 && nb <= 8; }  // NB 7, 8: two tile halves
 
 int launch_ecorr_schur(hipStream_t s, const EcorrSchurArgs& a) {
   switch (a.ldbx / 16) {

@@ -411,3 +411,47 @@ def test_ecorr_bdraw_chain_mask_mixed(ctx):
             assert np.array_equal(B[c], R[c]), c
         else:
             assert np.all(B[c] == sentinel), c
+
+
+@pytest.mark.parametrize("mR", [60, 100, 120])
+def test_ecorr_schur_direct(ctx, mR):
+    """gs_ecorr_schur through the C-ABI on random operands: TNT = A - B^T diag(1/a) B,
+    d = dR - B^T (d_E / a), aux = (sum log a, sum d_E^2 / a, sum log phi_E, 0), against
+    numpy.  mR = 100 / 120 use 7 / 8 tile columns, whose accumulators are split over two
+    launches (one would need ~290 VGPRs)."""
+    import torch
+    from pulsar_timing_gibbsspec_amd._lib import check, ptr
+    rng = np.random.default_rng(mR)
+    C, ne, n_bk = 5, 137, 3
+    ldbx = 16 * ((mR + 16) // 16)
+    Bx = np.zeros((ne, ldbx))
+    Bx[:, :mR + 1] = rng.standard_normal((ne, mR + 1))
+    Dg = rng.uniform(0.5, 2.0, ne)
+    ebk = rng.integers(0, n_bk, ne).astype(np.int32)
+    ldx = 7
+    x = rng.uniform(-1.0, 0.5, (C, ldx))
+    xcol = np.array([1, 3, 6], np.int32)
+    Araw = rng.standard_normal((mR, mR))
+    A = Araw @ Araw.T + mR * np.eye(mR)
+    dR = rng.standard_normal(mR)
+    dev = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=ctx.device)  # noqa: E731
+    g = {k: dev(v) for k, v in dict(Bx=Bx, Dg=Dg, x=x, A=A, dR=dR).items()}
+    g["ebk"], g["xcol"] = dev(ebk, torch.int32), dev(xcol, torch.int32)
+    TNT = torch.empty(C, mR, mR, dtype=torch.float64, device=ctx.device)
+    d = torch.empty(C, mR, dtype=torch.float64, device=ctx.device)
+    aux = torch.empty(C, 4, dtype=torch.float64, device=ctx.device)
+    check(ctx.lib.gs_ecorr_schur(ctx.handle, C, mR, ne, ldbx, ptr(g["Bx"]), ptr(g["Dg"]), ptr(g["ebk"]), n_bk,
+                                 ptr(g["xcol"]), ptr(g["x"]), ldx, ptr(g["A"]), ptr(g["dR"]), ptr(TNT), ptr(d),
+                                 ptr(aux)), "gs_ecorr_schur")
+    TNT, d, aux = TNT.cpu().numpy(), d.cpu().numpy(), aux.cpu().numpy()
+    B, dE = Bx[:, :mR], Bx[:, mR]
+    for c in range(C):
+        ph = 10.0 ** (2.0 * x[c, xcol])
+        a = Dg + 1.0 / ph[ebk]
+        want = A - B.T @ (B / a[:, None])
+        assert np.max(np.abs(TNT[c] - want)) <= 1e-12 * np.max(np.abs(want)), (mR, c)
+        assert np.array_equal(TNT[c], TNT[c].T)
+        assert normwise_rel(d[c], dR - B.T @ (dE / a)) < 1e-12
+        np.testing.assert_allclose(aux[c, :3], [np.sum(np.log(a)), np.sum(dE ** 2 / a), np.sum(np.log(ph[ebk]))],
+                                   rtol=1e-12)
+        assert aux[c, 3] == 0.0
