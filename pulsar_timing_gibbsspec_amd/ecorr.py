@@ -57,8 +57,8 @@ class EcorrModel:
         rc = np.setdiff1d(np.arange(m), ecid)
         self.mR = mR = rc.size
         self.ldbx = 16 * ((mR + 2 + 14) // 16)
-        if self.ldbx > 96:
-            raise NotImplementedError(f"ECORR Schur kernel supports mR <= 95 (got {mR})")
+        if self.ldbx > 128:
+            raise NotImplementedError(f"ECORR Schur kernel supports mR <= 127 (got {mR})")
         pos = {c: i for i, c in enumerate(rc)}
         fR = np.array([pos[c] for c in gwid], np.int32)
         mR_idx = np.array([i for i, c in enumerate(rc) if c not in set(gwid.tolist())], np.int32)

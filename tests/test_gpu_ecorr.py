@@ -455,3 +455,27 @@ def test_ecorr_schur_direct(ctx, mR):
         np.testing.assert_allclose(aux[c, :3], [np.sum(np.log(a)), np.sum(dE ** 2 / a), np.sum(np.log(ph[ebk]))],
                                    rtol=1e-12)
         assert aux[c, 3] == 0.0
+
+
+@pytest.mark.parametrize("n_tm", [40, 56])
+def test_ecorr_lnlike_wide_timing_model(ctx, n_tm):
+    """PulsarBlockGibbs.get_lnlikelihood on ECORR models whose R block (60 free-spectrum + n_tm
+    timing-model columns, m_R = 100 / 116) needs 7 / 8 Schur tile columns (the split launches):
+    against the oracle's get_lnlikelihood_fullmarg restatement (pulsar_gibbs.py:569-610)."""
+    from pulsar_timing_gibbsspec_amd import synthetic
+    from pulsar_timing_gibbsspec_amd.pulsar_gibbs import PulsarBlockGibbs
+    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=2, n_tm=n_tm)
+    gb = PulsarBlockGibbs(pta, nchains=4, seed=3)
+    T, r = pta.get_basis()[0], pta.get_residuals()[0]
+    rng = np.random.default_rng(n_tm)
+    for _ in range(3):
+        x = np.concatenate([p.sample().flatten() for p in gb.params])
+        x[gb.get_ecorr_indices()] = rng.uniform(-8.0, -5.5, len(gb.get_ecorr_indices()))
+        params = gb.map_params(x)
+        N = pta.get_ndiag(params)[0]
+        phiinv, logdet = pta.get_phiinv(params, logdet=True)[0]
+        TNT, d = O.tnt(T, N, r)
+        ref = O.lnlike_fullmarg(r, N, TNT, d, phiinv, logdet)
+        got = gb.get_lnlikelihood(x)
+        assert gb._em1.mR == 60 + n_tm and not gb._em1.fused
+        assert abs(got - ref) < 1e-7 * max(1.0, abs(ref)), (n_tm, got, ref)
