@@ -181,6 +181,7 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain"):
     bflop = C * float(np.sum(mm ** 3 / 3 + mm ** 2 / 2 + mm / 6 + 3 * mm ** 2))
     kernels = {"k_bdraw": dict(kernel_avg_ms=ms_b, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
                                achieved=bflop / (ms_b * 1e-3) / 1e12, alg_per_launch=bflop,
+                               traffic=(_ecorr_traffic(m.P * C, "pmc_traffic_curn.json") if kind == "curn" else None),
                                note="b|rho of every (pulsar, chain) system: sum_p m^3/3 + m^2/2 + m/6 + 3 m^2 "
                                     "flop per chain (SURVEY 8d)")}
     gp = grid_peak()

@@ -1,0 +1,15 @@
+#!/bin/bash
+# PMC traffic (FETCH_SIZE, WRITE_SIZE in separate passes) of k_bdraw in the configs[3] CURN
+# line (45 pulsars x 2048 chains = 92160 systems, one wavefront each: grid 92160 x 64).
+set -u
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/pmc_curn
+mkdir -p $OUT
+export OPENBLAS_NUM_THREADS=1
+ARGS="--no-cpu-baseline --pta curn --indep 0 --ecorr 0 --config5 0 --host-stream 0 --steps 10 --warmup 2 --pta-steps 5"
+cd /tmp && export TMPDIR=/tmp
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $R/bench.py $ARGS > $OUT/fetch.log 2>&1; rc=$?
+echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $R/bench.py $ARGS > $OUT/write.log 2>&1; rc=$?
+echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
+cd $R && SWEEPS=1 CHAINS=92160 HEAD_LAUNCHES=6 python tools/pmc_traffic.py $OUT "k_bdraw<60" $OUT/pmc_traffic_curn.json
