@@ -235,3 +235,42 @@ def test_history_straight_to_pinned_host(model, replay):
     assert torch.equal(xh, xa.cpu())
     assert torch.equal(bh, ba.cpu()[:, :K])
     assert torch.equal(rb.b, ra.b)
+
+
+def test_capi_edge_cases_and_errors():
+    """The C-ABI's empty batches and argument errors (include/pulsar_gibbs.h: 0 ok, positive =
+    1-based index of the offending argument, gs_last_error has the message): an empty chain
+    batch launches nothing and leaves b untouched; bad NF / ldb / NULL arrays / NULL ctx are
+    reported, not launched."""
+    import ctypes as C
+    import torch
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd._lib import ptr
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel
+    ctx = _lib.Context(0, seed=5)
+    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0)
+    T, N, r = pta.get_basis()[0], pta.get_ndiag({})[0], pta.get_residuals()[0]
+    model = DeviceModel(ctx, [T], [N], [r], [np.arange(60)], [np.full(T.shape[1] - 60, 1e-40)])
+    lib, h = ctx.lib, ctx.handle
+    ph = torch.ones(2, 60, dtype=torch.float64, device=ctx.device)
+    b = torch.full((2, model.ldb), 7.0, dtype=torch.float64, device=ctx.device)
+    info = torch.zeros(2, dtype=torch.int32, device=ctx.device)
+
+    def call(handle=h, n_chain=2, NF=60, ldb=model.ldb, phv=ph, out=b):
+        return lib.gs_bdraw(handle, 1, n_chain, NF, model.NMX, ldb, ptr(model.model), ptr(model.fidx),
+                            ptr(model.midx), ptr(model.nm_dev), ptr(phv) if phv is not None else None, None, 0,
+                            _lib.EV_B, 0, None, ptr(out), ptr(info))
+
+    assert call(n_chain=0) == 0
+    torch.cuda.synchronize()
+    assert bool((b == 7.0).all())
+    assert call(NF=61) == 4 and b"NF" in lib.gs_last_error()
+    assert call(ldb=60) == 6
+    assert call(phv=None) == 7
+    assert call(handle=C.c_void_p(0)) == 1
+    assert call(n_chain=-1) == 2
+    torch.cuda.synchronize()
+    assert bool((b == 7.0).all())
+    assert call() == 0 and not info.cpu().numpy().any()
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(b).all()) and not bool((b[:, :model.m[0]] == 7.0).any())
