@@ -3,8 +3,12 @@
 Workload (BASELINE.json configs[1]): the simulated J1713+0747 pulsar (720 TOAs,
 30-bin free spectrum + 16-column timing model, m = 76, fixed white noise),
 ``--chains`` independent chains per GPU (default 4096), batched on each MI355X.
-A "step" = one Gibbs sweep of every chain (rho|b then b|rho, with the chain
-rows recorded to HBM as PulsarBlockGibbs.sample records them).
+A "step" = one fused launch of ``--sweeps-per-launch`` (100) Gibbs sweeps of every
+chain (rho|b then b|rho, each sweep's chain rows recorded to HBM as
+PulsarBlockGibbs.sample records them; 100 = the reference's save cadence,
+pulsar_gibbs.py:701-710).  ``value`` counts chain-sweeps: chains x steps x 100 / time.
+ESS/s = value x (ESS per chain-sweep of the worst bin), the ESS fraction from a
+separate untimed 2000-sweep run (``--ess-sweeps``).
 
 N GPUs: one process per GPU (torch.distributed.run), chains sharded by rank
 (chain_base = rank * chains, disjoint Philox streams), no data-path collective
@@ -56,6 +60,16 @@ def pmc_traffic(S, C):
     if d.get("sweeps_per_launch") != S or d.get("chains") != C or "bytes_per_launch" not in d:
         return None
     return d["bytes_per_launch"]
+
+
+def ess_fraction(x_rec, max_chains=256):
+    """Min over the bins of the ESS per chain-sweep of log10 rho (mean over up to ``max_chains``
+    chains of 1 / IAT on the post-burn-in rows, first 20 % dropped)."""
+    from pulsar_timing_gibbsspec_amd.diagnostics import iat
+    xr = x_rec[:, :max_chains]                      # (K, C, n_f)
+    K, C, nf = xr.shape
+    burn = K // 5
+    return float(min(np.mean([1.0 / max(iat(xr[burn:, c, k]), 1.0) for c in range(C)]) for k in range(nf)))
 
 
 def ess_min_bin(x_rec, elapsed, n_chains_total, max_chains=256):
@@ -536,8 +550,9 @@ def launch_ranks(args_list, n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=20, help="headline steps = fused 100-sweep launches")
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--ess-sweeps", type=int, default=2000, help="untimed sweeps of the ESS estimate")
     ap.add_argument("--chains", type=int, default=4096, help="chains per GPU")
     ap.add_argument("--sweeps-per-launch", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -609,43 +624,46 @@ def main():
     run = FreeSpectrumChains(model, 1e-18, 1e-8, C, x0, chain_base=rank * C)
     K, W, S = args.steps, args.warmup, max(1, args.sweeps_per_launch)
     m = int(model.m[0])
-    x_rec = torch.empty(K, C, 30, dtype=torch.float64, device=dev)
-    b_rec = torch.empty(K, C, model.ldb, dtype=torch.float64, device=dev)
+    # one launch's history block in HBM, rewritten by every launch (the rows a save block holds)
+    x_rec = torch.empty(S, C, 30, dtype=torch.float64, device=dev)
+    b_rec = torch.empty(S, C, model.ldb, dtype=torch.float64, device=dev)
 
-    done = 0
-    while done < W:                                   # warmup (untimed)
-        n = min(S, W - done)
-        run.run(n, x_rec=x_rec[:n], b_rec=b_rec[:n])
-        done += n
+    for _ in range(W):                                # warmup (untimed)
+        run.run(S, x_rec=x_rec, b_rec=b_rec)
     stream = ctx.stream
     evs = []
 
     def headline():
-        done = 0
-        while done < K:
-            n = min(S, K - done)
+        for _ in range(K):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            run.run(n, x_rec=x_rec[done:done + n], b_rec=b_rec[done:done + n])
+            run.run(S, x_rec=x_rec, b_rec=b_rec)
             e1.record(stream)
-            evs.append((e0, e1, n))
-            done += n
+            evs.append((e0, e1))
     el = timed_region(world, dev, headline)
     info = run.info.cpu().numpy()
     if info.any():
         raise RuntimeError(f"{int((info != 0).sum())} chains hit a non-PD Sigma")
 
     total_chains = C * world
-    value = total_chains * K / el
-    # roofline of the fused sweep kernel (dominant kernel: one launch per S sweeps)
-    kern_ms = np.array([a.elapsed_time(b) for a, b, _ in evs])
-    sweeps = np.array([n for _, _, n in evs])
-    per_sweep_s = float(np.sum(kern_ms) / 1e3 / np.sum(sweeps))
+    value = total_chains * K * S / el
+    # roofline of the fused sweep kernel (dominant kernel: one launch per step of S sweeps)
+    kern_ms = np.array([a.elapsed_time(b) for a, b in evs])
+    launch_s = float(np.mean(kern_ms)) / 1e3
     alg_flops_launch = flops_per_chain_sweep(m) * C * S
-    launch_s = per_sweep_s * S
     achieved = alg_flops_launch / launch_s / 1e12
     exe = executed_flops_per_chain_sweep(model.NF, int(model.nm[0])) * C * S / launch_s / 1e12
-    ess = ess_min_bin(x_rec.cpu().numpy(), el, total_chains)
+    # ESS per chain-sweep from a separate untimed run of 256 chains (same kernel, same law)
+    ce = min(C, 256)
+    ess_run = FreeSpectrumChains(model, 1e-18, 1e-8, ce, x0[:ce], chain_base=rank * C)
+    xe = torch.empty(args.ess_sweeps, ce, 30, dtype=torch.float64, device=dev)
+    for i in range(0, args.ess_sweeps, S):
+        n = min(S, args.ess_sweeps - i)
+        ess_run.run(n, record_b=False, x_rec=xe[i:i + n])
+    ess_frac = ess_fraction(xe.cpu().numpy())
+    ess = value * ess_frac
+    del xe, ess_run
+    K_sweeps = K * S
 
     host = None
     if args.host_stream:
@@ -658,8 +676,8 @@ def main():
 
             def go():
                 done, slot, pending = 0, 0, None
-                while done < K:
-                    n = min(S, K - done)
+                while done < K_sweeps:
+                    n = min(S, K_sweeps - done)
                     xr, br = streamer.buffers(slot, n)
                     run.run(n, x_rec=xr, b_rec=br, record_b_chains=bk)
                     streamer.submit(slot, n)
@@ -669,10 +687,11 @@ def main():
                 if pending is not None:
                     streamer.fetch(pending)
             el_h = timed_region(world, dev, go)
-            return total_chains * K / el_h, el_h / K * 1e3
+            return total_chains * K_sweeps / el_h, el_h / K * 1e3
         v0, ms0 = streamed_rate(1, [True, True])
         v1, ms1 = streamed_rate(C, [True, False])
-        host = {"value": v0, "unit": "chain-iters/s", "ms_per_step": ms0, "bytes_per_step": C * 30 * 8 + model.ldb * 8,
+        host = {"value": v0, "unit": "chain-iters/s", "ms_per_step": ms0,
+                "bytes_per_step": S * (C * 30 * 8 + model.ldb * 8),
                 "note": "sample()'s default: the kernel writes x of every chain and b of chain 0 (the reference's "
                         "bchain, GS_OPT_BREC_CHAINS = 1) straight into pinned host memory (zero-copy over PCIe), "
                         "read while the next block runs (engine.HistoryStreamer)",
@@ -689,9 +708,13 @@ def main():
             "config": {"workload": "configs[1]: J1713+0747 sim (720 TOAs, m=76, 30-bin free spectrum), "
                                    f"{C} independent chains per GPU", "chains_per_gpu": C,
                        "global_chains": total_chains, "m": m, "n_f": 30,
-                       "sweeps_per_launch": S, "bcast": ctx.get_option(_lib.OPT_BCAST),
+                       "step": f"one fused launch of {S} sweeps of every chain", "sweeps_per_step": S,
+                       "bcast": ctx.get_option(_lib.OPT_BCAST),
                        "parallelism": f"chains sharded over {world} GPU(s), no collective"},
             "ess_per_s": ess,
+            "ess": {"per_chain_sweep_min_bin": ess_frac, "sweeps": args.ess_sweeps, "chains": ce,
+                    "note": "ess_per_s = value x the worst bin's mean ESS per chain-sweep (1/IAT, first 20 % "
+                            "dropped) from a separate untimed run"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
                          "traffic": pmc_traffic(S, C),

@@ -127,6 +127,15 @@ int gs_sweep_lds_bytes(int NF, int NMX);
  */
 int gs_tnt(gs_ctx* ctx, int n_psr, int m_max, const gs_tnt_desc* desc,
            const double* T, const double* Nvec, const double* r, double* TNT, double* d);
+/*
+ * Same in double-double: TNT + TNT_lo and d + d_lo equal T^T N^-1 T and T^T N^-1 r of the
+ * fp64 inputs to ~1e-30 relative (exact products, compensated sums; TNT exactly symmetric).
+ * TNT_lo / d_lo may be NULL.  Feed the pairs to gs_prefix_dd: the fp64 rounding of TNT is,
+ * relative to the Schur block the draw factorises, a perturbation of up to ~1e-9 at 10^4
+ * TOAs.  VALU work; once per noise state.
+ */
+int gs_tnt_dd(gs_ctx* ctx, int n_psr, int m_max, const gs_tnt_desc* desc, const double* T,
+              const double* Nvec, const double* r, double* TNT, double* TNT_lo, double* d, double* d_lo);
 
 /*
  * Fixed-prior prefix of the Cholesky of Sigma = TNT + diag(phiinv), with the
@@ -142,6 +151,8 @@ int gs_tnt(gs_ctx* ctx, int n_psr, int m_max, const gs_tnt_desc* desc,
  * fidx: [n_psr x NF] column index of each free-spectrum column (gwid);
  * midx: [n_psr x NMX] column index of each fixed-prior column;
  * phiinv_fixed: [n_psr x NMX] their (constant) phiinv (1e-40 for the TM).
+ * L_M, W = L_M^-1 A_MF, e, S0 and dF are computed in double-double (the fp64 Schur
+ * complement cancels 2-3 digits) and rounded; G, h, R in fp64.
  */
 int gs_prefix(gs_ctx* ctx, int n_psr, int NF, int NMX, const gs_prefix_desc* desc,
               const double* TNT, const double* d, const int32_t* fidx, const int32_t* midx,
@@ -376,6 +387,15 @@ int gs_prefix_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const gs
                   int64_t tnt_cstride, int64_t d_cstride, const double* TNT, const double* d,
                   const int32_t* fidx, const int32_t* midx, const double* phiinv_fixed,
                   double* model, int32_t* info);
+
+/*
+ * gs_prefix_sys from a double-double TNT / d (gs_tnt_dd): TNT_lo, d_lo at the same offsets and
+ * strides as TNT, d, or NULL (= gs_prefix_sys).  TNT full (symmetric), as for gs_prefix.
+ */
+int gs_prefix_dd(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const gs_prefix_desc* desc,
+                 int64_t tnt_cstride, int64_t d_cstride, const double* TNT, const double* TNT_lo,
+                 const double* d, const double* d_lo, const int32_t* fidx, const int32_t* midx,
+                 const double* phiinv_fixed, double* model, int32_t* info);
 
 /* gs_bdraw with one model block per system (model + sys * gs_model_stride). */
 int gs_bdraw_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,

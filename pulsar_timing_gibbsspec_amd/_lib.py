@@ -63,6 +63,8 @@ SIGNATURES = {
     "gs_pta_record": (_I, [_P, _I, _I, _P, _P, _P]),
     "gs_pta_gate_phiinv": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "gs_prefix_sys": (_I, [_P, _I, _I, _I, _I, _P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P]),
+    "gs_tnt_dd": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "gs_prefix_dd": (_I, [_P, _I, _I, _I, _I, _P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "gs_bdraw_sys": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _I, _I64, _P, _P, _P]),
     "gs_white_resid": (_I, [_P, _I, _I, _I64, _I, _P, _P, _P, _P, _I64, _P]),
     "gs_white_mh": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _I, _I, _P, _I64, _I64,

@@ -37,6 +37,20 @@ int check_hip(hipError_t e, const char* where) {
 
 int after_launch(const char* where) { return check_hip(hipGetLastError(), where); }
 
+// grow the context workspace (large-NF b-draw tiles, prefix scratch) to `need` bytes
+int ensure_ws(gs_ctx* ctx, size_t need) {
+  if (need <= ctx->ws_bytes) return 0;
+  int rc = check_hip(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+  if (rc) return rc;
+  if (ctx->ws) (void)hipFree(ctx->ws);
+  ctx->ws = nullptr;
+  ctx->ws_bytes = 0;
+  rc = check_hip(hipMalloc((void**)&ctx->ws, need), "hipMalloc(context workspace)");
+  if (rc) return rc;
+  ctx->ws_bytes = need;
+  return 0;
+}
+
 gs_key key_of(const gs_ctx* c) {
   gs_key k;
   k.k0 = (uint32_t)(c->seed & 0xffffffffu);
@@ -145,256 +159,6 @@ __global__ __launch_bounds__(256) void k_tnr(const gs_tnt_desc* desc, const doub
       e += red[1][u][l];
     }
     d[D.d_off + j] = h + e;
-  }
-}
-
-// ------------------------------------------------------------------ prefix, wide timing model
-// The same outputs as k_prefix for 64 < NMX <= GS_NMX_WIDE (real timing models with many DMX
-// columns): only L_M (NMX x NMX) lives in LDS (128 KB at NMX = 128).  W = L_M^-1 [A_MF | d_M]
-// is built column by column in the output's G region (each column by one thread: same-thread
-// reads after writes), S0 / dF / |e|^2 read it after an agent-scope fence + barrier, R = L_M^-T
-// goes straight to the output's R region (one column per thread), and G = R W overwrites W in
-// place top-down per column (row mm needs only rows >= mm of W).
-__global__ __launch_bounds__(256) void k_prefix_wide(const gs_prefix_desc* desc, int NF, int NMX,
-                                                     const double* TNT, const double* d,
-                                                     const int32_t* fidx, const int32_t* midx,
-                                                     const double* phfix, double* model, int64_t mstride,
-                                                     int32_t* info, int n_chain, int64_t tnt_cstride,
-                                                     int64_t d_cstride) {
-  extern __shared__ double sm[];
-  const int sys = blockIdx.x;
-  const int p = sys / n_chain, c = sys % n_chain;
-  const gs_prefix_desc D = desc[p];
-  const int m = (int)D.m, nM = (int)D.n_fixed;
-  const double* A = TNT + D.tnt_off + (int64_t)c * tnt_cstride;
-  const double* dv = d + D.d_off + (int64_t)c * d_cstride;
-  const int32_t* Fi = fidx + (int64_t)p * NF;
-  const int32_t* Mi = midx + (int64_t)p * NMX;
-  double* L = sm;  // NMX x NMX
-  __shared__ int s_fail;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int ldw = NF + 1;
-  double* out = model + (int64_t)sys * mstride;
-  double* S0 = out;
-  double* dF = S0 + NF * (NF + 1);
-  double* G = dF + NF;  // holds W first
-  double* h = G + NMX * (NF + 1);
-  double* R = h + NMX;
-  if (tid == 0) s_fail = 0;
-  for (int q = tid; q < NMX * NMX; q += nt) {
-    const int i = q / NMX, j = q % NMX;
-    double v = 0.0;
-    if (i < nM && j < nM) {
-      v = A[(int64_t)Mi[i] * m + Mi[j]];
-      if (i == j) v += phfix[(int64_t)p * NMX + i];
-    }
-    L[q] = v;
-  }
-  __syncthreads();
-  for (int k = 0; k < nM; ++k) {
-    if (tid == 0) {
-      const double piv = L[k * NMX + k];
-      if (!(piv > 0.0) && s_fail == 0) s_fail = k + 1;
-      L[k * NMX + k] = sqrt(piv);
-    }
-    __syncthreads();
-    const double lkk = L[k * NMX + k];
-    for (int i = k + 1 + tid; i < nM; i += nt) L[i * NMX + k] /= lkk;
-    __syncthreads();
-    const int len = nM - k - 1;
-    for (int q = tid; q < len * len; q += nt) {
-      const int i = k + 1 + q / len, j = k + 1 + q % len;
-      if (j <= i) L[i * NMX + j] -= L[i * NMX + k] * L[j * NMX + k];
-    }
-    __syncthreads();
-  }
-  // W (in G's region): column f by thread f; column NF is e = L_M^-1 d_M
-  for (int f = tid; f <= NF; f += nt) {
-    for (int i = 0; i < NMX; ++i) {
-      double s = 0.0;
-      if (i < nM) {
-        s = (f < NF) ? A[(int64_t)Mi[i] * m + Fi[f]] : dv[Mi[i]];
-        for (int j = 0; j < i; ++j) s -= L[i * NMX + j] * G[j * ldw + f];
-        s /= L[i * NMX + i];
-      }
-      G[i * ldw + f] = s;
-    }
-  }
-  // R = L_M^-T: column j by thread j
-  for (int j = tid; j < NMX; j += nt) {
-    for (int i = NMX - 1; i >= 0; --i) {
-      double s = 0.0;
-      if (i < nM && j < nM) {
-        s = (i == j) ? 1.0 : 0.0;
-        for (int q = i + 1; q < nM; ++q) s -= L[q * NMX + i] * R[q * NMX + j];
-        s /= L[i * NMX + i];
-      }
-      R[i * NMX + j] = s;
-    }
-  }
-  __threadfence();  // W and R columns written by other threads are read below
-  __syncthreads();
-  for (int q = tid; q < NF * (NF + 1); q += nt) {
-    const int f = q / (NF + 1), g = q % (NF + 1);
-    double s = (g < NF) ? A[(int64_t)Fi[f] * m + Fi[g]] : dv[Fi[f]];
-    for (int i = 0; i < nM; ++i) s -= G[i * ldw + f] * G[i * ldw + g];
-    S0[q] = s;
-  }
-  for (int f = tid; f < NF; f += nt) {
-    double s = dv[Fi[f]];
-    for (int i = 0; i < nM; ++i) s -= G[i * ldw + f] * G[i * ldw + NF];
-    dF[f] = s;
-  }
-  const int64_t ao = (int64_t)NF * (NF + 1) + NF + NMX * (NF + 1) + NMX + NMX * NMX;
-  if (tid == 0) {
-    double lm = 0.0, ee = 0.0;
-    for (int i = 0; i < nM; ++i) {
-      lm += log(L[i * NMX + i]);
-      ee += G[i * ldw + NF] * G[i * ldw + NF];
-    }
-    out[ao] = lm;
-    out[ao + 1] = ee;
-    if (info) info[sys] = s_fail;
-  }
-  __threadfence();
-  __syncthreads();
-  // G = R W in place (column f by thread f, rows top-down); column NF -> h, then G[:, NF] = 0
-  for (int f = tid; f <= NF; f += nt) {
-    for (int mm = 0; mm < NMX; ++mm) {
-      double s = 0.0;
-      for (int j = mm; j < nM; ++j) s += R[mm * NMX + j] * G[j * ldw + f];
-      if (f < NF)
-        G[mm * ldw + f] = s;
-      else
-        h[mm] = s;
-    }
-    if (f == NF)
-      for (int mm = 0; mm < NMX; ++mm) G[mm * ldw + NF] = 0.0;
-  }
-  for (int64_t q = ao + 2 + tid; q < mstride; q += nt) out[q] = 0.0;
-}
-
-// ------------------------------------------------------------------ prefix
-// One workgroup per pulsar; see include/pulsar_gibbs.h gs_prefix for the outputs.
-// Per-chain systems (white-noise runs): block sys = p * n_chain + c reads its TNT/d at
-// the pulsar's offsets + c * (tnt_cstride, d_cstride) and writes model block sys.
-__global__ __launch_bounds__(256) void k_prefix(const gs_prefix_desc* desc, int NF, int NMX,
-                                                const double* TNT, const double* d,
-                                                const int32_t* fidx, const int32_t* midx,
-                                                const double* phfix, double* model, int64_t mstride,
-                                                int32_t* info, int n_chain, int64_t tnt_cstride,
-                                                int64_t d_cstride) {
-  extern __shared__ double sm[];
-  const int sys = blockIdx.x;
-  const int p = sys / n_chain, c = sys % n_chain;
-  const gs_prefix_desc D = desc[p];
-  const int m = (int)D.m, nM = (int)D.n_fixed;
-  const double* A = TNT + D.tnt_off + (int64_t)c * tnt_cstride;
-  const double* dv = d + D.d_off + (int64_t)c * d_cstride;
-  const int32_t* Fi = fidx + (int64_t)p * NF;
-  const int32_t* Mi = midx + (int64_t)p * NMX;
-  double* L = sm;                  // NMX x NMX
-  double* W = L + NMX * NMX;       // NMX x (NF+1): column NF holds e = L^-1 d_M
-  double* Rm = W + NMX * (NF + 1); // NMX x NMX
-  __shared__ int s_fail;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int ldw = NF + 1;
-  if (tid == 0) s_fail = 0;
-  for (int q = tid; q < NMX * NMX; q += nt) {
-    const int i = q / NMX, j = q % NMX;
-    double v = 0.0;
-    if (i < nM && j < nM) {
-      v = A[(int64_t)Mi[i] * m + Mi[j]];
-      if (i == j) v += phfix[(int64_t)p * NMX + i];
-    }
-    L[q] = v;
-  }
-  __syncthreads();
-  // right-looking Cholesky of A_MM in LDS
-  for (int k = 0; k < nM; ++k) {
-    if (tid == 0) {
-      const double piv = L[k * NMX + k];
-      if (!(piv > 0.0) && s_fail == 0) s_fail = k + 1;
-      L[k * NMX + k] = sqrt(piv);
-    }
-    __syncthreads();
-    const double lkk = L[k * NMX + k];
-    for (int i = k + 1 + tid; i < nM; i += nt) L[i * NMX + k] /= lkk;
-    __syncthreads();
-    const int len = nM - k - 1;
-    for (int q = tid; q < len * len; q += nt) {
-      const int i = k + 1 + q / len, j = k + 1 + q % len;
-      if (j <= i) L[i * NMX + j] -= L[i * NMX + k] * L[j * NMX + k];
-    }
-    __syncthreads();
-  }
-  // W = L_M^-1 A_MF (columns 0..NF-1) and e = L_M^-1 d_M (column NF)
-  for (int f = tid; f <= NF; f += nt) {
-    for (int i = 0; i < nM; ++i) {
-      double s = (f < NF) ? A[(int64_t)Mi[i] * m + Fi[f]] : dv[Mi[i]];
-      for (int j = 0; j < i; ++j) s -= L[i * NMX + j] * W[j * ldw + f];
-      W[i * ldw + f] = s / L[i * NMX + i];
-    }
-  }
-  // R = L_M^-T (upper), column by column
-  for (int j = tid; j < NMX; j += nt) {
-    for (int i = NMX - 1; i >= 0; --i) {
-      double s = 0.0;
-      if (i < nM && j < nM) {
-        s = (i == j) ? 1.0 : 0.0;
-        for (int q = i + 1; q < nM; ++q) s -= L[q * NMX + i] * Rm[q * NMX + j];
-        s /= L[i * NMX + i];
-      }
-      Rm[i * NMX + j] = s;
-    }
-  }
-  __syncthreads();
-  double* out = model + (int64_t)sys * mstride;
-  double* S0 = out;
-  double* dF = S0 + NF * (NF + 1);
-  double* G = dF + NF;
-  double* h = G + NMX * (NF + 1);
-  double* R = h + NMX;
-  for (int q = tid; q < NF * (NF + 1); q += nt) {
-    const int f = q / (NF + 1), g = q % (NF + 1);
-    // column NF (padding of the odd row stride) carries dF[f]: the tile b-draw
-    // factorises the system augmented by dF (gibbs_tile.h)
-    double s = (g < NF) ? A[(int64_t)Fi[f] * m + Fi[g]] : dv[Fi[f]];
-    for (int i = 0; i < nM; ++i) s -= W[i * ldw + f] * W[i * ldw + g];
-    S0[q] = s;
-  }
-  for (int f = tid; f < NF; f += nt) {
-    double s = dv[Fi[f]];
-    for (int i = 0; i < nM; ++i) s -= W[i * ldw + f] * W[i * ldw + NF];
-    dF[f] = s;
-  }
-  for (int q = tid; q < NMX * (NF + 1); q += nt) {
-    const int mm = q / (NF + 1), f = q % (NF + 1);
-    double s = 0.0;
-    if (f < NF)
-      for (int j = mm; j < nM; ++j) s += Rm[mm * NMX + j] * W[j * ldw + f];
-    G[q] = s;
-  }
-  for (int mm = tid; mm < NMX; mm += nt) {
-    double s = 0.0;
-    for (int j = mm; j < nM; ++j) s += Rm[mm * NMX + j] * W[j * ldw + NF];
-    h[mm] = s;
-  }
-  for (int q = tid; q < NMX * NMX; q += nt) R[q] = Rm[q];
-  for (int64_t q = (int64_t)NF * (NF + 1) + NF + NMX * (NF + 1) + NMX + NMX * NMX + tid; q < mstride; q += nt)
-    out[q] = 0.0;
-  __syncthreads();
-  if (tid == 0) {
-    // aux for the marginalised likelihood: sum log diag L_M and |e|^2, e = L_M^-1 d_M
-    double lm = 0.0, ee = 0.0;
-    for (int i = 0; i < nM; ++i) {
-      lm += log(L[i * NMX + i]);
-      ee += W[i * ldw + NF] * W[i * ldw + NF];
-    }
-    const int64_t ao = (int64_t)NF * (NF + 1) + NF + NMX * (NF + 1) + NMX + NMX * NMX;
-    out[ao] = lm;
-    out[ao + 1] = ee;
-    if (info) info[sys] = s_fail;
   }
 }
 
@@ -534,10 +298,21 @@ int gs_tnt(gs_ctx* ctx, int n_psr, int m_max, const gs_tnt_desc* desc, const dou
   return 0;
 }
 
-int gs_prefix_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const gs_prefix_desc* desc,
-                  int64_t tnt_cstride, int64_t d_cstride, const double* TNT, const double* d,
-                  const int32_t* fidx, const int32_t* midx, const double* phiinv_fixed,
-                  double* model, int32_t* info) {
+int gs_tnt_dd(gs_ctx* ctx, int n_psr, int m_max, const gs_tnt_desc* desc, const double* T, const double* Nvec,
+              const double* r, double* TNT, double* TNT_lo, double* d, double* d_lo) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0) return fail_arg(2, "n_psr < 0");
+  if (m_max <= 0 || m_max > 4096) return fail_arg(3, "m_max out of range");
+  if (!desc) return fail_arg(4, "desc is NULL");
+  if (!T || !Nvec || !r) return fail_arg(5, "T/Nvec/r is NULL");
+  if (n_psr == 0) return 0;
+  return check_hip(launch_tnt_dd(ctx->stream, n_psr, m_max, desc, T, Nvec, r, TNT, TNT_lo, d, d_lo), "k_tnt_dd");
+}
+
+int gs_prefix_dd(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const gs_prefix_desc* desc,
+                 int64_t tnt_cstride, int64_t d_cstride, const double* TNT, const double* TNT_lo, const double* d,
+                 const double* d_lo, const int32_t* fidx, const int32_t* midx, const double* phiinv_fixed,
+                 double* model, int32_t* info) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_psr < 0) return fail_arg(2, "n_psr < 0");
   if (n_chain < 0) return fail_arg(3, "n_chain < 0");
@@ -548,25 +323,29 @@ int gs_prefix_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const gs
   if (d_cstride < 0) return fail_arg(8, "d_cstride < 0");
   if (!TNT || !d || !fidx || !midx || !phiinv_fixed || !model) return fail_arg(9, "NULL array");
   if (n_psr == 0 || n_chain == 0) return 0;
-  if (NMX > 64) {
-    const size_t lds = (size_t)NMX * NMX * sizeof(double);
-    int rc = check_hip(hipFuncSetAttribute((const void*)k_prefix_wide, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds), "hipFuncSetAttribute(k_prefix_wide)");
+  PrefixArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX;
+  a.tnt_cstride = tnt_cstride; a.d_cstride = d_cstride; a.mstride = model_stride_doubles(NF, NMX);
+  a.desc = desc; a.TNT = TNT; a.TNT_lo = TNT_lo; a.d = d; a.d_lo = d_lo; a.phfix = phiinv_fixed;
+  a.fidx = fidx; a.midx = midx; a.model = model; a.info = info;
+  a.gscr = nullptr;
+  a.gstride = prefix_scratch_doubles(NF, NMX);
+  if (!prefix_scratch_in_lds(NF, NMX)) {
+    const int rc = ensure_ws(ctx, (size_t)n_psr * n_chain * a.gstride * sizeof(double));
     if (rc) return rc;
-    hipLaunchKernelGGL(k_prefix_wide, dim3(n_psr * n_chain), dim3(256), lds, ctx->stream, desc, NF, NMX, TNT, d,
-                       fidx, midx, phiinv_fixed, model, model_stride_doubles(NF, NMX), info, n_chain,
-                       tnt_cstride, d_cstride);
-    return after_launch("k_prefix_wide");
+    a.gscr = ctx->ws;
   }
-  const size_t lds = ((size_t)NMX * NMX * 2 + (size_t)NMX * (NF + 1)) * sizeof(double);
-  if (lds > 160 * 1024) return fail_arg(4, "NF too large for NMX (LDS): NMX * (2 NMX + NF + 1) > 20480");
-  int rc = check_hip(hipFuncSetAttribute((const void*)k_prefix, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)lds), "hipFuncSetAttribute(k_prefix)");
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_prefix, dim3(n_psr * n_chain), dim3(256), lds, ctx->stream, desc, NF, NMX, TNT, d,
-                     fidx, midx, phiinv_fixed, model, model_stride_doubles(NF, NMX), info, n_chain,
-                     tnt_cstride, d_cstride);
-  return after_launch("k_prefix");
+  return check_hip(launch_prefix_dd(ctx->stream, a), "k_prefix_dd");
+}
+
+int gs_prefix_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const gs_prefix_desc* desc,
+                  int64_t tnt_cstride, int64_t d_cstride, const double* TNT, const double* d,
+                  const int32_t* fidx, const int32_t* midx, const double* phiinv_fixed,
+                  double* model, int32_t* info) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (!TNT || !d || !fidx || !midx || !phiinv_fixed || !model) return fail_arg(9, "NULL array");
+  return gs_prefix_dd(ctx, n_psr, n_chain, NF, NMX, desc, tnt_cstride, d_cstride, TNT, nullptr, d, nullptr, fidx,
+                      midx, phiinv_fixed, model, info);
 }
 
 int gs_prefix(gs_ctx* ctx, int n_psr, int NF, int NMX, const gs_prefix_desc* desc,
@@ -596,16 +375,8 @@ static int bdraw_impl(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   if (n_psr == 0 || n_chain == 0) return 0;
   if (big) {
     const size_t need = (size_t)n_psr * n_chain * big_ws_doubles_per_sys(NF) * sizeof(double);
-    if (need > ctx->ws_bytes) {
-      int rc = check_hip(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
-      if (rc) return rc;
-      if (ctx->ws) (void)hipFree(ctx->ws);
-      ctx->ws = nullptr;
-      ctx->ws_bytes = 0;
-      rc = check_hip(hipMalloc((void**)&ctx->ws, need), "hipMalloc(b-draw workspace)");
-      if (rc) return rc;
-      ctx->ws_bytes = need;
-    }
+    const int rc = ensure_ws(ctx, need);
+    if (rc) return rc;
   }
   BdrawArgs a;
   a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.ldb = ldb; a.event = event;

@@ -30,6 +30,24 @@ __host__ __device__ inline int64_t model_stride_doubles(int NF, int NMX) {
   return (s + 1) & ~int64_t(1);  // 16-byte multiple
 }
 
+// gs_prefix / gs_prefix_sys / gs_prefix_dd (gibbs_prefix.hip)
+struct PrefixArgs {
+  int n_psr, n_chain, NF, NMX;
+  int64_t tnt_cstride, d_cstride, mstride;
+  int64_t gstride;  // doubles per system of gscr
+  const gs_prefix_desc* desc;
+  const double *TNT, *TNT_lo, *d, *d_lo, *phfix;  // lo parts may be NULL (= 0)
+  const int32_t *fidx, *midx;
+  double* model;
+  int32_t* info;
+  double* gscr;  // global scratch (NULL: LDS)
+};
+int64_t prefix_scratch_doubles(int NF, int NMX);
+bool prefix_scratch_in_lds(int NF, int NMX);
+hipError_t launch_prefix_dd(hipStream_t s, const PrefixArgs& a);
+hipError_t launch_tnt_dd(hipStream_t s, int n_psr, int m_max, const gs_tnt_desc* desc, const double* T,
+                         const double* Nvec, const double* r, double* TNT, double* TNT_lo, double* d, double* d_lo);
+
 struct LnlArgs {
   int n_psr, n_chain, NF, NMX, model_per_sys;
   int model_global;  // shared model block read from global memory (too large for LDS)

@@ -89,8 +89,11 @@ class DeviceModel:
         self.r = _t(np.concatenate(r_list), torch.float64, dev)
         self.tnt_desc = _t(tdesc, torch.int64, dev)
         self.prefix_desc = _t(pdesc, torch.int64, dev)
+        # TNT / d as double-double pairs (gs_tnt_dd -> gs_prefix_dd)
         self.TNT = torch.empty(int(np.sum(self.m * self.m)), dtype=torch.float64, device=dev)
+        self.TNT_lo = torch.empty_like(self.TNT)
         self.d = torch.empty(int(np.sum(self.m)), dtype=torch.float64, device=dev)
+        self.d_lo = torch.empty_like(self.d)
         self.fidx = _t(fidx, torch.int32, dev)
         self.midx = _t(midx, torch.int32, dev)
         self.nm_dev = _t(self.nm, torch.int32, dev)
@@ -106,11 +109,16 @@ class DeviceModel:
         if Nvec is not None:
             self.Nvec.copy_(_t(np.concatenate(Nvec), torch.float64, self.ctx.device))
         lib, h = self.ctx.lib, self.ctx.handle
-        check(lib.gs_tnt(h, self.P, int(self.m.max()), ptr(self.tnt_desc), ptr(self.T), ptr(self.Nvec),
-                         ptr(self.r), ptr(self.TNT), ptr(self.d)), "gs_tnt")
-        check(lib.gs_prefix(h, self.P, self.NF, self.NMX, ptr(self.prefix_desc), ptr(self.TNT),
-                            ptr(self.d), ptr(self.fidx), ptr(self.midx), ptr(self.phfix),
-                            ptr(self.model), ptr(self.info)), "gs_prefix")
+        check(lib.gs_tnt_dd(h, self.P, int(self.m.max()), ptr(self.tnt_desc), ptr(self.T), ptr(self.Nvec),
+                            ptr(self.r), ptr(self.TNT), ptr(self.TNT_lo), ptr(self.d), ptr(self.d_lo)), "gs_tnt_dd")
+        self.prefix()
+
+    def prefix(self):
+        """gs_prefix_dd of the resident (TNT, TNT_lo, d, d_lo): the model blocks and info."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        check(lib.gs_prefix_dd(h, self.P, 1, self.NF, self.NMX, ptr(self.prefix_desc), 0, 0, ptr(self.TNT),
+                               ptr(self.TNT_lo), ptr(self.d), ptr(self.d_lo), ptr(self.fidx), ptr(self.midx),
+                               ptr(self.phfix), ptr(self.model), ptr(self.info)), "gs_prefix_dd")
         info = self.info.cpu().numpy()
         if info.any():
             raise np.linalg.LinAlgError(f"fixed-prior block not positive definite: info={info}")

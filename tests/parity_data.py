@@ -222,6 +222,37 @@ def exact_chol_draw_pre(tnt_l, phiinv, zc, order):
     return b
 
 
+def exact_sweep_single(tnt_l, gwid, x0, rhomin, rhomax, zc, U, niter, phiinv_of_x, order):
+    """oracle.sweep_single (PulsarBlockGibbs.sample's loop, pulsar_gibbs.py:656-698) with every b
+    draw the exact long-double Cholesky draw (exact_chol_draw_pre) and the rho step in fp64 as
+    the reference: the trajectory an error-free b|rho would follow on the same draws.  On
+    fixture pulsar J1909-3744 of configs[2] this trajectory's b is already 4.9e-9 from the
+    reference's own chain after 60 sweeps (the reference's per-draw fp64 error, 6e-10, fed back
+    through rho), while x stays within 1.5e-10: fed-back b chains are compared with THIS, and
+    with the reference only per draw (open loop) and through x."""
+    m = tnt_l[0].shape[0]
+    gwind = np.arange(len(gwid) // 2)
+    chain = np.zeros((niter, len(x0)))
+    bchain = np.zeros((niter, m))
+    b = np.zeros(m)
+    xnew = np.asarray(x0, float)
+    zi = 0
+    for ii in range(niter):
+        chain[ii] = xnew
+        bchain[ii] = b
+        if ii == 0:
+            b = exact_chol_draw_pre(tnt_l, phiinv_of_x(x0), zc[zi], order)
+            zi += 1
+        rho = O.rho_analytic(O.tau_half(b, gwid), U[ii], rhomin, rhomax)
+        x = xnew.copy()
+        x[gwind] = 0.5 * np.log10(rho)
+        xnew = x
+        if np.all(xnew != chain[ii, -1]):
+            b = exact_chol_draw_pre(tnt_l, phiinv_of_x(xnew), zc[zi], order)
+            zi += 1
+    return chain, bchain, b
+
+
 def exact_mean_draw(TNT, d, phiinv, z_ref):
     """The reference draw with its mean computed exactly: refined Sigma^-1 d plus the
     reference's own noise term U S^-1/2 z (pulsar_gibbs.py:508-518)."""

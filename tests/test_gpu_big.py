@@ -225,7 +225,7 @@ def test_full_size_config4_pulsar(ctx):
     phi[d["fidx"]] = ph[0]
     order = O.chol_order(m, d["fidx"])
     bx = exact_chol_draw(T, N, r, phi, z[0, :m], order)
-    # fp64 noise floor of this system (cond(S) ~ 1e11 at 10^4 TOAs): numpy's own fp64 draw
+    # numpy's own fp64 draw (cond(S) ~ 1e11 at 10^4 TOAs), for comparison
     # (blocked dgemm TNT, LAPACK Cholesky, the same normals) against the exact draw
     import scipy.linalg as sl
     S = (T.T @ (T / N[:, None]) + np.diag(phi))[np.ix_(order, order)]
@@ -235,4 +235,5 @@ def test_full_size_config4_pulsar(ctx):
     bn[order] = sl.solve_triangular(L.T, y, lower=False)
     floor = normwise_rel(bn, bx)
     err = normwise_rel(b.cpu().numpy()[0, :m], bx)
-    assert err < max(1e-9, 4 * floor), (err, floor)
+    # double-double TNT + prefix: measured 1.5e-11 on MI355X, numpy 7.3e-10
+    assert err < 1e-10 and err < floor, (err, floor)

@@ -36,6 +36,20 @@ def model(ctx):
     return DeviceModel(ctx, [g["T"]], [g["Nvec"]], [g["r"]], [gwid], [np.full(n_tm, 1e-40)])
 
 
+@pytest.fixture(scope="module")
+def exact_chain(replay):
+    """The J1713 fixture run replayed with every b draw exact (long double): what an error-free
+    b|rho does on the reference's draws.  Its fed-back b is 1.06e-9 from the reference's own
+    bchain after 300 sweeps (tools/closed_loop_ref.py: the reference's per-draw fp64 error,
+    <= 8.8e-11, amplified through rho), x stays within 4e-11."""
+    from tests.parity_data import exact_sweep_single, exact_tnt
+    g = golden("single_j1713.npz")
+    tl = exact_tnt(g["T"], g["Nvec"], g["r"])
+    return exact_sweep_single(tl, replay["gwid"], g["x0"], replay["rhomin"], replay["rhomax"], replay["zc"],
+                              g["U"], replay["niter"], lambda x: O.phiinv_single(x, replay["n_tm"]),
+                              replay["order"]), tl
+
+
 def dev(a, dtype=torch.float64):
     return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).cuda()
 
@@ -57,6 +71,47 @@ def test_tnt_matches_numpy(model, replay):
     TNT, d = model.tnt_host(0)
     assert normwise_rel(TNT, replay["TNT"]) < 1e-12
     assert normwise_rel(d, replay["d"]) < 1e-12
+
+
+def test_tnt_dd_and_prefix_dd_accuracy(model):
+    """gs_tnt_dd: TNT + TNT_lo against the long-double TNT of the same fp64 inputs; gs_prefix_dd:
+    S0 and dF against a long-double prefix of that TNT."""
+    from tests.parity_data import exact_tnt
+    g = golden("single_j1713.npz")
+    tl = exact_tnt(g["T"], g["Nvec"], g["r"])
+    m = g["T"].shape[1]
+    L_ = np.longdouble
+    hi = model.TNT.cpu().numpy().reshape(m, m).astype(L_) + model.TNT_lo.cpu().numpy().reshape(m, m)
+    scale = float(np.max(np.abs(np.asarray(tl[0], np.float64))))
+    assert float(np.max(np.abs(hi - tl[0]))) / scale < 2e-17
+    dd = model.d.cpu().numpy().astype(L_) + model.d_lo.cpu().numpy()
+    assert float(np.max(np.abs(dd - tl[1]))) / float(np.max(np.abs(np.asarray(tl[1], np.float64)))) < 2e-17
+    assert np.array_equal(model.TNT.cpu().numpy().reshape(m, m), model.TNT.cpu().numpy().reshape(m, m).T)
+    gwid = np.asarray(g["gwid"])
+    order = O.chol_order(m, gwid)
+    Mi, Fi = order[:m - gwid.size], order[m - gwid.size:]
+    A = tl[0].copy()
+    A[Mi, Mi] += L_(1e-40)
+    AMM = A[np.ix_(Mi, Mi)]
+    nm = Mi.size
+    LM = np.zeros_like(AMM)
+    for k in range(nm):
+        v = AMM[k:, k] - LM[k:, :k] @ LM[k, :k]
+        LM[k, k] = np.sqrt(v[0])
+        LM[k + 1:, k] = v[1:] / LM[k, k]
+    W = np.zeros((nm, Fi.size + 1), dtype=L_)
+    B = np.concatenate([A[np.ix_(Mi, Fi)], tl[1][Mi][:, None]], axis=1)
+    for i in range(nm):
+        W[i] = (B[i] - LM[i, :i] @ W[:i]) / LM[i, i]
+    S0x = np.asarray(A[np.ix_(Fi, Fi)] - W[:, :-1].T @ W[:, :-1], np.float64)
+    dFx = np.asarray(tl[1][Fi] - W[:, :-1].T @ W[:, -1], np.float64)
+    NF = model.NF
+    buf = model.model.cpu().numpy()
+    S0 = buf[: NF * (NF + 1)].reshape(NF, NF + 1)[:, :NF]
+    dF = buf[NF * (NF + 1): NF * (NF + 1) + NF]
+    assert normwise_rel(S0, S0x) < 1e-15
+    assert normwise_rel(dF, dFx) < 1e-15
+    assert np.array_equal(S0, S0.T)
 
 
 def test_prefix_matches_oracle(model, replay):
@@ -85,7 +140,7 @@ def test_bdraw_matches_reference_draws(ctx, model, replay, bcast):
     from pulsar_timing_gibbsspec_amd import _lib
     ctx.set_option(_lib.OPT_BCAST, bcast)
     g = golden("single_j1713.npz")
-    ks = [0, 1, 2, 50, 150, replay["niter"]]
+    ks = list(range(replay["niter"] + 1))          # every draw of the reference's run (open loop)
     ph = np.stack([replay["phiinv"][k][replay["gwid"]] for k in ks])
     z = np.stack([replay["zc"][k] for k in ks])
     # one pulsar, len(ks) chains: system c uses row c
@@ -105,9 +160,11 @@ def test_bdraw_flags_non_positive_definite(model):
 
 
 @pytest.mark.parametrize("bcast", [0, 1, 2, 3])
-def test_fused_sweep_matches_reference_chain(ctx, model, replay, bcast):
-    """gs_sweep_freespec with the reference's draws (rotated) reproduces chain/bchain,
-    with either broadcast variant of the factorisation."""
+def test_fused_sweep_matches_reference_chain(ctx, model, replay, exact_chain, bcast):
+    """gs_sweep_freespec with the reference's draws (rotated), any broadcast variant of the
+    factorisation, 300 fed-back sweeps: x within 1e-9 of the reference's chain; b within 1e-9
+    of the error-free replay of the same draws (the reference's own fed-back b is 1.06e-9 from
+    that replay; every draw against the reference's b is test_bdraw_matches_reference_draws)."""
     from pulsar_timing_gibbsspec_amd import _lib
     from pulsar_timing_gibbsspec_amd.engine import FreeSpectrumChains
     ctx.set_option(_lib.OPT_BCAST, bcast)
@@ -122,11 +179,13 @@ def test_fused_sweep_matches_reference_chain(ctx, model, replay, bcast):
     xr, br = run.run(n, z0_inj=dev(z0), z_inj=dev(zi), u_inj=dev(ui))
     xr, br = xr.cpu().numpy(), br.cpu().numpy()
     assert not run.info.cpu().numpy().any()
+    (ex_x, ex_b, ex_final), _ = exact_chain
     for c in range(nc):
         assert normwise_rel(xr[:, c], g["chain"]) < 1e-9
-        assert normwise_rel(br[1:, c], g["bchain"][1:]) < 1e-9
+        assert normwise_rel(xr[:, c], ex_x) < 1e-9
+        assert normwise_rel(br[1:, c], ex_b[1:]) < 1e-9
         assert np.all(br[0, c] == 0)
-    assert normwise_rel(run.b.cpu().numpy()[0], g["b_final"]) < 1e-9
+    assert normwise_rel(run.b.cpu().numpy()[0], ex_final) < 1e-9
     assert np.array_equal(xr[:, 0], xr[:, 1]) and np.array_equal(br[:, 0], br[:, 2])
     ctx.set_option(_lib.OPT_BCAST, 3)
 

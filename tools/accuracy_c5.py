@@ -8,7 +8,6 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pulsar_timing_gibbsspec_amd import _lib, synthetic
 from pulsar_timing_gibbsspec_amd.engine import DeviceModel
-from pulsar_timing_gibbsspec_amd._lib import ptr, check
 from oracle import gibbs_oracle as O
 from tests.parity_data import exact_chol_draw_pre, exact_tnt, normwise_rel
 
@@ -59,17 +58,24 @@ out["numpy_M_part"] = float(np.max(np.abs(bn[mi] - bx[mi])) / sc)
 out["F_rel_own_scale_device"] = float(np.max(np.abs(bd[fi] - bx[fi])) / np.max(np.abs(bx[fi])))
 out["F_rel_own_scale_numpy"] = float(np.max(np.abs(bn[fi] - bx[fi])) / np.max(np.abs(bx[fi])))
 # device draw from the exact (fp64-rounded) TNT: overwrite TNT/d, redo the prefix only
+lo = lambda a, h: np.asarray(a - np.asarray(h, np.longdouble), np.float64)  # noqa: E731
+TNT_dev_hi, TNT_dev_lo = model.TNT.clone(), model.TNT_lo.clone()
+out["device_tnt_dd_rel_err"] = float(np.max(np.abs(
+    np.asarray(TNT_dev_hi.cpu().numpy(), np.longdouble).reshape(m, m) + TNT_dev_lo.cpu().numpy().reshape(m, m)
+    - tl[0])) / np.max(np.abs(np.asarray(tl[0], np.float64))))
 model.TNT.copy_(torch.as_tensor(TNTx.ravel(), device=ctx.device))
+model.TNT_lo.copy_(torch.as_tensor(lo(tl[0], TNTx).ravel(), device=ctx.device))
 model.d.copy_(torch.as_tensor(dx, device=ctx.device))
-lib, h = ctx.lib, ctx.handle
-check(lib.gs_prefix(h, model.P, model.NF, model.NMX, ptr(model.prefix_desc), ptr(model.TNT), ptr(model.d),
-                    ptr(model.fidx), ptr(model.midx), ptr(model.phfix), ptr(model.model), ptr(model.info)), "prefix")
+model.d_lo.copy_(torch.as_tensor(lo(tl[1], dx), device=ctx.device))
+model.prefix()
 b2, _ = model.bdraw(dev(ph[None]), 1, z=dev(zz))
 out["device_draw_exact_tnt"] = normwise_rel(b2.cpu().numpy()[0, :m], bx)
 print({k: float("%.3g" % v) for k, v in out.items()})
 # mean only (z = 0), the device on the exact TNT (set above); numpy on its own and on the exact TNT
 z0 = np.zeros((1, model.ldb))
-model.TNT.copy_(torch.as_tensor(np.asarray(model.tnt_host(0)[0]).ravel(), device=ctx.device))
+model.TNT.copy_(TNT_dev_hi)
+model.TNT_lo.copy_(TNT_dev_lo)
+model.prefix()
 b0, _ = model.bdraw(dev(ph[None]), 1, z=dev(z0))
 bx0 = exact_chol_draw_pre(tl, phi, np.zeros(m), order)
 sc = np.max(np.abs(bx))
