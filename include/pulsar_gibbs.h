@@ -113,6 +113,15 @@ int gs_ctx_get_option(gs_ctx* ctx, int option); /* -1 on unknown option / NULL c
  * (captured with the sweep).  Attach before capturing.
  */
 int gs_ctx_set_sweep_counter(gs_ctx* ctx, const int64_t* sweep_dev);
+/*
+ * Non-positive-definite Sigma inside a run (the reference's LinAlgError branch,
+ * pulsar_gibbs.py:507-516): every b-draw kernel (gs_bdraw*, gs_sweep_freespec) keeps the
+ * system's previous b when its factorisation fails -- no NaN enters the chain state -- and
+ * reports the first failing pivot in info.  With a per-system counter array attached
+ * (int32 [n_sys], device, NULL detaches), each failed draw also adds 1 to counts[sys], so a
+ * caller can surface failures as they happen.  The counts persist across calls.
+ */
+int gs_ctx_set_fail_counts(gs_ctx* ctx, int32_t* counts);
 int gs_counter_add(gs_ctx* ctx, int64_t* counter, int64_t inc);
 
 /* Doubles per pulsar in a model buffer (see gs_prefix). */
@@ -250,6 +259,19 @@ int gs_lnlike_marg(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const d
  * equal to gs_rho_curn up to pdf rounding (1e-15 relative).  ngrid <= 2048.
  */
 int gs_tau_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, double* S);
+/*
+ * The tau sums in exact fixed point, for a pulsar-sharded run whose exchange must not depend on
+ * the number of shards or the collective's reduction order (shard counts 1/2/4/8
+ * give identical chains).  gs_tau_sum_fx: acc [3 x n_f x n_chain] int64 = the 48-bit digits of
+ * sum_p floor(tau_p / 2^e0) (every tau truncated to the grid 2^e0, exact integer sums; n_psr <
+ * 2^15), ovf (int32, may be NULL) set to 1 for a negative / non-finite tau or one >= 2^(e0+144).
+ * Digits of several shards add as int64 (all-reduce SUM, any order) to the digits of the whole
+ * array.  gs_fx_to_double: S [n] (n = n_f x n_chain) from summed digits, rounded the same way on
+ * every rank.  PTAChains uses e0 = floor(log2 rhomin) - 64.
+ */
+int gs_tau_sum_fx(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, int e0, int64_t* acc,
+                  int32_t* ovf);
+int gs_fx_to_double(gs_ctx* ctx, int64_t n, int e0, const int64_t* acc, double* S);
 int gs_rho_curn_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* S, int ngrid,
                     const double* grid3, const double* u, int64_t sweep, int64_t chain_base, double* x,
                     int ldx, const int32_t* xcol, int32_t* idx_out);

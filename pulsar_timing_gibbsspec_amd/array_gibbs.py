@@ -68,6 +68,13 @@ class PulsarArrayGibbs(object):
                 raise NotImplementedError("pulsars with different free-spectrum priors")
             if len(s.gwid) != len(s0.gwid):
                 raise NotImplementedError("pulsars with different numbers of free-spectrum bins")
+            # one fused free-spectrum sweep for all pulsars: every pulsar must be free-spectrum
+            # only (no red / ECORR / white Metropolis block, every parameter a gw rho)
+            if (s._red_loop() or s._ecorr_loop() or s._white_loop() or s.red_sig is not None
+                    or s.hypersample != "conditional" or len(s.param_names) != len(s.gwid) // 2):
+                raise NotImplementedError(
+                    f"{s.pulsar_name}: PulsarArrayGibbs runs free-spectrum-only pulsars (analytic rho|b); "
+                    "sample pulsars with red-noise, ECORR or white-noise blocks with PulsarBlockGibbs")
 
     @property
     def ctx(self):

@@ -16,6 +16,7 @@ struct gs_ctx {
   int grid_exact = 0;  // GS_OPT_GRID_EXACT
   int brec_nc = 0;     // GS_OPT_BREC_CHAINS
   const int64_t* sweep_dev = nullptr;  // gs_ctx_set_sweep_counter
+  int32_t* fail_counts = nullptr;      // gs_ctx_set_fail_counts
   double* ws = nullptr;  // tile workspace of the large-NF b-draw (grown on demand)
   size_t ws_bytes = 0;
 };
@@ -36,6 +37,17 @@ int check_hip(hipError_t e, const char* where) {
 }
 
 int after_launch(const char* where) { return check_hip(hipGetLastError(), where); }
+
+// the NF-dispatching launchers return 1 for an NF without an instantiation and 2 when the
+// dynamic-LDS attribute could not be set (hipFuncSetAttribute)
+int launch_rc(int rc, const char* kernel) {
+  if (rc == 1) return fail_arg(4, "unsupported NF");
+  if (rc == 2) {
+    g_err = std::string(kernel) + ": hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed";
+    return -(int)hipErrorInvalidValue;
+  }
+  return after_launch(kernel);
+}
 
 // grow the context workspace (large-NF b-draw tiles, prefix scratch) to `need` bytes
 int ensure_ws(gs_ctx* ctx, size_t need) {
@@ -264,6 +276,12 @@ int gs_ctx_set_sweep_counter(gs_ctx* ctx, const int64_t* sweep_dev) {
   return 0;
 }
 
+int gs_ctx_set_fail_counts(gs_ctx* ctx, int32_t* counts) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  ctx->fail_counts = counts;
+  return 0;
+}
+
 int gs_counter_add(gs_ctx* ctx, int64_t* counter, int64_t inc) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (!counter) return fail_arg(2, "counter is NULL");
@@ -385,14 +403,14 @@ static int bdraw_impl(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.model = model; a.fidx = fidx; a.midx = midx; a.nm = nm; a.chain_mask = chain_mask;
   a.phiinv_F = phiinv_F; a.z = z;
   a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = ctx->bcast; a.psr_base = ctx->psr_base;
+  a.fail_count = ctx->fail_counts;
   a.model_per_sys = per_sys;
   a.mask_per_sys = ctx->x_per_sys;
   if (big) {
     launch_bdraw_big(ctx->stream, a, ctx->ws);
     return after_launch("k_bdraw_big");
   }
-  if (launch_bdraw(ctx->stream, a)) return fail_arg(4, "unsupported NF");
-  return after_launch("k_bdraw");
+  return launch_rc(launch_bdraw(ctx->stream, a), "k_bdraw");
 }
 
 int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, const double* model,
@@ -472,10 +490,10 @@ int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.rhomin = rhomin; a.rhomax = rhomax; a.model = model; a.fidx = fidx; a.midx = midx; a.nm = nm;
   a.x_state = x_state; a.b_state = b_state; a.x_rec = x_rec; a.b_rec = b_rec;
   a.z0_inj = z0_inj; a.z_inj = z_inj; a.u_inj = u_inj; a.info = info; a.key = key_of(ctx);
+  a.fail_count = ctx->fail_counts;
   a.bcast = ctx->bcast; a.psr_base = ctx->psr_base;
   a.brec_nc = ctx->brec_nc < n_chain ? ctx->brec_nc : 0;
-  if (launch_sweep_freespec(ctx->stream, a)) return fail_arg(4, "unsupported NF");
-  return after_launch("k_sweep_freespec");
+  return launch_rc(launch_sweep_freespec(ctx->stream, a), "k_sweep_freespec");
 }
 
 int gs_tau(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const int32_t* fidx, const double* b,
@@ -532,8 +550,7 @@ int gs_lnlike_marg(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const d
   a.model_global = NMX > 64;
   a.mstride = model_stride_doubles(NF, NMX); a.model = model; a.nm = nm; a.phiinv_F = phiinv_F;
   a.lnl = lnl; a.info = info;
-  launch_lnlike_marg(ctx->stream, a);
-  return after_launch("k_lnlike_marg");
+  return launch_rc(launch_lnlike_marg(ctx->stream, a), "k_lnlike_marg");
 }
 
 int gs_tau_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, double* S) {
@@ -542,6 +559,26 @@ int gs_tau_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, 
   if (!tau || !S) return fail_arg(5, "NULL tau / S");
   launch_tau_sum(ctx->stream, n_psr, (int64_t)n_f * n_chain, tau, S);
   return after_launch("k_tau_sum");
+}
+
+int gs_tau_sum_fx(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, int e0, int64_t* acc,
+                  int32_t* ovf) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0 || n_f < 0) return fail_arg(2, "negative batch");
+  if (n_psr >= (1 << 15)) return fail_arg(2, "n_psr >= 32768 (int64 digit headroom)");
+  if (!tau || !acc) return fail_arg(5, "NULL tau / acc");
+  if (e0 < -1000 || e0 > 800) return fail_arg(6, "e0 out of range");
+  launch_tau_sum_fx(ctx->stream, n_psr, (int64_t)n_f * n_chain, tau, e0, (long long*)acc, ovf);
+  return after_launch("k_tau_sum_fx");
+}
+
+int gs_fx_to_double(gs_ctx* ctx, int64_t n, int e0, const int64_t* acc, double* S) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n < 0) return fail_arg(2, "n < 0");
+  if (e0 < -1000 || e0 > 800) return fail_arg(3, "e0 out of range");
+  if (!acc || !S) return fail_arg(4, "NULL acc / S");
+  launch_fx_to_double(ctx->stream, n, e0, (const long long*)acc, S);
+  return after_launch("k_fx_to_double");
 }
 
 int gs_rho_curn_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* S, int ngrid,

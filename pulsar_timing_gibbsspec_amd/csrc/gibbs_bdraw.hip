@@ -254,8 +254,12 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
   double* scr = lds + wave * gs_tile_scr(NF);
   double* brow = A.b + sys * A.ldb;
   const int fail = bdraw_tile_wide<NTC>(M, A.NMX, nM, lane, phinv, zF, zM, zMa, bF, bM, scr, NF, brow, mrow);
-  if (lane < NF) brow[fi] = bF;
-  if (lane < nM) brow[mi] = bM;
+  if (!fail) {  // non-PD Sigma: the previous b stays (wave-uniform)
+    if (lane < NF) brow[fi] = bF;
+    if (lane < nM) brow[mi] = bM;
+  } else if (A.fail_count && lane == 0) {
+    A.fail_count[sys] += 1;
+  }
   if (A.info && lane == 0) A.info[sys] = fail;
 }
 
@@ -292,8 +296,12 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
   double bF = 0.0, bM = 0.0;
   double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * GS_SCR_DOUBLES(BC, NF);
   const int fail = bdraw_sys<NFC, NTC, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
-  if (lane < NF) A.b[sys * A.ldb + fi] = bF;
-  if (lane < nM) A.b[sys * A.ldb + mi] = bM;
+  if (!fail) {  // non-PD Sigma: the previous b stays (wave-uniform)
+    if (lane < NF) A.b[sys * A.ldb + fi] = bF;
+    if (lane < nM) A.b[sys * A.ldb + mi] = bM;
+  } else if (A.fail_count && lane == 0) {
+    A.fail_count[sys] += 1;
+  }
   if (A.info && lane == 0) A.info[sys] = fail;
 }
 
@@ -472,8 +480,16 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
       }
       if (pass == 0) phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;  // first draw from xs
       GS_PH(7)
+      // a failed factorisation (non-PD Sigma, wave-uniform) keeps the previous b: no NaN ever
+      // enters the state (the reference's LinAlgError branch, pulsar_gibbs.py:507-516)
+      const double bF0 = bF, bM0 = bM;
       const int f = bdraw_sys<NFC, NTC, BC, true>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
-      if (!fail) fail = f;
+      if (f) {
+        bF = bF0;
+        bM = bM0;
+        if (!fail) fail = f;
+        if (A.fail_count && lane == 0) A.fail_count[sys] += 1;
+      }
     }
   }
   GS_PH_FLUSH(scr)
@@ -574,20 +590,27 @@ int launch_lnlike_marg(hipStream_t s, const LnlArgs& a) {
   dim3 grid((unsigned)(a.n_psr * nb));
   const size_t lds = ((size_t)(a.model_per_sys || a.model_global ? 0 : a.mstride) + gs_tile_scr(a.NF) * WPB) *
                      sizeof(double);
+  // a shared model block staged in LDS: above 64 KB (e.g. NF = 60 with NMX > 31) the launch needs
+  // the dynamic-LDS attribute, as GS_LAUNCH sets it
+#define GS_LNL_LAUNCH(NFC, NTC)                                                       \
+  if (lds > 65536 && set_lds(k_lnlike_marg<NFC, NTC, WPB>, lds)) return 2;            \
+  hipLaunchKernelGGL((k_lnlike_marg<NFC, NTC, WPB>), grid, dim3(64 * WPB), lds, s, a); \
+  return 0;
   switch (a.NF) {
-    case 20: hipLaunchKernelGGL((k_lnlike_marg<20, 0, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    case 40: hipLaunchKernelGGL((k_lnlike_marg<40, 0, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    case 60: hipLaunchKernelGGL((k_lnlike_marg<60, 0, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 20: GS_LNL_LAUNCH(20, 0)
+    case 40: GS_LNL_LAUNCH(40, 0)
+    case 60: GS_LNL_LAUNCH(60, 0)
     default: break;
   }
   if (a.NF <= 0 || a.NF > 64 || (a.NF & 1)) return 1;
   switch (a.NF / 16 + 1) {
-    case 1: hipLaunchKernelGGL((k_lnlike_marg<0, 1, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    case 2: hipLaunchKernelGGL((k_lnlike_marg<0, 2, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    case 3: hipLaunchKernelGGL((k_lnlike_marg<0, 3, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    case 4: hipLaunchKernelGGL((k_lnlike_marg<0, 4, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
-    default: hipLaunchKernelGGL((k_lnlike_marg<0, 5, WPB>), grid, dim3(64 * WPB), lds, s, a); return 0;
+    case 1: GS_LNL_LAUNCH(0, 1)
+    case 2: GS_LNL_LAUNCH(0, 2)
+    case 3: GS_LNL_LAUNCH(0, 3)
+    case 4: GS_LNL_LAUNCH(0, 4)
+    default: GS_LNL_LAUNCH(0, 5)
   }
+#undef GS_LNL_LAUNCH
 }
 
 int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {

@@ -179,7 +179,13 @@ __global__ __launch_bounds__(64 * BIG_WPB) void k_bdraw_big(BdrawArgs A, double*
     lds_fence();
   }
 
-  // ---- fixed-prior block: x_M = h + R z_M - G x_F (lane = row)
+  // ---- fixed-prior block: x_M = h + R z_M - G x_F (lane = row).  A failed factorisation
+  // (non-PD Sigma, wave-uniform) keeps the previous b.
+  if (fail) {
+    if (A.info && lane == 0) A.info[sys] = fail;
+    if (A.fail_count && lane == 0) A.fail_count[sys] += 1;
+    return;
+  }
   if (lane < nM) {
     double v = h[lane];
     for (int j = 0; j < nM; ++j) v = fma(R[lane * NMX + j], zb[NF + j], v);

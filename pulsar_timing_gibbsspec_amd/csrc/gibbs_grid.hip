@@ -132,6 +132,77 @@ __global__ __launch_bounds__(256) void k_tau_sum(int n_psr, int64_t nrow, const 
   S[r] = s;
 }
 
+// ---- the CURN tau sums in exact fixed point (pulsar-sharded runs: order-free exchange)
+// S_k = sum_p tau_p,k with every tau truncated to the grid 2^e0 and summed as integers in three
+// 48-bit digits held in int64 (exact for < 2^15 pulsars): integer addition is associative, so
+// the per-rank partial digits all-reduce (RCCL int64 sum, any ring / tree order) to the same
+// integers on every rank and for every number of shards, and gs_fx_to_double rounds them to the
+// same S.  e0 = floor(log2 rhomin) - 64 puts the truncation ~2^-64 below the smallest grid rho,
+// where S / (2 rho_g) cannot see it; 144 bits reach rhomin * 2^80.
+constexpr int FX_BITS = 48;
+constexpr unsigned long long FX_MASK = (1ull << FX_BITS) - 1;
+
+__global__ __launch_bounds__(256) void k_tau_sum_fx(int n_psr, int64_t nrow, const double* tau, int e0,
+                                                    long long* acc, int* ovf) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrow) return;
+  long long d0 = 0, d1 = 0, d2 = 0;
+  bool bad = false;
+  for (int p = 0; p < n_psr; ++p) {
+    const double v = tau[p * nrow + r];
+    if (v == 0.0) continue;
+    if (!(v > 0.0) || v == __builtin_inf()) {
+      bad = true;
+      continue;
+    }
+    int E;
+    const double fr = frexp(v, &E);                           // v = fr 2^E, fr in [0.5, 1)
+    const unsigned long long M = (unsigned long long)ldexp(fr, 53);  // exact 53-bit integer
+    const int sh = E - 53 - e0;                                // v = M 2^sh 2^e0
+    if (sh + 53 > 3 * FX_BITS) bad = true;                     // beyond the top digit
+    unsigned long long dg[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int t = sh - FX_BITS * i;                          // digit i = floor(M 2^t) mod 2^48
+      const unsigned long long u = t >= 0 ? (t < 64 ? M << t : 0ull) : (-t < 64 ? M >> (-t) : 0ull);
+      dg[i] = u & FX_MASK;
+    }
+    d0 += (long long)dg[0];
+    d1 += (long long)dg[1];
+    d2 += (long long)dg[2];
+  }
+  acc[r] = d0;
+  acc[nrow + r] = d1;
+  acc[2 * nrow + r] = d2;
+  if (bad && ovf) *ovf = 1;
+}
+
+__global__ __launch_bounds__(256) void k_fx_to_double(int64_t nrow, int e0, const long long* acc, double* S) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrow) return;
+  long long d0 = acc[r], d1 = acc[nrow + r], d2 = acc[2 * nrow + r];
+  d1 += d0 >> FX_BITS;  // carries (digits are sums of nonnegative 48-bit values)
+  d0 &= (long long)FX_MASK;
+  d2 += d1 >> FX_BITS;
+  d1 &= (long long)FX_MASK;
+  // four exact, non-overlapping terms, summed high to low with two-sums: the same bits on
+  // every rank (deterministic, ~correctly rounded)
+  const double t3 = ldexp((double)(d2 >> 24), 3 * FX_BITS - 24 + e0);
+  const double t2 = ldexp((double)(d2 & 0xffffff), 2 * FX_BITS + e0);
+  const double t1 = ldexp((double)d1, FX_BITS + e0);
+  const double t0 = ldexp((double)d0, e0);
+  double hi = t3, lo = 0.0;
+  const double terms[3] = {t2, t1, t0};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double sm = hi + terms[i];
+    const double bb = sm - hi;
+    lo += (hi - (sm - bb)) + (terms[i] - bb);
+    hi = sm;
+  }
+  S[r] = hi + lo;
+}
+
 constexpr int CS_MAXG = 32;  // grid points per lane (ngrid <= 2048)
 
 __global__ __launch_bounds__(256) void k_rho_curn_sum(GridArgs A) {
@@ -680,6 +751,18 @@ int launch_rho_curn(hipStream_t s, const GridArgs& a) {
 
 int launch_counter_add(hipStream_t s, int64_t* counter, int64_t inc) {
   hipLaunchKernelGGL(k_counter_add, dim3(1), dim3(64), 0, s, counter, inc);
+  return 0;
+}
+
+int launch_tau_sum_fx(hipStream_t s, int n_psr, int64_t nrow, const double* tau, int e0, long long* acc, int* ovf) {
+  if (nrow == 0) return 0;
+  hipLaunchKernelGGL(k_tau_sum_fx, grid1(nrow, 256), dim3(256), 0, s, n_psr, nrow, tau, e0, acc, ovf);
+  return 0;
+}
+
+int launch_fx_to_double(hipStream_t s, int64_t nrow, int e0, const long long* acc, double* S) {
+  if (nrow == 0) return 0;
+  hipLaunchKernelGGL(k_fx_to_double, grid1(nrow, 256), dim3(256), 0, s, nrow, e0, acc, S);
   return 0;
 }
 

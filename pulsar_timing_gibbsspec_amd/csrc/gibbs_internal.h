@@ -71,6 +71,7 @@ struct BdrawArgs {
   const double *phiinv_F, *z;
   double* b;
   int32_t* info;
+  int32_t* fail_count;  // gs_ctx_set_fail_counts: failed draws per system (b kept), or NULL
   gs_key key;
 };
 
@@ -84,6 +85,7 @@ struct SweepArgs {
   double *x_state, *b_state, *x_rec, *b_rec;
   const double *z0_inj, *z_inj, *u_inj;
   int32_t* info;
+  int32_t* fail_count;  // gs_ctx_set_fail_counts: failed draws per system (b kept), or NULL
   gs_key key;
 };
 
@@ -127,6 +129,8 @@ struct GridArgs {
 
 int launch_counter_add(hipStream_t s, int64_t* counter, int64_t inc);
 int launch_tau_sum(hipStream_t s, int n_psr, int64_t nrow, const double* tau, double* S);
+int launch_tau_sum_fx(hipStream_t s, int n_psr, int64_t nrow, const double* tau, int e0, long long* acc, int* ovf);
+int launch_fx_to_double(hipStream_t s, int64_t nrow, int e0, const long long* acc, double* S);
 int launch_rho_curn_sum(hipStream_t s, const GridArgs& a);
 
 struct PtaGateArgs {

@@ -153,6 +153,7 @@ __global__ __launch_bounds__(256) void k_prefix_dd(PrefixArgs a) {
   auto ldd = [&](int r) -> gs_dd { return {dv[r], dl ? dl[r] : 0.0}; };
   auto L = [&](int i, int j) -> gs_dd { return {Lh[i * NMX + j], Ll[i * NMX + j]}; };
 
+  __shared__ double rinv[2 * GS_NMX_WIDE];  // 1 / L_kk (double-double): divisions become products
   if (tid == 0) s_fail = 0;
   for (int q = tid; q < NMX * NMX; q += nt) {
     const int i = q / NMX, j = q % NMX;
@@ -173,11 +174,14 @@ __global__ __launch_bounds__(256) void k_prefix_dd(PrefixArgs a) {
       const gs_dd s = dd_sqrt(piv);
       Lh[k * NMX + k] = s.hi;
       Ll[k * NMX + k] = s.lo;
+      const gs_dd ri = dd_div(gs_dd{1.0, 0.0}, s);
+      rinv[2 * k] = ri.hi;
+      rinv[2 * k + 1] = ri.lo;
     }
     __syncthreads();
-    const gs_dd lkk = L(k, k);
+    const gs_dd rk = {rinv[2 * k], rinv[2 * k + 1]};
     for (int i = k + 1 + tid; i < nM; i += nt) {
-      const gs_dd v = dd_div(L(i, k), lkk);
+      const gs_dd v = dd_mul(L(i, k), rk);
       Lh[i * NMX + k] = v.hi;
       Ll[i * NMX + k] = v.lo;
     }
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(256) void k_prefix_dd(PrefixArgs a) {
       gs_dot2 s;
       s.init(f < NF ? ldA(Mi[i], Fi[f]) : ldd(Mi[i]));
       for (int j = 0; j < i; ++j) s.fma_dd(dd_neg(L(i, j)), gs_dd{Wh[j * ldw + f], Wl[j * ldw + f]});
-      const gs_dd w = dd_div(s.get(), L(i, i));
+      const gs_dd w = dd_mul(s.get(), gs_dd{rinv[2 * i], rinv[2 * i + 1]});
       Wh[i * ldw + f] = w.hi;
       Wl[i * ldw + f] = w.lo;
     }
@@ -211,16 +215,23 @@ __global__ __launch_bounds__(256) void k_prefix_dd(PrefixArgs a) {
   double* G = dF + NF;
   double* h = G + NMX * (NF + 1);
   double* R = h + NMX;
-  // S0 (upper triangle computed, mirrored: exactly symmetric) and its padding column NF = dF
-  for (int q = tid; q < NF * (NF + 1); q += nt) {
-    const int f = q / (NF + 1), g = q % (NF + 1);
-    if (g < f) continue;
+  // S0 (upper triangle computed, mirrored: exactly symmetric) and its padding column NF = dF:
+  // the NF (NF + 3) / 2 pairs f <= g <= NF enumerated row by row (row f: NF + 1 - f entries)
+  const int Lr = NF + 1, n_up = NF * (NF + 3) / 2;
+  for (int q = tid; q < n_up; q += nt) {
+    // f = the row whose offset f Lr - f (f - 1) / 2 is the last one <= q
+    const double B = 2.0 * Lr + 1.0;
+    int f = (int)((B - sqrt(B * B - 8.0 * q)) * 0.5);
+    auto off = [&](int r) { return r * Lr - (r * (r - 1)) / 2; };
+    if (f > 0 && off(f) > q) --f;
+    if (off(f + 1) <= q) ++f;
+    const int g = f + (q - off(f));
     gs_dot2 s;
     s.init(g < NF ? ldA(Fi[f], Fi[g]) : ldd(Fi[f]));
     for (int i = 0; i < nM; ++i)
       s.fma_dd(gs_dd{-Wh[i * ldw + f], -Wl[i * ldw + f]}, gs_dd{Wh[i * ldw + g], Wl[i * ldw + g]});
     const double v = s.get().hi;
-    S0[q] = v;
+    S0[f * (NF + 1) + g] = v;
     if (g < NF) S0[g * (NF + 1) + f] = v;
     else dF[f] = v;
   }
@@ -273,7 +284,8 @@ int64_t prefix_scratch_doubles(int NF, int NMX) {
   return 2 * (int64_t)NMX * NMX + 2 * (int64_t)NMX * (NF + 1);
 }
 
-bool prefix_scratch_in_lds(int NF, int NMX) { return prefix_scratch_doubles(NF, NMX) * 8 <= 160 * 1024; }
+// dynamic LDS next to the kernel's 2 KB of static LDS (rinv, s_fail)
+bool prefix_scratch_in_lds(int NF, int NMX) { return prefix_scratch_doubles(NF, NMX) * 8 <= 156 * 1024; }
 
 hipError_t launch_prefix_dd(hipStream_t s, const PrefixArgs& a) {
   const int64_t n_sys = (int64_t)a.n_psr * a.n_chain;

@@ -738,7 +738,7 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
     const double xm = rok ? M.h[row + z0] + p : 0.0;
     if (!WIDE || P < 4)
       ob[row] = xm;
-    else if (rok && q == 0)
+    else if (rok && q == 0 && !fail)  // a failed draw leaves the caller's b untouched
       bext[mrow[row]] = xm;
   }
   lds_fence();

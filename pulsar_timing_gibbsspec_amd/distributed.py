@@ -92,10 +92,13 @@ class PulsarAllGather:
 
 class TauSumAllReduce:
     """The CURN exchange without per-pulsar red noise: each rank holds the partial sums
-    S_k = sum over its pulsars of tau_p,k [n_f, n_chain]; one all-reduce (RCCL over xGMI
-    for backend 'nccl') leaves the global sums on every rank, identical on all ranks, so
-    every rank draws the common rho from the same Philox counters (north_star: the only
-    collective of the CURN config)."""
+    S_k = sum over its pulsars of tau_p,k as exact fixed-point digits [3, n_f, n_chain] int64
+    (gs_tau_sum_fx); one all-reduce SUM (RCCL over xGMI for backend 'nccl') leaves the digits of
+    the whole array on every rank.  Integer addition is associative, so the result does not
+    depend on the number of shards or on the collective's reduction order: every rank, and the
+    unsharded run, rounds the same integers to the same S (gs_fx_to_double) and draws the common
+    rho from the same Philox counters (north_star: the only collective of the CURN config).
+    A floating-point partial-sum all-reduce would not be reproducible across shard counts."""
 
     def __init__(self, group=None):
         self.group = group

@@ -172,6 +172,23 @@ class DeviceModel:
         return b, inf
 
 
+class fail_counts:
+    """Attach a per-system failed-draw counter (int32 device tensor) to the context for the
+    duration of a block of launches (gs_ctx_set_fail_counts); the previous attachment is
+    restored on exit (contexts are shared between engines)."""
+
+    def __init__(self, ctx, counts):
+        self.ctx, self.counts = ctx, counts
+
+    def __enter__(self):
+        check(self.ctx.lib.gs_ctx_set_fail_counts(self.ctx.handle, ptr(self.counts)), "gs_ctx_set_fail_counts")
+        return self.counts
+
+    def __exit__(self, *exc):
+        check(self.ctx.lib.gs_ctx_set_fail_counts(self.ctx.handle, None), "gs_ctx_set_fail_counts")
+        return False
+
+
 class FreeSpectrumChains:
     """n_chain independent free-spectrum Gibbs chains for each pulsar of a DeviceModel.
 
@@ -194,6 +211,8 @@ class FreeSpectrumChains:
         self.x = _t(x0, torch.float64, dev)
         self.b = torch.zeros(n_sys, model.ldb, dtype=torch.float64, device=dev)
         self.info = torch.zeros(n_sys, dtype=torch.int32, device=dev)
+        # failed (non-PD) draws per system: the kernels keep b and count (gs_ctx_set_fail_counts)
+        self.fail_count = torch.zeros(n_sys, dtype=torch.int32, device=dev)
         self.it = 0
         if not self.fused:
             self.xlast = torch.empty(n_sys, dtype=torch.float64, device=dev)
@@ -216,9 +235,15 @@ class FreeSpectrumChains:
             x_rec = torch.empty(n_sweeps, self.n_sys, self.n_f, dtype=torch.float64, device=dev)
         if record and record_b and b_rec is None:
             b_rec = torch.empty(n_sweeps, m.P * bk, m.ldb, dtype=torch.float64, device=dev)
-        if not self.fused:
-            self._run_sequence(n_sweeps, x_rec, b_rec if record_b else None, z0_inj, z_inj, u_inj, bk)
-            return x_rec, b_rec
+        with fail_counts(self.ctx, self.fail_count):
+            if not self.fused:
+                self._run_sequence(n_sweeps, x_rec, b_rec if record_b else None, z0_inj, z_inj, u_inj, bk)
+                return x_rec, b_rec
+            self._run_fused(n_sweeps, x_rec, b_rec, z0_inj, z_inj, u_inj, bk)
+        return x_rec, b_rec
+
+    def _run_fused(self, n_sweeps, x_rec, b_rec, z0_inj, z_inj, u_inj, bk):
+        m = self.model
         lib, h = self.ctx.lib, self.ctx.handle
         prev = self.ctx.get_option(_lib.OPT_BREC_CHAINS)
         self.ctx.set_option(_lib.OPT_BREC_CHAINS, bk if bk < self.n_chain else 0)
@@ -231,7 +256,6 @@ class FreeSpectrumChains:
         finally:
             self.ctx.set_option(_lib.OPT_BREC_CHAINS, prev)
         self.it += int(n_sweeps)
-        return x_rec, b_rec
 
     def _gate_phiinv(self, with_gate):
         check(self.ctx.lib.gs_pta_gate_phiinv(
@@ -354,9 +378,11 @@ class PTAChains:
     order.  ``sweep_begin`` / ``sweep_end`` expose the two halves around the exchange.
 
     curn_mode='sum' (no per-pulsar red noise only): the common draw uses the sufficient
-    statistic S_k = sum_p tau_p,k (gs_tau_sum, gs_rho_curn_sum); a pulsar-sharded run
-    then exchanges S with ``allreduce`` (distributed.TauSumAllReduce, one RCCL
-    all-reduce of n_f x n_chain doubles per sweep) instead of gathering tau.
+    statistic S_k = sum_p tau_p,k, summed exactly in fixed point (gs_tau_sum_fx ->
+    gs_fx_to_double -> gs_rho_curn_sum); a pulsar-sharded run exchanges the int64 digits with
+    ``allreduce`` (distributed.TauSumAllReduce, one RCCL all-reduce of 3 x n_f x n_chain int64 per
+    sweep) instead of gathering tau, and reproduces the unsharded chains bit for bit for any
+    number of shards.
     """
 
     def __init__(self, model: DeviceModel, n_param, gw_col, red_col, gw_bounds, red_bounds, n_chain, x0,
@@ -402,13 +428,19 @@ class PTAChains:
         self.tau = torch.empty(P, self.n_f, C, dtype=torch.float64, device=dev)
         self.tau_g = torch.empty(self.PG, self.n_f, C, dtype=torch.float64, device=dev) if self.sharded \
             else self.tau
-        self.S = torch.empty(self.n_f, C, dtype=torch.float64, device=dev)   # curn_mode='sum' 
+        self.S = torch.empty(self.n_f, C, dtype=torch.float64, device=dev)   # curn_mode='sum'
+        # ... as exact fixed-point digits (gs_tau_sum_fx): the exchanged quantity of a sharded run,
+        # order-free, so every shard count gives the 1-shard S bit for bit
+        self.S_fx = torch.empty(3, self.n_f, C, dtype=torch.int64, device=dev)
+        self.fx_e0 = int(np.floor(np.log2(gw_bounds[0]))) - 64
+        self.fx_ovf = torch.zeros(1, dtype=torch.int32, device=dev)
         self.gwphi = torch.empty(self.n_f, C, dtype=torch.float64, device=dev)
         self.irn = torch.empty(self.PG, self.n_f, C, dtype=torch.float64, device=dev) if self.red else None
         self.phiinv_F = torch.empty(P * C, model.NF, dtype=torch.float64, device=dev)
         self.gate = torch.ones(C, dtype=torch.int32, device=dev)
         self.xlast = torch.empty(C, dtype=torch.float64, device=dev)
         self.info = torch.zeros(P * C, dtype=torch.int32, device=dev)
+        self.fail_count = torch.zeros(P * C, dtype=torch.int32, device=dev)   # failed draws (b kept)
         self.slab_shape = ((2 if self.red else 1), self.n_f, C)
         self.it = 0
         self.redraw_b = False      # draw b | x first at the next sweep, as at sweep 0 (resume)
@@ -446,8 +478,9 @@ class PTAChains:
                                  ptr(self.grid_red), ptr(u_red), ii, self.chain_base, ptr(self.x),
                                  self.n_param, ptr(self.red_col), None), "gs_rho_red")
         if self.curn_mode == "sum":                            # sufficient statistic S_k
-            check(lib.gs_tau_sum(h, self.P, self.C, self.n_f, ptr(self.tau), ptr(self.S)), "gs_tau_sum")
-            return self.S if self.sharded else None
+            check(lib.gs_tau_sum_fx(h, self.P, self.C, self.n_f, ptr(self.tau), self.fx_e0, ptr(self.S_fx),
+                                    ptr(self.fx_ovf)), "gs_tau_sum_fx")
+            return self.S_fx if self.sharded else None
         if not self.sharded:
             return None
         parts = [self.tau.unsqueeze(1)]
@@ -461,8 +494,10 @@ class PTAChains:
         lib, h = self.ctx.lib, self.ctx.handle
         ii = self.it
         if self.curn_mode == "sum":
-            if self.sharded and slab_g is not None and slab_g.data_ptr() != self.S.data_ptr():
-                self.S.copy_(slab_g)
+            if self.sharded and slab_g is not None and slab_g.data_ptr() != self.S_fx.data_ptr():
+                self.S_fx.copy_(slab_g)
+            check(lib.gs_fx_to_double(h, self.n_f * self.C, self.fx_e0, ptr(self.S_fx), ptr(self.S)),
+                  "gs_fx_to_double")
             check(lib.gs_rho_curn_sum(h, self.PG, self.C, self.n_f, ptr(self.S), self.ngrid, ptr(self.grid_gw),
                                       ptr(u_curn), ii, self.chain_base, ptr(self.x), self.n_param,
                                       ptr(self.gw_col), None), "gs_rho_curn_sum")
@@ -530,7 +565,8 @@ class PTAChains:
         """One PTABlockGibbs sweep for every chain; x_rec: (n_chain, n_param) row or None.
         z0/z: (P*n_chain, ldb) injected normals (original column order); u_red
         (n_chain, P, n_f) and u_curn (n_chain, n_f): injected uniforms."""
-        slab = self.sweep_begin(x_rec=x_rec, z0=z0, u_red=u_red)
-        if self.sharded:
-            slab = self.allreduce(slab) if self.curn_mode == "sum" else self.gather(slab)
-        self.sweep_end(slab, z=z, u_curn=u_curn)
+        with fail_counts(self.ctx, self.fail_count):
+            slab = self.sweep_begin(x_rec=x_rec, z0=z0, u_red=u_red)
+            if self.sharded:
+                slab = self.allreduce(slab) if self.curn_mode == "sum" else self.gather(slab)
+            self.sweep_end(slab, z=z, u_curn=u_curn)

@@ -259,6 +259,7 @@ class PTABlockGibbs(object):
         buf = torch.empty(save_every + 1, nc, npar, dtype=torch.float64, device=dev)
         tstart = time.time()
         ii = start
+        seen_fail = 0
         if start > 0:
             eng.it = start
             if state is not None:
@@ -277,6 +278,11 @@ class PTABlockGibbs(object):
             for j in range(nxt - ii):
                 eng.sweep(x_rec=buf[j])
             rows = buf[:nxt - ii].cpu().numpy()
+            nfail = int(eng.fail_count.sum())          # failed (non-PD) b draws, b kept
+            if nfail > seen_fail:
+                print(f"WARNING: sweeps {ii}..{nxt - 1}: {nfail - seen_fail} b draws hit a non-positive-definite "
+                      "Sigma (previous b kept; pta_gibbs.py:537-546's LinAlgError branch)")
+                seen_fail = nfail
             self.chain[ii:nxt] = rows[:, 0]
             if nc > 1:
                 self.chains[:, ii:nxt] = np.moveaxis(rows, 1, 0)
@@ -298,6 +304,4 @@ class PTABlockGibbs(object):
             self._save_state(outdir, self.iter + 1, eng)
         b = eng.b.cpu().numpy()
         self._b = [b[p * eng.C, :eng.model.m[p]] for p in range(eng.P)]
-        if eng.info.cpu().numpy().any():
-            print("WARNING: non-positive-definite Sigma encountered")
         return self.chain

@@ -103,6 +103,7 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
         s.bchains = np.zeros((nc, niter, len(s._b))) if allb else None
         s.iter = 0
     start = 0
+    multi_x = multi_b = False
     if resume and all(os.path.exists(f"{o}/chain.npy") for o in outdirs):
         print("Resuming from previous run...")
         prev = [(np.load(f"{o}/chain.npy"), np.load(f"{o}/bchain.npy")) for o in outdirs]
@@ -110,29 +111,40 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
         for s, (c0, b0) in zip(samplers, prev):
             s.chain[:start] = c0[:start]
             s.bchain[:start] = b0[:start]
-        # every chain's rows when the multi-chain files hold them (else all chains restart
-        # from chain 0's recorded state)
-        multi = allb and all(os.path.exists(f"{o}/chains.npy") and os.path.exists(f"{o}/bchains.npy")
-                             for o in outdirs)
-        if multi:
-            prevc = [(np.load(f"{o}/chains.npy"), np.load(f"{o}/bchains.npy")) for o in outdirs]
-            multi = all(c.shape[0] == nc and min(c.shape[1], b.shape[1]) >= start for c, b in prevc)
-        if multi:
-            for s, (c0, b0) in zip(samplers, prevc):
-                s.chains[:, :start] = c0[:, :start]
-                s.bchains[:, :start] = b0[:, :start]
+        # every chain's x rows from chains.npy whenever it is there (nc > 1), whether or not
+        # every chain's b was kept; b rows from bchains.npy when it was (record_bchains)
+        if nc > 1 and all(os.path.exists(f"{o}/chains.npy") for o in outdirs):
+            prevc = [np.load(f"{o}/chains.npy") for o in outdirs]
+            multi_x = all(c.shape[0] == nc and c.shape[1] >= start for c in prevc)
+            if multi_x:
+                for s, c0 in zip(samplers, prevc):
+                    s.chains[:, :start] = c0[:, :start]
+        if multi_x and allb and all(os.path.exists(f"{o}/bchains.npy") for o in outdirs):
+            prevb = [np.load(f"{o}/bchains.npy") for o in outdirs]
+            multi_b = all(b.shape[0] == nc and b.shape[1] >= start for b in prevb)
+            if multi_b:
+                for s, b0 in zip(samplers, prevb):
+                    s.bchains[:, :start] = b0[:, :start]
     x0 = np.concatenate([np.broadcast_to(np.asarray(x, float), (nc, n_f)) for x in xs_list])
     ctx.set_option(_lib.OPT_PSR_BASE, int(psr_base))
     runner = FreeSpectrumChains(model, rhomin, rhomax, nc, x0)
     if start > 0:
         for p, s in enumerate(samplers):
             rows = slice(p * nc, (p + 1) * nc)
-            if multi:
-                runner.x[rows] = torch.as_tensor(s.chains[:, start - 1], device=dev)
-                runner.b[rows, :m[p]] = torch.as_tensor(s.bchains[:, start - 1], device=dev)
-            else:
-                runner.x[rows] = torch.as_tensor(s.chain[start - 1], device=dev)
-                runner.b[rows, :m[p]] = torch.as_tensor(s.bchain[start - 1], device=dev)
+            runner.x[rows] = torch.as_tensor(s.chains[:, start - 1] if multi_x else s.chain[start - 1], device=dev)
+            runner.b[rows, :m[p]] = torch.as_tensor(s.bchains[:, start - 1] if multi_b else s.bchain[start - 1],
+                                                    device=dev)
+        if multi_x and not multi_b:
+            # every chain's x is restored but only chain 0's b was kept (bchain.npy, the
+            # reference's file): chains 1.. get b drawn from b | x at their own x (Philox event
+            # GS_EV_B0 of sweep start-1), a valid Gibbs state; chain 0 keeps its recorded b, so
+            # its continuation is the uninterrupted run's bit for bit
+            ph = torch.pow(10.0, -2.0 * runner.x).repeat_interleave(2, dim=1).contiguous()
+            bnew, _ = model.bdraw(ph, nc, sweep=start - 1, event=_lib.EV_B0, chain_base=runner.chain_base)
+            keep = torch.zeros(model.P, nc, 1, dtype=torch.bool, device=dev)
+            keep[:, 0] = True
+            runner.b.copy_(torch.where(keep, runner.b.view(model.P, nc, -1),
+                                       bnew.view(model.P, nc, -1)).view_as(runner.b))
         runner.it = start - 1
         runner.run(1, record=False)        # re-run sweep start-1: row start-1's successor
     runner.it = max(runner.it, start)
@@ -144,9 +156,22 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
     bk = nc if (allb or nc == 1) else 1
     streamer = HistoryStreamer(ctx, [(blk, P * nc, n_f), (blk, P * bk, model.ldb)], direct=[True, not allb])
     bstride = bk
+    # failed (non-PD) draws, surfaced per block as they happen: the kernels keep b and count
+    # (gs_ctx_set_fail_counts); each block's counts reach pinned memory behind the block
+    fc_host = [torch.zeros(P * nc, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+    fc_ev = [torch.cuda.Event(), torch.cuda.Event()]
+    fc_seen = [int(runner.fail_count.sum())]
 
     def consume(slot, ii, nxt):
         xh, bh = (t.numpy() for t in streamer.fetch(slot))
+        fc_ev[slot].synchronize()
+        tot = int(fc_host[slot].sum())
+        if tot > fc_seen[0]:
+            bad = np.nonzero(fc_host[slot].numpy())[0]
+            print(f"WARNING: sweeps {ii}..{nxt - 1}: {tot - fc_seen[0]} b draws hit a non-positive-definite "
+                  f"Sigma (previous b kept; the reference's LinAlgError branch, pulsar_gibbs.py:507-516); "
+                  f"systems so far: {bad[:8].tolist()}{' ...' if bad.size > 8 else ''}")
+            fc_seen[0] = tot
         last = nxt - 1
         save = last % save_every == 0 and last > 0
         for p, (s, o) in enumerate(zip(samplers, outdirs)):
@@ -173,6 +198,9 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
         n = nxt - ii
         xr, br = streamer.buffers(slot, n)
         runner.run(n, x_rec=xr, b_rec=br, record_b_chains=bk)
+        with torch.cuda.stream(ctx.stream):
+            fc_host[slot].copy_(runner.fail_count, non_blocking=True)
+            fc_ev[slot].record(ctx.stream)
         streamer.submit(slot, n)
         if pending is not None:
             consume(*pending)
@@ -181,9 +209,6 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
         ii = nxt
     if pending is not None:
         consume(*pending)
-    info = runner.info.cpu().numpy()
-    if info.any():
-        print(f"WARNING: {int((info != 0).sum())} chains hit a non-positive-definite Sigma")
     b_end = runner.b.cpu().numpy()
     for p, s in enumerate(samplers):
         s._b = b_end[p * nc, :m[p]].copy()

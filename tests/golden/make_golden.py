@@ -284,6 +284,29 @@ def pta_sample_check(ref, out, niter=101, n_psr=4):
     print("pta sample:", out, g.chain.shape, saved.shape)
 
 
+def pta_long(ref, out, kind, niter=20000, seed=21, red_psr=(0,)):
+    """Long PTABlockGibbs.sample chain on the 45-pulsar array (configs[3], north_star's target
+    config) for the per-bin KS comparison of the device's CURN / CURN + red posteriors: the
+    reference's own sample loop (pta_gibbs.py:631-713), single-threaded BLAS, seeded; keeps the
+    common gw log10 rho columns (and the red bins of the pulsars in ``red_psr``) as float32."""
+    pta = synthetic.array_pta(kind=kind, seed=0)
+    np.random.seed(seed)
+    g = _quiet(ref.PTABlockGibbs, pta, hypersample="conditional",
+               redsample="conditional" if kind == "curn_red" else "mh")
+    x0 = np.concatenate([p.sample().flatten() for p in g.params])
+    with tempfile.TemporaryDirectory() as d:
+        np.random.seed(seed + 1)
+        _quiet(g.sample, x0, outdir=d, niter=niter)
+    names = list(g.param_names)
+    keep = [i for i, n in enumerate(names) if "gw" in n and "rho" in n]
+    if kind == "curn_red":
+        for p in red_psr:
+            keep += [i for i, n in enumerate(names) if n.startswith(pta.pulsars[p] + "_") and "rho" in n]
+    np.savez_compressed(out, chain=g.chain[:, keep].astype(np.float32), cols=np.array(keep),
+                        names=np.array([names[i] for i in keep]), niter=niter, x0=x0, kind=kind)
+    print("pta long:", kind, out, g.chain.shape)
+
+
 def likelihoods(ref, out):
     """White-noise and fully-marginalised likelihoods (pulsar_gibbs.py:523-546, 569-610)."""
     pta = synthetic.single_pulsar_pta("J1713+0747", seed=0, efac_vary=True, n_backends=3)
@@ -532,6 +555,10 @@ def main(root):
         if "--long" in sys.argv:
             ecorr_long(PB, os.path.join(HERE, "ecorr_long_j1713.npz"))
         return
+    for kind in ("curn", "curn_red"):
+        if f"--only-pta-long-{kind}" in sys.argv:
+            pta_long(PT, os.path.join(HERE, f"pta_long_{kind}.npz"), kind)
+            return
     if "--only-red" in sys.argv:
         red_likelihood(PB, os.path.join(HERE, "red_lnlike_j1713.npz"))
         return

@@ -42,12 +42,14 @@ void dot2(int n, const double* ah, const double* al, const double* bh, const dou
 void schur(int m, int nM, const double* A, const double* Al, double* S0) {
   const int NF = m - nM;
   std::vector<double> Lh(nM * nM, 0.0), Ll(nM * nM, 0.0), Wh(nM * NF), Wl(nM * NF);
+  std::vector<gs_dd> ri(nM);
   auto L = [&](int i, int j) -> gs_dd { return {Lh[i * nM + j], Ll[i * nM + j]}; };
   for (int i = 0; i < nM; ++i)
     for (int j = 0; j <= i; ++j) { Lh[i * nM + j] = A[i * m + j]; Ll[i * nM + j] = Al[i * m + j]; }
   for (int k = 0; k < nM; ++k) {
     gs_dd s = dd_sqrt(L(k, k)); Lh[k * nM + k] = s.hi; Ll[k * nM + k] = s.lo;
-    for (int i = k + 1; i < nM; ++i) { gs_dd v = dd_div(L(i, k), s); Lh[i * nM + k] = v.hi; Ll[i * nM + k] = v.lo; }
+    ri[k] = dd_div(gs_dd{1.0, 0.0}, s);   // k_prefix_dd: divisions as products with 1 / L_kk
+    for (int i = k + 1; i < nM; ++i) { gs_dd v = dd_mul(L(i, k), ri[k]); Lh[i * nM + k] = v.hi; Ll[i * nM + k] = v.lo; }
     for (int i = k + 1; i < nM; ++i)
       for (int j = k + 1; j <= i; ++j) {
         gs_dd v = dd_sub(L(i, j), dd_mul(L(i, k), L(j, k))); Lh[i * nM + j] = v.hi; Ll[i * nM + j] = v.lo; }
@@ -56,7 +58,7 @@ void schur(int m, int nM, const double* A, const double* Al, double* S0) {
     for (int i = 0; i < nM; ++i) {
       gs_dot2 s; s.init({A[i * m + nM + f], Al[i * m + nM + f]});
       for (int j = 0; j < i; ++j) s.fma_dd(dd_neg(L(i, j)), gs_dd{Wh[j * NF + f], Wl[j * NF + f]});
-      gs_dd w = dd_div(s.get(), L(i, i)); Wh[i * NF + f] = w.hi; Wl[i * NF + f] = w.lo;
+      gs_dd w = dd_mul(s.get(), ri[i]); Wh[i * NF + f] = w.hi; Wl[i * NF + f] = w.lo;
     }
   for (int f = 0; f < NF; ++f)
     for (int g = 0; g < NF; ++g) {

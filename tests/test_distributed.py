@@ -107,3 +107,64 @@ def test_tau_sum_allreduce_gloo_world2():
     assert out[0][0] == out[1][0]
     assert out[0][1] < 1e-12
 
+
+
+# ------------------------------------------------------------- order-free CURN exchange
+def fx_digits(tau, e0):
+    """Restatement of k_tau_sum_fx's encoding (csrc/gibbs_grid.hip) with Python integers: the
+    three 48-bit digits (as int64 sums) of sum_p floor(tau_p / 2^e0), tau [P, ...] >= 0."""
+    from fractions import Fraction
+    t = np.asarray(tau, np.float64)
+    out = np.zeros((3,) + t.shape[1:], np.int64)
+    flat = t.reshape(t.shape[0], -1)
+    o = out.reshape(3, -1)
+    for j in range(flat.shape[1]):
+        d = [0, 0, 0]
+        for v in flat[:, j]:
+            V = int(Fraction(float(v)) / Fraction(2) ** e0)      # floor (v >= 0)
+            for i in range(3):
+                d[i] += (V >> (48 * i)) & ((1 << 48) - 1)
+        o[:, j] = d
+    return out
+
+
+def fx_value(digits, e0):
+    """The exact value the digits stand for, correctly rounded to a double."""
+    from fractions import Fraction
+    d = np.asarray(digits).reshape(3, -1)
+    return np.array([float(Fraction(int(d[0, j]) + (int(d[1, j]) << 48) + (int(d[2, j]) << 96)) * Fraction(2) ** e0)
+                     for j in range(d.shape[1])])
+
+
+def _tau_case():
+    g = np.random.default_rng(5)
+    P, n_f, C = 45, 6, 4
+    # tau over 20 decades (b^2 of weak and strong bins), a few exact zeros
+    tau = 10.0 ** g.uniform(-30, -10, (P, n_f, C)) * g.uniform(0.5, 2.0, (P, n_f, C))
+    tau[g.random((P, n_f, C)) < 0.02] = 0.0
+    return tau, int(np.floor(np.log2(1e-18))) - 64
+
+
+def _fx_case(rank, world):
+    tau, e0 = _tau_case()
+    lo, hi = D.shard_range(tau.shape[0], rank, world)
+    part = torch.as_tensor(fx_digits(tau[lo:hi], e0))
+    out = D.TauSumAllReduce()(part)
+    return out.numpy().tolist()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tau_sum_fixed_point_exchange_is_shard_invariant(world):
+    """SURVEY §4 (shard counts 1/2/4/8 give identical chains) for the CURN exchange: the
+    per-rank fixed-point digits all-reduced over `world` gloo ranks equal the 1-shard digits
+    exactly, on every rank, and stand for the tau sums to double precision."""
+    tau, e0 = _tau_case()
+    one = fx_digits(tau, e0)
+    out = run_world(_fx_case, world)
+    for r in range(world):
+        assert np.array_equal(np.asarray(out[r], np.int64), one), r
+    S = fx_value(one, e0).reshape(tau.shape[1:])
+    exact = np.array([[__import__("math").fsum(tau[:, k, c]) for c in range(tau.shape[2])]
+                      for k in range(tau.shape[1])])
+    assert np.max(np.abs(S - exact) / exact) < 2.3e-16

@@ -60,8 +60,10 @@ def _worker(rank, world, port, kind, mode, S, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,mode", [("curn", "sum"), ("curn_red", "exact")])
-def test_pulsar_sharded_two_processes(tmp_path, kind, mode):
+@pytest.mark.parametrize("kind,mode,world", [("curn", "sum", 2), ("curn", "sum", 4), ("curn_red", "exact", 2)])
+def test_pulsar_sharded_processes(tmp_path, kind, mode, world):
+    """world processes on the one GPU, pulsars sharded, against the unsharded engine bit for bit
+    (CURN: the fixed-point tau-sum digits all-reduced, order-free for any shard count)."""
     if not gpu_available():
         pytest.skip("no GPU")
     import torch
@@ -71,7 +73,7 @@ def test_pulsar_sharded_two_processes(tmp_path, kind, mode):
     S = 5
     ctxm = mp.get_context("spawn")
     port = _free_port()
-    ps = [ctxm.Process(target=_worker, args=(r, 2, port, kind, mode, S, str(tmp_path))) for r in range(2)]
+    ps = [ctxm.Process(target=_worker, args=(r, world, port, kind, mode, S, str(tmp_path))) for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
@@ -86,5 +88,5 @@ def test_pulsar_sharded_two_processes(tmp_path, kind, mode):
     for i in range(S):
         ref.sweep(x_rec=xr[i])
     want = xr.cpu().numpy()
-    for r in range(2):
+    for r in range(world):
         assert np.array_equal(np.load(tmp_path / f"x{r}.npy"), want), r

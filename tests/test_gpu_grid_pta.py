@@ -364,3 +364,37 @@ def test_graph_replay_equals_eager_sweeps(kind, mode):
         xg[1 + r * K:1 + (r + 1) * K].copy_(g.graph_rec)
     torch.cuda.synchronize()
     assert torch.equal(xg, xr)
+
+
+def test_tau_sum_fixed_point_kernels():
+    """gs_tau_sum_fx: the int64 digits equal the Python-integer restatement bit for bit
+    (tests/test_distributed.fx_digits); gs_fx_to_double: the double those digits stand for,
+    correctly rounded (or at most 1 ulp off), identical for digits summed over any sharding."""
+    import torch
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd._lib import check, ptr
+    from tests.test_distributed import _tau_case, fx_digits, fx_value
+    tau, e0 = _tau_case()
+    P, n_f, C = tau.shape
+    ctx = _lib.Context(0, seed=1)
+    t = torch.as_tensor(tau, device="cuda")
+    acc = torch.zeros(3, n_f, C, dtype=torch.int64, device="cuda")
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    check(ctx.lib.gs_tau_sum_fx(ctx.handle, P, C, n_f, ptr(t), e0, ptr(acc), ptr(ovf)), "gs_tau_sum_fx")
+    want = fx_digits(tau, e0)
+    assert np.array_equal(acc.cpu().numpy(), want) and int(ovf) == 0
+    # shard digits (3 uneven blocks) added as int64 -> the same digits
+    parts = torch.zeros_like(acc)
+    for lo, hi in ((0, 7), (7, 30), (30, P)):
+        a = torch.zeros_like(acc)
+        check(ctx.lib.gs_tau_sum_fx(ctx.handle, hi - lo, C, n_f, ptr(t[lo:hi].contiguous()), e0, ptr(a), None), "fx")
+        parts += a
+    assert torch.equal(parts, acc)
+    S = torch.empty(n_f, C, dtype=torch.float64, device="cuda")
+    check(ctx.lib.gs_fx_to_double(ctx.handle, n_f * C, e0, ptr(acc), ptr(S)), "gs_fx_to_double")
+    got, ref = S.cpu().numpy().ravel(), fx_value(want, e0)
+    assert np.all(np.abs(got - ref) <= np.spacing(ref))
+    # overflow / invalid input is flagged
+    t[0, 0, 0] = -1.0
+    check(ctx.lib.gs_tau_sum_fx(ctx.handle, P, C, n_f, ptr(t), e0, ptr(acc), ptr(ovf)), "gs_tau_sum_fx")
+    assert int(ovf) == 1

@@ -100,7 +100,7 @@ def test_sweep_any_nf_matches_oracle_loop(ctx, n_f, nm):
             assert normwise_rel(br[j, c, :m], bx) < 1e-9, (n_f, nm, c, j)
 
 
-@pytest.mark.parametrize("n_f,nm", [(7, 16), (15, 0), (32, 16), (30, 100)])
+@pytest.mark.parametrize("n_f,nm", [(7, 16), (15, 0), (32, 16), (30, 48), (30, 64), (30, 100)])
 def test_lnlike_marg_any_nf(ctx, n_f, nm):
     model, T, N, r = _model(ctx, n_f, nm)
     rng = np.random.default_rng(n_f)
@@ -127,3 +127,17 @@ def test_pulsar_block_gibbs_with_15_bins_and_no_timing_model(tmp_path):
     assert chain.shape == (150, 15) and gb.bchain.shape == (150, 30)
     assert np.all(np.isfinite(gb.chains)) and gb.chains.min() >= -9 and gb.chains.max() <= -4
     assert np.load(tmp_path / "chain.npy").shape == (101, 15)
+
+
+def test_big_nf_non_pd_keeps_b(ctx):
+    """The workspace-tile draw (NF > 64): a non-PD system keeps its previous b and is flagged."""
+    model, T, N, r = _model(ctx, 40, 16)
+    assert model.NF == 80
+    rng = np.random.default_rng(4)
+    ph = np.full((2, 80), 1e12)
+    ph[0] = -1e30
+    prev = rng.standard_normal((2, model.ldb))
+    b, info = model.bdraw(dev(ph), 2, z=dev(rng.standard_normal((2, model.ldb))), out=dev(prev))
+    b, info = b.cpu().numpy(), info.cpu().numpy()
+    assert info[0] > 0 and info[1] == 0
+    assert np.array_equal(b[0], prev[0]) and np.all(np.isfinite(b[1])) and not np.array_equal(b[1], prev[1])

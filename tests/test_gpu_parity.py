@@ -154,9 +154,51 @@ def test_bdraw_matches_reference_draws(ctx, model, replay, bcast):
 
 
 def test_bdraw_flags_non_positive_definite(model):
-    ph = np.full((1, model.NF), -1e30)          # negative prior precision -> indefinite
-    b, info = model.bdraw(dev(ph), 1, z=dev(np.zeros((1, model.ldb))))
-    assert int(info[0]) > 0
+    """A non-PD system (negative prior precision) is flagged in info and keeps its previous b
+    (the reference's LinAlgError branch, pulsar_gibbs.py:507-516): no NaN reaches the state;
+    the other systems of the batch draw normally; an attached counter counts the failure."""
+    from pulsar_timing_gibbsspec_amd.engine import fail_counts
+    rng = np.random.default_rng(3)
+    C = 3
+    ph = np.full((C, model.NF), 1e12)
+    ph[1] = -1e30                               # system 1: indefinite
+    prev = rng.standard_normal((C, model.ldb))
+    out = dev(prev)
+    cnt = torch.zeros(C, dtype=torch.int32, device="cuda")
+    with fail_counts(model.ctx, cnt):
+        b, info = model.bdraw(dev(ph), C, z=dev(rng.standard_normal((C, model.ldb))), out=out)
+    b, info = b.cpu().numpy(), info.cpu().numpy()
+    assert info[1] > 0 and info[0] == 0 and info[2] == 0
+    assert np.array_equal(b[1], prev[1])
+    assert np.all(np.isfinite(b)) and not np.array_equal(b[0], prev[0])
+    assert cnt.cpu().tolist() == [0, 1, 0]
+
+
+def test_fused_sweep_non_pd_mid_run_keeps_b(ctx, model, replay):
+    """k_sweep_freespec with Sigma made indefinite mid-run (the model block's S0[0][0] set to
+    -1e300 after 10 sweeps): the failing draws keep each chain's previous b (never NaN), the
+    rho|b step goes on, every failure is counted as it happens, and once the model is restored
+    the chains draw again."""
+    from pulsar_timing_gibbsspec_amd.engine import FreeSpectrumChains
+    g = golden("single_j1713.npz")
+    C = 4
+    run = FreeSpectrumChains(model, replay["rhomin"], replay["rhomax"], C, g["x0"])
+    run.run(10)
+    b10 = run.b.clone()
+    saved = model.model.clone()
+    try:
+        model.model[0] = -1e300
+        xr, br = run.run(5)
+        assert torch.equal(run.b, b10)                       # b kept through 5 failed draws
+        assert torch.isfinite(xr).all() and torch.isfinite(br).all() and torch.isfinite(run.x).all()
+        assert not torch.equal(xr[0], xr[-1])                # rho|b kept sampling
+        assert (run.info.cpu().numpy() > 0).all()
+        assert run.fail_count.cpu().tolist() == [5] * C
+    finally:
+        model.model.copy_(saved)
+    run.run(5)
+    assert run.fail_count.cpu().tolist() == [5] * C
+    assert torch.isfinite(run.b).all() and not torch.equal(run.b, b10)
 
 
 @pytest.mark.parametrize("bcast", [0, 1, 2, 3])
@@ -273,6 +315,37 @@ def test_sample_flush_final_and_resume(tmp_path):
     res = PulsarBlockGibbs(pta, seed=8).sample(g["x0"], outdir=str(tmp_path / "b"), niter=260, resume=True,
                                                 flush_final=True)
     assert np.array_equal(res, full)
+
+
+@pytest.mark.parametrize("record_bchains", [False, True])
+def test_resume_many_chains(tmp_path, record_bchains):
+    """nchains > 16 (default: only chain 0's b reaches the host) or record_bchains=False: resume
+    reloads every chain's rows from chains.npy (rows [:start] equal the uninterrupted run's,
+    never zeros) and restarts each chain from its own x; chain 0 (the reference's chain) and,
+    with every b kept, all chains continue bit for bit; without every b, chains 1.. continue
+    from b | x redrawn (valid, finite, inside the prior)."""
+    from pulsar_timing_gibbsspec_amd import PulsarBlockGibbs, synthetic
+    g = golden("single_j1713.npz")
+    pta = synthetic.single_pulsar_pta("J1713+0747", seed=0)
+    nc = 20
+    kw = dict(record_bchains=record_bchains)
+    full = PulsarBlockGibbs(pta, seed=9, nchains=nc)
+    full.sample(g["x0"], outdir=str(tmp_path / "a"), niter=260, flush_final=True, **kw)
+    gb = PulsarBlockGibbs(pta, seed=9, nchains=nc)
+    gb.sample(g["x0"], outdir=str(tmp_path / "b"), niter=150, **kw)          # saves rows [:101]
+    res = PulsarBlockGibbs(pta, seed=9, nchains=nc)
+    res.sample(g["x0"], outdir=str(tmp_path / "b"), niter=260, resume=True, flush_final=True, **kw)
+    a = np.load(tmp_path / "a" / "chains.npy")
+    b = np.load(tmp_path / "b" / "chains.npy")
+    assert a.shape == b.shape == (nc, 260, 30)
+    assert np.array_equal(b[:, :101], a[:, :101])                  # restored, not zero rows
+    assert np.array_equal(b[0], a[0])                              # chain 0 bit for bit
+    assert np.array_equal(np.load(tmp_path / "b" / "chain.npy"), np.load(tmp_path / "a" / "chain.npy"))
+    if record_bchains:
+        assert np.array_equal(b, a)
+    else:
+        assert np.all(np.isfinite(b)) and b.min() >= -9 and b.max() <= -4
+        assert not np.array_equal(b[1:, 101:], a[1:, 101:])        # b of chains 1.. was redrawn
 
 
 def test_history_straight_to_pinned_host(model, replay):

@@ -90,3 +90,16 @@ def test_indep_array_and_pulsar_sharding():
         w = [np.sum(m[lo:hi].astype(float) ** 3) for lo, hi in blocks]
         assert max(w) <= np.sum(m.astype(float) ** 3) / world + (m.max() ** 3)
     assert balanced_blocks([1.0] * 4, 4) == [(0, 1), (1, 2), (2, 3), (3, 4)]
+
+
+def test_pulsar_array_gibbs_rejects_non_free_spectrum_pulsars():
+    """PulsarArrayGibbs fuses every pulsar into one free-spectrum sweep: a pulsar with a white-noise
+    (or red / ECORR) Metropolis block is refused up front, not by a shape error mid-run."""
+    import pytest
+    from pulsar_timing_gibbsspec_amd import synthetic
+    from pulsar_timing_gibbsspec_amd.array_gibbs import PulsarArrayGibbs
+    ok = synthetic.pulsar_ptas(synthetic.array_pta(kind="indep", seed=0))[:2]
+    PulsarArrayGibbs(ok, seed=1)                      # no GPU touched: the context is lazy
+    white = synthetic.single_pulsar_pta("J1713+0747", seed=0, efac_vary=True, n_backends=3)
+    with pytest.raises(NotImplementedError, match="free-spectrum-only"):
+        PulsarArrayGibbs([ok[0], white], seed=1)
