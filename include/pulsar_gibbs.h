@@ -65,10 +65,13 @@ enum {
                          PulsarBlockGibbs, config 5).  Read by gs_white_mh, gs_white_tnt;
                          with 1, gs_bdraw*'s chain_mask and gs_white_mh's nsteps_chain
                          are indexed by system too. */
-  GS_OPT_GRID_EXACT = 4, /* gs_rho_curn: 1 = numpy's operation order (sequential product of
-                         per-pulsar pdfs, sequential cumsum: bit-identical pdfs); 0 (default)
-                         = log-space product (one log + one exp per grid point, rcp for the
-                         ratios), equal pdfs to ~1e-15 relative */
+  GS_OPT_GRID_EXACT = 4, /* grid conditionals: 1 = numpy's operation order (sequential product
+                         of per-pulsar pdfs, sequential cumsum: bit-identical pdfs); 2 = the f64
+                         wave kernels (log-space product, one rcp per four ratios, short exp:
+                         pdfs equal to ~1e-15 relative); 0 (default) = as 2, except gs_rho_red:
+                         every point in f32 with a per-row error certificate, rows whose index
+                         the certificate cannot prove redone in f64 (indices of exact
+                         arithmetic, as 2's) */
   GS_OPT_BREC_CHAINS = 5 /* gs_sweep_freespec b_rec: 0 (default) = every system, row
                          sweep * n_psr * n_chain + p * n_chain + c; K > 0 = chains c < K of
                          each pulsar only, compact rows (sweep * n_psr + p) * K + c (the
@@ -123,6 +126,9 @@ int gs_ctx_set_sweep_counter(gs_ctx* ctx, const int64_t* sweep_dev);
  */
 int gs_ctx_set_fail_counts(gs_ctx* ctx, int32_t* counts);
 int gs_counter_add(gs_ctx* ctx, int64_t* counter, int64_t inc);
+/* int32 device counter (NULL detaches) incremented by the grid rows the certified f32 draw had to
+   redo in f64 (GS_OPT_GRID_EXACT = 0). */
+int gs_ctx_set_grid_fallback_counter(gs_ctx* ctx, int32_t* counter);
 
 /* Doubles per pulsar in a model buffer (see gs_prefix). */
 int64_t gs_model_stride(int NF, int NMX);

@@ -59,6 +59,7 @@ SIGNATURES = {
     "gs_ctx_set_sweep_counter": (_I, [_P, _P]),
     "gs_counter_add": (_I, [_P, _P, _I64]),
     "gs_ctx_set_fail_counts": (_I, [_P, _P]),
+    "gs_ctx_set_grid_fallback_counter": (_I, [_P, _P]),
     "gs_lnlike_marg": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P]),
     "gs_rho_curn_sum": (_I, [_P, _I, _I, _I, _P, _I, _P, _P, _I64, _I64, _P, _I, _P, _P]),
     "gs_rho_gumbel": (_I, [_P, _I, _I, _P, _P, _I, _P, _P, _I64, _I64, _P, _I, _P, _P]),

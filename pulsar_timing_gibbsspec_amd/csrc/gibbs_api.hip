@@ -17,6 +17,7 @@ struct gs_ctx {
   int brec_nc = 0;     // GS_OPT_BREC_CHAINS
   const int64_t* sweep_dev = nullptr;  // gs_ctx_set_sweep_counter
   int32_t* fail_counts = nullptr;      // gs_ctx_set_fail_counts
+  int32_t* grid_fallback = nullptr;    // gs_ctx_set_grid_fallback_counter
   double* ws = nullptr;  // tile workspace of the large-NF b-draw (grown on demand)
   size_t ws_bytes = 0;
 };
@@ -244,7 +245,7 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
       ctx->psr_base = value;
       return 0;
     case GS_OPT_GRID_EXACT:
-      if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_GRID_EXACT must be 0 or 1");
+      if (value < 0 || value > 2) return fail_arg(3, "GS_OPT_GRID_EXACT must be 0, 1 or 2");
       ctx->grid_exact = value;
       return 0;
     case GS_OPT_BREC_CHAINS:
@@ -279,6 +280,12 @@ int gs_ctx_set_sweep_counter(gs_ctx* ctx, const int64_t* sweep_dev) {
 int gs_ctx_set_fail_counts(gs_ctx* ctx, int32_t* counts) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   ctx->fail_counts = counts;
+  return 0;
+}
+
+int gs_ctx_set_grid_fallback_counter(gs_ctx* ctx, int32_t* counter) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  ctx->grid_fallback = counter;
   return 0;
 }
 
@@ -523,6 +530,7 @@ static int grid_common(gs_ctx* ctx, GridArgs& a, int n_psr, int n_chain, int n_f
   a.chain_base = chain_base; a.tau = tau; a.irn = irn; a.grid3 = grid3; a.u = u; a.xcol = xcol; a.x = x;
   a.idx_out = idx_out; a.key = key_of(ctx); a.psr_base = ctx->psr_base;
   a.exact = ctx->grid_exact;
+  a.n_fallback = ctx->grid_fallback;
   return 0;
 }
 

@@ -477,6 +477,9 @@ __device__ __forceinline__ double red_ratio(double tau, double a) {
 // mode uses the short exp (gibbs_common.h, <= 2 ulp), EXACT the device library's
 template <bool EXACT>
 __device__ __forceinline__ double red_pdf(double tau, double a) {
+  // numpy's rounding: no fma contraction (-ffp-contract=fast would fuse the product into the
+  // caller's running sum, which numpy does not)
+#pragma clang fp contract(off)
   const double ratio = red_ratio<EXACT>(tau, a);
   return ratio * (EXACT ? exp(-ratio / 2) : gs_exp_neg(-0.5 * ratio)) * LN10;
 }
@@ -507,7 +510,10 @@ __global__ void k_rho_red(GridArgs A) {
   for (int j = 0; j < GS_RED_NCH; ++j) {
     const int g1 = min(A.ngrid, (j + 1) * ch);
 #pragma unroll 8
-    for (int g = j * ch; g < g1; ++g) cum += red_pdf<EXACT>(tau, gw + A.grid3[g]);
+    for (int g = j * ch; g < g1; ++g) {
+#pragma clang fp contract(off)
+      cum += red_pdf<EXACT>(tau, gw + A.grid3[g]);
+    }
     ck[j] = cum;
   }
   const double total = cum;
@@ -534,6 +540,7 @@ __global__ void k_rho_red(GridArgs A) {
     const int g1 = min(A.ngrid, (jx + 1) * ch);
 #pragma unroll 4
     for (int g = jx * ch; g < g1; ++g) {
+#pragma clang fp contract(off)
       cc += red_pdf<EXACT>(tau, gw + A.grid3[g]);
       cnt += below(cc) ? 1 : 0;
     }
@@ -617,6 +624,159 @@ __global__ __launch_bounds__(256) void k_rho_red_wave(GridArgs A) {
     if (A.idx_out) A.idx_out[r] = myidx;
     A.x[(int64_t)c * A.ldx + A.xcol[p * A.n_f + k]] = A.grid3[2 * A.ngrid + myidx];
   }
+}
+
+// ------------------------------------------------------------ a7 default: certified two-level draw
+// k_rho_red_wave's row walk with every grid point evaluated in FP32, and the index accepted only
+// when it is provably the exact-arithmetic one; otherwise the row is redone in FP64 (the
+// k_rho_red_wave arithmetic).  Per point (all f32): a = gw' + rho'_g, y = 1/a (v_rcp_f32),
+// t = tl y, x = tl2 y, E = 2^-x (v_exp_f32), pdf' = t E, with the row's scales
+// th = (tau/2) = thm 2^e, tl = thm log2e, tl2 = th log2e 2^S, gw' = gw 2^S, rho'_g = rho_g 2^S
+// (S = -ilogb(rho_min): every a in [1, 2^120)), so pdf' = h e^-h up to a row constant
+// (h = th / (gw + rho_g) = x ln2): no f32 underflow in the ratios, only in e^-h itself.
+//
+// E = 2^(xm - x) with xm = the row's smallest x (at rho_max): the row constant 2^xm cancels in
+// cdf / max, and the largest E is ~1, so the row never underflows as a whole.
+//
+// Certificate.  Relative error of each pdf' (first order, eps = 2^-24): the inputs' f32
+// roundings and the add (3 eps), v_rcp_f32 (2 eps), tl (3 eps), the products (2 eps), v_exp_f32
+// (2 eps) and the exponents' own errors carried through 2^(xm - x) (ln2 (8 eps x + 7 eps xm)):
+// below (12 + 5.6 x + 4.9 xm) eps.  Sums of positives: 21 additions per prefix (16 in the lane,
+// 6 in the scan) and 3 roundings in the thresholds.  So every computed cum_j and the total are
+// within D = eps (80 T + 18 w + 12 xm T) + 2e-35 of the exact ones, T = total, w = sum pdf' x,
+// the last term for points whose E is subnormal or flushed (t <= 1.45, <= 1024 points), with a
+// margin of ~2 on every term.  The exact index is #{j : cum*_j < u T*} - 1; if no computed cum_j
+// lies in [u T - 2D, u T + 2D) that count equals the computed one, and the f64 cdfs (within
+// ~1e-15 of exact) give the same index too.  Otherwise (probability
+// below), or if the f32 row degenerates (T not a normal float), the wave redoes the row in f64.  Indices are therefore those of exact
+// arithmetic wherever the f32 path answers, the same contract as the f64 wave kernel's (which
+// differs from numpy's order only within ~1e-16 of a cdf value); an unproven row is redone with
+// that kernel's f64 arithmetic, so the default mode returns GS_OPT_GRID_EXACT = 2's index on every
+// row.  Fallback rate: u lands within 2D of one of the ~1000 cdf values with probability
+// ~ 1000 x 4 D / T, about 1 % of rows (measured 1.3 % on rows spanning 16 decades of tau).
+__global__ __launch_bounds__(256) void k_rho_red_cert(GridArgs A, int32_t* n_fallback) {
+  __shared__ double tb[64];  // the f64 redo's exp table
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
+  __syncthreads();
+  const int64_t nrow = (int64_t)A.n_psr * A.n_f * A.n_chain;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
+  if (r0 >= nrow) return;
+  const int64_t r = r0 + lane;
+  const bool rok = r < nrow;
+  const int64_t rr = rok ? r : r0;
+  const int c = (int)(rr % A.n_chain);
+  const int k = (int)((rr / A.n_chain) % A.n_f);
+  const int p = (int)(rr / ((int64_t)A.n_chain * A.n_f));
+  double u;
+  if (A.u) {
+    u = A.u[((int64_t)c * A.n_psr + p) * A.n_f + k];
+  } else {
+    double u2;
+    gs_uniform2(gs_counter(k, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, p + A.psr_base, GS_EV_RED), A.key, u, u2);
+  }
+  const double tau = A.tau[rr];
+  const double gw = A.irn[(int64_t)k * A.n_chain + c];
+  const int S = -ilogb(A.grid3[0]);  // rho_min 2^S in [1, 2)
+  float rg32[RW_G];
+#pragma unroll
+  for (int j = 0; j < RW_G; ++j) {
+    const int g = RW_G * lane + j;
+    // off-grid slots: a = inf -> y = 0 -> t = 0 and 2^min(xm - x, 0) = 1: pdf' exactly 0
+    rg32[j] = g < A.ngrid ? (float)ldexp(A.grid3[g], S) : __builtin_inff();
+  }
+  unsigned long long valid[RW_G];
+#pragma unroll
+  for (int j = 0; j < RW_G; ++j) valid[j] = __ballot(RW_G * lane + j < A.ngrid);
+  const int nr = (int)min((int64_t)64, nrow - r0);
+  const double sc = 1.4426950408889634 * 0.5 * ldexp(1.0, S);
+  const float rgmax32 = (float)ldexp(A.grid3[A.ngrid - 1], S);
+  int myidx = 0, nfb = 0;
+  for (int i = 0; i < nr; ++i) {
+    const double taui = rdlane(tau, i), gwi = rdlane(gw, i), ui = rdlane(u, i);
+    int e;
+    const double thm = frexp(0.5 * taui, &e);
+    const float tl = (float)thm * 1.44269504f;
+    const float tl2 = (float)(taui * sc);
+    const float gw32 = (float)ldexp(gwi, S);
+    // the row's smallest exponent (largest rho): E = 2^(xm - x) <= 1, the row maximum of e^-h
+    // scaled to ~1, so the row never underflows as a whole
+    const float xm = tl2 * __builtin_amdgcn_rcpf(gw32 + rgmax32);
+    float cum[RW_G];
+    float loc = 0.0f, w = 0.0f;
+#pragma unroll
+    for (int j = 0; j < RW_G; ++j) {
+      const float a = gw32 + rg32[j];
+      const float y = __builtin_amdgcn_rcpf(a);
+      const float t = tl * y, x = tl2 * y;
+      const float pdf = t * __builtin_amdgcn_exp2f(fminf(xm - x, 0.0f));
+      w = fmaf(pdf, x, w);
+      loc += pdf;
+      cum[j] = loc;
+    }
+    float incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    float excl = __shfl_up(incl, 1);
+    if (lane == 0) excl = 0.0f;
+    float wsum = w;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wsum += __shfl_xor(wsum, o);
+    const float T = __shfl(incl, 63);
+    int idx = 0;
+    bool done = false;
+    if (T > 1e-33f && T < 3e38f && wsum < 3e38f) {  // wave-uniform
+      // + the absolute error of points whose 2^(xm - x) is subnormal or flushed (t <= 1.45)
+      const float D = 5.9604645e-08f * (80.0f * T + 18.0f * wsum + 12.0f * xm * T) + 2e-35f;
+      const float uT = (float)ui * T;
+      const float tlo = (uT - 2.0f * D) - excl, thr = (uT + 2.0f * D) - excl;
+      int clo = 0, chi = 0;
+#pragma unroll
+      for (int j = 0; j < RW_G; ++j) {
+        clo += __popcll(__ballot(cum[j] < tlo) & valid[j]);
+        chi += __popcll(__ballot(cum[j] < thr) & valid[j]);
+      }
+      if (clo == chi) {
+        idx = clo - 1;
+        done = true;
+      }
+    }
+    if (!done) {
+      // unproven row (~1 % of rows: 1000 cdf values, each known to ~1e-6): redone in f64 with
+      // k_rho_red_wave's arithmetic, so the default mode returns GS_OPT_GRID_EXACT = 2's index
+      // on every row
+      ++nfb;
+      double rg[RW_G], cumd[RW_G];
+#pragma unroll
+      for (int j = 0; j < RW_G; ++j) {
+        const int g = RW_G * lane + j;
+        rg[j] = g < A.ngrid ? A.grid3[g] : 1e60;
+      }
+      const double locd = red_lane_cumsum<RW_G>(0.5 * taui, gwi, rg, tb, cumd);
+      double incd = locd;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double v = __shfl_up(incd, o);
+        if (lane >= o) incd += v;
+      }
+      const double total = rdlane(incd, 63);
+      const double thd = ui * total - (incd - locd);
+      int cnt = 0;
+#pragma unroll
+      for (int j = 0; j < RW_G; ++j) cnt += __popcll(__ballot(cumd[j] < thd) & valid[j]);
+      idx = cnt - 1;
+    }
+    if (idx < 0) idx += A.ngrid;
+    myidx = (lane == i) ? idx : myidx;
+  }
+  if (rok) {
+    if (A.idx_out) A.idx_out[r] = myidx;
+    A.x[(int64_t)c * A.ldx + A.xcol[p * A.n_f + k]] = A.grid3[2 * A.ngrid + myidx];
+  }
+  if (n_fallback && lane == 0 && nfb) atomicAdd(n_fallback, nfb);
 }
 
 // ------------------------------------------------------------ a4: Gumbel-max
@@ -740,7 +900,7 @@ int launch_tau(hipStream_t s, const TauArgs& a) {
 int launch_rho_curn(hipStream_t s, const GridArgs& a) {
   const int64_t n = (int64_t)a.n_f * a.n_chain;
   if (n == 0) return 0;
-  if (!a.exact && a.ngrid <= 64 * CF_MAXG) {
+  if (a.exact != 1 && a.ngrid <= 64 * CF_MAXG) {
     hipLaunchKernelGGL(k_rho_curn_fast, grid1(n, 4), dim3(256), 0, s, a);
     return 0;
   }
@@ -785,8 +945,10 @@ int launch_rho_curn_sum(hipStream_t s, const GridArgs& a) {
 int launch_rho_red(hipStream_t s, const GridArgs& a) {
   const int64_t n = (int64_t)a.n_psr * a.n_f * a.n_chain;
   if (n == 0) return 0;
-  if (a.exact)
+  if (a.exact == 1)
     hipLaunchKernelGGL(k_rho_red<true>, grid1(n, 64), dim3(64), 0, s, a);
+  else if (a.ngrid <= 64 * RW_G && a.exact == 0)
+    hipLaunchKernelGGL(k_rho_red_cert, grid1(n, 256), dim3(256), 0, s, a, a.n_fallback);
   else if (a.ngrid <= 64 * RW_G)
     hipLaunchKernelGGL(k_rho_red_wave, grid1(n, 256), dim3(256), 0, s, a);
   else

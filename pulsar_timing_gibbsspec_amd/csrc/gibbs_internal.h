@@ -117,7 +117,9 @@ struct TauArgs {
 
 struct GridArgs {
   int n_psr, n_chain, n_f, ngrid, ldx, psr_base;
-  int exact;  // GS_OPT_GRID_EXACT: numpy's operation order (bit-exact pdfs)
+  int exact;  // GS_OPT_GRID_EXACT: 1 numpy's operation order (bit-exact pdfs); 0 certified f32 /
+              // f64 two-level draw (red grid); 2 the f64 wave kernels
+  int32_t* n_fallback;  // gs_ctx_set_grid_fallback_counter: rows redone in f64, or NULL
   int64_t sweep, chain_base;
   const int64_t* sweep_dev;  // ctx sweep counter (graph replay) or NULL
   const double *tau, *irn, *grid3, *u;

@@ -394,7 +394,9 @@ class PTAChains:
         self.P, self.C, self.n_param = P, C, int(n_param)
         self.PG = int(P_global) if P_global is not None else P
         self.psr_lo = int(psr_lo)
-        self.sharded = self.PG != P
+        # the exchange runs when pulsars are split over ranks, or whenever one is given (a
+        # 1-rank group exercises the same launch sequence, e.g. to capture it in a graph)
+        self.sharded = self.PG != P or (allreduce if curn_mode == "sum" else gather) is not None
         self.gather = gather
         if curn_mode not in ("exact", "sum"):
             raise ValueError("curn_mode must be 'exact' or 'sum'")
@@ -521,17 +523,26 @@ class PTAChains:
         self.it += 1
 
     def capture(self, n_sweeps):
-        """Capture n_sweeps steady-state sweeps (device Philox, unsharded) into a hipGraph
+        """Capture n_sweeps steady-state sweeps (device Philox) into a hipGraph
         (torch.cuda.CUDAGraph around the C-ABI launches on the context's stream).
 
         Philox counters take sweep = launch argument + a device counter
         (gs_ctx_set_sweep_counter), which the graph advances itself (gs_counter_add),
         so every replay draws the next n_sweeps sweeps: replays are bit-identical to
-        eager sweeps.  The graph records x into ``graph_rec`` (n_sweeps, C, n_param)."""
+        eager sweeps.  The graph records x into ``graph_rec`` (n_sweeps, C, n_param).
+
+        A pulsar-sharded engine captures its per-sweep exchange too: the RCCL all-reduce of
+        the fixed-point tau-sum digits (or the [tau | x_red] all-gather) is issued on the
+        capture stream and becomes a node of the graph, so a replay runs n_sweeps sweeps with
+        no return to the host.  That needs the 'nccl' (RCCL) backend; gloo collectives run on
+        the host and cannot be captured."""
         if self.it == 0:
             raise ValueError("run sweep 0 eagerly first (it draws b from x0, pta_gibbs.py:669-670)")
         if self.sharded:
-            raise NotImplementedError("graph capture of the pulsar-sharded exchange")
+            import torch.distributed as dist
+            if not dist.is_initialized() or dist.get_backend() != "nccl":
+                raise NotImplementedError("graph capture of the pulsar-sharded exchange needs the 'nccl' "
+                                          "(RCCL) backend; gloo collectives run on the host")
         lib, h, dev = self.ctx.lib, self.ctx.handle, self.ctx.device
         n = int(n_sweeps)
         self.graph_rec = torch.empty(n, self.C, self.n_param, dtype=torch.float64, device=dev)

@@ -31,7 +31,13 @@ class PTABlockGibbs(object):
     (van Haasteren & Vallisneri 2014)."""
 
     def __init__(self, pta, hypersample="conditional", redsample="mh", *, nchains=1, device=0,
-                 seed=None):
+                 seed=None, curn_mode="auto"):
+        # the common draw (pta_gibbs.py:181-214): 'exact' = the product of per-pulsar pdfs;
+        # 'sum' = the same law from the tau sums (no per-pulsar red noise only); 'auto' picks
+        # 'sum' when the model has no per-pulsar red free spectrum
+        if curn_mode not in ("auto", "exact", "sum"):
+            raise ValueError("curn_mode must be 'auto', 'exact' or 'sum'")
+        self.curn_mode = curn_mode
         self.pta = pta
         self.hypersample = hypersample
         self.redsample = redsample
@@ -147,9 +153,10 @@ class PTABlockGibbs(object):
         model = self._model(xs)
         hind = self.get_hyper_param_indices()
         red_col = hind.reshape(len(self.pta.pulsars), -1) if hind.size else None
+        mode = self.curn_mode if self.curn_mode != "auto" else ("exact" if red_col is not None else "sum")
         return PTAChains(model, len(self.param_names), self.get_rho_param_indices(), red_col,
                          (self.rhomin_gw, self.rhomax_gw), (self.rhomin_red, self.rhomax_red),
-                         self.nchains, np.asarray(xs, float), chain_base=chain_base)
+                         self.nchains, np.asarray(xs, float), chain_base=chain_base, curn_mode=mode)
 
     # ------------------------------------------------------------ conditionals (single-call API)
     def _engine_at(self, xs):

@@ -90,3 +90,53 @@ def test_pulsar_sharded_processes(tmp_path, kind, mode, world):
     want = xr.cpu().numpy()
     for r in range(world):
         assert np.array_equal(np.load(tmp_path / f"x{r}.npy"), want), r
+
+
+def _capture_worker(port, kind, mode, out_dir):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        from pulsar_timing_gibbsspec_amd import _lib
+        from pulsar_timing_gibbsspec_amd.distributed import PulsarAllGather, TauSumAllReduce
+        from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
+        T, N, R, names, rind, red_col, gwid, fixed = _setup(kind)
+        C = 8
+        x0 = np.random.default_rng(0).uniform(-9, -4, (C, len(names)))
+        ex = dict(allreduce=TauSumAllReduce()) if mode == "sum" else \
+            dict(gather=PulsarAllGather([np.arange(len(T))], ((2 if red_col is not None else 1), 30, C), device="cuda"))
+        # the exchange engine (RCCL collective in every sweep) and the plain one, same seeds
+        eng = PTAChains(DeviceModel(_lib.Context(0, seed=31), T, N, R, gwid, fixed), len(names), rind, red_col,
+                        (1e-18, 1e-8), (1e-20, 1e-8), C, x0, curn_mode=mode, **ex)
+        ref = PTAChains(DeviceModel(_lib.Context(0, seed=31), T, N, R, gwid, fixed), len(names), rind, red_col,
+                        (1e-18, 1e-8), (1e-20, 1e-8), C, x0, curn_mode=mode)
+        assert eng.sharded and not ref.sharded
+        eng.sweep()
+        rec = eng.capture(4)                      # sweeps 1..4, the all-reduce / all-gather inside
+        got = []
+        for _ in range(2):
+            got.append(eng.replay().clone())
+        want = torch.zeros(9, C, len(names), dtype=torch.float64, device="cuda")
+        for i in range(9):
+            ref.sweep(x_rec=want[i])
+        np.save(os.path.join(out_dir, "got.npy"), torch.cat(got).cpu().numpy())
+        np.save(os.path.join(out_dir, "want.npy"), want[1:].cpu().numpy())
+        assert rec.shape == (4, C, len(names))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,mode", [("curn", "sum"), ("curn_red", "exact")])
+def test_graph_capture_with_rccl_exchange(tmp_path, kind, mode):
+    """PTAChains.capture of sweeps whose exchange is an RCCL collective (1-rank 'nccl' group on the
+    one GPU): the collective is a node of the hipGraph, and two replays (8 sweeps) equal 8 eager
+    sweeps of the engine without an exchange bit for bit."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch.multiprocessing as mp
+    p = mp.get_context("spawn").Process(target=_capture_worker, args=(_free_port(), kind, mode, str(tmp_path)))
+    p.start()
+    p.join(timeout=240)
+    assert p.exitcode == 0
+    assert np.array_equal(np.load(tmp_path / "got.npy"), np.load(tmp_path / "want.npy"))

@@ -62,13 +62,14 @@ def test_gumbel_kernel_exact(ctx):
     assert np.array_equal(x.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("grid_exact", [1, 0])
+@pytest.mark.parametrize("grid_exact", [1, 0, 2])
 @pytest.mark.parametrize("kind", ["curn", "curn_red"])
 def test_grid_cdf_kernels_exact(ctx, kind, grid_exact, request):
     """a6 (and a7) on every sweep's recorded inputs: indices equal to the reference's.
-    grid_exact=1: numpy's operation order (bit-identical pdfs/cdfs); grid_exact=0 (the
-    default): log-space CURN product and rcp-Newton ratios (pdfs within ~1e-15 relative:
-    an index could differ only for u within that of a cdf value — none on the fixtures)."""
+    grid_exact=1: numpy's operation order (bit-identical pdfs/cdfs); grid_exact=2: log-space CURN
+    product and rcp-Newton ratios (pdfs within ~1e-15 relative: an index could differ only for u
+    within that of a cdf value — none on the fixtures); grid_exact=0 (the default): as 2 with the
+    red grid in certified f32 (rows the certificate cannot prove redone in f64)."""
     from pulsar_timing_gibbsspec_amd import _lib
     _lib.check(ctx.lib.gs_ctx_set_option(ctx.handle, _lib.OPT_GRID_EXACT, grid_exact), "set_option")
     request.addfinalizer(lambda: ctx.lib.gs_ctx_set_option(ctx.handle, _lib.OPT_GRID_EXACT, 0))
@@ -398,3 +399,69 @@ def test_tau_sum_fixed_point_kernels():
     t[0, 0, 0] = -1.0
     check(ctx.lib.gs_tau_sum_fx(ctx.handle, P, C, n_f, ptr(t), e0, ptr(acc), ptr(ovf)), "gs_tau_sum_fx")
     assert int(ovf) == 1
+
+
+def test_red_grid_certified_f32_matches_exact(ctx, request):
+    """The default red-grid draw (GS_OPT_GRID_EXACT = 0: f32 points + per-row error certificate,
+    f64 redo of unproven rows) on 86k random rows spanning 16 decades of tau and 10 of gw: the
+    same index as the f64 wave kernel (= 2) on every row, and as numpy's operation order (= 1) on
+    every row whose u is not placed on a cdf value.  Rows with u exactly on a cdf value (computed
+    in f64 as the reference does) cannot be certified in f32: they take the f64 path (counted)."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import grid3
+    request.addfinalizer(lambda: ctx.lib.gs_ctx_set_option(ctx.handle, _lib.OPT_GRID_EXACT, 0))
+    rng = np.random.default_rng(11)
+    P, n_f, C = 45, 30, 64
+    lo, hi = 1e-20, 1e-8
+    tau = 10 ** rng.uniform(-22, -6, (P, n_f, C))
+    gw = 10 ** rng.uniform(-18, -8, (n_f, C))
+    u = rng.random((C, P, n_f))
+    # adversarial rows: u exactly at the f64 cdf value of a random index
+    rho = O.rho_grid(lo, hi)
+    adv = [(p, k, c) for p, k, c in zip(rng.integers(0, P, 40), rng.integers(0, n_f, 40), rng.integers(0, C, 40))]
+    for p, k, c in adv:
+        ratio = tau[p, k, c] / (gw[k, c] + rho)
+        cdf = np.cumsum(ratio * np.exp(-ratio / 2) * np.log(10))
+        cdf /= cdf.max()
+        j = int(rng.integers(100, 900))
+        u[c, p, k] = cdf[j]
+    G = grid3(lo, hi)
+    xcol = torch.arange(P * n_f, dtype=torch.int32, device="cuda")
+    out = {}
+    fb = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for mode in (1, 2, 0):
+        _lib.check(ctx.lib.gs_ctx_set_option(ctx.handle, _lib.OPT_GRID_EXACT, mode), "set_option")
+        x = torch.zeros(C, P * n_f, dtype=torch.float64, device="cuda")
+        idx = torch.zeros(P * n_f * C, dtype=torch.int32, device="cuda")
+        K = Keep()
+        _lib.check(ctx.lib.gs_ctx_set_grid_fallback_counter(ctx.handle, _lib.ptr(fb)), "counter")
+        try:
+            _lib.check(ctx.lib.gs_rho_red(ctx.handle, P, C, n_f, K(tau), K(gw), 1000, _lib.ptr(G), K(u), 0, 0,
+                                          _lib.ptr(x), P * n_f, _lib.ptr(xcol), _lib.ptr(idx)), "gs_rho_red")
+        finally:
+            _lib.check(ctx.lib.gs_ctx_set_grid_fallback_counter(ctx.handle, None), "counter")
+        out[mode] = idx.cpu().numpy()
+        if mode != 0:
+            fb.zero_()
+    nfb = int(fb)
+    advset = {(p * n_f + k) * C + c for p, k, c in adv}   # row r = (p * n_f + k) * C + c
+    assert np.array_equal(out[0], out[2]), int(np.sum(out[0] != out[2]))
+    keep = np.ones(out[0].size, bool)
+    keep[list(advset)] = False
+    bad = np.nonzero((out[0] != out[1]) & keep)[0]
+    if bad.size:
+        info = []
+        for q in bad[:6]:
+            p_, rem = divmod(int(q), n_f * C)
+            k_, c_ = divmod(rem, C)
+            ratio = tau[p_, k_, c_] / (gw[k_, c_] + rho)
+            cdf = np.cumsum(ratio * np.exp(-ratio / 2) * np.log(10))
+            cdf /= cdf.max()
+            j0 = int(out[1][q])
+            info.append(dict(row=int(q), adversarial=int(q) in advset, cert=int(out[0][q]), exact=j0,
+                             u=float(u[c_, p_, k_]), cdf=cdf[max(0, j0 - 1):j0 + 2].tolist(),
+                             tau=float(tau[p_, k_, c_]), gw=float(gw[k_, c_])))
+        pytest.fail(f"{bad.size} rows differ (fallbacks {nfb}): {info}")
+    # the adversarial rows, and ~1 % of the others (u within the certificate's margin of one of
+    # ~1000 cdf values)
+    assert len(adv) <= nfb < 0.03 * out[0].size, nfb
