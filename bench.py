@@ -117,11 +117,33 @@ def event_ms(stream, fn, reps):
 
 
 def grid_peak():
-    """Measured grid-evaluation ceiling (tools/probe/grid_probe.hip -> profiles/grid_probe.json)."""
+    """Measured ceiling of the round-2 kernels' own op mixes (tools/probe/grid_probe.hip ->
+    profiles/grid_probe.json); reported beside the hardware roof as `op_mix_ceiling`."""
     try:
         return json.load(open(os.path.join(ROOT, "profiles", "grid_probe.json")))
     except (OSError, ValueError):
         return None
+
+
+# Hardware VALU roof (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'; the FP64 vector peak
+# 78.6 TF = 1024 SIMDs x 2.4 GHz x 16 FMA lanes per clock): a wave64 add/mul/fma/min/cmp (f64 or
+# f32) issues in 4 SIMD cycles, a transcendental (v_rcp / v_exp / v_log) in 8.
+SIMDS, CLOCK_HZ = 1024, 2.4e9
+
+
+def valu_roof(plain, transc):
+    """Units/s the whole chip can issue when one unit needs `plain` 4-cycle and `transc` 8-cycle
+    lane operations (the grid kernels' stated minimal op counts)."""
+    return SIMDS * CLOCK_HZ * 64 / (4.0 * plain + 8.0 * transc)
+
+
+# minimal lane operations per unit: red grid point h e^-h (pta_gibbs.py:265-266) = gw + rho,
+# 1/a, tau y, e^-h, h e^-h, the running sum and the searchsorted compare; CURN term of the pdf
+# product (pta_gibbs.py:192-205) = one Horner FMA each for the product D(rho) = prod (rho + irn)
+# and the ratio numerator N(rho) (no per-term division or log; the kernel groups 4 pulsars and
+# spends 2.5); CURN-from-sums grid point = one FMA (c_g - S w_g), the row max, e^x, the running
+# sum and the compare.
+GRID_MIN_OPS = {"red": (5, 2), "curn_term": (2, 0), "curn_sum": (4, 1)}
 
 
 def cpu_line(kind, seconds):
@@ -207,12 +229,14 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain"):
             h, eng.P, C, n_f, _lib.ptr(eng.tau), _lib.ptr(eng.gwphi), eng.ngrid, _lib.ptr(eng.grid_red), None,
             eng.it, eng.chain_base, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.red_col), None)), 5)
         ev = eng.P * n_f * C * eng.ngrid
-        kernels["k_rho_red"] = dict(kernel_avg_ms=ms_r, bound="valu", unit="Geval/s",
-                                    achieved=ev / (ms_r * 1e-3) / 1e9, alg_per_launch=ev,
-                                    peak=(gp["red_evals_per_s"] / 1e9) if gp else None,
-                                    note="grid-point evaluations ratio*exp(-ratio/2)*ln10 (pta_gibbs.py:265-266): "
-                                         "P x n_f x C x 1000 per launch; peak = the op mix's register-only ceiling "
-                                         "(tools/probe/grid_probe.hip, profiles/grid_probe.json)")
+        kernels["k_rho_red_cert"] = dict(
+            kernel_avg_ms=ms_r, bound="valu", unit="Geval/s", achieved=ev / (ms_r * 1e-3) / 1e9,
+            alg_per_launch=ev, peak=valu_roof(*GRID_MIN_OPS["red"]) / 1e9,
+            min_ops_per_unit=dict(zip(("plain", "transcendental"), GRID_MIN_OPS["red"])),
+            op_mix_ceiling_f64_wave=(gp["red_evals_per_s"] / 1e9) if gp else None,
+            note="grid-point evaluations ratio*exp(-ratio/2)*ln10 (pta_gibbs.py:265-266): P x n_f x C x 1000 "
+                 "per launch (certified f32 pass, f64 redo of unproven rows); peak = hardware VALU issue rate "
+                 "/ the minimal op count per point (5 plain at 4 cycles + rcp and exp at 8 per wave64)")
         if not sharded:
             check(lib, lib.gs_phi_from_x(h, C, eng.PG * n_f, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.red_col_g),
                                          _lib.ptr(eng.irn)))
@@ -222,9 +246,11 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain"):
             ev = eng.PG * n_f * C * eng.ngrid
             kernels["k_rho_curn_fast"] = dict(
                 kernel_avg_ms=ms_c, bound="valu", unit="Gterm/s", achieved=ev / (ms_c * 1e-3) / 1e9,
-                alg_per_launch=ev, peak=(gp["curn_pulsar_terms_per_s"] / 1e9) if gp else None,
+                alg_per_launch=ev, peak=valu_roof(*GRID_MIN_OPS["curn_term"]) / 1e9,
+                min_ops_per_unit=dict(zip(("plain", "transcendental"), GRID_MIN_OPS["curn_term"])),
+                op_mix_ceiling=(gp["curn_pulsar_terms_per_s"] / 1e9) if gp else None,
                 note="(grid point, pulsar) terms of the common pdf product (pta_gibbs.py:192-205): "
-                     "P x n_f x C x 1000 per launch; peak from tools/probe/grid_probe.hip")
+                     "P x n_f x C x 1000 per launch; peak = hardware f64 VALU issue rate / 2 FMAs per term")
     else:
         ms_s = event_ms(st, lambda: check(lib, lib.gs_rho_curn_sum(
             h, eng.PG, C, n_f, _lib.ptr(eng.S), eng.ngrid, _lib.ptr(eng.grid_gw), None, eng.it, eng.chain_base,
@@ -232,11 +258,14 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain"):
         ev = n_f * C * eng.ngrid
         kernels["k_rho_curn_sum"] = dict(kernel_avg_ms=ms_s, bound="valu", unit="Geval/s",
                                          achieved=ev / (ms_s * 1e-3) / 1e9, alg_per_launch=ev,
-                                         peak=(gp.get("curn_sum_evals_per_s", gp["red_evals_per_s"]) / 1e9)
+                                         peak=valu_roof(*GRID_MIN_OPS["curn_sum"]) / 1e9,
+                                         min_ops_per_unit=dict(zip(("plain", "transcendental"),
+                                                                   GRID_MIN_OPS["curn_sum"])),
+                                         op_mix_ceiling=(gp.get("curn_sum_evals_per_s", gp["red_evals_per_s"]) / 1e9)
                                          if gp else None,
-                                         note="n_f x C x 1000 grid points of the common pdf from the tau sums "
-                                              "(one FMA + one exp each); peak = that op mix's register-only "
-                                              "ceiling (tools/probe/grid_probe.hip k_curn_sum)")
+                                         note="n_f x C x 1000 grid points of the common pdf from the tau sums; "
+                                              "peak = hardware VALU issue rate / the minimal op count per point "
+                                              "(4 plain at 4 cycles + one exp at 8 per wave64)")
     for k in kernels.values():
         k["frac"] = (k["achieved"] / k["peak"]) if k.get("peak") else None
     dom = max(kernels, key=lambda k: kernels[k]["kernel_avg_ms"])
@@ -445,15 +474,23 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
     mR, NF, nM = em.mR, em.NF, em.nm
     flops = C * (ne * (mR + 1) * (mR + 2) + nM * (NF + 1) * (NF + 2) + (NF + 1) ** 3 // 3)
     tflops = flops / (k_ms * 1e-3) / 1e12
+    # algorithmic HBM bytes of one launch: every chain's own operands, read once -- the [B | d_E]
+    # rows (ne x ldbx), the upper 16x16 tiles of Ap (nb (nb + 1) / 2 of them, nb = ldbx / 16),
+    # the epoch diagonal, phiinv_F -- and lnl + aux written
+    nb = em.ldbx // 16
+    alg_bytes = C * 8 * (ne * em.ldbx + 256 * nb * (nb + 1) // 2 + ne + NF + 5)
+    traffic = _ecorr_traffic(C, "pmc_traffic_ecorr_white.json")
     return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 chains_per_gpu=C, m=m, n_epoch=ne, aclength_white=aclength, aclength_ecorr=aclength,
                 roofline={"bound": "mfma", "kernel": "k_ecorr_prefix<likelihood mode, per-chain operands>",
                           "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": tflops / FP64_PEAK_TFLOPS, "kernel_avg_ms": k_ms, "alg_flops_per_launch": flops,
-                          "traffic": _ecorr_traffic(C, "pmc_traffic_ecorr_white.json"),
-                          "note": "as the ecorr line; each chain's [B | d_E] rows stream from HBM (343 MB of "
-                                  "algorithmic reads per 4096-chain launch; traffic = PMC FETCH_SIZE x2 + "
-                                  "WRITE_SIZE, the x2 wide-read correction makes it an upper estimate)"},
+                          "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
+                          "traffic_over_alg": (traffic / alg_bytes) if traffic else None,
+                          "hbm_frac": alg_bytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                          "note": "as the ecorr line; each chain's own [B | d_E] rows and Ap tiles stream from "
+                                  "HBM (alg_bytes_per_launch); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE, the x2 "
+                                  "wide-read correction makes it an upper estimate"},
                 config="SURVEY 8f-4 with EFAC/EQUAD sampled: J1713-like pulsar, 2 backends, 136 ECORR epochs, "
                        "white MH + per-chain TNT + ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
 

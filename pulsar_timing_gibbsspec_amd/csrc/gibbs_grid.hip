@@ -270,24 +270,30 @@ __global__ __launch_bounds__(256) void k_rho_curn_sum(GridArgs A) {
 // uniform as k_rho_red_wave, each lane's 16 grid points prepared once per wave as
 // c_g = -P log rho_g and w_g = 1 / (2 rho_g), so a row costs one FMA (log pdf = c_g - S w_g),
 // the wave maximum, the LDS-table exp and the scan / count per point.
+// RPW rows per wave: 64 at the round-2 default; the CURN line's 30 x 2048 rows are then only 960
+// waves (under one per SIMD), so fewer rows per wave buy occupancy for the per-wave grid setup.
 constexpr int CSW_G = 16;
+#ifndef GS_CSW_RPW
+#define GS_CSW_RPW 16
+#endif
 
+template <int RPW>
 __global__ __launch_bounds__(256) void k_rho_curn_sum_wave(GridArgs A) {
   __shared__ double tb[64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
   __syncthreads();
   const int64_t nrow = (int64_t)A.n_f * A.n_chain;
-  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * RPW;
   if (r0 >= nrow) return;
   const int64_t r = r0 + lane;
-  const bool rok = r < nrow;
+  const bool rok = lane < RPW && r < nrow;
   const int64_t rr = rok ? r : r0;
   const int c = (int)(rr % A.n_chain), k = (int)(rr / A.n_chain);
-  double u;
+  double u = 0.0;
   if (A.u) {
     u = A.u[(int64_t)c * A.n_f + k];
-  } else {
+  } else if (lane < RPW) {
     double u2;
     gs_uniform2(gs_counter(k, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, 0, GS_EV_CURN), A.key, u, u2);
   }
@@ -304,7 +310,7 @@ __global__ __launch_bounds__(256) void k_rho_curn_sum_wave(GridArgs A) {
   unsigned long long valid[CSW_G];
 #pragma unroll
   for (int j = 0; j < CSW_G; ++j) valid[j] = __ballot(CSW_G * lane + j < A.ngrid);
-  const int nr = (int)min((int64_t)64, nrow - r0);
+  const int nr = (int)min((int64_t)RPW, nrow - r0);
   int myidx = 0;
   for (int i = 0; i < nr; ++i) {
     const double nS = -rdlane(S, i), ui = rdlane(u, i);
@@ -347,16 +353,28 @@ __global__ __launch_bounds__(256) void k_rho_curn_sum_wave(GridArgs A) {
 // ------------------------------------------------------------ a6 fast: CURN product in log space
 // The same draw as k_rho_curn without numpy's operation order (GS_OPT_GRID_EXACT = 0,
 // the default): log pdf_g = -sum_p log(irn_p + rho_g) - 1/2 sum_p tau_p / (irn_p + rho_g)
-// + const (sum_p log tau_p and P log ln10 cancel in cdf / max).  Per (grid point, pulsar):
-// one add, two multiplies and one FMA (the ratio sum kept as a fraction N / D over the
-// product D of (irn + rho), renormalised by frexp every 8 pulsars) -- instead of a
-// division and an exp; one log, one division and one exp per grid point.  pdf rounding differs from
-// numpy's by ~1e-15 relative, so the index can only differ when u falls that close to a
-// cdf value (tested equal to the reference on every fixture sweep).  One wavefront per
-// row, lane l owns grid points [l G, (l+1) G), wave scan of the lane sums.
+// + const (sum_p log tau_p and P log ln10 cancel in cdf / max).  The ratio sum is kept as one
+// fraction N / D over the product D of (irn + rho), taken CF_K pulsars at a time: for a group,
+// D_grp(rho) = prod_i (rho + irn_i) and N_grp(rho) = sum_i tau_i prod_{j != i} (rho + irn_j) are
+// polynomials in rho whose coefficients (all positive: no cancellation) depend on the row only,
+// so lane q computes group q's once per row and every grid point evaluates them by Horner
+// (CF_K + CF_K - 1 FMAs), then N <- N D_grp + D N_grp, D <- D D_grp: 2 CF_K + 2 f64 ops per
+// (point, group), 2.5 per (point, pulsar) at CF_K = 4 instead of 4 (add, two multiplies and an
+// FMA per pulsar).  D and N are rescaled together every CF_RN groups by one power of two per
+// lane (the lane's 16 neighbouring grid points keep D within a few decades of each other).  One
+// log, one division and one exp per grid point at the end.  pdf rounding differs from numpy's
+// by ~1e-15 relative, so the index can only differ when u falls that close to a cdf value
+// (tested equal to the reference on every fixture sweep and to the numpy-order kernel on random
+// rows).  One wavefront per row, lane l owns grid points [l G, (l+1) G), wave scan of the lane
+// sums.
 constexpr int CF_MAXG = 16;  // grid points per lane (ngrid <= 1024)
+constexpr int CF_K = 4;      // pulsars per coefficient group
+constexpr int CF_RN = 2;     // groups between rescalings: (2 rho_min)^(CF_K CF_RN) must stay normal
 
-__global__ __launch_bounds__(256) void k_rho_curn_fast(GridArgs A) {
+#ifndef GS_CF_MINW
+#define GS_CF_MINW 3
+#endif
+__global__ __launch_bounds__(256, GS_CF_MINW) void k_rho_curn_fast(GridArgs A) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + wave;
   const int64_t nrow = (int64_t)A.n_f * A.n_chain;
@@ -364,42 +382,64 @@ __global__ __launch_bounds__(256) void k_rho_curn_fast(GridArgs A) {
   const int c = (int)(r % A.n_chain), k = (int)(r / A.n_chain);
   const int G = (A.ngrid + 63) / 64;
   const int g0 = lane * G;
-  // Per grid point: D = prod_p (irn_p + rho), N / D = sum_p tau_p / (irn_p + rho) kept as one
-  // fraction (N <- N a + tau D, D <- D a: three multiplies and an FMA per (point, pulsar),
-  // no division); D and N are rescaled together by D's binary exponent every 8 pulsars.
   double rg[CF_MAXG], dd[CF_MAXG], nn[CF_MAXG];
-  int ex[CF_MAXG];
 #pragma unroll
   for (int j = 0; j < CF_MAXG; ++j) {
     const int g = min(g0 + j, A.ngrid - 1);
     rg[j] = A.grid3[g];
     dd[j] = 1.0;
     nn[j] = 0.0;
-    ex[j] = 0;
   }
+  int ex = 0;  // the lane's common binary exponent of dd (and nn)
   const int P = A.n_psr;
-  // the row's (tau_p, irn_p) for up to 64 pulsars at a time: lane p loads pulsar p0 + p once
-  // (instead of two loads + a full memory-latency wait per pulsar inside the product loop),
-  // the loop reads them back by v_readlane
-  for (int p0 = 0; p0 < P; p0 += 64) {
-    const int np = min(64, P - p0);
-    const double tl = lane < np ? A.tau[(int64_t)(p0 + lane) * nrow + r] : 0.0;
-    const double il = (lane < np && A.irn) ? A.irn[(int64_t)(p0 + lane) * nrow + r] : 0.0;
-    for (int q = 0; q < np; ++q) {
-      const int p = p0 + q;
-      const double tau = rdlane(tl, q), irn = rdlane(il, q);
+  // 64 groups (256 pulsars) at a time: lane q builds group q's coefficients from its pulsars'
+  // (tau, irn), ascending powers: D_grp = sum_e pc[e] rho^e, N_grp = sum_e qc[e] rho^e
+  for (int p0 = 0; p0 < P; p0 += 64 * CF_K) {
+    const int ng = min(64, (P - p0 + CF_K - 1) / CF_K);
+    double pc[CF_K + 1], qc[CF_K];
+#pragma unroll
+    for (int e = 0; e <= CF_K; ++e) pc[e] = e == 0 ? 1.0 : 0.0;
+#pragma unroll
+    for (int e = 0; e < CF_K; ++e) qc[e] = 0.0;
+    if (lane < ng) {
+#pragma unroll
+      for (int i = 0; i < CF_K; ++i) {
+        const int p = p0 + CF_K * lane + i;
+        if (p < P) {
+          const double tau = A.tau[(int64_t)p * nrow + r];
+          const double irn = A.irn ? A.irn[(int64_t)p * nrow + r] : 0.0;
+          // N <- N (rho + irn) + tau D, D <- D (rho + irn), on the coefficients
+#pragma unroll
+          for (int e = CF_K - 1; e >= 0; --e) qc[e] = fma(irn, qc[e], (e > 0 ? qc[e - 1] : 0.0) + tau * pc[e]);
+#pragma unroll
+          for (int e = CF_K; e >= 0; --e) pc[e] = fma(irn, pc[e], e > 0 ? pc[e - 1] : 0.0);
+        }
+      }
+    }
+    for (int q = 0; q < ng; ++q) {
+      double a[CF_K + 1], b[CF_K];
+#pragma unroll
+      for (int e = 0; e <= CF_K; ++e) a[e] = rdlane(pc[e], q);
+#pragma unroll
+      for (int e = 0; e < CF_K; ++e) b[e] = rdlane(qc[e], q);
 #pragma unroll
       for (int j = 0; j < CF_MAXG; ++j) {
-        const double a = irn + rg[j];
-        nn[j] = fma(nn[j], a, tau * dd[j]);
-        dd[j] *= a;
+        const double x = rg[j];
+        double pd = fma(a[CF_K], x, a[CF_K - 1]);
+#pragma unroll
+        for (int e = CF_K - 2; e >= 0; --e) pd = fma(pd, x, a[e]);
+        double qn = fma(b[CF_K - 1], x, b[CF_K - 2]);
+#pragma unroll
+        for (int e = CF_K - 3; e >= 0; --e) qn = fma(qn, x, b[e]);
+        nn[j] = fma(nn[j], pd, dd[j] * qn);
+        dd[j] *= pd;
       }
-      if ((p & 7) == 7 || p == P - 1) {
+      if ((q % CF_RN) == CF_RN - 1 || q == ng - 1) {
+        const int e = __builtin_amdgcn_frexp_exp(dd[0]);
+        ex += e;
 #pragma unroll
         for (int j = 0; j < CF_MAXG; ++j) {
-          const int e = __builtin_amdgcn_frexp_exp(dd[j]);
-          ex[j] += e;
-          dd[j] = __builtin_amdgcn_frexp_mant(dd[j]);
+          dd[j] = ldexp(dd[j], -e);
           nn[j] = ldexp(nn[j], -e);
         }
       }
@@ -412,7 +452,7 @@ __global__ __launch_bounds__(256) void k_rho_curn_fast(GridArgs A) {
   for (int j = 0; j < CF_MAXG; ++j) {
     lp[j] = -__builtin_inf();
     if (j < G && g0 + j < A.ngrid) {
-      lp[j] = -(gs_log_pos(dd[j]) + ex[j] * LN2) - 0.5 * (nn[j] * rcp_nr2(dd[j]));
+      lp[j] = -(gs_log_pos(dd[j]) + ex * LN2) - 0.5 * (nn[j] * rcp_nr2(dd[j]));
       mx = fmax(mx, lp[j]);
     }
   }
@@ -564,6 +604,7 @@ __global__ void k_rho_red(GridArgs A) {
 // in cdf / max.  Sums differ from np.cumsum's sequential order by rounding (~1e-16 relative),
 // so an index can only differ when u falls that close to a cdf value.
 constexpr int RW_G = 16;  // grid points per lane (ngrid <= 1024)
+typedef float gs_f2 __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(256) void k_rho_red_wave(GridArgs A) {
   __shared__ double tb[64];
@@ -629,14 +670,17 @@ __global__ __launch_bounds__(256) void k_rho_red_wave(GridArgs A) {
 // ------------------------------------------------------------ a7 default: certified two-level draw
 // k_rho_red_wave's row walk with every grid point evaluated in FP32, and the index accepted only
 // when it is provably the exact-arithmetic one; otherwise the row is redone in FP64 (the
-// k_rho_red_wave arithmetic).  Per point (all f32): a = gw' + rho'_g, y = 1/a (v_rcp_f32),
-// t = tl y, x = tl2 y, E = 2^-x (v_exp_f32), pdf' = t E, with the row's scales
+// k_rho_red_wave arithmetic).  Per point (all f32, two points per packed v_pk_* op): a = gw' +
+// rho'_g, y = 1/a (v_rcp_f32), t = tl y, x = tl2 y, E = 2^-x (v_exp_f32), pdf' = t E, with the
+// row's scales
 // th = (tau/2) = thm 2^e, tl = thm log2e, tl2 = th log2e 2^S, gw' = gw 2^S, rho'_g = rho_g 2^S
 // (S = -ilogb(rho_min): every a in [1, 2^120)), so pdf' = h e^-h up to a row constant
 // (h = th / (gw + rho_g) = x ln2): no f32 underflow in the ratios, only in e^-h itself.
 //
 // E = 2^(xm - x) with xm = the row's smallest x (at rho_max): the row constant 2^xm cancels in
-// cdf / max, and the largest E is ~1, so the row never underflows as a whole.
+// cdf / max, and the largest E is ~1, so the row never underflows as a whole.  The exponent
+// xm - x is one FMA, fma(-tl2, y, xm): 7 x + 6 xm eps of absolute error, within the 8 x + 7 xm of
+// the separately rounded x and difference that the bound below is written for.
 //
 // Certificate.  Relative error of each pdf' (first order, eps = 2^-24): the inputs' f32
 // roundings and the add (3 eps), v_rcp_f32 (2 eps), tl (3 eps), the products (2 eps), v_exp_f32
@@ -678,12 +722,15 @@ __global__ __launch_bounds__(256) void k_rho_red_cert(GridArgs A, int32_t* n_fal
   const double tau = A.tau[rr];
   const double gw = A.irn[(int64_t)k * A.n_chain + c];
   const int S = -ilogb(A.grid3[0]);  // rho_min 2^S in [1, 2)
-  float rg32[RW_G];
+  // the lane's points in pairs for the packed f32 ops (v_pk_add / v_pk_mul / v_pk_fma_f32)
+  gs_f2 rg2[RW_G / 2], on2[RW_G / 2];
 #pragma unroll
   for (int j = 0; j < RW_G; ++j) {
     const int g = RW_G * lane + j;
-    // off-grid slots: a = inf -> y = 0 -> t = 0 and 2^min(xm - x, 0) = 1: pdf' exactly 0
-    rg32[j] = g < A.ngrid ? (float)ldexp(A.grid3[g], S) : __builtin_inff();
+    // off-grid slots: a = inf -> y = 0 -> t = 0, and the exponent's xm is masked by on = 0, so
+    // e = 0 and E = 1: pdf' exactly 0
+    rg2[j / 2][j % 2] = g < A.ngrid ? (float)ldexp(A.grid3[g], S) : __builtin_inff();
+    on2[j / 2][j % 2] = g < A.ngrid ? 1.0f : 0.0f;
   }
   unsigned long long valid[RW_G];
 #pragma unroll
@@ -702,18 +749,28 @@ __global__ __launch_bounds__(256) void k_rho_red_cert(GridArgs A, int32_t* n_fal
     // the row's smallest exponent (largest rho): E = 2^(xm - x) <= 1, the row maximum of e^-h
     // scaled to ~1, so the row never underflows as a whole
     const float xm = tl2 * __builtin_amdgcn_rcpf(gw32 + rgmax32);
+    // Per pair of points: a = gw' + rho', y = 1/a, t = tl y, e = xm - tl2 y (one FMA: the
+    // exponent's error is within the two-rounding form's the certificate assumes), E = 2^e,
+    // pdf' = t E; w' = sum pdf' (-e), so that sum pdf' x = xm T + w' (x = xm - e).
+    const gs_f2 gw2 = {gw32, gw32}, tlv = {tl, tl}, ntl2v = {-tl2, -tl2}, xm2 = {xm, xm};
     float cum[RW_G];
-    float loc = 0.0f, w = 0.0f;
+    float loc = 0.0f;
+    gs_f2 w2 = {0.0f, 0.0f};
 #pragma unroll
-    for (int j = 0; j < RW_G; ++j) {
-      const float a = gw32 + rg32[j];
-      const float y = __builtin_amdgcn_rcpf(a);
-      const float t = tl * y, x = tl2 * y;
-      const float pdf = t * __builtin_amdgcn_exp2f(fminf(xm - x, 0.0f));
-      w = fmaf(pdf, x, w);
-      loc += pdf;
+    for (int j = 0; j < RW_G; j += 2) {
+      const gs_f2 a = gw2 + rg2[j / 2];
+      const gs_f2 y = {__builtin_amdgcn_rcpf(a[0]), __builtin_amdgcn_rcpf(a[1])};
+      const gs_f2 t = tlv * y;
+      const gs_f2 e = __builtin_elementwise_fma(ntl2v, y, xm2 * on2[j / 2]);
+      const gs_f2 E = {__builtin_amdgcn_exp2f(e[0]), __builtin_amdgcn_exp2f(e[1])};
+      const gs_f2 pdf = t * E;
+      w2 = __builtin_elementwise_fma(pdf, -e, w2);
+      loc += pdf[0];
       cum[j] = loc;
+      loc += pdf[1];
+      cum[j + 1] = loc;
     }
+    const float w = w2[0] + w2[1];
     float incl = loc;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -726,6 +783,7 @@ __global__ __launch_bounds__(256) void k_rho_red_cert(GridArgs A, int32_t* n_fal
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wsum += __shfl_xor(wsum, o);
     const float T = __shfl(incl, 63);
+    wsum = fmaf(xm, T, wsum);  // sum pdf' x
     int idx = 0;
     bool done = false;
     if (T > 1e-33f && T < 3e38f && wsum < 3e38f) {  // wave-uniform
@@ -936,7 +994,7 @@ int launch_rho_curn_sum(hipStream_t s, const GridArgs& a) {
   const int64_t n = (int64_t)a.n_f * a.n_chain;
   if (n == 0) return 0;
   if (a.ngrid <= 64 * CSW_G)
-    hipLaunchKernelGGL(k_rho_curn_sum_wave, grid1(n, 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_rho_curn_sum_wave<GS_CSW_RPW>, grid1(n, 4 * GS_CSW_RPW), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(k_rho_curn_sum, grid1(n, 4), dim3(256), 0, s, a);
   return 0;

@@ -465,3 +465,39 @@ def test_red_grid_certified_f32_matches_exact(ctx, request):
     # the adversarial rows, and ~1 % of the others (u within the certificate's margin of one of
     # ~1000 cdf values)
     assert len(adv) <= nfb < 0.03 * out[0].size, nfb
+
+
+@pytest.mark.parametrize("with_red", [True, False])
+def test_curn_fast_matches_numpy_order_on_random_rows(ctx, request, with_red):
+    """The default CURN draw (k_rho_curn_fast: grouped-polynomial N / D product, log-space pdf)
+    against numpy's operation order (GS_OPT_GRID_EXACT = 1) on 7680 random rows of 45 pulsars
+    whose tau follows each row's own rho (ratio / 2 ~ Exp(1) at rho_true, so the product over
+    pulsars stays representable as in a real chain), with and without per-pulsar red noise
+    spanning 9 decades: the same index on every row (pdfs agree to ~1e-15 relative, so a row could
+    only differ if u fell that close to a cdf value)."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import grid3
+    request.addfinalizer(lambda: ctx.lib.gs_ctx_set_option(ctx.handle, _lib.OPT_GRID_EXACT, 0))
+    rng = np.random.default_rng(5 + with_red)
+    P, n_f, C = 45, 30, 256
+    lo, hi = 1e-18, 1e-8
+    rho_true = 10 ** rng.uniform(-16, -9, (1, n_f, C))
+    irn = 10 ** rng.uniform(-18, -9, (P, n_f, C)) if with_red else np.zeros((P, n_f, C))
+    tau = (irn + rho_true) * rng.exponential(2.0, (P, n_f, C))
+    u = rng.random((C, n_f))
+    G = grid3(lo, hi)
+    xcol = torch.arange(n_f, dtype=torch.int32, device="cuda")
+    out = {}
+    for mode in (1, 0):
+        _lib.check(ctx.lib.gs_ctx_set_option(ctx.handle, _lib.OPT_GRID_EXACT, mode), "set_option")
+        x = torch.zeros(C, n_f, dtype=torch.float64, device="cuda")
+        idx = torch.zeros(n_f * C, dtype=torch.int32, device="cuda")
+        K = Keep()
+        _lib.check(ctx.lib.gs_rho_curn(ctx.handle, P, C, n_f, K(tau), K(irn) if with_red else None, 1000,
+                                       _lib.ptr(G), K(u), 0, 0, _lib.ptr(x), n_f, _lib.ptr(xcol), _lib.ptr(idx)),
+                   "gs_rho_curn")
+        out[mode] = idx.cpu().numpy()
+    bad = np.nonzero(out[0] != out[1])[0]
+    assert bad.size == 0, (bad.size, bad[:8].tolist(), out[0][bad[:8]].tolist(), out[1][bad[:8]].tolist())
+    # the draws are spread over the grid, not piled on one end
+    assert len(np.unique(out[1])) > 200

@@ -31,9 +31,10 @@ def one(res, frag):
 HOT = [
     ("k_bdrawILi60ELi0ELi4ELi3E", 3, 0),           # PTA / CURN b|rho (configs[3])
     ("k_sweep_freespecILi60ELi0ELi4ELi3E", 2, 0),  # headline fused sweep (configs[1], [2])
-    ("k_rho_red_waveE", 4, 0),                     # CURN + red grid CDF
-    ("k_rho_curn_fastE", 2, 0),
-    ("k_rho_curn_sum_waveE", 2, 0),
+    ("k_rho_red_waveE", 4, 0),                     # CURN + red grid CDF (f64 wave kernel)
+    ("k_rho_red_certE", 4, 0),                     # CURN + red grid CDF (default: certified f32)
+    ("k_rho_curn_fastE", 3, 0),                    # 0.60 -> 0.53 ms at 3 waves/SIMD (round 3)
+    ("k_rho_curn_sum_waveILi16EE", 2, 0),
     ("k_white_syrkILi14EE", 2, 0),                 # configs[4] per-chain TNT (m = 216)
     ("k_tntEPK", 4, 0),                            # TNT / d, compensated block sums
 ]
