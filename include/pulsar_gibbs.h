@@ -72,11 +72,15 @@ enum {
                          every point in f32 with a per-row error certificate, rows whose index
                          the certificate cannot prove redone in f64 (indices of exact
                          arithmetic, as 2's) */
-  GS_OPT_BREC_CHAINS = 5 /* gs_sweep_freespec b_rec: 0 (default) = every system, row
+  GS_OPT_BREC_CHAINS = 5, /* gs_sweep_freespec b_rec: 0 (default) = every system, row
                          sweep * n_psr * n_chain + p * n_chain + c; K > 0 = chains c < K of
                          each pulsar only, compact rows (sweep * n_psr + p) * K + c (the
                          reference's bchain is chain 0: K = 1 puts n_psr rows per sweep on
                          the host instead of staging every chain's b in HBM) */
+  GS_OPT_PHI_PER_CHAIN = 6 /* 1: gs_bdraw*'s phiinv_F holds ONE row per chain (n_chain x NF),
+                         shared by every pulsar -- the CURN sweep without per-pulsar red noise,
+                         whose phiinv is the common spectrum alone (pta_gibbs.py:512-548); 0
+                         (default): one row per (pulsar, chain) system */
 };
 
 typedef struct gs_ctx gs_ctx;
@@ -278,6 +282,9 @@ int gs_tau_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, 
 int gs_tau_sum_fx(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, int e0, int64_t* acc,
                   int32_t* ovf);
 int gs_fx_to_double(gs_ctx* ctx, int64_t n, int e0, const int64_t* acc, double* S);
+/* gs_tau followed by gs_tau_sum_fx in one pass over b (tau never stored): the same digits. */
+int gs_tau_sum_fx_b(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const int32_t* fidx, const double* b,
+                    int e0, int64_t* acc, int32_t* ovf);
 int gs_rho_curn_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* S, int ngrid,
                     const double* grid3, const double* u, int64_t sweep, int64_t chain_base, double* x,
                     int ldx, const int32_t* xcol, int32_t* idx_out);

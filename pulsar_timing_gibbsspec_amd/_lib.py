@@ -23,6 +23,7 @@ OPT_PSR_BASE = 2
 OPT_X_PER_SYS = 3
 OPT_GRID_EXACT = 4
 OPT_BREC_CHAINS = 5
+OPT_PHI_PER_CHAIN = 6
 EV_B0, EV_RHO, EV_B, EV_RED, EV_CURN, EV_GUMBEL, EV_WHITE, EV_REDMH, EV_USER = 1, 2, 3, 4, 5, 6, 7, 8, 16
 EV_ECORR, EV_ECORR_B, EV_ECORR_B0 = 9, 10, 11
 
@@ -55,6 +56,7 @@ SIGNATURES = {
     "gs_rho_red": (_I, [_P, _I, _I, _I, _P, _P, _I, _P, _P, _I64, _I64, _P, _I, _P, _P]),
     "gs_tau_sum": (_I, [_P, _I, _I, _I, _P, _P]),
     "gs_tau_sum_fx": (_I, [_P, _I, _I, _I, _P, _I, _P, _P]),
+    "gs_tau_sum_fx_b": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _P, _P]),
     "gs_fx_to_double": (_I, [_P, _I64, _I, _P, _P]),
     "gs_ctx_set_sweep_counter": (_I, [_P, _P]),
     "gs_counter_add": (_I, [_P, _P, _I64]),

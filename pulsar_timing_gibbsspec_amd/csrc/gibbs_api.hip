@@ -15,6 +15,7 @@ struct gs_ctx {
   int x_per_sys = 0;  // GS_OPT_X_PER_SYS
   int grid_exact = 0;  // GS_OPT_GRID_EXACT
   int brec_nc = 0;     // GS_OPT_BREC_CHAINS
+  int phi_per_chain = 0;  // GS_OPT_PHI_PER_CHAIN
   const int64_t* sweep_dev = nullptr;  // gs_ctx_set_sweep_counter
   int32_t* fail_counts = nullptr;      // gs_ctx_set_fail_counts
   int32_t* grid_fallback = nullptr;    // gs_ctx_set_grid_fallback_counter
@@ -256,6 +257,10 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
       if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_X_PER_SYS must be 0 or 1");
       ctx->x_per_sys = value;
       return 0;
+    case GS_OPT_PHI_PER_CHAIN:
+      if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_PHI_PER_CHAIN must be 0 or 1");
+      ctx->phi_per_chain = value;
+      return 0;
     default:
       return fail_arg(2, "unknown option");
   }
@@ -268,6 +273,7 @@ int gs_ctx_get_option(gs_ctx* ctx, int option) {
   if (option == GS_OPT_X_PER_SYS) return ctx->x_per_sys;
   if (option == GS_OPT_GRID_EXACT) return ctx->grid_exact;
   if (option == GS_OPT_BREC_CHAINS) return ctx->brec_nc;
+  if (option == GS_OPT_PHI_PER_CHAIN) return ctx->phi_per_chain;
   return -1;
 }
 
@@ -413,6 +419,7 @@ static int bdraw_impl(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.fail_count = ctx->fail_counts;
   a.model_per_sys = per_sys;
   a.mask_per_sys = ctx->x_per_sys;
+  a.phi_per_chain = ctx->phi_per_chain;
   if (big) {
     launch_bdraw_big(ctx->stream, a, ctx->ws);
     return after_launch("k_bdraw_big");
@@ -578,6 +585,22 @@ int gs_tau_sum_fx(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* ta
   if (e0 < -1000 || e0 > 800) return fail_arg(6, "e0 out of range");
   launch_tau_sum_fx(ctx->stream, n_psr, (int64_t)n_f * n_chain, tau, e0, (long long*)acc, ovf);
   return after_launch("k_tau_sum_fx");
+}
+
+int gs_tau_sum_fx_b(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const int32_t* fidx, const double* b,
+                    int e0, int64_t* acc, int32_t* ovf) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
+  if (n_psr >= (1 << 15)) return fail_arg(2, "n_psr >= 32768 (int64 digit headroom)");
+  if (NF <= 0 || (NF & 1)) return fail_arg(4, "NF must be even");
+  if (ldb < NF) return fail_arg(5, "ldb < NF");
+  if (!fidx || !b || !acc) return fail_arg(6, "NULL array");
+  if (e0 < -1000 || e0 > 800) return fail_arg(8, "e0 out of range");
+  TauArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.ldb = ldb; a.half = 0; a.fidx = fidx; a.b = b;
+  a.tau = nullptr;
+  launch_tau_sum_fx_b(ctx->stream, a, e0, (long long*)acc, ovf);
+  return after_launch("k_tau_sum_fx_b");
 }
 
 int gs_fx_to_double(gs_ctx* ctx, int64_t n, int e0, const int64_t* acc, double* S) {

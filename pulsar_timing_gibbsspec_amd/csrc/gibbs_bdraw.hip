@@ -238,7 +238,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
   const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
   const int mi = lane < nM ? mrow[lane] : 0;
   const int mia = 64 + lane < nM ? mrow[64 + lane] : 0;
-  const double phinv = lane < NF ? A.phiinv_F[sys * NF + lane] : 0.0;
+  const double phinv = lane < NF ? A.phiinv_F[(A.phi_per_chain ? (int64_t)c : sys) * NF + lane] : 0.0;
   double zF = 0.0, zM = 0.0, zMa = 0.0;
   if (A.z) {
     zF = lane < NF ? A.z[sys * A.ldb + fi] : 0.0;
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
   const int nM = A.nm[p];
   const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
   const int mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
-  const double phinv = lane < NF ? A.phiinv_F[sys * NF + lane] : 0.0;
+  const double phinv = lane < NF ? A.phiinv_F[(A.phi_per_chain ? (int64_t)c : sys) * NF + lane] : 0.0;
   double zF = 0.0, zM = 0.0;
   if (A.z) {
     zF = lane < NF ? A.z[sys * A.ldb + fi] : 0.0;

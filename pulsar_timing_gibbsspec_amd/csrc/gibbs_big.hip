@@ -75,7 +75,7 @@ __global__ __launch_bounds__(64 * BIG_WPB) void k_bdraw_big(BdrawArgs A, double*
   const int32_t* midx = A.midx + (int64_t)p * NMX;
 
   // ---- per-system vectors into LDS: phiinv_F, [z_F | z_M]
-  for (int f = lane; f < 16 * NT; f += 64) ph[f] = (f < NF) ? A.phiinv_F[sys * NF + f] : 1.0;
+  for (int f = lane; f < 16 * NT; f += 64) ph[f] = (f < NF) ? A.phiinv_F[(A.phi_per_chain ? (int64_t)ch : sys) * NF + f] : 1.0;
   if (A.z) {
     for (int f = lane; f < NF; f += 64) zb[f] = A.z[sys * A.ldb + fidx[f]];
     if (lane < nM) zb[NF + lane] = A.z[sys * A.ldb + midx[lane]];

@@ -31,6 +31,16 @@ __device__ __forceinline__ double ec_wave_sum(double v) {
   return v;
 }
 
+// the wave sum as a wave-uniform value in an SGPR pair (readfirstlane): kept across the
+// 256-VGPR epilogue of k_ecorr_prefix<5> without holding (or spilling) a VGPR pair
+__device__ __forceinline__ double ec_wave_sum_u(double v) {
+  v = ec_wave_sum(v);
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u & 0xffffffffull));
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // 1/phi_k and log phi_k of backend k from log10_ecorr (phi = 10**(2 x), get_phiinv = 1/phi)
 __device__ __forceinline__ void ec_phi(double x, double& inv, double& lg) {
   const double ph = pow(10.0, 2.0 * x);
@@ -175,7 +185,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
 // the M diagonal, d as row/column 16 + NF, (d, d) = 0 and 1 on every padded diagonal.
 // Accumulated tiles are the UPPER ones, (j, r) for j <= r (block row M first), so the
 // C layout of every off-diagonal tile is directly the B operand of a left product.
-// Epilogue per wavefront, all in registers: T = Ap - P; tile_elim (DPP column
+// Epilogue per wavefront, all in registers: T = Ap - P (the accumulators start at Ap); tile_elim (DPP column
 // elimination, gibbs_tile.h) factors T_MM = U^T U -> V = U^-1 = L_M^-T; W_r = V^T T_0r,
 // S_jr = T_jr - W_j^T W_r (4 MFMA each).
 //   LNL = false: G_r = V W_r and S are written into the model block (gs_prefix layout) that
@@ -211,9 +221,24 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
 
   // tile slots: 0 = (0,0); r = (0,r) for r = 1..NTF; (j,r), 1 <= j <= r: NB + tix(j-1, r-1)
   auto ts = [](int j, int r) { return NB + gtile::tix(j - 1, r - 1, NTF); };
+  // The accumulators start at Ap and the MFMAs subtract (weights negated): T = Ap - P comes
+  // out of the epoch loop with no epilogue loads (loaded after the loop, the 60 Ap doubles sat
+  // beside the 60 accumulated ones and spilled).
+  const double* Apc = A.Ap + (int64_t)(live ? ch_id : 0) * A.ap_cs;
+  auto Aq = [&](int r0, int c0, int s) { return Apc[(int64_t)(r0 + 4 * s + q) * LDB + c0 + c]; };
   gs_d4_t acc[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = gs_d4_t{0.0, 0.0, 0.0, 0.0};
+  for (int s = 0; s < 4; ++s) acc[0][s] = live ? Aq(0, 0, s) : 0.0;
+#pragma unroll
+  for (int r = 1; r < NB; ++r)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc[r][s] = live ? Aq(0, 16 * r, s) : 0.0;
+#pragma unroll
+  for (int jj = 1; jj < NB; ++jj)
+#pragma unroll
+    for (int r = jj; r < NB; ++r)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[ts(jj, r)][s] = live ? Aq(16 * jj, 16 * r, s) : 0.0;
   double sla = 0.0, slp = 0.0;
   constexpr int LPT = EC_CH * LDB / (64 * EC_WAVES);  // chunk elements per thread
   double reg[LPT];
@@ -280,7 +305,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
       for (int kk = 0; kk < PCH / 4; ++kk) {
         if (kk >= nk) break;
         const double* row = buf + (4 * kk + q) * LDB + c;
-        const double wk = wsl[4 * kk + q];
+        const double wk = -wsl[4 * kk + q];
         double v[NB];
 #pragma unroll
         for (int r = 0; r < NB; ++r) v[r] = row[16 * r];
@@ -310,7 +335,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
     for (int kk = 0; kk < EC_CH / 4; ++kk) {
       if (kk >= nk) break;
       const double* row = cur + (4 * kk + q) * LDB + c;
-      const double wv = wb[cb][w][4 * kk + q];
+      const double wv = -wb[cb][w][4 * kk + q];
       double v[NB];
 #pragma unroll
       for (int r = 0; r < NB; ++r) v[r] = row[16 * r];
@@ -328,32 +353,16 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
     __syncthreads();
   }
   }
-  sla = ec_wave_sum(sla);
-  slp = ec_wave_sum(slp);
+  sla = ec_wave_sum_u(sla);
+  slp = ec_wave_sum_u(slp);
   if (!live) return;  // no workgroup barriers below
 
   constexpr int LD_D = NF % 16;            // d's position in the last F tile
-  double pdd = 0.0;                        // sum d_E^2 / a = P_dd
+  double pdd = 0.0;                        // sum d_E^2 / a = P_dd = -T_dd (Ap_dd = 0)
 #pragma unroll
   for (int s = 0; s < 4; ++s)
-    if (c == LD_D && 4 * s + q == LD_D) pdd = acc[ts(NTF, NTF)][s];
-  pdd = ec_wave_sum(pdd);
-  // T = Ap - P
-  const double* Apc = A.Ap + (int64_t)ch_id * A.ap_cs;
-  auto Aq = [&](int r0, int c0, int s) { return Apc[(int64_t)(r0 + 4 * s + q) * LDB + c0 + c]; };
-#pragma unroll
-  for (int s = 0; s < 4; ++s) acc[0][s] = Aq(0, 0, s) - acc[0][s];
-#pragma unroll
-  for (int r = 1; r < NB; ++r)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc[r][s] = Aq(0, 16 * r, s) - acc[r][s];
-#pragma unroll
-  for (int j = 1; j < NB; ++j)
-#pragma unroll
-    for (int r = j; r < NB; ++r)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc[ts(j, r)][s] = Aq(16 * j, 16 * r, s) - acc[ts(j, r)][s];
-
+    if (c == LD_D && 4 * s + q == LD_D) pdd = -acc[ts(NTF, NTF)][s];
+  pdd = ec_wave_sum_u(pdd);
   // T_MM = U^T U: V = U^-1 = L_M^-T (upper), L_M^-1 = V^T
   gs_d4_t V, Ecol = acc[0];
   double rsd;
@@ -367,7 +376,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
     if (m) fail = __builtin_ctzll(m) + 1;
   }
   double ldl = (q == 0 && c < nM) ? -log(rsd) : 0.0;  // sum log diag L_M
-  ldl = ec_wave_sum(ldl);
+  ldl = ec_wave_sum_u(ldl);
 
   // W_r = L_M^-1 T_0r = V^T T_0r;  S_jr = T_jr - W_j^T W_r
   gs_d4_t W[NB];
@@ -426,10 +435,10 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
           for (int s = 0; s < 4; ++s)
             acc[ts(I, J)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-acc[ts(K, I)][s], acc[ts(K, J)][s], acc[ts(I, J)], 0, 0, 0);
     }
-    ldS = ec_wave_sum(ldS);
-    quad = ec_wave_sum(quad);
+    ldS = ec_wave_sum_u(ldS);
+    quad = ec_wave_sum_u(quad);
     double lph = (l < NF) ? log(ph[l]) : 0.0;
-    lph = ec_wave_sum(lph);
+    lph = ec_wave_sum_u(lph);
     if (l == 0) {
       // in gs_ecorr_accept's convention: lnl + (aux1 - aux0 - aux2) / 2, with aux1 = 0 here
       A.lnl[ch_id] = 0.5 * (quad - 2.0 * ldl - ldS + lph);
@@ -468,7 +477,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
         }
       }
     }
-    e2 = ec_wave_sum(e2);
+    e2 = ec_wave_sum_u(e2);
     // S0 (rows < NF, cols <= NF, column NF = dF) from the upper tiles
 #pragma unroll
     for (int j = 1; j < NB; ++j)

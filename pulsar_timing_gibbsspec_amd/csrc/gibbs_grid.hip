@@ -177,6 +177,49 @@ __global__ __launch_bounds__(256) void k_tau_sum_fx(int n_psr, int64_t nrow, con
   if (bad && ovf) *ovf = 1;
 }
 
+// k_tau and k_tau_sum_fx fused (CURN from the tau sums, no per-pulsar red noise): thread (k, c)
+// forms tau_p,k = b_sin^2 + b_cos^2 of every pulsar from b and adds its digits; tau never goes to
+// HBM.  Same digits as the two kernels (integer sums: any order).
+__device__ __forceinline__ bool fx_add(double v, int e0, long long& d0, long long& d1, long long& d2) {
+  if (v == 0.0) return true;
+  if (!(v > 0.0) || v == __builtin_inf()) return false;
+  int E;
+  const double fr = frexp(v, &E);
+  const unsigned long long M = (unsigned long long)ldexp(fr, 53);
+  const int sh = E - 53 - e0;
+  unsigned long long dg[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int t = sh - FX_BITS * i;
+    const unsigned long long u = t >= 0 ? (t < 64 ? M << t : 0ull) : (-t < 64 ? M >> (-t) : 0ull);
+    dg[i] = u & FX_MASK;
+  }
+  d0 += (long long)dg[0];
+  d1 += (long long)dg[1];
+  d2 += (long long)dg[2];
+  return sh + 53 <= 3 * FX_BITS;
+}
+
+__global__ __launch_bounds__(256) void k_tau_sum_fx_b(TauArgs A, int e0, long long* acc, int* ovf) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int NFR = A.NF / 2;
+  const int64_t nrow = (int64_t)NFR * A.n_chain;
+  if (t >= nrow) return;
+  const int c = (int)(t % A.n_chain), k = (int)(t / A.n_chain);
+  long long d0 = 0, d1 = 0, d2 = 0;
+  bool ok = true;
+  for (int p = 0; p < A.n_psr; ++p) {
+    const int64_t sys = (int64_t)p * A.n_chain + c;
+    const double bs = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k]];
+    const double bc = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k + 1]];
+    ok &= fx_add(bs * bs + bc * bc, e0, d0, d1, d2);
+  }
+  acc[t] = d0;
+  acc[nrow + t] = d1;
+  acc[2 * nrow + t] = d2;
+  if (!ok && ovf) *ovf = 1;
+}
+
 __global__ __launch_bounds__(256) void k_fx_to_double(int64_t nrow, int e0, const long long* acc, double* S) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= nrow) return;
@@ -975,6 +1018,13 @@ int launch_counter_add(hipStream_t s, int64_t* counter, int64_t inc) {
 int launch_tau_sum_fx(hipStream_t s, int n_psr, int64_t nrow, const double* tau, int e0, long long* acc, int* ovf) {
   if (nrow == 0) return 0;
   hipLaunchKernelGGL(k_tau_sum_fx, grid1(nrow, 256), dim3(256), 0, s, n_psr, nrow, tau, e0, acc, ovf);
+  return 0;
+}
+
+int launch_tau_sum_fx_b(hipStream_t s, const TauArgs& a, int e0, long long* acc, int* ovf) {
+  const int64_t n = (int64_t)(a.NF / 2) * a.n_chain;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_tau_sum_fx_b, grid1(n, 256), dim3(256), 0, s, a, e0, acc, ovf);
   return 0;
 }
 

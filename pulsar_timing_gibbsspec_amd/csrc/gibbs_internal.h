@@ -64,6 +64,7 @@ struct BdrawArgs {
   int n_psr, n_chain, NF, NMX, ldb, event, bcast, psr_base;
   int model_per_sys;  // 1: model block per (pulsar, chain) system, read from global
   int mask_per_sys;   // chain_mask indexed by system (GS_OPT_X_PER_SYS)
+  int phi_per_chain;  // phiinv_F holds one row per chain, shared by every pulsar (GS_OPT_PHI_PER_CHAIN)
   int64_t mstride, sweep, chain_base;
   const int64_t* sweep_dev;  // ctx sweep counter (graph replay) or NULL
   const double* model;
@@ -133,6 +134,7 @@ int launch_counter_add(hipStream_t s, int64_t* counter, int64_t inc);
 int launch_tau_sum(hipStream_t s, int n_psr, int64_t nrow, const double* tau, double* S);
 int launch_tau_sum_fx(hipStream_t s, int n_psr, int64_t nrow, const double* tau, int e0, long long* acc, int* ovf);
 int launch_fx_to_double(hipStream_t s, int64_t nrow, int e0, const long long* acc, double* S);
+int launch_tau_sum_fx_b(hipStream_t s, const TauArgs& a, int e0, long long* acc, int* ovf);
 int launch_rho_curn_sum(hipStream_t s, const GridArgs& a);
 
 struct PtaGateArgs {

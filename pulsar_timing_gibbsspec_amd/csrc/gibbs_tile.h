@@ -291,9 +291,6 @@ __device__ __forceinline__ constexpr int tix(int I, int J, int NT) {
 #ifndef GS_EXEC_MASK
 #define GS_EXEC_MASK 1
 #endif
-#ifndef GS_SPLIT_ACC  // split dependent FMA chains of the solves into per-tile partial sums
-#define GS_SPLIT_ACC 0
-#endif
 template <int KMAX, bool PR = false>
 __device__ __forceinline__ void tile_elim1(gs_d4& A, gs_d4& B, double& rsd, int q, int c) {
   using namespace gtile;
@@ -687,27 +684,12 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
 #pragma unroll
   for (int K = NT - 1; K >= 0; --K) {
     double p = 0.0;
-#if GS_SPLIT_ACC
-    // one partial sum per tile column J, summed at the end: the dependent FMA chain of the
-    // solve's critical path is 4 long instead of 4 (NT - 1 - K)
-    double pj[NT];
-#pragma unroll
-    for (int J = K + 1; J < NT; ++J) {
-      const gs_d4 ut = AUG ? t[tix(K, J, NT)] : transpose(t[tix(K, J, NT)], tb, q, c);
-      pj[J] = ut[0] * xrow[J][0];
-#pragma unroll
-      for (int s = 1; s < 4; ++s) pj[J] = fma(ut[s], xrow[J][s], pj[J]);
-    }
-#pragma unroll
-    for (int J = K + 1; J < NT; ++J) p = (J == K + 1) ? pj[J] : p + pj[J];
-#else
 #pragma unroll
     for (int J = K + 1; J < NT; ++J) {
       const gs_d4 ut = AUG ? t[tix(K, J, NT)] : transpose(t[tix(K, J, NT)], tb, q, c);
 #pragma unroll
       for (int s = 0; s < 4; ++s) p = fma(ut[s], xrow[J][s], p);
     }
-#endif
     if (K + 1 < NT) p = qsum(p);
     const gs_d4 sr = to_row(ycol[K] + zfc[K] - p, vb, q, c);
     const gs_d4 W = AUG ? t[tix(K, K, NT)] : transpose(t[tix(K, K, NT)], tb, q, c);
@@ -737,22 +719,6 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
     const int row = 16 * P + c;
     const bool rok = row < nM;
     double p = 0.0;
-#if GS_SPLIT_ACC
-    // per-tile partial sums (a 4-long dependent chain instead of 4 NT)
-    double pj[NT];
-#pragma unroll
-    for (int J = 0; J < NT; ++J) {
-      pj[J] = 0.0;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int f = 16 * J + 4 * s + q;
-        const double g = (rok && f < NF) ? M.G[row * LD + f + z0] : 0.0;
-        pj[J] = fma(-g, xrow[J][s], pj[J]);
-      }
-    }
-#pragma unroll
-    for (int J = 0; J < NT; ++J) p += pj[J];
-#else
 #pragma unroll
     for (int J = 0; J < NT; ++J)
 #pragma unroll
@@ -761,7 +727,6 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
         const double g = (rok && f < NF) ? M.G[row * LD + f + z0] : 0.0;
         p = fma(-g, xrow[J][s], p);
       }
-#endif
     for (int Q = P; Q < nP; ++Q)
 #pragma unroll
       for (int s = 0; s < 4; ++s) {

@@ -438,7 +438,10 @@ class PTAChains:
         self.fx_ovf = torch.zeros(1, dtype=torch.int32, device=dev)
         self.gwphi = torch.empty(self.n_f, C, dtype=torch.float64, device=dev)
         self.irn = torch.empty(self.PG, self.n_f, C, dtype=torch.float64, device=dev) if self.red else None
-        self.phiinv_F = torch.empty(P * C, model.NF, dtype=torch.float64, device=dev)
+        # without per-pulsar red noise phiinv is the common spectrum alone, the same for every
+        # pulsar: one row per chain (GS_OPT_PHI_PER_CHAIN) instead of P rows of it
+        self.phi_shared = not self.red
+        self.phiinv_F = torch.empty((1 if self.phi_shared else P) * C, model.NF, dtype=torch.float64, device=dev)
         self.gate = torch.ones(C, dtype=torch.int32, device=dev)
         self.xlast = torch.empty(C, dtype=torch.float64, device=dev)
         self.info = torch.zeros(P * C, dtype=torch.int32, device=dev)
@@ -448,15 +451,19 @@ class PTAChains:
         self.redraw_b = False      # draw b | x first at the next sweep, as at sweep 0 (resume)
 
     def _bdraw(self, z, event, mask):
-        m = self.model
-        check(self.ctx.lib.gs_bdraw(self.ctx.handle, m.P, self.C, m.NF, m.NMX, m.ldb, ptr(m.model),
-                                    ptr(m.fidx), ptr(m.midx), ptr(m.nm_dev), ptr(self.phiinv_F), ptr(z),
-                                    self.it, event, self.chain_base, ptr(mask), ptr(self.b), ptr(self.info)),
-              "gs_bdraw")
+        m, lib, h = self.model, self.ctx.lib, self.ctx.handle
+        prev = self.ctx.get_option(_lib.OPT_PHI_PER_CHAIN)
+        self.ctx.set_option(_lib.OPT_PHI_PER_CHAIN, int(self.phi_shared))
+        try:
+            check(lib.gs_bdraw(h, m.P, self.C, m.NF, m.NMX, m.ldb, ptr(m.model), ptr(m.fidx), ptr(m.midx),
+                               ptr(m.nm_dev), ptr(self.phiinv_F), ptr(z), self.it, event, self.chain_base,
+                               ptr(mask), ptr(self.b), ptr(self.info)), "gs_bdraw")
+        finally:
+            self.ctx.set_option(_lib.OPT_PHI_PER_CHAIN, prev)
 
     def _gate_phiinv(self, with_gate):
         check(self.ctx.lib.gs_pta_gate_phiinv(
-            self.ctx.handle, self.P, self.C, self.n_f, self.n_param, ptr(self.x),
+            self.ctx.handle, 1 if self.phi_shared else self.P, self.C, self.n_f, self.n_param, ptr(self.x),
             ptr(self.xlast) if with_gate else None, ptr(self.gw_col), ptr(self.red_col),
             ptr(self.phiinv_F), ptr(self.gate)), "gs_pta_gate_phiinv")
 
@@ -471,6 +478,11 @@ class PTAChains:
             self._gate_phiinv(with_gate=False)
             self._bdraw(z0, _lib.EV_B0, None)
             self.redraw_b = False
+        if self.curn_mode == "sum":                            # sufficient statistic S_k
+            # tau and its fixed-point digits in one pass over b (tau itself is not needed)
+            check(lib.gs_tau_sum_fx_b(h, self.P, self.C, m.NF, m.ldb, ptr(m.fidx), ptr(self.b), self.fx_e0,
+                                      ptr(self.S_fx), ptr(self.fx_ovf)), "gs_tau_sum_fx_b")
+            return self.S_fx if self.sharded else None
         check(lib.gs_tau(h, self.P, self.C, m.NF, m.ldb, ptr(m.fidx), ptr(self.b), 0, ptr(self.tau)),
               "gs_tau")
         if self.red:                                           # pta_gibbs.py:252-276
@@ -479,10 +491,6 @@ class PTAChains:
             check(lib.gs_rho_red(h, self.P, self.C, self.n_f, ptr(self.tau), ptr(self.gwphi), self.ngrid,
                                  ptr(self.grid_red), ptr(u_red), ii, self.chain_base, ptr(self.x),
                                  self.n_param, ptr(self.red_col), None), "gs_rho_red")
-        if self.curn_mode == "sum":                            # sufficient statistic S_k
-            check(lib.gs_tau_sum_fx(h, self.P, self.C, self.n_f, ptr(self.tau), self.fx_e0, ptr(self.S_fx),
-                                    ptr(self.fx_ovf)), "gs_tau_sum_fx")
-            return self.S_fx if self.sharded else None
         if not self.sharded:
             return None
         parts = [self.tau.unsqueeze(1)]
