@@ -304,8 +304,8 @@ int gs_counter_add(gs_ctx* ctx, int64_t* counter, int64_t inc) {
 
 int64_t gs_model_stride(int NF, int NMX) { return model_stride_doubles(NF, NMX); }
 
-int gs_sweep_lds_bytes(int NF, int NMX) {
-  return (int)((model_stride_doubles(NF, NMX) + gs_tile_scr(NF) * GS_SWEEP_WPB) * 8);
+int gs_sweep_lds_bytes(int NF, int NMX) {  // the default (tile) variant: model block in the tile layout
+  return (int)((model_tiled_doubles(NF, NMX) + (gs_tile_scr(NF) + 128) * GS_SWEEP_WPB) * 8);
 }
 
 int gs_tnt(gs_ctx* ctx, int n_psr, int m_max, const gs_tnt_desc* desc, const double* T,

@@ -31,14 +31,17 @@
 #define GS_BCAST_BATCH 2
 #define GS_BCAST_TILE 3
 
-// min workgroups per CU (launch bounds) of the tile variant: 2 (256 VGPRs).  Measured on
-// MI355X against 3 (<= 168 VGPRs, 3 waves/SIMD; NF = 60, 4096 chains, one box, interleaved):
-// 3.05 vs 2.85 ms per launch -- the 35 spilled VGPRs and the tighter schedule of the
-// latency-bound factorisation cost more than the extra wave hides (tools/gpu_ab_variants.sh).
+// min waves per SIMD (launch bounds) of the tile variant: 3 (<= 168 VGPRs).  Round 2 measured 3
+// slower than 2 (3.05 vs 2.85 ms per launch: 35 spilled VGPRs, 54 spilled SGPRs at 207 VGPRs).
+// Round 3 (r03f, MI355X, NF = 60, 4096 chains, interleaved A/B): with the tiled model block (no
+// SGPR spills, 196 VGPRs) and z_F / the previous b parked in LDS (186 VGPRs) the 3-wave build
+// spills 13 VGPRs, all outside the sweep's inner body, and runs 2.235 vs 2.281-2.287 ms per
+// launch.  The run-time-NF instantiations with 4-5 tile rows keep 2 (24 / 84 spills at 3).
 #ifndef GS_TILE_MINW
-#define GS_TILE_MINW 2
+#define GS_TILE_MINW 3
 #endif
-#define GS_MINW(bc) ((bc) == GS_BCAST_TILE ? GS_TILE_MINW : GS_SWEEP_MINW)
+#define GS_MINW(bc, nfc, ntc) \
+  (((bc) == GS_BCAST_TILE || (nfc) == 0) ? (((nfc) == 0 && (ntc) >= 4) ? 2 : GS_TILE_MINW) : GS_SWEEP_MINW)
 
 // per-wave LDS scratch (doubles) of each factorisation variant
 #define GS_SCR_DOUBLES(bc, nf) ((bc) == GS_BCAST_TILE ? gs_tile_scr(nf) : 64)
@@ -180,8 +183,8 @@ __device__ __forceinline__ int bdraw_wave(const ModelLds& M, int NMX, int nM, in
 // One b|rho draw with the variant BC (tile MFMA or lane-row broadcast).  NFC > 0: the
 // fixed-NF instantiations (20 / 40 / 60, every variant); NFC == 0: any even NF < 16 NTC at
 // run time (tile variant only).
-template <int NFC, int NTC, int BC, bool PR = false>
-__device__ __forceinline__ int bdraw_sys(const ModelLds& M, int NMX, int nM, int lane, double phinv,
+template <int NFC, int NTC, int BC, bool PR = false, typename ModelT>
+__device__ __forceinline__ int bdraw_sys(const ModelT& M, int NMX, int nM, int lane, double phinv,
                                          double zF, double zM, double& bF, double& bM, double* scr, int NF) {
   if constexpr (NFC == 0)
     return bdraw_tile_n<NTC, false, PR>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
@@ -214,6 +217,54 @@ __device__ __forceinline__ void stage_model(double* lds, const double* g, int64_
 #pragma unroll 4
   for (int i = threadIdx.x; i < n2; i += blockDim.x) l2[i] = g2[i];
 #endif
+  __syncthreads();
+}
+
+// The fused sweep's model block in the register-tile layout (gibbs_tile.h ModelTiled,
+// gibbs_internal.h model_tiled_*), built in LDS once per launch from the row-major block in
+// global memory (L2): one double per thread and step, amortised over the launch's sweeps.
+// Values are copied (or negated, G) exactly, so the draws are bit-identical to the row-major path.
+#ifndef GS_SWEEP_TILED
+#define GS_SWEEP_TILED 1
+#endif
+__device__ void stage_model_tiled(double* __restrict__ L, const double* __restrict__ g, int NF, int NMX, int nM) {
+  const int NT = model_tiled_nt(NF), LD = NF + 1, nP = model_tiled_np(NMX);
+  const int oG = (int)model_tiled_g_offset(NF), oR = (int)model_tiled_r_offset(NF, NMX);
+  const int oH = (int)model_tiled_h_offset(NF, NMX), n = (int)model_tiled_doubles(NF, NMX);
+  const double* S0 = g;  // NF x (NF + 1), column NF = dF
+  const double* G = g + NF * LD + NF;
+  const double* h = G + NMX * LD;
+  const double* R = h + NMX;
+  for (int idx = threadIdx.x; idx < n; idx += blockDim.x) {
+    const int l = idx & 63, s = (idx >> 6) & 3, q = l >> 4, c = l & 15;
+    double v = 0.0;
+    if (idx < oG) {  // S': tile (I, J), I <= J, row-major over the upper triangle of tiles
+      int t = idx >> 8, I = 0;
+      while (t >= NT - I) t -= NT - I++;
+      const int J = I + t, r = 16 * I + 4 * s + q, col = 16 * J + c;
+      if (r < NF && col < NF)
+        v = S0[r * LD + col];
+      else if (r < NF && col == NF)
+        v = S0[r * LD + NF];  // dF on the augmented column ...
+      else if (r == NF && col < NF)
+        v = S0[col * LD + NF];  // ... and row
+      else if (r == col)
+        v = 1.0;  // identity padding (the augmented pivot too)
+    } else if (idx < oR) {  // G' = -G: chunk P (rows 16 P + c), tile column J
+      const int k = idx - oG, P = k / (NT * 256), J = (k >> 8) % NT;
+      const int row = 16 * P + c, f = 16 * J + 4 * s + q;
+      if (row < nM && f < NF) v = -G[row * LD + f];
+    } else if (idx < oH) {  // R': chunk pair (P, Q >= P)
+      int t = (idx - oR) >> 8, P = 0;
+      while (t >= nP - P) t -= nP - P++;
+      const int Q = P + t, row = 16 * P + c, mm = 16 * Q + 4 * s + q;
+      if (row < nM && mm < nM) v = R[row * NMX + mm];
+    } else {
+      const int k = idx - oH;
+      if (k < NMX) v = h[k];
+    }
+    L[idx] = v;
+  }
   __syncthreads();
 }
 
@@ -264,8 +315,16 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
 }
 
 // ------------------------------------------------------------ batched b draw
+// A/B knobs (variant builds): GS_BDRAW_PR = the fused sweep's issue priorities inside k_bdraw;
+// GS_BDRAW_LDS_PAD = extra LDS doubles per workgroup (caps the workgroups per CU, e.g. 2 waves/SIMD)
+#ifndef GS_BDRAW_PR
+#define GS_BDRAW_PR false
+#endif
+#ifndef GS_BDRAW_LDS_PAD
+#define GS_BDRAW_LDS_PAD 0
+#endif
 template <int NFC, int NTC, int WPB, int BC>
-__global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
+__global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_bdraw(BdrawArgs A) {
   extern __shared__ double lds[];
   const int NF = NFC ? NFC : A.NF;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -295,7 +354,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_bdraw(BdrawArgs A) {
   }
   double bF = 0.0, bM = 0.0;
   double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * GS_SCR_DOUBLES(BC, NF);
-  const int fail = bdraw_sys<NFC, NTC, BC>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
+  const int fail = bdraw_sys<NFC, NTC, BC, GS_BDRAW_PR>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
   if (!fail) {  // non-PD Sigma: the previous b stays (wave-uniform)
     if (lane < NF) A.b[sys * A.ldb + fi] = bF;
     if (lane < nM) A.b[sys * A.ldb + mi] = bM;
@@ -349,7 +408,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
 #define GS_RHO_EXP 0
 #endif
 template <int NFC, int NTC, int WPB, int BC>
-__global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepArgs A) {
+__global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_sweep_freespec(SweepArgs A) {
   extern __shared__ double lds[];
   const int NF = NFC ? NFC : A.NF;
   const int NFR = NF / 2;
@@ -357,18 +416,38 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
   const int nb = (A.n_chain + WPB - 1) / WPB;
   const int p = blockIdx.x / nb;
   const int c = (blockIdx.x % nb) * WPB + wave;
-  stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+  // tile variant: the model block in the register-tile layout (stage_model_tiled); the lane-row
+  // broadcast variants read the row-major block
+  constexpr bool TL = GS_SWEEP_TILED && (BC == GS_BCAST_TILE || NFC == 0);
+  const int nM = A.nm[p];
+  int64_t mlds;
+  if constexpr (TL) {
+    stage_model_tiled(lds, A.model + (int64_t)p * A.mstride, NF, A.NMX, nM);
+    mlds = model_tiled_doubles(NF, A.NMX);
+  } else {
+    stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+    mlds = A.mstride;
+  }
   if (c >= A.n_chain) return;
-  const ModelLds M = model_view(lds, NF, A.NMX);
+  using ModelT = typename std::conditional<TL, ModelTiled, ModelLds>::type;
+  ModelT M;
+  if constexpr (TL) {
+    M.S = lds;
+    M.G = lds + model_tiled_g_offset(NF);
+    M.R = lds + model_tiled_r_offset(NF, A.NMX);
+    M.h = lds + model_tiled_h_offset(NF, A.NMX);
+  } else {
+    M = model_view(lds, NF, A.NMX);
+  }
   const int64_t sys = (int64_t)p * A.n_chain + c;
   const int64_t n_sys = (int64_t)A.n_psr * A.n_chain;
   const long long gchain = A.chain_base + c;
-  const int nM = A.nm[p];
   const bool act = lane < NF, actm = lane < nM;
   const int kf = act ? (lane >> 1) : 0;  // frequency of this lane
   const int fi = act ? A.fidx[p * NF + lane] : 0;
   const int mi = actm ? A.midx[p * A.NMX + lane] : 0;
-  double* scr = lds + A.mstride + wave * GS_SCR_DOUBLES(BC, NF);
+  double* scr = lds + mlds + wave * GS_SCR_DOUBLES(BC, NF);
+  double* bsave = lds + mlds + WPB * GS_SCR_DOUBLES(BC, NF) + wave * 128;  // previous b (failed draws)
   GS_PH_INIT(scr)
 #ifdef GS_STATIC_PRIO
   // A/B knob: half of the workgroups (one of the two co-resident waves of a SIMD) at priority 1
@@ -481,12 +560,15 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC)) void k_sweep_freespec(SweepA
       if (pass == 0) phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;  // first draw from xs
       GS_PH(7)
       // a failed factorisation (non-PD Sigma, wave-uniform) keeps the previous b: no NaN ever
-      // enters the state (the reference's LinAlgError branch, pulsar_gibbs.py:507-516)
-      const double bF0 = bF, bM0 = bM;
+      // enters the state (the reference's LinAlgError branch, pulsar_gibbs.py:507-516).  The
+      // previous b waits in the wave's LDS save slot, not in 4 VGPRs across the draw.
+      bsave[lane] = bF;
+      bsave[64 + lane] = bM;
       const int f = bdraw_sys<NFC, NTC, BC, true>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
       if (f) {
-        bF = bF0;
-        bM = bM0;
+        gtile::lds_fence();
+        bF = bsave[lane];
+        bM = bsave[64 + lane];
         if (!fail) fail = f;
         if (A.fail_count && lane == 0) A.fail_count[sys] += 1;
       }
@@ -617,8 +699,10 @@ int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
   const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
-  const size_t lds = ((size_t)a.mstride + (fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) * GS_SWEEP_WPB) *
-                     sizeof(double);
+  const bool tiled = GS_SWEEP_TILED && (!fixed || a.bcast == GS_BCAST_TILE);
+  const size_t mlds = tiled ? (size_t)model_tiled_doubles(a.NF, a.NMX) : (size_t)a.mstride;
+  const size_t lds =
+      (mlds + ((fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) + 128) * GS_SWEEP_WPB) * sizeof(double);
   return dispatch_nf_sweep<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
 
@@ -642,7 +726,8 @@ int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
   dim3 grid((unsigned)(a.n_psr * nb));
   const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
   const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) +
-                      (fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) * WPB) * sizeof(double);
+                      (fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) * WPB + GS_BDRAW_LDS_PAD) *
+                     sizeof(double);
   return dispatch_nf_bdraw<WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
 

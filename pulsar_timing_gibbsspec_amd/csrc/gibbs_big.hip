@@ -133,10 +133,10 @@ __global__ __launch_bounds__(64 * BIG_WPB) void k_bdraw_big(BdrawArgs A, double*
     }
     st_tile(ws, tix(K, K, NT), lane, transpose(V, tb, q, c));  // U_KK^-T for the backward solve
     for (int I = K + 1; I < NT; ++I) {
-      const gs_d4 nx = -ld_tile(ws, tix(K, I, NT), lane);
+      const gs_d4 xk = ld_tile(ws, tix(K, I, NT), lane);
       for (int J = I; J < NT; ++J) {
         const int tl = tix(I, J, NT);
-        st_tile(ws, tl, lane, mfma_tn(ld_tile(ws, tl, lane), nx, ld_tile(ws, tix(K, J, NT), lane)));
+        st_tile(ws, tl, lane, mfma_tn_sub(ld_tile(ws, tl, lane), xk, ld_tile(ws, tix(K, J, NT), lane)));
       }
     }
     for (int J = K + 1; J < NT; ++J) {  // block row K final: keep U_KJ^T

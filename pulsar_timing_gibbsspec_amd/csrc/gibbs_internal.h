@@ -30,6 +30,27 @@ __host__ __device__ inline int64_t model_stride_doubles(int NF, int NMX) {
   return (s + 1) & ~int64_t(1);  // 16-byte multiple
 }
 
+// The fused sweep's LDS copy of a model block in the register-tile layout (gibbs_tile.h
+// ModelTiled): S' (NT(NT+1)/2 tiles: the augmented, identity-padded Schur block), G' (nP x NT
+// tiles), R' (nP(nP+1)/2 tiles), each tile 4 registers x 64 lanes, then h (NMX, even).
+// NT = NF/16 + 1 tile rows, nP = ceil(NMX/16) fixed-block chunks.
+__host__ __device__ inline int model_tiled_nt(int NF) { return NF / 16 + 1; }
+__host__ __device__ inline int model_tiled_np(int NMX) { return (NMX + 15) / 16; }
+__host__ __device__ inline int64_t model_tiled_g_offset(int NF) {
+  const int NT = model_tiled_nt(NF);
+  return (int64_t)NT * (NT + 1) / 2 * 256;
+}
+__host__ __device__ inline int64_t model_tiled_r_offset(int NF, int NMX) {
+  return model_tiled_g_offset(NF) + (int64_t)model_tiled_np(NMX) * model_tiled_nt(NF) * 256;
+}
+__host__ __device__ inline int64_t model_tiled_h_offset(int NF, int NMX) {
+  const int nP = model_tiled_np(NMX);
+  return model_tiled_r_offset(NF, NMX) + (int64_t)nP * (nP + 1) / 2 * 256;
+}
+__host__ __device__ inline int64_t model_tiled_doubles(int NF, int NMX) {
+  return model_tiled_h_offset(NF, NMX) + ((NMX + 1) & ~1);
+}
+
 // gs_prefix / gs_prefix_sys / gs_prefix_dd (gibbs_prefix.hip)
 struct PrefixArgs {
   int n_psr, n_chain, NF, NMX;

@@ -74,6 +74,24 @@ __device__ __forceinline__ gs_d4 mfma_tn(gs_d4 acc, const gs_d4 x, const gs_d4 y
   return acc;
 }
 
+// acc - X^T Y: on gfx950 the f64 MFMA's blgp field is the operand-negate modifier (blgp = 1:
+// neg:[1,0,0]), so the trailing update needs no v_xor per register to negate X (bit-identical:
+// (-x) y and -(x y) round the same)
+#ifndef GS_MFMA_NEG
+#define GS_MFMA_NEG 1
+#endif
+__device__ __forceinline__ gs_d4 mfma_tn_sub(gs_d4 acc, const gs_d4 x, const gs_d4 y) {
+#if GS_MFMA_NEG
+  acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x[0], y[0], acc, 0, 0, 1);
+  acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x[1], y[1], acc, 0, 0, 1);
+  acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x[2], y[2], acc, 0, 0, 1);
+  acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x[3], y[3], acc, 0, 0, 1);
+  return acc;
+#else
+  return mfma_tn(acc, -x, y);
+#endif
+}
+
 __device__ __forceinline__ gs_d4 transpose(const gs_d4 t, double* tb, int q, int c) {
   lds_fence();
 #pragma unroll
@@ -318,6 +336,8 @@ __device__ __forceinline__ void tile_elim1(gs_d4& A, gs_d4& B, double& rsd, int 
 #endif
       // -A[k][c]/A[k][k] = akm i0 (akk i0 - 2) (one Newton step on v_rcp_f64): the two
       // products run side by side, 4 dependent ops from pivot to multiplier
+      // (akk keeps two uses: a single-use DPP move feeding v_rcp_f64 is folded by the compiler's
+      // DPP combiner into v_rcp_f64_dpp, which returns 1/0 on MI355X -- tools/probe/rcpdpp_probe.hip)
       const double i0 = __builtin_amdgcn_rcp(akk);
 #if GS_PIV_NR2
       // two Newton steps: -1/akk to ~1 ulp instead of ~2^-50 relative
@@ -476,7 +496,56 @@ __device__ __forceinline__ double d4_get(const gs_d4 v, int i) {
   r = (i == 3) ? v[3] : r;
   return r;
 }
+
+// v + a on the four diagonal lanes of register S of a C-layout tile (lane 16q + c with
+// c = 4S + q), v elsewhere: exec set by two SALU moves around one v_add_f64 (instead of two
+// v_cndmask_b32 and an add per register)
+template <int S>
+__device__ __forceinline__ double add_on_diag(double v, double a) {
+  constexpr unsigned LO = (1u << (4 * S)) | (1u << (17 + 4 * S));     // q = 0, 1
+  constexpr unsigned HI = (1u << (4 * S + 2)) | (1u << (19 + 4 * S));  // q = 2, 3
+  asm("s_mov_b32 exec_lo, %2\n\t"
+      "s_mov_b32 exec_hi, %3\n\t"
+      "v_add_f64 %0, %0, %1\n\t"
+      "s_mov_b64 exec, -1"
+      : "+v"(v)
+      : "v"(a), "n"(LO), "n"(HI));
+  return v;
+}
+__device__ __forceinline__ double add_on_diag(double v, double a, int s) {
+  switch (s) {  // s constant after unrolling
+    case 0: return add_on_diag<0>(v, a);
+    case 1: return add_on_diag<1>(v, a);
+    case 2: return add_on_diag<2>(v, a);
+    default: return add_on_diag<3>(v, a);
+  }
+}
 }  // namespace gtile
+
+// A pulsar's model block in the register-tile layout (gibbs_internal.h model_tiled_*), built
+// once per fused-sweep launch in LDS (gibbs_bdraw.hip stage_model_tiled): every tile element a
+// lane needs sits at lane + 64 (4 tile + register), so the per-draw loads are lane-linear with
+// immediate offsets -- no per-element address arithmetic, no exec branches for the ragged edges,
+// no bank conflicts.  S: the augmented Schur block with dF on its first padding row/column and
+// 1 on the padding diagonal (phiinv_F is added on the real diagonal); G: -G, zero beyond nM rows
+// / NF columns; R: zero beyond nM.
+struct ModelTiled {
+  static constexpr bool tiled = true;
+  const double* S;
+  const double* G;
+  const double* R;
+  const double* h;
+  const double* S0 = nullptr;  // unused (the row-major fields of ModelLds)
+  const double* dF = nullptr;
+};
+template <typename ModelT>
+struct model_is_tiled {
+  static constexpr bool value = false;
+};
+template <>
+struct model_is_tiled<ModelTiled> {
+  static constexpr bool value = true;
+};
 
 // Model block view (see gibbs_bdraw.hip ModelLds): S0 NF x (NF+1), dF, G NMX x (NF+1),
 // h, R NMX x NMX.  Same interface and outputs as bdraw_wave.
@@ -504,6 +573,8 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
   // CPC >= 0: NF = 16 (NT - 1) + CPC fixed at compile time; CPC < 0: NF = nf_rt
   const int NF = CPC >= 0 ? 16 * (NT - 1) + CPC : nf_rt;
   const int LD = NF + 1;
+  constexpr bool TILED = model_is_tiled<ModelT>::value;
+  static_assert(!(TILED && WIDE), "the tiled model block serves nM <= 64 only");
   constexpr int NTILE = NT * (NT + 1) / 2;
   const int q = lane >> 4, c = lane & 15;
   GS_PH_BEGIN
@@ -512,16 +583,18 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
   double* ob = scr + 336;  // 80
 
   // phinv_F and z_F (lane-row) -> column layout per tile row
+  // z_F stays in ob (zero beyond NF) until the backward solve reads it back per tile row:
+  // not held in registers through the factorisation
   lds_fence();
   vb[lane] = phinv;
-  ob[lane] = zF;
+  ob[lane] = (lane < NF) ? zF : 0.0;
+  if (NT > 4 && lane < 16) ob[64 + lane] = 0.0;
   lds_fence();
-  double phc[NT], zfc[NT];
+  double phc[NT];
 #pragma unroll
   for (int K = 0; K < NT; ++K) {
     const int i = 16 * K + c;
-    phc[K] = (i < NF) ? vb[i] : 1.0;
-    zfc[K] = (i < NF) ? ob[i] : 0.0;
+    phc[K] = (i < NF) ? vb[i] : (TILED ? 0.0 : 1.0);  // tiled: S' holds the padding's 1
   }
   lds_fence();
 
@@ -537,6 +610,28 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
   constexpr bool AUG = true;
   const int CP = NF - 16 * (NT - 1);  // local index of the augmented column (0..15)
   gs_d4 t[NTILE];
+  if constexpr (TILED) {
+    // lane-linear loads at immediate offsets (ModelTiled), phiinv_F added on the diagonal lanes
+    const double* Sl = M.S + lane + z0;
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+#pragma unroll
+      for (int J = I; J < NT; ++J) {
+        const int ti = tix(I, J, NT);
+        gs_d4 v;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          v[s] = Sl[(4 * ti + s) * 64];
+#if GS_EXEC_MASK
+          if (I == J) v[s] = add_on_diag(v[s], phc[I], s);
+#else
+          if (I == J) v[s] += (4 * s + q == c) ? phc[I] : 0.0;
+#endif
+        }
+        t[ti] = v;
+      }
+    }
+  } else
 #pragma unroll
   for (int I = 0; I < NT; ++I) {
 #pragma unroll
@@ -620,9 +715,8 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
     // trailing update: T_IJ -= U_KI^T U_KJ
 #pragma unroll
     for (int I = K + 1; I < NT; ++I) {
-      const gs_d4 nx = -t[tix(K, I, NT)];
 #pragma unroll
-      for (int J = I; J < NT; ++J) t[tix(I, J, NT)] = mfma_tn(t[tix(I, J, NT)], nx, t[tix(K, J, NT)]);
+      for (int J = I; J < NT; ++J) t[tix(I, J, NT)] = mfma_tn_sub(t[tix(I, J, NT)], t[tix(K, I, NT)], t[tix(K, J, NT)]);
     }
     if constexpr (AUG) {
       // block row K is final: keep U_KJ^T (what the backward solve reads)
@@ -691,7 +785,7 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
       for (int s = 0; s < 4; ++s) p = fma(ut[s], xrow[J][s], p);
     }
     if (K + 1 < NT) p = qsum(p);
-    const gs_d4 sr = to_row(ycol[K] + zfc[K] - p, vb, q, c);
+    const gs_d4 sr = to_row(ycol[K] + ob[16 * K + c] - p, vb, q, c);
     const gs_d4 W = AUG ? t[tix(K, K, NT)] : transpose(t[tix(K, K, NT)], tb, q, c);
     double p2 = 0.0;
 #pragma unroll
@@ -719,6 +813,19 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
     const int row = 16 * P + c;
     const bool rok = row < nM;
     double p = 0.0;
+    if constexpr (TILED) {
+      // G' = -G and R' as C-layout tiles, zero beyond nM rows / NF columns (ModelTiled)
+      const int nPl = (NMX + 15) >> 4;
+      const double* Gl = M.G + lane + z0 + P * (NT * 256);
+#pragma unroll
+      for (int J = 0; J < NT; ++J)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) p = fma(Gl[(4 * J + s) * 64], xrow[J][s], p);
+      const double* Rl = M.R + lane + z0 + (P * nPl - (P * (P - 1)) / 2) * 256;
+      for (int Q = P; Q < nP; ++Q)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) p = fma(Rl[(4 * (Q - P) + s) * 64], zb[16 * Q + 4 * s + q], p);
+    } else {
 #pragma unroll
     for (int J = 0; J < NT; ++J)
 #pragma unroll
@@ -734,6 +841,7 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
         const double rv = (rok && mm < nM) ? M.R[row * NMX + mm + z0] : 0.0;
         p = fma(rv, zb[mm], p);
       }
+    }
     p = qsum(p);
     const double xm = rok ? M.h[row + z0] + p : 0.0;
     if (!WIDE || P < 4)
