@@ -323,37 +323,28 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
 #ifndef GS_BDRAW_LDS_PAD
 #define GS_BDRAW_LDS_PAD 0
 #endif
-template <int NFC, int NTC, int WPB, int BC>
-__global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_bdraw(BdrawArgs A) {
-  extern __shared__ double lds[];
-  const int NF = NFC ? NFC : A.NF;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nb = (A.n_chain + WPB - 1) / WPB;
-  const int p = blockIdx.x / nb;
-  const int c = (blockIdx.x % nb) * WPB + wave;
-  // shared pulsar model: staged once per workgroup; per-system models (white-noise
-  // runs, TNT differs per chain) are read from global memory (L2) directly.  (Looping a
-  // workgroup over several chain groups to stage less often measured slower: the loop
-  // raised the kernel from 164 to 231 VGPRs, 3 -> 2 waves/SIMD.)
-  if (!A.model_per_sys) stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
-  if (c >= A.n_chain) return;
+#ifndef GS_BDRAW_LOOP
+#define GS_BDRAW_LOOP 1
+#endif
+#ifndef GS_BDRAW_TILED  // shared model in the register-tile layout (stage_model_tiled), tile variant
+#define GS_BDRAW_TILED 0
+#endif
+// one (pulsar p, chain c) system of k_bdraw
+template <int NFC, int NTC, int BC, typename ModelT>
+__device__ __forceinline__ void bdraw_item(const BdrawArgs& A, const ModelT& M, int p, int c, int NF, int nM, int fi,
+                                           int mi, double* scr, int lane) {
   const int64_t sys = (int64_t)p * A.n_chain + c;
   if (A.chain_mask && A.chain_mask[A.mask_per_sys ? sys : (int64_t)c] == 0) return;  // gate closed: keep b
-  const ModelLds M = A.model_per_sys ? model_view(A.model + sys * A.mstride, NF, A.NMX)
-                                     : model_view(lds, NF, A.NMX);
-  const int nM = A.nm[p];
-  const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
-  const int mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
   const double phinv = lane < NF ? A.phiinv_F[(A.phi_per_chain ? (int64_t)c : sys) * NF + lane] : 0.0;
   double zF = 0.0, zM = 0.0;
   if (A.z) {
     zF = lane < NF ? A.z[sys * A.ldb + fi] : 0.0;
     zM = lane < nM ? A.z[sys * A.ldb + mi] : 0.0;
   } else {
-    gs_normal2(gs_counter(lane, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, p + A.psr_base, A.event), A.key, zF, zM);
+    gs_normal2(gs_counter(lane, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, p + A.psr_base, A.event), A.key, zF,
+               zM);
   }
   double bF = 0.0, bM = 0.0;
-  double* scr = lds + (A.model_per_sys ? 0 : A.mstride) + wave * GS_SCR_DOUBLES(BC, NF);
   const int fail = bdraw_sys<NFC, NTC, BC, GS_BDRAW_PR>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
   if (!fail) {  // non-PD Sigma: the previous b stays (wave-uniform)
     if (lane < NF) A.b[sys * A.ldb + fi] = bF;
@@ -362,6 +353,57 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_bdraw(Bdraw
     A.fail_count[sys] += 1;
   }
   if (A.info && lane == 0) A.info[sys] = fail;
+}
+
+template <int NFC, int NTC, int WPB, int BC>
+__global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_bdraw(BdrawArgs A) {
+  extern __shared__ double lds[];
+  const int NF = NFC ? NFC : A.NF;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nb = (A.n_chain + WPB - 1) / WPB;
+  if (A.model_per_sys) {
+    // per-system models (white-noise runs, TNT differs per chain): read from global memory (L2)
+    const int p = blockIdx.x / nb;
+    const int c = (blockIdx.x % nb) * WPB + wave;
+    if (c >= A.n_chain) return;
+    const int nM = A.nm[p];
+    const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
+    const int mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
+    const int64_t sys = (int64_t)p * A.n_chain + c;
+    bdraw_item<NFC, NTC, BC>(A, model_view(A.model + sys * A.mstride, NF, A.NMX), p, c, NF, nM, fi, mi,
+                             lds + wave * GS_SCR_DOUBLES(BC, NF), lane);
+    return;
+  }
+  // shared pulsar model: staged once per workgroup for GS_BDRAW_LOOP chain groups of the pulsar
+  const int nbl = (nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP;
+  const int p = blockIdx.x / nbl;
+  const int g0 = (blockIdx.x % nbl) * GS_BDRAW_LOOP;
+  const int nM = A.nm[p];
+  const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
+  const int mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
+  constexpr bool TL = GS_BDRAW_TILED && (BC == GS_BCAST_TILE || NFC == 0);
+  using ModelT = typename std::conditional<TL, ModelTiled, ModelLds>::type;
+  ModelT M;
+  int64_t mlds;
+  if constexpr (TL) {
+    stage_model_tiled(lds, A.model + (int64_t)p * A.mstride, NF, A.NMX, nM);
+    mlds = model_tiled_doubles(NF, A.NMX);
+    M.S = lds;
+    M.G = lds + model_tiled_g_offset(NF);
+    M.R = lds + model_tiled_r_offset(NF, A.NMX);
+    M.h = lds + model_tiled_h_offset(NF, A.NMX);
+  } else {
+    stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+    mlds = A.mstride;
+    M = model_view(lds, NF, A.NMX);
+  }
+  double* scr = lds + mlds + wave * GS_SCR_DOUBLES(BC, NF);
+#pragma unroll 1
+  for (int r = 0; r < GS_BDRAW_LOOP; ++r) {
+    const int c = (g0 + r) * WPB + wave;
+    if (c >= A.n_chain) break;
+    bdraw_item<NFC, NTC, BC>(A, M, p, c, NF, nM, fi, mi, scr, lane);
+  }
 }
 
 // ------------------------------------------------------------ marginalised likelihood
@@ -723,10 +765,11 @@ int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
   }
   constexpr int WPB = GS_BDRAW_WPB;
   const int nb = (a.n_chain + WPB - 1) / WPB;
-  dim3 grid((unsigned)(a.n_psr * nb));
+  dim3 grid((unsigned)(a.n_psr * (a.model_per_sys ? nb : (nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP)));
   const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
-  const size_t lds = ((size_t)(a.model_per_sys ? 0 : a.mstride) +
-                      (fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) * WPB + GS_BDRAW_LDS_PAD) *
+  const bool tiled = GS_BDRAW_TILED && (!fixed || a.bcast == GS_BCAST_TILE);
+  const size_t mlds = a.model_per_sys ? 0 : tiled ? (size_t)model_tiled_doubles(a.NF, a.NMX) : (size_t)a.mstride;
+  const size_t lds = (mlds + (fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) * WPB + GS_BDRAW_LDS_PAD) *
                      sizeof(double);
   return dispatch_nf_bdraw<WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
