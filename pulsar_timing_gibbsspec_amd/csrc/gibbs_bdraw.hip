@@ -323,10 +323,16 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
 #ifndef GS_BDRAW_LDS_PAD
 #define GS_BDRAW_LDS_PAD 0
 #endif
+// Chain groups per workgroup (shared model: staged once for all of them).  Measured on MI355X
+// (r03h, CURN line, 2048 chains x 45 pulsars, k_bdraw per launch): 1 -> 0.563-0.570 ms, 4 -> 0.545,
+// 8 -> 0.566 (fewer, longer workgroups: the last round of the grid runs part-empty).
 #ifndef GS_BDRAW_LOOP
-#define GS_BDRAW_LOOP 1
+#define GS_BDRAW_LOOP 4
 #endif
-#ifndef GS_BDRAW_TILED  // shared model in the register-tile layout (stage_model_tiled), tile variant
+// Shared model converted to the register-tile layout by each workgroup from global memory
+// (stage_model_tiled) -- measured slower in k_bdraw (0.873 ms at loop 1, 0.631-0.661 at loop 4/8):
+// unlike the fused sweep, one launch draws too few systems per workgroup to amortise the conversion.
+#ifndef GS_BDRAW_TILED
 #define GS_BDRAW_TILED 0
 #endif
 // one (pulsar p, chain c) system of k_bdraw

@@ -29,7 +29,8 @@ def one(res, frag):
 
 # (mangled-name fragment, minimum waves per SIMD, VGPR spills allowed)
 HOT = [
-    ("k_bdrawILi60ELi0ELi4ELi3E", 3, 0),           # PTA / CURN b|rho (configs[3])
+    ("k_bdrawILi60ELi0ELi4ELi3E", 3, 2),           # PTA / CURN b|rho (configs[3]); 4 chain groups
+                                                   # per workgroup: 2 spills, measured faster (r03h)
     ("k_sweep_freespecILi60ELi0ELi4ELi3E", 3, 16),  # headline fused sweep (configs[1], [2]): 3 waves,
                                                     # 13 spills outside the inner body (round 3)
     ("k_rho_red_waveE", 4, 0),                     # CURN + red grid CDF (f64 wave kernel)
