@@ -218,6 +218,7 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain"):
     kernels = {"k_bdraw": dict(kernel_avg_ms=ms_b, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
                                achieved=bflop / (ms_b * 1e-3) / 1e12, alg_per_launch=bflop,
                                traffic=(_ecorr_traffic(m.P * C, "pmc_traffic_curn.json") if kind == "curn" else None),
+                               name="k_bdraw_tiled" if m.model_tiled is not None else "k_bdraw",
                                note="b|rho of every (pulsar, chain) system: sum_p m^3/3 + m^2/2 + m/6 + 3 m^2 "
                                     "flop per chain (SURVEY 8d)")}
     gp = grid_peak()
@@ -340,7 +341,8 @@ def bench_indep(C, K, W, S, rank, world, dev):
                 sharding=(f"pulsars over {world} GPUs (no collective)" if world > 1 else "one GPU"),
                 pulsar_iters_per_s=C * K * len(ptas) / el,
                 ess_per_s=ess,
-                roofline={"kernel": "k_sweep_freespec", "bound": "mfma", "unit": "TFLOP/s", "achieved": ach,
+                roofline={"kernel": "k_sweep_freespec" + ("" if model.NMX <= 16 else "_rm"),
+                          "bound": "mfma", "unit": "TFLOP/s", "achieved": ach,
                           "peak": FP64_PEAK_TFLOPS, "frac": ach / FP64_PEAK_TFLOPS,
                           "kernel_avg_ms": per_sweep * S * 1e3, "sweeps_per_launch": S,
                           "alg_flops_per_launch": flops_sweep * S, "traffic": None,

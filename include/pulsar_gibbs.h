@@ -197,6 +197,23 @@ int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,
              int64_t chain_base, const int32_t* chain_mask, double* b, int32_t* info);
 
 /*
+ * Register-tile copies of n_psr shared model blocks (NF <= 64, NMX <= 64) for gs_bdraw_tiled:
+ * per pulsar p, at tiled + p * gs_model_tiled_stride(NF, NMX), the augmented Schur block, -G and
+ * R as 16x16 tiles in the MFMA C layout (4 registers x 64 lanes each) and h.  Once per model
+ * (white-noise) state, after gs_prefix / gs_prefix_dd; the values are copies (G negated), so
+ * gs_bdraw_tiled's draws equal gs_bdraw's bit for bit.
+ */
+int64_t gs_model_tiled_stride(int NF, int NMX);
+int gs_model_tile(gs_ctx* ctx, int n_psr, int NF, int NMX, const double* model, const int32_t* nm,
+                  double* tiled);
+/* gs_bdraw on gs_model_tile's blocks (the register-tile variant whatever GS_OPT_BCAST says):
+ * same arguments and results, the model staged in the layout the draw loads lane-linearly. */
+int gs_bdraw_tiled(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb,
+                   const double* tiled, const int32_t* fidx, const int32_t* midx, const int32_t* nm,
+                   const double* phiinv_F, const double* z, int64_t sweep, int event,
+                   int64_t chain_base, const int32_t* chain_mask, double* b, int32_t* info);
+
+/*
  * (a3) rho|b analytic draw: tau_k = (b_sin^2 + b_cos^2)/2 over fidx,
  * truncated inverse-gamma inverse CDF, x = 0.5 log10 rho.
  * Replaces pulsar_gibbs.py:206-216,236.  u: [n_sys x NF/2] injected U(0,1)

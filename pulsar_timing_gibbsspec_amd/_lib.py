@@ -47,6 +47,9 @@ SIGNATURES = {
     "gs_tnt": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
     "gs_prefix": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "gs_bdraw": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _I, _I64, _P, _P, _P]),
+    "gs_model_tiled_stride": (_I64, [_I, _I]),
+    "gs_model_tile": (_I, [_P, _I, _I, _I, _P, _P, _P]),
+    "gs_bdraw_tiled": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _I, _I64, _P, _P, _P]),
     "gs_rho_analytic": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I64, _I64, _D, _D, _P, _I]),
     "gs_sweep_freespec": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _D, _D, _I64, _P, _P,
                                _I64, _I, _P, _P, _P, _P, _P, _P]),

@@ -435,6 +435,44 @@ int gs_bdraw(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, cons
                     chain_base, chain_mask, b, info, 0);
 }
 
+int64_t gs_model_tiled_stride(int NF, int NMX) { return model_tiled_doubles(NF, NMX); }
+
+int gs_model_tile(gs_ctx* ctx, int n_psr, int NF, int NMX, const double* model, const int32_t* nm, double* tiled) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0) return fail_arg(2, "n_psr < 0");
+  if (!nf_supported(NF)) return fail_arg(3, "NF must be even and <= 64");
+  if (NMX < 0 || NMX > 64) return fail_arg(4, "NMX must be in 0..64");
+  if (!model || !nm || !tiled) return fail_arg(5, "NULL array");
+  if (n_psr == 0) return 0;
+  launch_model_tile(ctx->stream, model, n_psr, NF, NMX, nm, tiled);
+  return after_launch("k_model_tile");
+}
+
+int gs_bdraw_tiled(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, const double* tiled,
+                   const int32_t* fidx, const int32_t* midx, const int32_t* nm, const double* phiinv_F,
+                   const double* z, int64_t sweep, int event, int64_t chain_base, const int32_t* chain_mask,
+                   double* b, int32_t* info) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
+  if (!nf_supported(NF)) return fail_arg(4, "NF must be even and <= 64");
+  if (NMX < 0 || NMX > 64) return fail_arg(5, "NMX must be in 0..64");
+  if (ldb < NF + 1) return fail_arg(6, "ldb too small");
+  if (!tiled || !fidx || !midx || !nm || !phiinv_F || !b) return fail_arg(7, "NULL array");
+  if (n_psr == 0 || n_chain == 0) return 0;
+  BdrawArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.ldb = ldb; a.event = event;
+  a.mstride = model_tiled_doubles(NF, NMX); a.sweep = sweep; a.chain_base = chain_base;
+  a.sweep_dev = ctx->sweep_dev;
+  a.model = tiled; a.fidx = fidx; a.midx = midx; a.nm = nm; a.chain_mask = chain_mask;
+  a.phiinv_F = phiinv_F; a.z = z;
+  a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = 3;  /* tile variant */ a.psr_base = ctx->psr_base;
+  a.fail_count = ctx->fail_counts;
+  a.model_per_sys = 0;
+  a.mask_per_sys = ctx->x_per_sys;
+  a.phi_per_chain = ctx->phi_per_chain;
+  return launch_rc(launch_bdraw_tiled(ctx->stream, a), "k_bdraw_tiled");
+}
+
 int gs_bdraw_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, const double* model,
                  const int32_t* fidx, const int32_t* midx, const int32_t* nm, const double* phiinv_F,
                  const double* z, int64_t sweep, int event, int64_t chain_base, const int32_t* chain_mask,

@@ -68,6 +68,23 @@ struct ModelLds {
   const double* R;   // NMX x NMX
 };
 
+template <bool FX>
+__device__ __forceinline__ ModelTiled model_tiled_view(const double* base, int NF, int NMX) {
+  ModelTiled m;
+  m.S = base;
+  m.fixt = FX;  // == model_tiled_fix(NMX): the launcher picks the instantiation
+  if (FX) {
+    m.G = base + model_tiled_g_offset(NF);
+    m.R = base + model_tiled_r_offset(NF, NMX);
+    m.h = base + model_tiled_h_offset(NF, NMX);
+  } else {  // row-major G | h | R after S'
+    m.G = base + model_tiled_g_offset(NF);
+    m.h = m.G + (int64_t)NMX * (NF + 1);
+    m.R = m.h + NMX;
+  }
+  return m;
+}
+
 __device__ __forceinline__ ModelLds model_view(const double* base, int NF, int NMX) {
   ModelLds m;
   m.S0 = base;
@@ -229,8 +246,9 @@ __device__ __forceinline__ void stage_model(double* lds, const double* g, int64_
 #endif
 __device__ void stage_model_tiled(double* __restrict__ L, const double* __restrict__ g, int NF, int NMX, int nM) {
   const int NT = model_tiled_nt(NF), LD = NF + 1, nP = model_tiled_np(NMX);
-  const int oG = (int)model_tiled_g_offset(NF), oR = (int)model_tiled_r_offset(NF, NMX);
-  const int oH = (int)model_tiled_h_offset(NF, NMX), n = (int)model_tiled_doubles(NF, NMX);
+  const bool fixt = model_tiled_fix(NMX);
+  const int oG = (int)model_tiled_g_offset(NF), n = (int)model_tiled_doubles(NF, NMX);
+  const int oR = fixt ? (int)model_tiled_r_offset(NF, NMX) : n, oH = fixt ? (int)model_tiled_h_offset(NF, NMX) : n;
   const double* S0 = g;  // NF x (NF + 1), column NF = dF
   const double* G = g + NF * LD + NF;
   const double* h = G + NMX * LD;
@@ -250,6 +268,9 @@ __device__ void stage_model_tiled(double* __restrict__ L, const double* __restri
         v = S0[col * LD + NF];  // ... and row
       else if (r == col)
         v = 1.0;  // identity padding (the augmented pivot too)
+    } else if (!fixt) {  // row-major G | h | R, copied as they are
+      const int k = idx - oG;
+      if (k < NMX * LD + NMX + NMX * NMX) v = G[k];
     } else if (idx < oR) {  // G' = -G: chunk P (rows 16 P + c), tile column J
       const int k = idx - oG, P = k / (NT * 256), J = (k >> 8) % NT;
       const int row = 16 * P + c, f = 16 * J + 4 * s + q;
@@ -394,10 +415,10 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_bdraw(Bdraw
   if constexpr (TL) {
     stage_model_tiled(lds, A.model + (int64_t)p * A.mstride, NF, A.NMX, nM);
     mlds = model_tiled_doubles(NF, A.NMX);
-    M.S = lds;
-    M.G = lds + model_tiled_g_offset(NF);
-    M.R = lds + model_tiled_r_offset(NF, A.NMX);
-    M.h = lds + model_tiled_h_offset(NF, A.NMX);
+    if (model_tiled_fix(A.NMX))
+      M = model_tiled_view<true>(lds, NF, A.NMX);
+    else
+      M = model_tiled_view<false>(lds, NF, A.NMX);
   } else {
     stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
     mlds = A.mstride;
@@ -409,6 +430,41 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_bdraw(Bdraw
     const int c = (g0 + r) * WPB + wave;
     if (c >= A.n_chain) break;
     bdraw_item<NFC, NTC, BC>(A, M, p, c, NF, nM, fi, mi, scr, lane);
+  }
+}
+
+// ------------------------------------------------------------ tiled shared models (gs_bdraw_tiled)
+// Register-tile copies of n_psr shared model blocks (one workgroup per pulsar, the fused sweep's
+// stage_model_tiled writing to global memory), once per white-noise state.
+__global__ void k_model_tile(const double* __restrict__ model, int64_t mstride, int NF, int NMX,
+                             const int32_t* __restrict__ nm, double* __restrict__ tiled, int64_t tstride) {
+  const int p = blockIdx.x;
+  stage_model_tiled(tiled + p * tstride, model + p * mstride, NF, NMX, nm[p]);
+}
+
+// k_bdraw on precomputed tiled blocks: each workgroup DMA-stages its pulsar's tile-layout block
+// (30.8 KB at NF = 60, nm = 16, against 40.5 KB row-major) for GS_BDRAW_LOOP chain groups, and
+// the draw loads its tiles lane-linearly (tile variant only).
+template <int NFC, int NTC, int WPB, bool FX>
+__global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_bdraw_tiled(BdrawArgs A) {
+  extern __shared__ double lds[];
+  const int NF = NFC ? NFC : A.NF;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nb = (A.n_chain + WPB - 1) / WPB;
+  const int nbl = (nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP;
+  const int p = blockIdx.x / nbl;
+  const int g0 = (blockIdx.x % nbl) * GS_BDRAW_LOOP;
+  const int nM = A.nm[p];
+  const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
+  const int mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
+  stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+  const ModelTiled M = model_tiled_view<FX>(lds, NF, A.NMX);
+  double* scr = lds + A.mstride + wave * gs_tile_scr(NF);
+#pragma unroll 1
+  for (int r = 0; r < GS_BDRAW_LOOP; ++r) {
+    const int c = (g0 + r) * WPB + wave;
+    if (c >= A.n_chain) break;
+    bdraw_item<NFC, NTC, GS_BCAST_TILE>(A, M, p, c, NF, nM, fi, mi, scr, lane);
   }
 }
 
@@ -455,8 +511,11 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
 #ifndef GS_RHO_EXP
 #define GS_RHO_EXP 0
 #endif
-template <int NFC, int NTC, int WPB, int BC>
-__global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_sweep_freespec(SweepArgs A) {
+// FX: the tiled model block's fixed-prior part in tiles (nm <= 16, k_sweep_freespec) or row-major
+// (k_sweep_freespec_rm): a compile-time choice, so each kernel carries only its own fixed-block
+// code (both in one kernel cost the headline 7 more spilled VGPRs, +1.2 %, r03j).
+template <int NFC, int NTC, int WPB, int BC, bool FX>
+__device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
   extern __shared__ double lds[];
   const int NF = NFC ? NFC : A.NF;
   const int NFR = NF / 2;
@@ -480,10 +539,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_sweep_frees
   using ModelT = typename std::conditional<TL, ModelTiled, ModelLds>::type;
   ModelT M;
   if constexpr (TL) {
-    M.S = lds;
-    M.G = lds + model_tiled_g_offset(NF);
-    M.R = lds + model_tiled_r_offset(NF, A.NMX);
-    M.h = lds + model_tiled_h_offset(NF, A.NMX);
+    M = model_tiled_view<FX>(lds, NF, A.NMX);
   } else {
     M = model_view(lds, NF, A.NMX);
   }
@@ -629,6 +685,15 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_sweep_frees
   if (A.info && lane == 0) A.info[sys] = fail;
 }
 
+template <int NFC, int NTC, int WPB, int BC>
+__global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_sweep_freespec(SweepArgs A) {
+  sweep_freespec_body<NFC, NTC, WPB, BC, true>(A);
+}
+template <int NFC, int NTC, int WPB, int BC>
+__global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_sweep_freespec_rm(SweepArgs A) {
+  sweep_freespec_body<NFC, NTC, WPB, BC, false>(A);
+}
+
 // ------------------------------------------------------------ rho|b analytic
 __global__ void k_rho_analytic(RhoArgs A) {
   const int64_t n_sys = (int64_t)A.n_psr * A.n_chain;
@@ -704,7 +769,11 @@ int set_lds(K kernel, size_t lds) {
 
 template <int WPB>
 int dispatch_nf_sweep(int NF, int bc, dim3 grid, size_t lds, hipStream_t s, const SweepArgs& a) {
-  GS_NF_CASES(k_sweep_freespec, a)
+  if (model_tiled_fix(a.NMX)) {
+    GS_NF_CASES(k_sweep_freespec, a)
+  } else {
+    GS_NF_CASES(k_sweep_freespec_rm, a)
+  }
 }
 
 template <int WPB>
@@ -778,6 +847,47 @@ int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
   const size_t lds = (mlds + (fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) * WPB + GS_BDRAW_LDS_PAD) *
                      sizeof(double);
   return dispatch_nf_bdraw<WPB>(a.NF, a.bcast, grid, lds, s, a);
+}
+
+int launch_model_tile(hipStream_t s, const double* model, int n_psr, int NF, int NMX, const int32_t* nm,
+                      double* tiled) {
+  if (n_psr == 0) return 0;
+  hipLaunchKernelGGL(k_model_tile, dim3((unsigned)n_psr), dim3(256), 0, s, model, model_stride_doubles(NF, NMX), NF,
+                     NMX, nm, tiled, model_tiled_doubles(NF, NMX));
+  return 0;
+}
+
+int launch_bdraw_tiled(hipStream_t s, const BdrawArgs& a) {
+  constexpr int WPB = GS_BDRAW_WPB;
+  const int nb = (a.n_chain + WPB - 1) / WPB;
+  dim3 grid((unsigned)(a.n_psr * ((nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP)));
+  const size_t lds = ((size_t)a.mstride + (size_t)gs_tile_scr(a.NF) * WPB) * sizeof(double);
+  const int NF = a.NF;
+#define GS_TL_LAUNCH(NFC, NTC)                                                                   \
+  if (fx) {                                                                                     \
+    if (lds > 65536 && set_lds(k_bdraw_tiled<NFC, NTC, WPB, true>, lds)) return 2;             \
+    hipLaunchKernelGGL((k_bdraw_tiled<NFC, NTC, WPB, true>), grid, dim3(64 * WPB), lds, s, a);  \
+  } else {                                                                                      \
+    if (lds > 65536 && set_lds(k_bdraw_tiled<NFC, NTC, WPB, false>, lds)) return 2;            \
+    hipLaunchKernelGGL((k_bdraw_tiled<NFC, NTC, WPB, false>), grid, dim3(64 * WPB), lds, s, a); \
+  }                                                                                             \
+  return 0;
+  const bool fx = model_tiled_fix(a.NMX);
+  switch (NF) {
+    case 20: GS_TL_LAUNCH(20, 0)
+    case 40: GS_TL_LAUNCH(40, 0)
+    case 60: GS_TL_LAUNCH(60, 0)
+    default: break;
+  }
+  if (NF <= 0 || NF > 64 || (NF & 1)) return 1;
+  switch (NF / 16 + 1) {
+    case 1: GS_TL_LAUNCH(0, 1)
+    case 2: GS_TL_LAUNCH(0, 2)
+    case 3: GS_TL_LAUNCH(0, 3)
+    case 4: GS_TL_LAUNCH(0, 4)
+    default: GS_TL_LAUNCH(0, 5)
+  }
+#undef GS_TL_LAUNCH
 }
 
 int launch_rho_analytic(hipStream_t s, const RhoArgs& a) {

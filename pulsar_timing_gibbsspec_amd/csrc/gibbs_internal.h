@@ -32,7 +32,8 @@ __host__ __device__ inline int64_t model_stride_doubles(int NF, int NMX) {
 
 // The fused sweep's LDS copy of a model block in the register-tile layout (gibbs_tile.h
 // ModelTiled): S' (NT(NT+1)/2 tiles: the augmented, identity-padded Schur block), G' (nP x NT
-// tiles), R' (nP(nP+1)/2 tiles), each tile 4 registers x 64 lanes, then h (NMX, even).
+// tiles), R' (nP(nP+1)/2 tiles), each tile 4 registers x 64 lanes, then h (NMX, even) -- or, for
+// NMX > 16, S' followed by the row-major G | h | R (model_tiled_fix).
 // NT = NF/16 + 1 tile rows, nP = ceil(NMX/16) fixed-block chunks.
 __host__ __device__ inline int model_tiled_nt(int NF) { return NF / 16 + 1; }
 __host__ __device__ inline int model_tiled_np(int NMX) { return (NMX + 15) / 16; }
@@ -47,8 +48,15 @@ __host__ __device__ inline int64_t model_tiled_h_offset(int NF, int NMX) {
   const int nP = model_tiled_np(NMX);
   return model_tiled_r_offset(NF, NMX) + (int64_t)nP * (nP + 1) / 2 * 256;
 }
+// With more than 16 timing-model columns the fixed block stays row-major (G | h | R exactly as in
+// the model block, right after S'): two 16-row chunks of mostly-zero G'/R' tiles would take the
+// block past the LDS budget of 3 workgroups per CU (nm = 17 in configs[2]/[3]: 43 KB tiled vs
+// 30 KB S' + row-major G/h/R).
+__host__ __device__ inline bool model_tiled_fix(int NMX) { return NMX <= 16; }
 __host__ __device__ inline int64_t model_tiled_doubles(int NF, int NMX) {
-  return model_tiled_h_offset(NF, NMX) + ((NMX + 1) & ~1);
+  if (model_tiled_fix(NMX)) return model_tiled_h_offset(NF, NMX) + ((NMX + 1) & ~1);
+  const int64_t n = model_tiled_g_offset(NF) + (int64_t)NMX * (NF + 1) + NMX + (int64_t)NMX * NMX;
+  return (n + 1) & ~int64_t(1);
 }
 
 // gs_prefix / gs_prefix_sys / gs_prefix_dd (gibbs_prefix.hip)
@@ -124,6 +132,9 @@ struct RhoArgs {
 
 int launch_sweep_freespec(hipStream_t s, const SweepArgs& a);
 int launch_bdraw(hipStream_t s, const BdrawArgs& a);
+int launch_bdraw_tiled(hipStream_t s, const BdrawArgs& a);
+int launch_model_tile(hipStream_t s, const double* model, int n_psr, int NF, int NMX, const int32_t* nm,
+                      double* tiled);
 // large free-spectrum blocks (64 < NF <= 255), tiles in a context-owned workspace
 bool big_nf_supported(int NF);
 int64_t big_ws_doubles_per_sys(int NF);

@@ -532,9 +532,10 @@ __device__ __forceinline__ double add_on_diag(double v, double a, int s) {
 struct ModelTiled {
   static constexpr bool tiled = true;
   const double* S;
-  const double* G;
-  const double* R;
+  const double* G;  // G' tiles, or row-major G (NMX x (NF+1)) when !fixt
+  const double* R;  // R' tiles, or row-major R (NMX x NMX) when !fixt
   const double* h;
+  bool fixt = true;  // fixed block in tiles (NMX <= 16, model_tiled_fix)
   const double* S0 = nullptr;  // unused (the row-major fields of ModelLds)
   const double* dF = nullptr;
 };
@@ -813,7 +814,9 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
     const int row = 16 * P + c;
     const bool rok = row < nM;
     double p = 0.0;
-    if constexpr (TILED) {
+    bool fixt = false;
+    if constexpr (TILED) fixt = M.fixt;
+    if (fixt) {
       // G' = -G and R' as C-layout tiles, zero beyond nM rows / NF columns (ModelTiled)
       const int nPl = (NMX + 15) >> 4;
       const double* Gl = M.G + lane + z0 + P * (NT * 256);

@@ -9,6 +9,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -122,6 +124,15 @@ class DeviceModel:
         info = self.info.cpu().numpy()
         if info.any():
             raise np.linalg.LinAlgError(f"fixed-prior block not positive definite: info={info}")
+        # register-tile copies for the one-draw-per-system b|rho launches (gs_bdraw_tiled)
+        if self.NF <= FUSED_NF_MAX and self.NMX <= NMX_FUSED:
+            ts = int(lib.gs_model_tiled_stride(self.NF, self.NMX))
+            if getattr(self, "model_tiled", None) is None:
+                self.model_tiled = torch.empty(self.P * ts, dtype=torch.float64, device=self.ctx.device)
+            check(lib.gs_model_tile(h, self.P, self.NF, self.NMX, ptr(self.model), ptr(self.nm_dev),
+                                    ptr(self.model_tiled)), "gs_model_tile")
+        else:
+            self.model_tiled = None
 
     def lnl_constants(self):
         """-1/2 (sum log N + r^T N^-1 r) + 1/2 sum_M log phiinv_M per pulsar (the model
@@ -454,10 +465,14 @@ class PTAChains:
         m, lib, h = self.model, self.ctx.lib, self.ctx.handle
         prev = self.ctx.get_option(_lib.OPT_PHI_PER_CHAIN)
         self.ctx.set_option(_lib.OPT_PHI_PER_CHAIN, int(self.phi_shared))
+        # the register-tile copies of the model blocks when the tile variant is selected (the default)
+        tiled = (m.model_tiled is not None and self.ctx.get_option(_lib.OPT_BCAST) == 3
+                 and os.environ.get("GS_PTA_TILED", "1") != "0")        # A/B knob
+        fn, name = (lib.gs_bdraw_tiled, "gs_bdraw_tiled") if tiled else (lib.gs_bdraw, "gs_bdraw")
         try:
-            check(lib.gs_bdraw(h, m.P, self.C, m.NF, m.NMX, m.ldb, ptr(m.model), ptr(m.fidx), ptr(m.midx),
-                               ptr(m.nm_dev), ptr(self.phiinv_F), ptr(z), self.it, event, self.chain_base,
-                               ptr(mask), ptr(self.b), ptr(self.info)), "gs_bdraw")
+            check(fn(h, m.P, self.C, m.NF, m.NMX, m.ldb, ptr(m.model_tiled if tiled else m.model), ptr(m.fidx),
+                     ptr(m.midx), ptr(m.nm_dev), ptr(self.phiinv_F), ptr(z), self.it, event, self.chain_base,
+                     ptr(mask), ptr(self.b), ptr(self.info)), name)
         finally:
             self.ctx.set_option(_lib.OPT_PHI_PER_CHAIN, prev)
 

@@ -501,3 +501,42 @@ def test_curn_fast_matches_numpy_order_on_random_rows(ctx, request, with_red):
     assert bad.size == 0, (bad.size, bad[:8].tolist(), out[0][bad[:8]].tolist(), out[1][bad[:8]].tolist())
     # the draws are spread over the grid, not piled on one end
     assert len(np.unique(out[1])) > 200
+
+
+@pytest.mark.parametrize("phi_shared,masked", [(False, False), (True, True)])
+def test_bdraw_tiled_equals_row_major(ctx, phi_shared, masked):
+    """gs_bdraw_tiled (register-tile copies of the model blocks, gs_model_tile) draws the same b,
+    bit for bit, as gs_bdraw on the row-major blocks: 45 ragged pulsars, Philox normals, both
+    phiinv layouts (GS_OPT_PHI_PER_CHAIN), with and without a chain gate."""
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel
+    pta = synthetic.array_pta(kind="curn", seed=0)
+    T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
+    gwid = [np.arange(60) for _ in T]
+    model = DeviceModel(ctx, T, N, R, gwid, [np.full(T[p].shape[1] - 60, 1e-40) for p in range(len(T))])
+    assert model.model_tiled is not None
+    C = 37                                                  # ragged last chain group
+    rng = np.random.default_rng(5)
+    rows = C if phi_shared else model.P * C
+    phi = dev(10.0 ** rng.uniform(12, 16, (rows, model.NF)))
+    mask = dev((rng.uniform(size=C) < 0.7).astype(np.int32), torch.int32) if masked else None
+    lib, h = ctx.lib, ctx.handle
+    prev = ctx.get_option(_lib.OPT_PHI_PER_CHAIN)
+    ctx.set_option(_lib.OPT_PHI_PER_CHAIN, int(phi_shared))
+    out = []
+    try:
+        for fn, mb in ((lib.gs_bdraw, model.model), (lib.gs_bdraw_tiled, model.model_tiled)):
+            b = torch.full((model.P * C, model.ldb), 7.0, dtype=torch.float64, device="cuda")
+            info = torch.zeros(model.P * C, dtype=torch.int32, device="cuda")
+            _lib.check(fn(h, model.P, C, model.NF, model.NMX, model.ldb, _lib.ptr(mb), _lib.ptr(model.fidx),
+                          _lib.ptr(model.midx), _lib.ptr(model.nm_dev), _lib.ptr(phi), None, 3, _lib.EV_B, 0,
+                          _lib.ptr(mask), _lib.ptr(b), _lib.ptr(info)), "bdraw")
+            out.append((b.cpu().numpy(), info.cpu().numpy()))
+    finally:
+        ctx.set_option(_lib.OPT_PHI_PER_CHAIN, prev)
+    (b0, i0), (b1, i1) = out
+    assert not i0.any() and not i1.any()
+    assert np.array_equal(b0, b1)
+    if masked:                                              # gated systems keep b
+        keep = np.tile(mask.cpu().numpy() == 0, model.P)
+        assert keep.any() and np.all(b1[keep] == 7.0)

@@ -31,6 +31,9 @@ def one(res, frag):
 HOT = [
     ("k_bdrawILi60ELi0ELi4ELi3E", 3, 2),           # PTA / CURN b|rho (configs[3]); 4 chain groups
                                                    # per workgroup: 2 spills, measured faster (r03h)
+    ("k_bdraw_tiledILi60ELi0ELi4ELb1E", 3, 0),     # PTA b|rho on register-tile model copies (nm <= 16)
+    ("k_bdraw_tiledILi60ELi0ELi4ELb0E", 3, 0),     # ... nm > 16 (configs[3]: row-major fixed block)
+    ("k_sweep_freespec_rmILi60ELi0ELi4ELi3E", 3, 16),  # configs[2] (nm up to 17)
     ("k_sweep_freespecILi60ELi0ELi4ELi3E", 3, 16),  # headline fused sweep (configs[1], [2]): 3 waves,
                                                     # 13 spills outside the inner body (round 3)
     ("k_rho_red_waveE", 4, 0),                     # CURN + red grid CDF (f64 wave kernel)

@@ -12,4 +12,4 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_f
 echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $R/bench.py $ARGS > $OUT/write.log 2>&1; rc=$?
 echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
-cd $R && SWEEPS=1 CHAINS=92160 HEAD_LAUNCHES=6 python tools/pmc_traffic.py $OUT "k_bdraw<60" $OUT/pmc_traffic_curn.json
+cd $R && SWEEPS=1 CHAINS=92160 HEAD_LAUNCHES=6 python tools/pmc_traffic.py $OUT "k_bdraw_tiled<60" $OUT/pmc_traffic_curn.json
