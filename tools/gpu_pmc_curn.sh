@@ -1,6 +1,7 @@
 #!/bin/bash
-# PMC traffic (FETCH_SIZE, WRITE_SIZE in separate passes) of k_bdraw in the configs[3] CURN
-# line (45 pulsars x 2048 chains = 92160 systems, one wavefront each: grid 92160 x 64).
+# PMC traffic (FETCH_SIZE, WRITE_SIZE in separate passes) of k_bdraw_tiled in the configs[3] CURN
+# line (45 pulsars x 2048 chains = 92160 systems, one wavefront each, 4 chain groups of 4 waves per
+# workgroup: grid 45 x 128 workgroups x 256 work-items).
 set -u
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/pmc_curn
@@ -12,4 +13,4 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_f
 echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $R/bench.py $ARGS > $OUT/write.log 2>&1; rc=$?
 echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
-cd $R && SWEEPS=1 CHAINS=92160 HEAD_LAUNCHES=6 python tools/pmc_traffic.py $OUT "k_bdraw_tiled<60" $OUT/pmc_traffic_curn.json
+cd $R && SWEEPS=1 CHAINS=92160 GRID=1474560 HEAD_LAUNCHES=6 python tools/pmc_traffic.py $OUT "k_bdraw_tiled<60" $OUT/pmc_traffic_curn.json

@@ -39,7 +39,9 @@ def main():
     d = sys.argv[1]
     kernel = sys.argv[2] if len(sys.argv) > 2 else "k_sweep_freespec"
     out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(d, "pmc_traffic.json")
-    grid = int(os.environ.get("CHAINS", "4096")) * 64
+    # GRID (work-items per launch) when it is not one wavefront per chain (k_bdraw_tiled: 4 chain
+    # groups of 4 waves per workgroup)
+    grid = int(os.environ["GRID"]) if "GRID" in os.environ else int(os.environ.get("CHAINS", "4096")) * 64
     first = int(os.environ.get("HEAD_LAUNCHES", "6"))      # 1 warmup + 5 timed (bench defaults)
     fetch = per_dispatch(os.path.join(d, "pmc_fetch"), "FETCH_SIZE", kernel, grid, first)
     write = per_dispatch(os.path.join(d, "pmc_write"), "WRITE_SIZE", kernel, grid, first)
