@@ -338,8 +338,11 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
 // ------------------------------------------------------------ batched b draw
 // A/B knobs (variant builds): GS_BDRAW_PR = the fused sweep's issue priorities inside k_bdraw;
 // GS_BDRAW_LDS_PAD = extra LDS doubles per workgroup (caps the workgroups per CU, e.g. 2 waves/SIMD)
+// Issue priorities in k_bdraw / k_bdraw_tiled: on since the 4-group loop made its waves long-lived
+// (r03l: CURN k_bdraw 0.535/0.526 vs 0.549/0.535 ms, CURN + red 0.540/0.540 vs 0.554/0.551; round 2's
+// one-draw waves lost 25 % with them)
 #ifndef GS_BDRAW_PR
-#define GS_BDRAW_PR false
+#define GS_BDRAW_PR true
 #endif
 #ifndef GS_BDRAW_LDS_PAD
 #define GS_BDRAW_LDS_PAD 0
