@@ -336,16 +336,11 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
 }
 
 // ------------------------------------------------------------ batched b draw
-// A/B knobs (variant builds): GS_BDRAW_PR = the fused sweep's issue priorities inside k_bdraw;
-// GS_BDRAW_LDS_PAD = extra LDS doubles per workgroup (caps the workgroups per CU, e.g. 2 waves/SIMD)
 // Issue priorities in k_bdraw / k_bdraw_tiled: on since the 4-group loop made its waves long-lived
 // (r03l: CURN k_bdraw 0.535/0.526 vs 0.549/0.535 ms, CURN + red 0.540/0.540 vs 0.554/0.551; round 2's
 // one-draw waves lost 25 % with them)
 #ifndef GS_BDRAW_PR
 #define GS_BDRAW_PR true
-#endif
-#ifndef GS_BDRAW_LDS_PAD
-#define GS_BDRAW_LDS_PAD 0
 #endif
 // Chain groups per workgroup (shared model: staged once for all of them).  Measured on MI355X
 // (r03h, CURN line, 2048 chains x 45 pulsars, k_bdraw per launch): 1 -> 0.563-0.570 ms, 4 -> 0.545,
@@ -847,7 +842,7 @@ int launch_bdraw(hipStream_t s, const BdrawArgs& a) {
   const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
   const bool tiled = GS_BDRAW_TILED && (!fixed || a.bcast == GS_BCAST_TILE);
   const size_t mlds = a.model_per_sys ? 0 : tiled ? (size_t)model_tiled_doubles(a.NF, a.NMX) : (size_t)a.mstride;
-  const size_t lds = (mlds + (fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) * WPB + GS_BDRAW_LDS_PAD) *
+  const size_t lds = (mlds + (fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) * WPB) *
                      sizeof(double);
   return dispatch_nf_bdraw<WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
