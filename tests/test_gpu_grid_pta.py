@@ -503,17 +503,24 @@ def test_curn_fast_matches_numpy_order_on_random_rows(ctx, request, with_red):
     assert len(np.unique(out[1])) > 200
 
 
-@pytest.mark.parametrize("phi_shared,masked", [(False, False), (True, True)])
-def test_bdraw_tiled_equals_row_major(ctx, phi_shared, masked):
+@pytest.mark.parametrize("phi_shared,masked,nf,small_nm", [(False, False, 60, False), (True, True, 60, False),
+                                                           (False, True, 60, True), (True, False, 40, False)])
+def test_bdraw_tiled_equals_row_major(ctx, phi_shared, masked, nf, small_nm):
     """gs_bdraw_tiled (register-tile copies of the model blocks, gs_model_tile) draws the same b,
-    bit for bit, as gs_bdraw on the row-major blocks: 45 ragged pulsars, Philox normals, both
-    phiinv layouts (GS_OPT_PHI_PER_CHAIN), with and without a chain gate."""
+    bit for bit, as gs_bdraw on the row-major blocks: ragged pulsars, Philox normals, both
+    phiinv layouts (GS_OPT_PHI_PER_CHAIN), with and without a chain gate; all 45 pulsars (nm up to
+    17: the fixed block stays row-major), only those with nm <= 16 (the fixed block in tiles too),
+    and NF = 40 (the other 20 columns fixed-prior: nm up to 37)."""
     from pulsar_timing_gibbsspec_amd import _lib, synthetic
     from pulsar_timing_gibbsspec_amd.engine import DeviceModel
     pta = synthetic.array_pta(kind="curn", seed=0)
     T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
-    gwid = [np.arange(60) for _ in T]
-    model = DeviceModel(ctx, T, N, R, gwid, [np.full(T[p].shape[1] - 60, 1e-40) for p in range(len(T))])
+    keep = [p for p in range(len(T)) if not small_nm or T[p].shape[1] - nf <= 16]
+    assert len(keep) >= 2
+    T, N, R = [T[p] for p in keep], [N[p] for p in keep], [R[p] for p in keep]
+    gwid = [np.arange(nf) for _ in T]
+    model = DeviceModel(ctx, T, N, R, gwid, [np.full(T[p].shape[1] - nf, 1e-40) for p in range(len(T))])
+    assert (model.NMX <= 16) == small_nm
     assert model.model_tiled is not None
     C = 37                                                  # ragged last chain group
     rng = np.random.default_rng(5)
