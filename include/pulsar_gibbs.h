@@ -77,10 +77,16 @@ enum {
                          each pulsar only, compact rows (sweep * n_psr + p) * K + c (the
                          reference's bchain is chain 0: K = 1 puts n_psr rows per sweep on
                          the host instead of staging every chain's b in HBM) */
-  GS_OPT_PHI_PER_CHAIN = 6 /* 1: gs_bdraw*'s phiinv_F holds ONE row per chain (n_chain x NF),
+  GS_OPT_PHI_PER_CHAIN = 6, /* 1: gs_bdraw*'s phiinv_F holds ONE row per chain (n_chain x NF),
                          shared by every pulsar -- the CURN sweep without per-pulsar red noise,
                          whose phiinv is the common spectrum alone (pta_gibbs.py:512-548); 0
                          (default): one row per (pulsar, chain) system */
+  GS_OPT_SWEEP_SCHED = 7 /* gs_sweep_freespec's workgroup shape (tile variant; same draws): 0
+                         (default) = chosen by a cost model of the launch; 1 = 12-wave workgroups
+                         of 16 chains, each trio of waves running a 13th..16th chain in thirds of
+                         the sweeps (every wave draws 4/3 chains: n_psr x n_chain = 4096 fills the
+                         3072 wave slots of 3 waves/SIMD in one round); 2 = 4-wave workgroups,
+                         one chain per wave */
 };
 
 typedef struct gs_ctx gs_ctx;

@@ -16,6 +16,7 @@ struct gs_ctx {
   int grid_exact = 0;  // GS_OPT_GRID_EXACT
   int brec_nc = 0;     // GS_OPT_BREC_CHAINS
   int phi_per_chain = 0;  // GS_OPT_PHI_PER_CHAIN
+  int sweep_sched = 0;    // GS_OPT_SWEEP_SCHED
   const int64_t* sweep_dev = nullptr;  // gs_ctx_set_sweep_counter
   int32_t* fail_counts = nullptr;      // gs_ctx_set_fail_counts
   int32_t* grid_fallback = nullptr;    // gs_ctx_set_grid_fallback_counter
@@ -261,6 +262,10 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
       if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_PHI_PER_CHAIN must be 0 or 1");
       ctx->phi_per_chain = value;
       return 0;
+    case GS_OPT_SWEEP_SCHED:
+      if (value < 0 || value > 2) return fail_arg(3, "GS_OPT_SWEEP_SCHED must be 0, 1 or 2");
+      ctx->sweep_sched = value;
+      return 0;
     default:
       return fail_arg(2, "unknown option");
   }
@@ -274,6 +279,7 @@ int gs_ctx_get_option(gs_ctx* ctx, int option) {
   if (option == GS_OPT_GRID_EXACT) return ctx->grid_exact;
   if (option == GS_OPT_BREC_CHAINS) return ctx->brec_nc;
   if (option == GS_OPT_PHI_PER_CHAIN) return ctx->phi_per_chain;
+  if (option == GS_OPT_SWEEP_SCHED) return ctx->sweep_sched;
   return -1;
 }
 
@@ -545,6 +551,7 @@ int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.fail_count = ctx->fail_counts;
   a.bcast = ctx->bcast; a.psr_base = ctx->psr_base;
   a.brec_nc = ctx->brec_nc < n_chain ? ctx->brec_nc : 0;
+  a.sched = ctx->sweep_sched;
   return launch_rc(launch_sweep_freespec(ctx->stream, a), "k_sweep_freespec");
 }
 

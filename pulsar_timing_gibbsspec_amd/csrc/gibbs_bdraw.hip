@@ -18,6 +18,8 @@
 // Reference: PulsarBlockGibbs.update_b pulsar_gibbs.py:489-520 (SVD draw);
 // the draw law is identical (b ~ N(Sigma^-1 d, Sigma^-1)); with injected normals
 // rotated by the oracle (z' = L^T U S^-1/2 z) the samples coincide.
+#include <cmath>
+
 #include "gibbs_common.h"
 #include "gibbs_internal.h"
 #include "gibbs_tile.h"
@@ -518,14 +520,28 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
   const int NF = NFC ? NFC : A.NF;
   const int NFR = NF / 2;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nb = (A.n_chain + WPB - 1) / WPB;
-  const int p = blockIdx.x / nb;
-  const int c = (blockIdx.x % nb) * WPB + wave;
   // tile variant: the model block in the register-tile layout (stage_model_tiled); the lane-row
   // broadcast variants read the row-major block
   constexpr bool TL = GS_SWEEP_TILED && (BC == GS_BCAST_TILE || NFC == 0);
+  // BAL (12-wave workgroups = 3 waves on each SIMD of a CU, tile variant): 16 chains per
+  // workgroup, waves 0..11 own chains 0..11 and each trio (waves 3e, 3e+1, 3e+2) runs chain 12 + e
+  // in thirds of the sweeps, handed from wave to wave through LDS -- every wave draws 4/3 chains,
+  // so 4096 chains fill the 3072 wave slots of a 3-waves/SIMD launch in one round instead of a
+  // full round plus a third of a round at 1 wave/SIMD.
+  constexpr bool BAL = TL && WPB == 12;
+  constexpr int CPB = BAL ? 16 : WPB;  // chains per workgroup
+  constexpr int NTRIO = BAL ? 4 : 1;
+  const int nb = (A.n_chain + CPB - 1) / CPB;
+  const int p = blockIdx.x / nb;
+  const int cblk = (blockIdx.x % nb) * CPB;
+  const int c_own = cblk + wave;
   const int nM = A.nm[p];
   int64_t mlds;
+  if constexpr (BAL) {  // hand-off flags (the staging's barrier orders this before any use)
+    if (threadIdx.x < NTRIO)
+      reinterpret_cast<int*>(lds + model_tiled_doubles(NF, A.NMX) + WPB * (GS_SCR_DOUBLES(BC, NF) + 128 + 256) +
+                             NTRIO * 256)[threadIdx.x] = 0;
+  }
   if constexpr (TL) {
     stage_model_tiled(lds, A.model + (int64_t)p * A.mstride, NF, A.NMX, nM);
     mlds = model_tiled_doubles(NF, A.NMX);
@@ -533,7 +549,7 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
     stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
     mlds = A.mstride;
   }
-  if (c >= A.n_chain) return;
+  if (c_own >= A.n_chain) return;  // (then no extra chain either: 12 + e > wave)
   using ModelT = typename std::conditional<TL, ModelTiled, ModelLds>::type;
   ModelT M;
   if constexpr (TL) {
@@ -541,41 +557,83 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
   } else {
     M = model_view(lds, NF, A.NMX);
   }
-  const int64_t sys = (int64_t)p * A.n_chain + c;
   const int64_t n_sys = (int64_t)A.n_psr * A.n_chain;
-  const long long gchain = A.chain_base + c;
   const bool act = lane < NF, actm = lane < nM;
   const int kf = act ? (lane >> 1) : 0;  // frequency of this lane
   const int fi = act ? A.fidx[p * NF + lane] : 0;
   const int mi = actm ? A.midx[p * A.NMX + lane] : 0;
   double* scr = lds + mlds + wave * GS_SCR_DOUBLES(BC, NF);
   double* bsave = lds + mlds + WPB * GS_SCR_DOUBLES(BC, NF) + wave * 128;  // previous b (failed draws)
+  // BAL: the wave's parked own-chain state (x, bF, bM, fail) while it runs the extra chain, and
+  // the trio's hand-off slot of the extra chain (+ its progress flag), after the save slots
+  double* park = lds + mlds + WPB * (GS_SCR_DOUBLES(BC, NF) + 128) + wave * 256;
+  double* hand = lds + mlds + WPB * (GS_SCR_DOUBLES(BC, NF) + 128 + 256) + (wave / 3) * 256;
+  int* hflag =
+      reinterpret_cast<int*>(lds + mlds + WPB * (GS_SCR_DOUBLES(BC, NF) + 128 + 256) + NTRIO * 256) + wave / 3;
   GS_PH_INIT(scr)
 #ifdef GS_STATIC_PRIO
   // A/B knob: half of the workgroups (one of the two co-resident waves of a SIMD) at priority 1
   if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
 #endif
 
-  // state: x replicated on the (sin, cos) lane pair, b split over F/M lanes
-  double x = act ? A.x_state[sys * NFR + kf] : 0.0;
-  double bF = act ? A.b_state[sys * A.ldb + fi] : 0.0;
-  double bM = actm ? A.b_state[sys * A.ldb + mi] : 0.0;
-  int fail = 0;
-
   const double rhomin = A.rhomin, rhomax = A.rhomax;
   const double irhomin = 1.0 / rhomin, irhomax = 1.0 / rhomax;
-  // record pointers of this lane, advanced by one sweep's rows per iteration (no per-sweep
-  // 64-bit index products, and the SweepArgs pointers are dead inside the loop): x rows of every
-  // system; b rows of every system, or of the first brec_nc chains of each pulsar, compact
-  double* xrp = (A.x_rec && act && !(lane & 1)) ? A.x_rec + sys * NFR + kf : nullptr;
   const int64_t xr_step = n_sys * NFR;
-  const bool brec = A.b_rec && (A.brec_nc == 0 || c < A.brec_nc);
-  const int64_t brow0 = A.brec_nc == 0 ? sys : (int64_t)p * A.brec_nc + c;
-  double* bFp = (brec && act) ? A.b_rec + brow0 * A.ldb + fi : nullptr;
-  double* bMp = (brec && actm) ? A.b_rec + brow0 * A.ldb + mi : nullptr;
   const int64_t br_step = (A.brec_nc == 0 ? n_sys : (int64_t)A.n_psr * A.brec_nc) * A.ldb;
+  // segments (uniform per wave): chain, sweep range, where the state comes from / goes to
+  // (0 global state arrays, 1 the wave's park slot, 2 the trio's hand-off slot)
+  const int S = A.n_sweeps, s1 = S / 3, s2 = 2 * S / 3, t = wave % 3;
+  const int c_ext = cblk + 12 + wave / 3;
+  const bool ext = BAL && c_ext < A.n_chain;
+  const int nseg = ext ? (t == 0 ? 2 : 3) : 1;
 #pragma unroll 1
-  for (int sw = 0; sw < A.n_sweeps; ++sw) {
+  for (int seg = 0; seg < nseg; ++seg) {
+    int c = c_own, sw_a = 0, sw_b = S, src = 0, dst = 0, need = 0;
+    if (ext) {
+      if (t == 0) {  // extra [0, s1) -> hand-off, then own [0, S)
+        if (seg == 0) { c = c_ext; sw_b = s1; dst = 2; }
+      } else {       // own [0, sN) -> park, extra [sN, sN') from / to hand-off, own [sN, S) from park
+        const int sa = t == 1 ? s1 : s2, sb = t == 1 ? s2 : S;
+        if (seg == 0) { sw_b = sa; dst = 1; }
+        if (seg == 1) { c = c_ext; sw_a = sa; sw_b = sb; src = 2; dst = t == 1 ? 2 : 0; need = t; }
+        if (seg == 2) { sw_a = sa; src = 1; }
+      }
+    }
+    const int64_t sys = (int64_t)p * A.n_chain + c;
+    const long long gchain = A.chain_base + c;
+    double x, bF, bM;
+    int fail;
+    if (src == 0) {
+      x = act ? A.x_state[sys * NFR + kf] : 0.0;
+      bF = act ? A.b_state[sys * A.ldb + fi] : 0.0;
+      bM = actm ? A.b_state[sys * A.ldb + mi] : 0.0;
+      fail = 0;
+    } else {
+      double* slot = src == 1 ? park : hand;
+      if (src == 2) {
+        // wait for the trio's previous third of the extra chain (its waves are co-resident: same
+        // workgroup); bounded, so a logic error cannot hang the device
+        int spins = 0;
+        while (__hip_atomic_load(hflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1 << 24)) break;
+        }
+      }
+      gtile::lds_fence();
+      x = slot[lane];
+      bF = slot[64 + lane];
+      bM = slot[128 + lane];
+      fail = (int)slot[192];
+    }
+    // record pointers of this lane, advanced by one sweep's rows per iteration: x rows of every
+    // system; b rows of every system, or of the first brec_nc chains of each pulsar, compact
+    double* xrp = (A.x_rec && act && !(lane & 1)) ? A.x_rec + sw_a * xr_step + sys * NFR + kf : nullptr;
+    const bool brec = A.b_rec && (A.brec_nc == 0 || c < A.brec_nc);
+    const int64_t brow0 = A.brec_nc == 0 ? sys : (int64_t)p * A.brec_nc + c;
+    double* bFp = (brec && act) ? A.b_rec + sw_a * br_step + brow0 * A.ldb + fi : nullptr;
+    double* bMp = (brec && actm) ? A.b_rec + sw_a * br_step + brow0 * A.ldb + mi : nullptr;
+#pragma unroll 1
+  for (int sw = sw_a; sw < sw_b; ++sw) {
     const long long ii = A.it0 + sw;
     const int64_t rec = (int64_t)sw * n_sys + sys;
     GS_PH_BEGIN
@@ -676,11 +734,23 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
       }
     }
   }
+    if (dst == 0) {
+      if (act && !(lane & 1)) A.x_state[sys * NFR + kf] = x;
+      if (act) A.b_state[sys * A.ldb + fi] = bF;
+      if (actm) A.b_state[sys * A.ldb + mi] = bM;
+      if (A.info && lane == 0) A.info[sys] = fail;
+    } else {
+      double* slot = dst == 1 ? park : hand;
+      gtile::lds_fence();
+      slot[lane] = x;
+      slot[64 + lane] = bF;
+      slot[128 + lane] = bM;
+      if (lane == 0) slot[192] = (double)fail;
+      gtile::lds_fence();
+      if (dst == 2) __hip_atomic_store(hflag, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
   GS_PH_FLUSH(scr)
-  if (act && !(lane & 1)) A.x_state[sys * NFR + kf] = x;
-  if (act) A.b_state[sys * A.ldb + fi] = bF;
-  if (actm) A.b_state[sys * A.ldb + mi] = bM;
-  if (A.info && lane == 0) A.info[sys] = fail;
 }
 
 template <int NFC, int NTC, int WPB, int BC>
@@ -810,12 +880,45 @@ int launch_lnlike_marg(hipStream_t s, const LnlArgs& a) {
 #undef GS_LNL_LAUNCH
 }
 
+// Workgroup shape of the tile-variant sweep (GS_OPT_SWEEP_SCHED 0: this cost model).  In units
+// of one full round R (3 waves on each SIMD for the launch's sweeps; measured on MI355X, NF = 60,
+// r03n/r03q): 4-wave workgroups take floor(q/3) R + g(q mod 3) with q = waves per SIMD and a
+// part-filled last round of 1 / 2 waves per SIMD costing g = 0.46 / 0.74 R (latency-bound); the
+// 12-wave hand-off workgroups (4/3 chains per wave) take ceil(workgroups / CUs) x 4/3 R whatever
+// the last round's fill.  4096 chains: 1.46 R vs 1.33 R (2.232 vs 2.072 ms); 3072: 1 R vs 1.33 R;
+// configs[2] (45 x 256): 3.74 R vs 4 R.
+static int device_cus() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  return ncu;
+}
+static bool sweep_handoff_wins(const SweepArgs& a) {
+  if (a.sched) return a.sched == 1;
+  const double ncu = device_cus();
+  const double q = (double)a.n_psr * a.n_chain / (4.0 * ncu);
+  const double k = std::floor(q / 3.0), r = q - 3.0 * k;
+  const double g = r <= 0.0 ? 0.0 : r <= 1.0 ? 0.46 * r : r <= 2.0 ? 0.46 + 0.28 * (r - 1.0) : 0.74 + 0.26 * (r - 2.0);
+  const double wg = (double)a.n_psr * ((a.n_chain + 15) / 16);
+  const double c12 = std::ceil(wg / ncu) * (4.0 / 3.0);
+  return c12 < 0.97 * (k + g);
+}
 int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
-  const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
-  dim3 grid((unsigned)(a.n_psr * nb));
   const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
   const bool tiled = GS_SWEEP_TILED && (!fixed || a.bcast == GS_BCAST_TILE);
   const size_t mlds = tiled ? (size_t)model_tiled_doubles(a.NF, a.NMX) : (size_t)a.mstride;
+  if (tiled && sweep_handoff_wins(a)) {
+    const int nb = (a.n_chain + 15) / 16;
+    dim3 grid((unsigned)(a.n_psr * nb));
+    const size_t lds = (mlds + (size_t)12 * (gs_tile_scr(a.NF) + 128 + 256) + 4 * 256 + 2) * sizeof(double);
+    return dispatch_nf_sweep<12>(a.NF, a.bcast, grid, lds, s, a);
+  }
+  const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
+  dim3 grid((unsigned)(a.n_psr * nb));
   const size_t lds =
       (mlds + ((fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) + 128) * GS_SWEEP_WPB) * sizeof(double);
   return dispatch_nf_sweep<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);

@@ -108,6 +108,7 @@ struct BdrawArgs {
 struct SweepArgs {
   int n_psr, n_chain, NF, NMX, ldb, n_sweeps, bcast, psr_base;
   int brec_nc;  // GS_OPT_BREC_CHAINS: 0 = b_rec holds every system, K = chains c < K only
+  int sched;    // GS_OPT_SWEEP_SCHED
   int64_t mstride, it0, chain_base;
   double rhomin, rhomax;
   const double* model;

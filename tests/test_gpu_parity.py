@@ -406,3 +406,29 @@ def test_capi_edge_cases_and_errors():
     assert call() == 0 and not info.cpu().numpy().any()
     torch.cuda.synchronize()
     assert bool(torch.isfinite(b).all()) and not bool((b[:, :model.m[0]] == 7.0).any())
+
+
+@pytest.mark.parametrize("C,S", [(37, 10), (16, 1), (48, 31)])
+def test_sweep_handoff_workgroups_equal_one_chain_per_wave(ctx, model, replay, C, S):
+    """GS_OPT_SWEEP_SCHED = 1 (12-wave workgroups: each trio of waves runs a 13th..16th chain in
+    thirds of the sweeps, the chain state handed over through LDS) gives bit for bit the chains
+    of GS_OPT_SWEEP_SCHED = 2 (one chain per wave): ragged chain counts (16 chains = no extra
+    chain ran by a full trio; 37 = a partial workgroup), 1 sweep (empty thirds), sweep 0's first
+    draw, every recorded row and the final state."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import FreeSpectrumChains
+    x0 = np.random.default_rng(3).uniform(-9, -5, (C, 30))
+    out = []
+    prev = ctx.get_option(_lib.OPT_SWEEP_SCHED)
+    try:
+        for sched in (1, 2):
+            ctx.set_option(_lib.OPT_SWEEP_SCHED, sched)
+            run = FreeSpectrumChains(model, replay["rhomin"], replay["rhomax"], C, x0)
+            xr, br = run.run(S)
+            xr2, br2 = run.run(S + 2)                       # a second launch continues the state
+            out.append([t.cpu().numpy() for t in (xr, br, xr2, br2, run.x, run.b, run.info)])
+    finally:
+        ctx.set_option(_lib.OPT_SWEEP_SCHED, prev)
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    assert not out[0][-1].any()

@@ -34,7 +34,9 @@ HOT = [
     ("k_bdraw_tiledILi60ELi0ELi4ELb1E", 3, 0),     # PTA b|rho on register-tile model copies (nm <= 16)
     ("k_bdraw_tiledILi60ELi0ELi4ELb0E", 3, 0),     # ... nm > 16 (configs[3]: row-major fixed block)
     ("k_sweep_freespec_rmILi60ELi0ELi4ELi3E", 3, 16),  # configs[2] (nm up to 17)
-    ("k_sweep_freespecILi60ELi0ELi4ELi3E", 3, 16),  # headline fused sweep (configs[1], [2]): 3 waves,
+    ("k_sweep_freespecILi60ELi0ELi4ELi3E", 3, 16),
+    ("k_sweep_freespecILi60ELi0ELi12ELi3E", 3, 40),    # 12-wave hand-off workgroups (the headline's
+    ("k_sweep_freespec_rmILi60ELi0ELi12ELi3E", 3, 40),  # 4096 chains): 38 spills outside the body  # headline fused sweep (configs[1], [2]): 3 waves,
                                                     # 13 spills outside the inner body (round 3)
     ("k_rho_red_waveE", 4, 0),                     # CURN + red grid CDF (f64 wave kernel)
     ("k_rho_red_certE", 4, 0),                     # CURN + red grid CDF (default: certified f32)
