@@ -142,7 +142,8 @@ int gs_ctx_set_grid_fallback_counter(gs_ctx* ctx, int32_t* counter);
 
 /* Doubles per pulsar in a model buffer (see gs_prefix). */
 int64_t gs_model_stride(int NF, int NMX);
-/* Dynamic LDS bytes per workgroup of the b-draw / sweep kernels for (NF, NMX). */
+/* Dynamic LDS bytes per workgroup of the fused sweep (tile variant, 4-wave workgroups) for
+ * (NF, NMX); the 12-wave hand-off workgroups of GS_OPT_SWEEP_SCHED take more. */
 int gs_sweep_lds_bytes(int NF, int NMX);
 
 /*
