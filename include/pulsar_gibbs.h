@@ -49,6 +49,7 @@ enum {
   GS_EV_ECORR = 9,  /* basis-ECORR MH draws              (pulsar_gibbs.py:458-470) */
   GS_EV_ECORR_B = 10, /* epoch coefficients of a gated b draw (b_E | b_R)          */
   GS_EV_ECORR_B0 = 11, /* epoch coefficients of the first b draw                   */
+  GS_EV_HYPER = 12, /* PTA red hyper-parameter MH draws  (pta_gibbs.py:319-340)     */
   GS_EV_USER = 16   /* first id free for callers                                    */
 };
 
@@ -81,12 +82,20 @@ enum {
                          shared by every pulsar -- the CURN sweep without per-pulsar red noise,
                          whose phiinv is the common spectrum alone (pta_gibbs.py:512-548); 0
                          (default): one row per (pulsar, chain) system */
-  GS_OPT_SWEEP_SCHED = 7 /* gs_sweep_freespec's workgroup shape (tile variant; same draws): 0
+  GS_OPT_SWEEP_SCHED = 7, /* gs_sweep_freespec's workgroup shape (tile variant; same draws): 0
                          (default) = chosen by a cost model of the launch; 1 = 12-wave workgroups
                          of 16 chains, each trio of waves running a 13th..16th chain in thirds of
                          the sweeps (every wave draws 4/3 chains: n_psr x n_chain = 4096 fills the
                          3072 wave slots of 3 waves/SIMD in one round); 2 = 4-wave workgroups,
-                         one chain per wave */
+                         one chain per wave.  The 12-wave shape is used only when its LDS (model
+                         block + 12 waves' scratch, save, park and hand-off slots) fits the
+                         device's per-workgroup limit; otherwise the 4-wave shape runs.  A
+                         hand-off that does not arrive within the bounded wait (or arrives from a
+                         chain already marked failed) is never read: the chain's remaining sweeps
+                         are skipped, nothing stale is recorded, and its info is set to -1. */
+  GS_OPT_DEBUG_HANDOFF = 8 /* test only: 1 = workgroup 0's first trio never publishes its first
+                         hand-off (and the wait is shortened), so the 13th chain of workgroup 0
+                         must end with info = -1 */
 };
 
 typedef struct gs_ctx gs_ctx;
@@ -110,6 +119,9 @@ typedef struct {
 } gs_prefix_desc;
 
 int gs_version(void);
+/* Build stamp: "sources <hash of every .hip/.h source>; hipcc <HIP version>; built <UTC time> on
+ * <host>" (not an ABI entry the reference has; a provenance check for the shipped library). */
+const char* gs_build_info(void);
 const char* gs_last_error(void);
 
 int gs_ctx_create(int device, uint64_t seed, void* hip_stream, gs_ctx** out);
@@ -372,6 +384,39 @@ int gs_pta_record(gs_ctx* ctx, int n_chain, int n_param, const double* x, double
 int gs_pta_gate_phiinv(gs_ctx* ctx, int n_psr, int n_chain, int n_f, int n_param, const double* x,
                        const double* xlast, const int32_t* gw_col, const int32_t* red_col,
                        double* phiinv_F, int32_t* gate);
+/* gs_pta_gate_phiinv with the per-pulsar red phi given: phi = 10**(2 x_gw) + irn[p][k][c]
+ * (irn [n_psr x n_f x n_chain], e.g. gs_phi_powerlaw's power-law red noise, pta_gibbs.py:518-519). */
+int gs_pta_gate_phiinv_irn(gs_ctx* ctx, int n_psr, int n_chain, int n_f, int n_param, const double* x,
+                           const double* xlast, const int32_t* gw_col, const double* irn, double* phiinv_F,
+                           int32_t* gate);
+
+/*
+ * PTA red-noise hyper-parameters (PTABlockGibbs, redsample='mh', the reference's default;
+ * pta_gibbs.py:278-340 with get_lnlikelihood :577-621).
+ * gs_phi_powerlaw: out [n_psr x n_f x n_chain] = power-law red phi at the sin columns,
+ *   exp((a_pk log10_A_p + c_pk) + g_pk gamma_p) (red_sig[p].get_phi(params)[::2], :198), with
+ *   (log10_A_p, gamma_p) = x[c][pl_col[2p]], x[c][pl_col[2p+1]] and lnphi [n_psr x 3 x n_f] =
+ *   (c, a, g) (a power-law PSD is log-linear in its parameters; host-probed from get_phi).
+ * gs_hyper_mh: nsteps single-parameter Metropolis steps per chain, one wavefront each:
+ *   scale = choice([.1, .5, 1, 3, 10], p=[.1, .15, .5, .15, .1]), j = choice(n_h), q[hcol[j]] +=
+ *   randn * (0.05 n_h) * scale, accept if lnL(q) - lnL(x) > log(rand), lnL the summed
+ *   marginalised likelihood.  Parameter j belongs to pulsar hpsr[j], so only that pulsar's term
+ *   is re-evaluated: lnl_p [n_psr x n_chain] holds every pulsar's phi-dependent lnL at x (seed it
+ *   with gs_lnlike_marg on the phiinv of x) and is updated in place.  A proposal outside [hlo[j],
+ *   hhi[j]] (uniform prior) is rejected without a likelihood.  Red phi of pulsar p: red_kind 0 =
+ *   free spectrum 10**(2 x[red_col[p][k]]) (red_col [n_psr x n_f]); 1 = power law (pl_col,
+ *   lnphi as above).  phi = 10**(2 x[gw_col[k]]) + red (the common spectrum is held fixed in the
+ *   block).  inj [nsteps x n_chain x 4] = (scale, j, randn, rand) per step, or NULL (Philox event
+ *   12, slots 3 s .. 3 s + 2).  q_rec [nsteps x n_chain x 3] = (j, proposed value, accepted) or
+ *   NULL; n_acc [n_chain] accepted steps or NULL.  model: gs_prefix blocks, one per pulsar.
+ */
+int gs_phi_powerlaw(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* x, int ldx, const int32_t* pl_col,
+                    const double* lnphi, double* out);
+int gs_hyper_mh(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const double* model, const int32_t* nm,
+                double* x, int ldx, const int32_t* gw_col, int n_h, const int32_t* hcol, const int32_t* hpsr,
+                const double* hlo, const double* hhi, int red_kind, const int32_t* red_col, const int32_t* pl_col,
+                const double* lnphi, double* lnl_p, int nsteps, int64_t sweep, int64_t chain_base,
+                const double* inj, double* q_rec, int32_t* n_acc);
 
 /* ------------------------------------------------------------------------
  * (a10) White-noise Metropolis block and the per-chain TNT it forces

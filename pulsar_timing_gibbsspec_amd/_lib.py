@@ -25,8 +25,9 @@ OPT_GRID_EXACT = 4
 OPT_BREC_CHAINS = 5
 OPT_PHI_PER_CHAIN = 6
 OPT_SWEEP_SCHED = 7
+OPT_DEBUG_HANDOFF = 8
 EV_B0, EV_RHO, EV_B, EV_RED, EV_CURN, EV_GUMBEL, EV_WHITE, EV_REDMH, EV_USER = 1, 2, 3, 4, 5, 6, 7, 8, 16
-EV_ECORR, EV_ECORR_B, EV_ECORR_B0 = 9, 10, 11
+EV_ECORR, EV_ECORR_B, EV_ECORR_B0, EV_HYPER = 9, 10, 11, 12
 
 _P = C.c_void_p
 _I = C.c_int
@@ -36,6 +37,7 @@ _D = C.c_double
 # name -> (restype, argtypes)
 SIGNATURES = {
     "gs_version": (_I, []),
+    "gs_build_info": (C.c_char_p, []),
     "gs_last_error": (C.c_char_p, []),
     "gs_ctx_create": (_I, [_I, C.c_uint64, _P, C.POINTER(_P)]),
     "gs_ctx_destroy": (_I, [_P]),
@@ -72,6 +74,10 @@ SIGNATURES = {
     "gs_phi_from_x": (_I, [_P, _I, _I, _P, _I, _P, _P]),
     "gs_pta_record": (_I, [_P, _I, _I, _P, _P, _P]),
     "gs_pta_gate_phiinv": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "gs_pta_gate_phiinv_irn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "gs_phi_powerlaw": (_I, [_P, _I, _I, _I, _P, _I, _P, _P, _P]),
+    "gs_hyper_mh": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I,
+                         _I64, _I64, _P, _P, _P]),
     "gs_prefix_sys": (_I, [_P, _I, _I, _I, _I, _P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P]),
     "gs_tnt_dd": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "gs_prefix_dd": (_I, [_P, _I, _I, _I, _I, _P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -17,6 +17,7 @@ struct gs_ctx {
   int brec_nc = 0;     // GS_OPT_BREC_CHAINS
   int phi_per_chain = 0;  // GS_OPT_PHI_PER_CHAIN
   int sweep_sched = 0;    // GS_OPT_SWEEP_SCHED
+  int dbg_handoff = 0;    // GS_OPT_DEBUG_HANDOFF
   const int64_t* sweep_dev = nullptr;  // gs_ctx_set_sweep_counter
   int32_t* fail_counts = nullptr;      // gs_ctx_set_fail_counts
   int32_t* grid_fallback = nullptr;    // gs_ctx_set_grid_fallback_counter
@@ -198,6 +199,19 @@ extern "C" {
 
 int gs_version(void) { return GS_ABI_VERSION; }
 
+#ifndef GS_SRC_HASH
+#define GS_SRC_HASH "unknown"
+#endif
+#ifndef GS_HIPCC_VER
+#define GS_HIPCC_VER "unknown"
+#endif
+#ifndef GS_BUILD_STAMP
+#define GS_BUILD_STAMP "unknown"
+#endif
+const char* gs_build_info(void) {
+  return "sources " GS_SRC_HASH "; hipcc " GS_HIPCC_VER "; built " GS_BUILD_STAMP;
+}
+
 const char* gs_last_error(void) { return g_err.c_str(); }
 
 int gs_ctx_create(int device, uint64_t seed, void* stream, gs_ctx** out) {
@@ -266,6 +280,10 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
       if (value < 0 || value > 2) return fail_arg(3, "GS_OPT_SWEEP_SCHED must be 0, 1 or 2");
       ctx->sweep_sched = value;
       return 0;
+    case GS_OPT_DEBUG_HANDOFF:
+      if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_DEBUG_HANDOFF must be 0 or 1");
+      ctx->dbg_handoff = value;
+      return 0;
     default:
       return fail_arg(2, "unknown option");
   }
@@ -280,6 +298,7 @@ int gs_ctx_get_option(gs_ctx* ctx, int option) {
   if (option == GS_OPT_BREC_CHAINS) return ctx->brec_nc;
   if (option == GS_OPT_PHI_PER_CHAIN) return ctx->phi_per_chain;
   if (option == GS_OPT_SWEEP_SCHED) return ctx->sweep_sched;
+  if (option == GS_OPT_DEBUG_HANDOFF) return ctx->dbg_handoff;
   return -1;
 }
 
@@ -552,6 +571,7 @@ int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.bcast = ctx->bcast; a.psr_base = ctx->psr_base;
   a.brec_nc = ctx->brec_nc < n_chain ? ctx->brec_nc : 0;
   a.sched = ctx->sweep_sched;
+  a.dbg_handoff = ctx->dbg_handoff;
   return launch_rc(launch_sweep_freespec(ctx->stream, a), "k_sweep_freespec");
 }
 
@@ -718,9 +738,64 @@ int gs_pta_gate_phiinv(gs_ctx* ctx, int n_psr, int n_chain, int n_f, int n_param
   if (!x || !gw_col || !phiinv_F || !gate) return fail_arg(6, "NULL array");
   PtaGateArgs a;
   a.n_psr = n_psr; a.n_chain = n_chain; a.n_f = n_f; a.n_param = n_param; a.x = x; a.xlast = xlast;
-  a.gw_col = gw_col; a.red_col = red_col; a.irn = nullptr; a.phiinv_F = phiinv_F; a.gate = gate;
+  a.gw_col = gw_col; a.red_col = red_col; a.irn = nullptr; a.irn_pp = nullptr; a.phiinv_F = phiinv_F;
+  a.gate = gate;
   launch_pta_gate_phiinv(ctx->stream, a);
   return after_launch("k_pta_gate_phiinv");
+}
+
+int gs_pta_gate_phiinv_irn(gs_ctx* ctx, int n_psr, int n_chain, int n_f, int n_param, const double* x,
+                           const double* xlast, const int32_t* gw_col, const double* irn, double* phiinv_F,
+                           int32_t* gate) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0 || n_f <= 0 || n_param <= 0) return fail_arg(2, "bad size");
+  if (!x || !gw_col || !irn || !phiinv_F || !gate) return fail_arg(6, "NULL array");
+  PtaGateArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.n_f = n_f; a.n_param = n_param; a.x = x; a.xlast = xlast;
+  a.gw_col = gw_col; a.red_col = nullptr; a.irn = nullptr; a.irn_pp = irn; a.phiinv_F = phiinv_F; a.gate = gate;
+  launch_pta_gate_phiinv(ctx->stream, a);
+  return after_launch("k_pta_gate_phiinv");
+}
+
+int gs_phi_powerlaw(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* x, int ldx, const int32_t* pl_col,
+                    const double* lnphi, double* out) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0 || n_f <= 0) return fail_arg(2, "bad size");
+  if (!x) return fail_arg(5, "x is NULL");
+  if (ldx <= 0) return fail_arg(6, "ldx must be > 0");
+  if (!pl_col || !lnphi || !out) return fail_arg(7, "NULL array");
+  launch_phi_powerlaw(ctx->stream, n_psr, n_chain, n_f, x, ldx, pl_col, lnphi, out);
+  return after_launch("k_phi_powerlaw");
+}
+
+int gs_hyper_mh(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const double* model, const int32_t* nm,
+                double* x, int ldx, const int32_t* gw_col, int n_h, const int32_t* hcol, const int32_t* hpsr,
+                const double* hlo, const double* hhi, int red_kind, const int32_t* red_col, const int32_t* pl_col,
+                const double* lnphi, double* lnl_p, int nsteps, int64_t sweep, int64_t chain_base,
+                const double* inj, double* q_rec, int32_t* n_acc) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr <= 0 || n_chain < 0) return fail_arg(2, "bad batch");
+  if (!nf_supported(NF)) return fail_arg(4, "NF must be even and <= 64");
+  if (NMX < 0 || NMX > GS_NMX_WIDE) return fail_arg(5, "NMX must be in 0..128");
+  if (!model || !nm) return fail_arg(6, "model/nm is NULL");
+  if (!x) return fail_arg(8, "x is NULL");
+  if (ldx <= 0 || ldx > 8192) return fail_arg(9, "ldx must be in 1..8192");
+  if (!gw_col) return fail_arg(10, "gw_col is NULL");
+  if (n_h <= 0) return fail_arg(11, "n_h must be > 0");
+  if (!hcol || !hpsr || !hlo || !hhi) return fail_arg(12, "hyper tables are NULL");
+  if (red_kind == 0 && !red_col) return fail_arg(17, "red_kind 0 needs red_col");
+  if (red_kind == 1 && (!pl_col || !lnphi)) return fail_arg(18, "red_kind 1 needs pl_col and lnphi");
+  if (red_kind != 0 && red_kind != 1) return fail_arg(16, "red_kind must be 0 or 1");
+  if (!lnl_p) return fail_arg(20, "lnl_p is NULL");
+  if (nsteps < 0 || nsteps > (1 << 20)) return fail_arg(21, "nsteps out of range");
+  if (n_chain == 0 || nsteps == 0) return 0;
+  HyperMhArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.ldx = ldx; a.n_h = n_h; a.nsteps = nsteps;
+  a.red_kind = red_kind; a.mstride = model_stride_doubles(NF, NMX); a.sweep = sweep; a.chain_base = chain_base;
+  a.sweep_dev = ctx->sweep_dev; a.key = key_of(ctx); a.model = model; a.nm = nm; a.gw_col = gw_col;
+  a.hcol = hcol; a.hpsr = hpsr; a.red_col = red_col; a.pl_col = pl_col; a.hlo = hlo; a.hhi = hhi;
+  a.lnphi = lnphi; a.inj = inj; a.x = x; a.lnl_p = lnl_p; a.q_rec = q_rec; a.n_acc = n_acc;
+  return launch_rc(launch_hyper_mh(ctx->stream, a), "k_hyper_mh");
 }
 
 int gs_gate_phiinv_irn(gs_ctx* ctx, int n_chain, int n_f, int n_param, const double* x, const double* xlast,
@@ -730,7 +805,7 @@ int gs_gate_phiinv_irn(gs_ctx* ctx, int n_chain, int n_f, int n_param, const dou
   if (!x || !gw_col || !irn || !phiinv_F || !gate) return fail_arg(5, "NULL array");
   PtaGateArgs a;
   a.n_psr = 1; a.n_chain = n_chain; a.n_f = n_f; a.n_param = n_param; a.x = x; a.xlast = xlast;
-  a.gw_col = gw_col; a.red_col = nullptr; a.irn = irn; a.phiinv_F = phiinv_F; a.gate = gate;
+  a.gw_col = gw_col; a.red_col = nullptr; a.irn = irn; a.irn_pp = nullptr; a.phiinv_F = phiinv_F; a.gate = gate;
   launch_pta_gate_phiinv(ctx->stream, a);
   return after_launch("k_pta_gate_phiinv");
 }

@@ -507,6 +507,113 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
   }
 }
 
+// ------------------------------------------------------------ PTA red hyper-parameter MH
+// PTABlockGibbs.update_hyper_params with redsample='mh' (pta_gibbs.py:278-340), the reference's
+// default: `nsteps` single-parameter Metropolis steps per chain on the summed marginalised
+// likelihood get_lnlikelihood (:577-621).  A step moves one red parameter of ONE pulsar p, so
+// only lnL_p changes: diff = lnL_p(q) - lnL_p(x) (the reference's full sums (lnlike1 + lnprior1)
+// - (lnlike0 + lnprior0) differ from it only by rounding: the other pulsars' terms and the
+// uniform prior constants cancel), and a proposal outside its prior box is rejected without a
+// likelihood (the reference evaluates it first and can die in cho_factor on the overflowed phi).
+// One wavefront per chain (one per workgroup), the chain's x row and lnL_p of every pulsar in LDS,
+// the pulsar's model block read from global memory (all blocks ~2 MB: L2-resident), the
+// likelihood from the augmented tile factorisation of gs_lnlike_marg (same arithmetic, so
+// lnl_p seeded by gs_lnlike_marg and the in-kernel values agree exactly).
+// Proposal (pta_gibbs.py:322-328): scale = choice(sizes, p), par = choice(hind), q[par] +=
+// randn * (0.05 len(hind)) * scale; accept if diff > log(rand).  Philox event GS_EV_HYPER,
+// slots 3 s .. 3 s + 2 of step s: (u_scale, u_par), (Box-Muller pair), (u_acc, -).
+
+template <int NFC, int NTC>
+__global__ __launch_bounds__(64, 2) void k_hyper_mh(HyperMhArgs A) {
+  extern __shared__ double lds[];
+  const int NF = NFC ? NFC : A.NF;
+  const int n_f = NF / 2;
+  const int lane = threadIdx.x;
+  const int c = blockIdx.x;
+  double* xs = lds;              // the chain's x row
+  double* Ls = lds + A.ldx;      // lnL_p of every pulsar at x
+  double* scr = lds + ((A.ldx + A.n_psr + 1) & ~1);
+  double* xg = A.x + (int64_t)c * A.ldx;
+  for (int i = lane; i < A.ldx; i += 64) xs[i] = xg[i];
+  for (int p = lane; p < A.n_psr; p += 64) Ls[p] = A.lnl_p[(int64_t)p * A.n_chain + c];
+  wave_lds_sync();
+  const bool act = lane < NF;
+  const int kf = act ? (lane >> 1) : 0;
+  // the common spectrum is fixed during the block (only red parameters move)
+  const double gw = act ? pow(10.0, 2.0 * xs[A.gw_col[kf]]) : 0.0;
+  const double sig = 0.05 * A.n_h;  // sigmas = 0.05 * len(hind)
+  const long long chain = A.chain_base + c;
+  const long long sw = gs_sweep(A.sweep, A.sweep_dev);
+  int nacc = 0;
+  for (int st = 0; st < A.nsteps; ++st) {
+    double sc, z, u;
+    int j;
+    if (A.inj) {
+      const double* q = A.inj + ((int64_t)st * A.n_chain + c) * 4;
+      sc = q[0];
+      j = (int)q[1];
+      z = q[2];
+      u = q[3];
+    } else {
+      double u1, u2, v1, v2, u4;
+      gs_uniform2(gs_counter(3u * st, sw, chain, 0, GS_EV_HYPER), A.key, u1, u2);
+      gs_normal2(gs_counter(3u * st + 1, sw, chain, 0, GS_EV_HYPER), A.key, v1, v2);
+      gs_uniform2(gs_counter(3u * st + 2, sw, chain, 0, GS_EV_HYPER), A.key, u, u4);
+      sc = gs_mh_scale(u1);
+      j = min((int)(u2 * A.n_h), A.n_h - 1);
+      z = v1;
+    }
+    const int col = A.hcol[j], p = A.hpsr[j];
+    const double xq = xs[col] + (z * sig) * sc;
+    bool accepted = false;
+    if (xq >= A.hlo[j] && xq <= A.hhi[j]) {  // uniform prior: -inf outside (:298, :624-628)
+      double red;
+      if (A.red_kind == 0) {  // free spectrum: phi_red = 10^(2 rho_red)
+        const int rc = A.red_col[p * n_f + kf];
+        red = pow(10.0, 2.0 * (rc == col ? xq : xs[rc]));
+      } else {                // power law: log phi_red = (a log10_A + c) + g gamma
+        const int ca = A.pl_col[2 * p], cg = A.pl_col[2 * p + 1];
+        const double la = ca == col ? xq : xs[ca], ga = cg == col ? xq : xs[cg];
+        const double* L = A.lnphi + (int64_t)p * 3 * n_f;
+        red = exp(__dadd_rn(__dadd_rn(__dmul_rn(L[n_f + kf], la), L[kf]), __dmul_rn(L[2 * n_f + kf], ga)));
+      }
+      const double phinv = act ? 1.0 / (gw + red) : 1.0;
+      const double* mb = A.model + (int64_t)p * A.mstride;
+      const ModelLds M = model_view(mb, NF, A.NMX);
+      double yy = 0.0, ldS = 0.0;
+      int fail;
+      if constexpr (NFC == 0)
+        fail = bdraw_tile_n<NTC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr, NF);
+      else
+        fail = bdraw_tile<NFC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr);
+      double lph = act ? log(phinv) : 0.0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) lph += __shfl_xor(lph, o);
+      const int64_t ao = model_aux_offset(NF, A.NMX);
+      const double L1 = fail ? -__builtin_inf() : 0.5 * (mb[ao + 1] + yy - 2.0 * mb[ao] - ldS) + 0.5 * lph;
+      const double diff = L1 - Ls[p];
+      if (diff > log(u)) {
+        accepted = true;
+        ++nacc;
+        if (lane == 0) {
+          xs[col] = xq;
+          Ls[p] = L1;
+        }
+      }
+      wave_lds_sync();
+    }
+    if (A.q_rec && lane == 0) {
+      double* qr = A.q_rec + ((int64_t)st * A.n_chain + c) * 3;
+      qr[0] = (double)j;
+      qr[1] = xq;
+      qr[2] = accepted ? 1.0 : 0.0;
+    }
+  }
+  for (int i = lane; i < A.ldx; i += 64) xg[i] = xs[i];
+  for (int p = lane; p < A.n_psr; p += 64) A.lnl_p[(int64_t)p * A.n_chain + c] = Ls[p];
+  if (A.n_acc && lane == 0) A.n_acc[c] = nacc;
+}
+
 // ------------------------------------------------------------ fused sweep
 #ifndef GS_RHO_EXP
 #define GS_RHO_EXP 0
@@ -601,30 +708,42 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
     }
     const int64_t sys = (int64_t)p * A.n_chain + c;
     const long long gchain = A.chain_base + c;
-    double x, bF, bM;
-    int fail;
+    double x = 0.0, bF = 0.0, bM = 0.0;
+    int fail = 0;
+    // dead (wave-uniform): the hand-off of the extra chain did not arrive in time, or arrived
+    // poisoned by an earlier dead third -- the segment's sweeps are skipped, nothing stale is
+    // recorded or stored, and the chain ends with info = -1 (the host raises on it)
+    bool dead = false;
     if (src == 0) {
       x = act ? A.x_state[sys * NFR + kf] : 0.0;
       bF = act ? A.b_state[sys * A.ldb + fi] : 0.0;
       bM = actm ? A.b_state[sys * A.ldb + mi] : 0.0;
-      fail = 0;
     } else {
       double* slot = src == 1 ? park : hand;
       if (src == 2) {
         // wait for the trio's previous third of the extra chain (its waves are co-resident: same
-        // workgroup); bounded, so a logic error cannot hang the device
+        // workgroup); bounded, so a logic error cannot hang the device -- and on expiry the chain
+        // is marked failed instead of continuing from a stale slot
+        const int limit = A.dbg_handoff ? (1 << 16) : (1 << 24);
         int spins = 0;
         while (__hip_atomic_load(hflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
           __builtin_amdgcn_s_sleep(2);
-          if (++spins > (1 << 24)) break;
+          if (++spins > limit) {
+            dead = true;
+            break;
+          }
         }
       }
-      gtile::lds_fence();
-      x = slot[lane];
-      bF = slot[64 + lane];
-      bM = slot[128 + lane];
-      fail = (int)slot[192];
+      if (!dead) {
+        gtile::lds_fence();
+        x = slot[lane];
+        bF = slot[64 + lane];
+        bM = slot[128 + lane];
+        fail = (int)slot[192];
+        dead = fail < 0;
+      }
     }
+    if (dead) sw_b = sw_a;
     // record pointers of this lane, advanced by one sweep's rows per iteration: x rows of every
     // system; b rows of every system, or of the first brec_nc chains of each pulsar, compact
     double* xrp = (A.x_rec && act && !(lane & 1)) ? A.x_rec + sw_a * xr_step + sys * NFR + kf : nullptr;
@@ -735,19 +854,24 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
     }
   }
     if (dst == 0) {
-      if (act && !(lane & 1)) A.x_state[sys * NFR + kf] = x;
-      if (act) A.b_state[sys * A.ldb + fi] = bF;
-      if (actm) A.b_state[sys * A.ldb + mi] = bM;
-      if (A.info && lane == 0) A.info[sys] = fail;
+      if (!dead) {
+        if (act && !(lane & 1)) A.x_state[sys * NFR + kf] = x;
+        if (act) A.b_state[sys * A.ldb + fi] = bF;
+        if (actm) A.b_state[sys * A.ldb + mi] = bM;
+      }
+      if (A.info && lane == 0) A.info[sys] = dead ? -1 : fail;
     } else {
       double* slot = dst == 1 ? park : hand;
       gtile::lds_fence();
       slot[lane] = x;
       slot[64 + lane] = bF;
       slot[128 + lane] = bM;
-      if (lane == 0) slot[192] = (double)fail;
+      if (lane == 0) slot[192] = dead ? -1.0 : (double)fail;
       gtile::lds_fence();
-      if (dst == 2) __hip_atomic_store(hflag, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // (GS_OPT_DEBUG_HANDOFF: workgroup 0's first trio never publishes its first third, so the
+      // test sees the wait expire)
+      const bool skip = A.dbg_handoff && blockIdx.x == 0 && wave == 0;
+      if (dst == 2 && !skip) __hip_atomic_store(hflag, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
   GS_PH_FLUSH(scr)
@@ -880,6 +1004,31 @@ int launch_lnlike_marg(hipStream_t s, const LnlArgs& a) {
 #undef GS_LNL_LAUNCH
 }
 
+int launch_hyper_mh(hipStream_t s, const HyperMhArgs& a) {
+  if (a.n_chain == 0) return 0;
+  const size_t lds = ((size_t)((a.ldx + a.n_psr + 1) & ~1) + gs_tile_scr(a.NF)) * sizeof(double);
+  dim3 grid((unsigned)a.n_chain);
+#define GS_HY_LAUNCH(NFC, NTC)                                                   \
+  if (lds > 65536 && set_lds(k_hyper_mh<NFC, NTC>, lds)) return 2;               \
+  hipLaunchKernelGGL((k_hyper_mh<NFC, NTC>), grid, dim3(64), lds, s, a);         \
+  return 0;
+  switch (a.NF) {
+    case 20: GS_HY_LAUNCH(20, 0)
+    case 40: GS_HY_LAUNCH(40, 0)
+    case 60: GS_HY_LAUNCH(60, 0)
+    default: break;
+  }
+  if (a.NF <= 0 || a.NF > 64 || (a.NF & 1)) return 1;
+  switch (a.NF / 16 + 1) {
+    case 1: GS_HY_LAUNCH(0, 1)
+    case 2: GS_HY_LAUNCH(0, 2)
+    case 3: GS_HY_LAUNCH(0, 3)
+    case 4: GS_HY_LAUNCH(0, 4)
+    default: GS_HY_LAUNCH(0, 5)
+  }
+#undef GS_HY_LAUNCH
+}
+
 // Workgroup shape of the tile-variant sweep (GS_OPT_SWEEP_SCHED 0: this cost model).  In units
 // of one full round R (3 waves on each SIMD for the launch's sweeps; measured on MI355X, NF = 60,
 // r03n/r03q): 4-wave workgroups take floor(q/3) R + g(q mod 3) with q = waves per SIMD and a
@@ -897,6 +1046,17 @@ static int device_cus() {
   }
   return ncu;
 }
+// Largest dynamic LDS a workgroup may request (hipFuncSetAttribute opt-in limit; 160 KB on gfx950).
+static size_t device_lds_optin() {
+  static int lim = 0;
+  if (!lim) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&lim, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess || lim <= 0)
+      lim = 160 * 1024;
+  }
+  return (size_t)lim;
+}
 static bool sweep_handoff_wins(const SweepArgs& a) {
   if (a.sched) return a.sched == 1;
   const double ncu = device_cus();
@@ -911,11 +1071,14 @@ int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
   const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
   const bool tiled = GS_SWEEP_TILED && (!fixed || a.bcast == GS_BCAST_TILE);
   const size_t mlds = tiled ? (size_t)model_tiled_doubles(a.NF, a.NMX) : (size_t)a.mstride;
-  if (tiled && sweep_handoff_wins(a)) {
+  // the 12-wave hand-off shape holds 12 waves' scratch, save and park slots beside the model
+  // block: at large NF x NMX (e.g. NF = 60, NMX = 64: 168 KB) it does not fit, and the 4-wave
+  // shape (~102 KB there) runs instead, whatever the cost model or GS_OPT_SWEEP_SCHED say
+  const size_t lds12 = (mlds + (size_t)12 * (gs_tile_scr(a.NF) + 128 + 256) + 4 * 256 + 2) * sizeof(double);
+  if (tiled && lds12 <= device_lds_optin() && sweep_handoff_wins(a)) {
     const int nb = (a.n_chain + 15) / 16;
     dim3 grid((unsigned)(a.n_psr * nb));
-    const size_t lds = (mlds + (size_t)12 * (gs_tile_scr(a.NF) + 128 + 256) + 4 * 256 + 2) * sizeof(double);
-    return dispatch_nf_sweep<12>(a.NF, a.bcast, grid, lds, s, a);
+    return dispatch_nf_sweep<12>(a.NF, a.bcast, grid, lds12, s, a);
   }
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
   dim3 grid((unsigned)(a.n_psr * nb));

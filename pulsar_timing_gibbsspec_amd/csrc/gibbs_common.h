@@ -241,6 +241,18 @@ __device__ __forceinline__ void gs_normal2(gs_u4 c, gs_key k, double& n1, double
   n2 = r * s;
 }
 
+// ---------------------------------------------------------------- Metropolis jump scale
+// scale = np.random.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]) of every one-parameter
+// MH block of the reference (pulsar_gibbs.py:377-381, 430-433; pta_gibbs.py:290-293): numpy's
+// choice draws u and takes searchsorted(cumsum(p), u, side='right').
+__device__ __forceinline__ double gs_mh_scale(double u) {
+  if (u < 0.1) return 0.1;
+  if (u < 0.25) return 0.5;
+  if (u < 0.75) return 1.0;
+  if (u < 0.9) return 3.0;
+  return 10.0;
+}
+
 // ---------------------------------------------------------------- numpy npy_logaddexp
 __device__ __forceinline__ double np_logaddexp(double x, double y) {
   if (x == y) return x + 0.693147180559945309417232121458176568;  // x + log(2)

@@ -514,15 +514,6 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
   }
 }
 
-// scale = np.random.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]) (pulsar_gibbs.py:430-433)
-__device__ __forceinline__ double ec_scale(double u) {
-  if (u < 0.1) return 0.1;
-  if (u < 0.25) return 0.5;
-  if (u < 0.75) return 1.0;
-  if (u < 0.9) return 3.0;
-  return 10.0;
-}
-
 // One Metropolis proposal per chain (pulsar_gibbs.py:458-462): scale, one ECORR parameter
 // uniformly, q[par] += randn * (0.05 n_e) * scale.  xq = x with the jump applied;
 // prop[c] = {x column, log U, inside prior, proposed value}.  Only the ECORR columns of xq
@@ -543,7 +534,7 @@ __device__ __forceinline__ void ecorr_propose_one(const EcorrMhArgs& A, int c, i
     gs_uniform2(gs_counter(s3, sw, gc, 0, GS_EV_ECORR), A.key, u1, u2);
     gs_uniform2(gs_counter(s3 + 1, sw, gc, 0, GS_EV_ECORR), A.key, v1, v2);
     gs_uniform2(gs_counter(s3 + 2, sw, gc, 0, GS_EV_ECORR), A.key, u, u4);
-    sc = ec_scale(u1);
+    sc = gs_mh_scale(u1);
     p = min((int)(u2 * A.n_e), A.n_e - 1);
     z = sqrt(-2.0 * log(1.0 - v1)) * cospi(2.0 * v2);
   }

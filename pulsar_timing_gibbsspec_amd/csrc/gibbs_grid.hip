@@ -925,6 +925,23 @@ __global__ void k_phi_from_x(int n_chain, int ncol, const double* x, int ldx, co
   out[t] = pow(10.0, 2.0 * x[(int64_t)c * ldx + cols[j]]);
 }
 
+// Per-pulsar power-law red phi at the sin columns: out[p][k][c] = exp((a_pk la_p + c_pk) +
+// g_pk ga_p) with (la_p, ga_p) = x[c][pl_col[2p]], x[c][pl_col[2p+1]] and lnphi [n_psr x 3 x n_f]
+// = (c, a, g) -- the red_sig[p].get_phi(params)[::2] of pta_gibbs.py:198, rounded as gs_hyper_mh
+// computes it.
+__global__ void k_phi_powerlaw(int n_psr, int n_chain, int n_f, const double* x, int ldx, const int32_t* pl_col,
+                               const double* lnphi, double* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)n_psr * n_f * n_chain) return;
+  const int c = (int)(t % n_chain);
+  const int64_t pk = t / n_chain;
+  const int p = (int)(pk / n_f), k = (int)(pk % n_f);
+  const double* xc = x + (int64_t)c * ldx;
+  const double la = xc[pl_col[2 * p]], ga = xc[pl_col[2 * p + 1]];
+  const double* L = lnphi + (int64_t)p * 3 * n_f;
+  out[t] = exp(__dadd_rn(__dadd_rn(__dmul_rn(L[n_f + k], la), L[k]), __dmul_rn(L[2 * n_f + k], ga)));
+}
+
 // ------------------------------------------------------------ PTA record / gate / phiinv
 // record: x_rec[c][:] = x[c][:], xlast[c] = x[c][n_param-1]  (pta_gibbs.py:666)
 __global__ void k_pta_record(int n_chain, int n_param, const double* x, double* x_rec, double* xlast) {
@@ -959,7 +976,10 @@ __global__ void k_pta_gate_phiinv(PtaGateArgs A) {
     for (int t = lane; t < A.n_psr * A.n_f; t += 64) {
       const int p = t / A.n_f, k = t % A.n_f;
       double pinv;
-      if (A.red_col) {
+      if (A.irn_pp) {
+        const double phi = phg_s[k] + A.irn_pp[((int64_t)p * A.n_f + k) * A.n_chain + c];
+        pinv = 1.0 / phi;
+      } else if (A.red_col) {
         const double phi = phg_s[k] + pow(10.0, 2.0 * xc[A.red_col[p * A.n_f + k]]);
         pinv = 1.0 / phi;
       } else {
@@ -975,6 +995,7 @@ __global__ void k_pta_gate_phiinv(PtaGateArgs A) {
       double phi = pow(10.0, 2.0 * xc[A.gw_col[k]]);
       if (A.red_col) phi = phi + pow(10.0, 2.0 * xc[A.red_col[p * A.n_f + k]]);
       if (A.irn) phi = phi + A.irn[(int64_t)k * A.n_chain + c];
+      if (A.irn_pp) phi = phi + A.irn_pp[((int64_t)p * A.n_f + k) * A.n_chain + c];
       const double pinv = 1.0 / phi;
       double* o = A.phiinv_F + ((int64_t)p * A.n_chain + c) * (2 * A.n_f);
       o[2 * k] = pinv;
@@ -1076,6 +1097,15 @@ int launch_phi_from_x(hipStream_t s, int n_chain, int ncol, const double* x, int
   const int64_t n = (int64_t)n_chain * ncol;
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_phi_from_x, grid1(n, 256), dim3(256), 0, s, n_chain, ncol, x, ldx, cols, out);
+  return 0;
+}
+
+int launch_phi_powerlaw(hipStream_t s, int n_psr, int n_chain, int n_f, const double* x, int ldx,
+                        const int32_t* pl_col, const double* lnphi, double* out) {
+  const int64_t n = (int64_t)n_psr * n_f * n_chain;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_phi_powerlaw, grid1(n, 256), dim3(256), 0, s, n_psr, n_chain, n_f, x, ldx, pl_col, lnphi,
+                     out);
   return 0;
 }
 

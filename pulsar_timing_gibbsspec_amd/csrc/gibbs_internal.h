@@ -89,6 +89,20 @@ struct LnlArgs {
 };
 int launch_lnlike_marg(hipStream_t s, const LnlArgs& a);
 
+// PTA red-noise hyper-parameter Metropolis block (gs_hyper_mh, gibbs_bdraw.hip)
+struct HyperMhArgs {
+  int n_psr, n_chain, NF, NMX, ldx, n_h, nsteps, red_kind;
+  int64_t mstride, sweep, chain_base;
+  const int64_t* sweep_dev;
+  gs_key key;
+  const double* model;  // per-pulsar prefix model blocks (row-major), read from global / L2
+  const int32_t *nm, *gw_col, *hcol, *hpsr, *red_col, *pl_col;
+  const double *hlo, *hhi, *lnphi, *inj;
+  double *x, *lnl_p, *q_rec;
+  int32_t* n_acc;
+};
+int launch_hyper_mh(hipStream_t s, const HyperMhArgs& a);
+
 struct BdrawArgs {
   int n_psr, n_chain, NF, NMX, ldb, event, bcast, psr_base;
   int model_per_sys;  // 1: model block per (pulsar, chain) system, read from global
@@ -109,6 +123,7 @@ struct SweepArgs {
   int n_psr, n_chain, NF, NMX, ldb, n_sweeps, bcast, psr_base;
   int brec_nc;  // GS_OPT_BREC_CHAINS: 0 = b_rec holds every system, K = chains c < K only
   int sched;    // GS_OPT_SWEEP_SCHED
+  int dbg_handoff;  // GS_OPT_DEBUG_HANDOFF (test only)
   int64_t mstride, it0, chain_base;
   double rhomin, rhomax;
   const double* model;
@@ -175,6 +190,7 @@ struct PtaGateArgs {
   const double *x, *xlast;
   const int32_t *gw_col, *red_col;
   const double* irn;  // [n_f x n_chain] power-law red phi added to every pulsar's phi, or NULL
+  const double* irn_pp;  // [n_psr x n_f x n_chain] per-pulsar red phi (gs_pta_gate_phiinv_irn), or NULL
   double* phiinv_F;
   int32_t* gate;
 };
@@ -187,6 +203,8 @@ int launch_phi_from_x(hipStream_t s, int n_chain, int ncol, const double* x, int
                       double* out);
 int launch_pta_record(hipStream_t s, int n_chain, int n_param, const double* x, double* x_rec, double* xlast);
 int launch_pta_gate_phiinv(hipStream_t s, const PtaGateArgs& a);
+int launch_phi_powerlaw(hipStream_t s, int n_psr, int n_chain, int n_f, const double* x, int ldx,
+                        const int32_t* pl_col, const double* lnphi, double* out);
 
 struct WhiteMhArgs {
   int n_psr, n_chain, ldx, n_steps, psr_base;

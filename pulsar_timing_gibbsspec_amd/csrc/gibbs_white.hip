@@ -45,16 +45,6 @@ __device__ __forceinline__ double backend_sum(const double* __restrict__ s2, con
   return wave_sum(s);
 }
 
-// scale = np.random.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]) (pulsar_gibbs.py:377-381):
-// numpy's choice draws u and takes searchsorted(cdf, u, side='right').
-__device__ __forceinline__ double scale_choice(double u) {
-  if (u < 0.1) return 0.1;
-  if (u < 0.25) return 0.5;
-  if (u < 0.75) return 1.0;
-  if (u < 0.9) return 3.0;
-  return 10.0;
-}
-
 constexpr int MH_WPB = 4;
 
 // grid (ceil(n_chain / MH_WPB), n_psr); one wavefront per (pulsar, chain) system.
@@ -125,7 +115,7 @@ __global__ __launch_bounds__(64 * MH_WPB) void k_white_mh(WhiteMhArgs A) {
       gs_uniform2(gs_counter(3u * st, gs_sweep(A.sweep, A.sweep_dev), gchain, ps, GS_EV_WHITE), A.key, u1, u2);
       gs_uniform2(gs_counter(3u * st + 1, gs_sweep(A.sweep, A.sweep_dev), gchain, ps, GS_EV_WHITE), A.key, v1, v2);
       gs_uniform2(gs_counter(3u * st + 2, gs_sweep(A.sweep, A.sweep_dev), gchain, ps, GS_EV_WHITE), A.key, u, u4);
-      sc = scale_choice(u1);
+      sc = gs_mh_scale(u1);
       w = min((int)(u2 * nw), nw - 1);
       z = sqrt(-2.0 * log(1.0 - v1)) * cospi(2.0 * v2);
     }

@@ -186,18 +186,33 @@ class DeviceModel:
 class fail_counts:
     """Attach a per-system failed-draw counter (int32 device tensor) to the context for the
     duration of a block of launches (gs_ctx_set_fail_counts); the previous attachment is
-    restored on exit (contexts are shared between engines)."""
+    restored on exit (contexts are shared between engines, and scopes may nest).  The
+    context's current attachment is tracked on the Python Context object."""
 
     def __init__(self, ctx, counts):
         self.ctx, self.counts = ctx, counts
+        self._prev = None
 
     def __enter__(self):
+        self._prev = getattr(self.ctx, "_fail_counts_attached", None)
         check(self.ctx.lib.gs_ctx_set_fail_counts(self.ctx.handle, ptr(self.counts)), "gs_ctx_set_fail_counts")
+        self.ctx._fail_counts_attached = self.counts
         return self.counts
 
     def __exit__(self, *exc):
-        check(self.ctx.lib.gs_ctx_set_fail_counts(self.ctx.handle, None), "gs_ctx_set_fail_counts")
+        check(self.ctx.lib.gs_ctx_set_fail_counts(self.ctx.handle, ptr(self._prev)), "gs_ctx_set_fail_counts")
+        self.ctx._fail_counts_attached = self._prev
         return False
+
+
+def check_handoff(info):
+    """Raise if a fused-sweep chain was marked failed by the hand-off workgroups (info = -1:
+    the bounded wait for the trio's previous third expired, so the chain's remaining sweeps
+    were skipped instead of continuing from a stale slot).  Syncs."""
+    bad = torch.nonzero(info < 0).flatten()
+    if bad.numel():
+        raise RuntimeError(f"fused sweep: {bad.numel()} chain(s) lost their hand-off (systems "
+                           f"{bad[:8].tolist()}): their state was not advanced")
 
 
 class FreeSpectrumChains:
@@ -234,6 +249,10 @@ class FreeSpectrumChains:
     @property
     def n_sys(self):
         return self.model.P * self.n_chain
+
+    def check_info(self):
+        """Raise if any chain was marked failed by the hand-off workgroups (check_handoff)."""
+        check_handoff(self.info)
 
     def run(self, n_sweeps, record=True, record_b=True, z0_inj=None, z_inj=None, u_inj=None,
             x_rec=None, b_rec=None, record_b_chains=None):
@@ -398,20 +417,31 @@ class PTAChains:
 
     def __init__(self, model: DeviceModel, n_param, gw_col, red_col, gw_bounds, red_bounds, n_chain, x0,
                  chain_base=0, ngrid=1000, P_global=None, psr_lo=0, gather=None, curn_mode="exact",
-                 allreduce=None):
+                 allreduce=None, hyper=None, hyper_acl=None, hyper_warmup=None):
+        """hyper (pta_hyper.HyperSpec): per-pulsar red noise sampled by the Metropolis block
+        (PTABlockGibbs redsample='mh', pta_gibbs.py:278-340) instead of red_col's conditional
+        grid draws; hyper_acl steps per sweep (None: estimated from sweep 0's hyper_warmup
+        steps, pta_hyper.hyper_aclength)."""
         self.model, self.ctx = model, model.ctx
         dev = self.ctx.device
         P, C = model.P, int(n_chain)
         self.P, self.C, self.n_param = P, C, int(n_param)
         self.PG = int(P_global) if P_global is not None else P
         self.psr_lo = int(psr_lo)
+        if hyper is not None:
+            if red_col is not None:
+                raise ValueError("give either red_col (conditional red draws) or hyper (Metropolis), not both")
+            if self.PG != P or gather is not None or allreduce is not None:
+                raise NotImplementedError("redsample='mh' runs chain-sharded only (each rank holds every pulsar)")
+            if hyper.kind == 0:
+                red_col = hyper.red_col_host           # the free-spectrum red columns (irn, phiinv)
         # the exchange runs when pulsars are split over ranks, or whenever one is given (a
         # 1-rank group exercises the same launch sequence, e.g. to capture it in a graph)
         self.sharded = self.PG != P or (allreduce if curn_mode == "sum" else gather) is not None
         self.gather = gather
         if curn_mode not in ("exact", "sum"):
             raise ValueError("curn_mode must be 'exact' or 'sum'")
-        if curn_mode == "sum" and red_col is not None:
+        if curn_mode == "sum" and (red_col is not None or hyper is not None):
             raise ValueError("curn_mode='sum' needs irn = 0 (no per-pulsar red noise)")
         self.curn_mode = curn_mode
         self.allreduce = allreduce
@@ -424,8 +454,13 @@ class PTAChains:
         self.ngrid = ngrid
         self.ctx.set_option(_lib.OPT_PSR_BASE, self.psr_lo)
         self.gw_col = _t(np.asarray(gw_col, np.int32), torch.int32, dev)
-        self.red = red_col is not None
-        if self.red:
+        self.hyper_spec = hyper
+        self.hyper_pl = hyper is not None and hyper.kind == 1       # power-law red phi (gs_phi_powerlaw)
+        # self.red: per-pulsar red noise in phi (irn in the common draw); red_cond: drawn by the grid
+        # conditional (redsample='conditional'); otherwise by the hyper MH block
+        self.red = red_col is not None or self.hyper_pl
+        self.red_cond = red_col is not None and hyper is None
+        if red_col is not None:
             rg = np.asarray(red_col, np.int32).reshape(self.PG, self.n_f)
             self.red_col_g = _t(rg.ravel(), torch.int32, dev)
             self.red_col = _t(rg[self.psr_lo:self.psr_lo + P].ravel(), torch.int32, dev)
@@ -435,7 +470,7 @@ class PTAChains:
         else:
             self.red_col = self.red_col_g = None
         self.grid_gw = grid3(*gw_bounds, n=ngrid, device=dev)
-        self.grid_red = grid3(*red_bounds, n=ngrid, device=dev) if self.red else None
+        self.grid_red = grid3(*red_bounds, n=ngrid, device=dev) if self.red_cond else None
         self.x = _t(np.broadcast_to(np.asarray(x0, float), (C, self.n_param)), torch.float64, dev)
         self.b = torch.zeros(P * C, model.ldb, dtype=torch.float64, device=dev)
         self.tau = torch.empty(P, self.n_f, C, dtype=torch.float64, device=dev)
@@ -460,6 +495,17 @@ class PTAChains:
         self.slab_shape = ((2 if self.red else 1), self.n_f, C)
         self.it = 0
         self.redraw_b = False      # draw b | x first at the next sweep, as at sweep 0 (resume)
+        self.hyper = None
+        if hyper is not None:
+            from .pta_hyper import HYPER_WARMUP, HyperMH
+            self.hyper = HyperMH(hyper, model, C, self.n_param, self.gw_col)
+            self.hyper_acl = None if hyper_acl is None else int(hyper_acl)
+            self.hyper_warmup = HYPER_WARMUP if hyper_warmup is None else int(hyper_warmup)
+            self.hyper_short_chain = None      # chain 0's sweep-0 warm-up proposals (q[hind] rows)
+            # phiinv of every (pulsar, chain) at the block's start (seeds lnL_p), separate from the
+            # b draw's rows so the gate's phiinv is untouched
+            self.phiinv_h = torch.empty(P * C, model.NF, dtype=torch.float64, device=dev)
+            self._gate_h = torch.empty(C, dtype=torch.int32, device=dev)
 
     def _bdraw(self, z, event, mask):
         m, lib, h = self.model, self.ctx.lib, self.ctx.handle
@@ -476,23 +522,64 @@ class PTAChains:
         finally:
             self.ctx.set_option(_lib.OPT_PHI_PER_CHAIN, prev)
 
-    def _gate_phiinv(self, with_gate):
+    def _gate_phiinv(self, with_gate, out=None, gate=None):
+        out = self.phiinv_F if out is None else out
+        gate = self.gate if gate is None else gate
+        if self.hyper_pl:       # power-law red: phi = 10^(2 x_gw) + irn (irn current with x)
+            check(self.ctx.lib.gs_pta_gate_phiinv_irn(
+                self.ctx.handle, self.P, self.C, self.n_f, self.n_param, ptr(self.x),
+                ptr(self.xlast) if with_gate else None, ptr(self.gw_col), ptr(self.irn), ptr(out),
+                ptr(gate)), "gs_pta_gate_phiinv_irn")
+            return
         check(self.ctx.lib.gs_pta_gate_phiinv(
             self.ctx.handle, 1 if self.phi_shared else self.P, self.C, self.n_f, self.n_param, ptr(self.x),
             ptr(self.xlast) if with_gate else None, ptr(self.gw_col), ptr(self.red_col),
-            ptr(self.phiinv_F), ptr(self.gate)), "gs_pta_gate_phiinv")
+            ptr(out), ptr(gate)), "gs_pta_gate_phiinv")
 
-    def sweep_begin(self, x_rec=None, z0=None, u_red=None):
-        """Record, [first draw], tau and the local red draws.  Returns the local
+    def _update_irn(self):
+        """Per-pulsar red phi at the current x (the common draw's irn, pta_gibbs.py:197-198)."""
+        if self.hyper_pl:
+            self.hyper.irn(self.x, self.irn)
+        elif self.red:
+            check(self.ctx.lib.gs_phi_from_x(self.ctx.handle, self.C, self.PG * self.n_f, ptr(self.x), self.n_param,
+                                             ptr(self.red_col_g), ptr(self.irn)), "gs_phi_from_x")
+
+    def hyper_block(self, nsteps, inj=None, q_rec=None):
+        """The red hyper-parameter Metropolis block (pta_gibbs.py:278-340) for every chain:
+        lnL_p of every (pulsar, chain) seeded at the current x, then nsteps steps in place."""
+        h = self.hyper
+        if self.hyper_pl:
+            self._update_irn()
+        self._gate_phiinv(with_gate=False, out=self.phiinv_h, gate=self._gate_h)
+        h.seed(self.phiinv_h)
+        h.steps(self.x, nsteps, self.it, self.chain_base, inj=inj, q_rec=q_rec)
+
+    def sweep_begin(self, x_rec=None, z0=None, u_red=None, mh_inj=None):
+        """Record, [first draw], [hyper MH], tau and the local red draws.  Returns the local
         exchange slab [P_local, 1 or 2, n_f, C] (None when not sharded)."""
         lib, h, m = self.ctx.lib, self.ctx.handle, self.model
         ii = self.it
         check(lib.gs_pta_record(h, self.C, self.n_param, ptr(self.x), ptr(x_rec), ptr(self.xlast)),
               "gs_pta_record")
         if ii == 0 or self.redraw_b:                           # pta_gibbs.py:669-670
+            if self.hyper_pl:
+                self._update_irn()
             self._gate_phiinv(with_gate=False)
             self._bdraw(z0, _lib.EV_B0, None)
             self.redraw_b = False
+        if self.hyper is not None:                             # pta_gibbs.py:689-697 (redsample='mh')
+            if ii == 0:
+                n = self.hyper_warmup
+                q_rec = torch.empty(n, self.C, 3, dtype=torch.float64, device=self.ctx.device) \
+                    if self.hyper_acl is None else None
+                x_start = self.x[0].cpu().numpy() if q_rec is not None else None
+                self.hyper_block(n, inj=mh_inj, q_rec=q_rec)
+                if q_rec is not None:                          # aclength_hyper from the warm-up (:311-315)
+                    from .pta_hyper import hyper_aclength
+                    self.hyper_short_chain = self.hyper_spec.short_chain(x_start, q_rec[:, 0].cpu().numpy())
+                    self.hyper_acl = hyper_aclength(self.hyper_short_chain)
+            else:
+                self.hyper_block(self.hyper_acl, inj=mh_inj)
         if self.curn_mode == "sum":                            # sufficient statistic S_k
             # tau and its fixed-point digits in one pass over b (tau itself is not needed)
             check(lib.gs_tau_sum_fx_b(h, self.P, self.C, m.NF, m.ldb, ptr(m.fidx), ptr(self.b), self.fx_e0,
@@ -500,7 +587,7 @@ class PTAChains:
             return self.S_fx if self.sharded else None
         check(lib.gs_tau(h, self.P, self.C, m.NF, m.ldb, ptr(m.fidx), ptr(self.b), 0, ptr(self.tau)),
               "gs_tau")
-        if self.red:                                           # pta_gibbs.py:252-276
+        if self.red_cond:                                      # pta_gibbs.py:252-276
             check(lib.gs_phi_from_x(h, self.C, self.n_f, ptr(self.x), self.n_param, ptr(self.gw_col),
                                     ptr(self.gwphi)), "gs_phi_from_x")
             check(lib.gs_rho_red(h, self.P, self.C, self.n_f, ptr(self.tau), ptr(self.gwphi), self.ngrid,
@@ -535,15 +622,21 @@ class PTAChains:
             if self.red:
                 xr = slab_g[:, 1].reshape(self.PG * self.n_f, self.C).T
                 self.x.index_copy_(1, self.red_col_g64, xr.contiguous())
-        if self.red:
-            check(lib.gs_phi_from_x(h, self.C, self.PG * self.n_f, ptr(self.x), self.n_param,
-                                    ptr(self.red_col_g), ptr(self.irn)), "gs_phi_from_x")
+        self._update_irn()
         check(lib.gs_rho_curn(h, self.PG, self.C, self.n_f, ptr(self.tau_g), ptr(self.irn), self.ngrid,
                               ptr(self.grid_gw), ptr(u_curn), ii, self.chain_base, ptr(self.x),
                               self.n_param, ptr(self.gw_col), None), "gs_rho_curn")   # pta_gibbs.py:181-214
         self._gate_phiinv(with_gate=True)                      # pta_gibbs.py:703
         self._bdraw(z, _lib.EV_B, self.gate)                   # pta_gibbs.py:704
         self.it += 1
+
+    def check_fx(self):
+        """curn_mode='sum': raise if gs_tau_sum_fx_b saw a tau it cannot sum exactly (negative,
+        non-finite or >= rhomin_gw * 2^80, the fixed-point window) since the engine was built:
+        S would then be wrong.  Syncs."""
+        if self.curn_mode == "sum" and int(self.fx_ovf.item()):
+            raise RuntimeError("curn_mode='sum': a tau fell outside the fixed-point window (negative, "
+                               "non-finite or >= rhomin_gw * 2**80); rerun with curn_mode='exact'")
 
     def capture(self, n_sweeps):
         """Capture n_sweeps steady-state sweeps (device Philox) into a hipGraph
@@ -595,12 +688,13 @@ class PTAChains:
         self.it += self._gn
         return self.graph_rec
 
-    def sweep(self, x_rec=None, z0=None, z=None, u_red=None, u_curn=None):
+    def sweep(self, x_rec=None, z0=None, z=None, u_red=None, u_curn=None, mh_inj=None):
         """One PTABlockGibbs sweep for every chain; x_rec: (n_chain, n_param) row or None.
         z0/z: (P*n_chain, ldb) injected normals (original column order); u_red
-        (n_chain, P, n_f) and u_curn (n_chain, n_f): injected uniforms."""
+        (n_chain, P, n_f) and u_curn (n_chain, n_f): injected uniforms; mh_inj (steps, n_chain,
+        4): injected hyper-MH draws (scale, j, randn, rand)."""
         with fail_counts(self.ctx, self.fail_count):
-            slab = self.sweep_begin(x_rec=x_rec, z0=z0, u_red=u_red)
+            slab = self.sweep_begin(x_rec=x_rec, z0=z0, u_red=u_red, mh_inj=mh_inj)
             if self.sharded:
                 slab = self.allreduce(slab) if self.curn_mode == "sum" else self.gather(slab)
             self.sweep_end(slab, z=z, u_curn=u_curn)

@@ -8,8 +8,14 @@ parsing, per-pulsar gwid discovery, ``update_b`` / ``update_rho_params`` /
 arithmetic runs on the GPU (engine.PTAChains); chains are batched
 (``nchains``), chain 0 is written in the reference layout.
 
-Outside the device hot path (raise NotImplementedError): Metropolis blocks —
-white noise, ECORR, ``redsample='mh'`` hyper-parameters, ``hypersample='mh'``.
+Per-pulsar red noise: ``redsample='conditional'`` (free spectrum, grid-CDF draws) or the
+reference's default ``redsample='mh'`` (power-law or free-spectrum red noise by the
+single-parameter Metropolis block on the summed marginalised likelihood,
+pta_gibbs.py:278-340; device kernels in ``pta_hyper``).
+
+Outside the device hot path (raise NotImplementedError): the white-noise / ECORR Metropolis
+blocks of the PTA class (single-pulsar code inside the array sampler, pta_gibbs.py:551-575)
+and ``hypersample='mh'`` (dead code).
 """
 from __future__ import annotations
 
@@ -23,6 +29,7 @@ import torch
 from . import _lib
 from .engine import DeviceModel, PTAChains
 from .plumbing import basis_layout, expand_names, last_match, matching_indices, power_bounds, vector_to_dict
+from .pta_hyper import HYPER_WARMUP, HyperSpec, hyper_aclength
 from .pulsar_gibbs import HOST_CHAIN, resolve_seed
 
 
@@ -121,10 +128,13 @@ class PTABlockGibbs(object):
         if self.get_efacequad_indices().size or self.get_ecorr_indices().size:
             raise NotImplementedError("white-noise / ECORR Metropolis blocks are outside the device PTA path")
         hind = self.get_hyper_param_indices()
-        if hind.size and self.redsample != "conditional":
-            raise NotImplementedError("redsample='mh' is outside the device hot path; use 'conditional'")
-        if hind.size and hind.size != len(self.pta.pulsars) * (len(self.gwid[0]) // 2):
-            raise NotImplementedError("per-pulsar red noise must be a free spectrum on the gw basis")
+        if self.redsample not in ("conditional", "mh"):
+            raise ValueError("redsample must be 'conditional' or 'mh'")
+        if hind.size and self.redsample == "conditional" and \
+                hind.size != len(self.pta.pulsars) * (len(self.gwid[0]) // 2):
+            raise NotImplementedError("redsample='conditional' needs per-pulsar red free spectra on the gw basis")
+        if hind.size and self.redsample == "mh":
+            self._hyper_spec()          # raises for red models other than power law / free spectrum
         n_known = self.get_rho_param_indices().size + hind.size
         if n_known != len(self.param_names):
             raise NotImplementedError("parameters other than gw/red free-spectrum powers are not supported")
@@ -148,12 +158,32 @@ class PTABlockGibbs(object):
             self.d.append(b)
         return self._device_model
 
+    def _hyper_spec(self):
+        """Device tables of the red hyper-parameters (redsample='mh'), built once."""
+        if getattr(self, "_hspec", None) is None:
+            n_f = len(self.gwid[0]) // 2
+            x_ref = np.zeros(len(self.param_names))    # only each red signal's own parameters are probed
+            self._hspec = HyperSpec(self.pta, self.params, self.red_sig, self.get_hyper_param_indices(), x_ref,
+                                    n_f, self.ctx.device)
+        return self._hspec
+
     def _new_engine(self, xs, chain_base=0):
         self._check_supported()
         model = self._model(xs)
         hind = self.get_hyper_param_indices()
+        if hind.size and self.redsample == "mh":
+            return PTAChains(model, len(self.param_names), self.get_rho_param_indices(), None,
+                             (self.rhomin_gw, self.rhomax_gw), (self.rhomin_red, self.rhomax_red),
+                             self.nchains, np.asarray(xs, float), chain_base=chain_base, curn_mode="exact",
+                             hyper=self._hyper_spec(), hyper_acl=getattr(self, "aclength_hyper", None),
+                             hyper_warmup=HYPER_WARMUP)
         red_col = hind.reshape(len(self.pta.pulsars), -1) if hind.size else None
-        mode = self.curn_mode if self.curn_mode != "auto" else ("exact" if red_col is not None else "sum")
+        mode = self.curn_mode
+        if mode == "auto":
+            # 'sum' needs every tau inside its fixed-point window [rhomin_gw 2^-64, rhomin_gw 2^80):
+            # a prior wider than ~2^80 / 1e4 (tau reaches a few x 1e3 rhomax) falls back to 'exact'
+            wide = self.rhomax_gw / self.rhomin_gw > 2.0 ** 80 / 1e4
+            mode = "exact" if (red_col is not None or wide) else "sum"
         return PTAChains(model, len(self.param_names), self.get_rho_param_indices(), red_col,
                          (self.rhomin_gw, self.rhomax_gw), (self.rhomin_red, self.rhomax_red),
                          self.nchains, np.asarray(xs, float), chain_base=chain_base, curn_mode=mode)
@@ -196,10 +226,48 @@ class PTABlockGibbs(object):
         eng.it += 1
         return eng.x[0].cpu().numpy()
 
+    def get_lnlikelihood(self, xs):
+        """Summed marginalised likelihood of every pulsar (pta_gibbs.py:577-621) at xs, on the
+        GPU: -1/2 (log det N + r^T N^-1 r) + 1/2 (d^T Sigma^-1 d - log det Sigma - log det phi) per
+        pulsar; -inf if a Sigma is not positive definite."""
+        eng = self._engine_at(xs)
+        if eng.hyper_pl:
+            eng._update_irn()
+        ph = torch.empty(eng.P * eng.C, eng.model.NF, dtype=torch.float64, device=self.ctx.device)
+        gate = torch.empty(eng.C, dtype=torch.int32, device=self.ctx.device)
+        if eng.phi_shared:
+            check_phi = eng.phiinv_F
+            eng._gate_phiinv(with_gate=False)
+            ph.copy_(check_phi[:eng.C].repeat(eng.P, 1))
+        else:
+            eng._gate_phiinv(with_gate=False, out=ph, gate=gate)
+        lnl, info = eng.model.lnlike_marg(ph, eng.C)
+        lnl = lnl.view(eng.P, eng.C)[:, 0].cpu().numpy()
+        if info.view(eng.P, eng.C)[:, 0].any():
+            return -np.inf
+        return float(np.sum(lnl))
+
     def update_hyper_params(self, xs, iters=None):
-        """Per-pulsar red free spectra | b, phi_gw (pta_gibbs.py:246-276), on the GPU."""
-        if self.redsample != "conditional":
-            raise NotImplementedError("redsample='mh' is outside the device hot path")
+        """Per-pulsar red noise (pta_gibbs.py:246-342), on the GPU: redsample='conditional' ->
+        red free spectra | b, phi_gw by the grid CDF; redsample='mh' -> ``iters`` (warm-up: sets
+        cov_hyper, sigma_hyper, svd_hyper and aclength_hyper from the proposal chain,
+        :309-315) or ``aclength_hyper`` Metropolis steps on the marginalised likelihood."""
+        if self.redsample == "mh":
+            eng = self._engine_at(xs)
+            if eng.hyper is None:
+                return np.asarray(xs, float).copy()
+            n = int(iters) if iters is not None else int(self.aclength_hyper)
+            q_rec = torch.empty(n, eng.C, 3, dtype=torch.float64, device=self.ctx.device) if iters else None
+            eng.hyper_block(n, q_rec=q_rec)
+            eng.it += 1
+            if iters is not None:
+                sc = self._hspec.short_chain(np.asarray(xs, float), q_rec[:, 0].cpu().numpy())
+                body = sc[100:] if sc.shape[0] > 100 else sc
+                self.cov_hyper = np.atleast_2d(np.cov(body, rowvar=False))
+                self.sigma_hyper = np.diag(self.cov_hyper) ** 0.5
+                self.svd_hyper = np.linalg.svd(self.cov_hyper)
+                self.aclength_hyper = hyper_aclength(sc)
+            return eng.x[0].cpu().numpy()
         eng = self._engine_at(xs)
         if not eng.red:
             return np.asarray(xs, float).copy()
@@ -220,7 +288,8 @@ class PTABlockGibbs(object):
         """gibbs_state.npz next to chain.txt: every chain's x and every (pulsar, chain)
         b BEFORE sweep ``rows`` -- what resume needs to continue bit for bit (the reference
         keeps no b on disk, pta_gibbs.py:707-712)."""
-        np.savez(f"{outdir}/gibbs_state.npz", rows=rows, x=eng.x.cpu().numpy(), b=eng.b.cpu().numpy())
+        extra = {} if eng.hyper is None else {"aclength_hyper": eng.hyper_acl}
+        np.savez(f"{outdir}/gibbs_state.npz", rows=rows, x=eng.x.cpu().numpy(), b=eng.b.cpu().numpy(), **extra)
 
     def _load_state(self, outdir, rows, npar):
         f = f"{outdir}/gibbs_state.npz"
@@ -269,6 +338,12 @@ class PTABlockGibbs(object):
         seen_fail = 0
         if start > 0:
             eng.it = start
+            if eng.hyper is not None and eng.hyper_acl is None:
+                if state is not None and "aclength_hyper" in state.files:
+                    eng.hyper_acl = int(state["aclength_hyper"])
+                else:
+                    raise NotImplementedError("resuming a redsample='mh' run needs aclength_hyper (set the "
+                                              "attribute, or keep gibbs_state.npz)")
             if state is not None:
                 # the device state saved with these rows (gibbs_state.npz): the run continues
                 # exactly where the uninterrupted one would be
@@ -285,10 +360,13 @@ class PTABlockGibbs(object):
             for j in range(nxt - ii):
                 eng.sweep(x_rec=buf[j])
             rows = buf[:nxt - ii].cpu().numpy()
+            eng.check_fx()                             # curn_mode='sum': tau inside the fixed-point window
             nfail = int(eng.fail_count.sum())          # failed (non-PD) b draws, b kept
             if nfail > seen_fail:
                 print(f"WARNING: sweeps {ii}..{nxt - 1}: {nfail - seen_fail} b draws hit a non-positive-definite "
-                      "Sigma (previous b kept; pta_gibbs.py:537-546's LinAlgError branch)")
+                      "Sigma; those systems KEEP their previous b -- unlike the reference, whose LinAlgError "
+                      "branch (pta_gibbs.py:539-544) redraws b from a QR/SVD of Sigma with the wrong covariance "
+                      "(SURVEY Appendix A.7)")
                 seen_fail = nfail
             self.chain[ii:nxt] = rows[:, 0]
             if nc > 1:
@@ -311,4 +389,7 @@ class PTABlockGibbs(object):
             self._save_state(outdir, self.iter + 1, eng)
         b = eng.b.cpu().numpy()
         self._b = [b[p * eng.C, :eng.model.m[p]] for p in range(eng.P)]
+        if eng.hyper is not None:
+            self.aclength_hyper = eng.hyper_acl
+            self.hyper_acceptance = eng.hyper.acceptance()
         return self.chain

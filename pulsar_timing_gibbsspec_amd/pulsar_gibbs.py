@@ -39,17 +39,12 @@ import torch
 from . import _lib
 from .diagnostics import white_aclength
 from .ecorr import EcorrFreeSpectrumChains, EcorrModel, EcorrWhiteChains
-from .engine import DeviceModel, FreeSpectrumChains, HistoryStreamer, grid3
+from .engine import DeviceModel, FreeSpectrumChains, HistoryStreamer, check_handoff, grid3
 from .plumbing import (basis_layout, expand_names, last_match, matching_indices, power_bounds,
                        uniform_bounds, vector_to_dict)
 from .rednoise import (DE_BUFFER, RED_STEPS, RedJumps, RedNoiseChains, powerlaw_loglinear,
                        warmup as red_warmup)
 from .white import MAX_W, WhiteFreeSpectrumChains, WhiteNoiseModel, white_kind
-
-
-def _parse_uniform_bounds(param):
-    """'name:Uniform(pmin=a, pmax=b)[n]' -> (a, b)  (pulsar_gibbs.py:84-87)."""
-    return uniform_bounds(param)
 
 
 # Global chain id base of the single-call API (update_b, update_white_params, ...): its
@@ -159,18 +154,23 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
     # failed (non-PD) draws, surfaced per block as they happen: the kernels keep b and count
     # (gs_ctx_set_fail_counts); each block's counts reach pinned memory behind the block
     fc_host = [torch.zeros(P * nc, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+    info_host = [torch.zeros(P * nc, dtype=torch.int32, pin_memory=True) for _ in range(2)]
     fc_ev = [torch.cuda.Event(), torch.cuda.Event()]
     fc_seen = [int(runner.fail_count.sum())]
 
     def consume(slot, ii, nxt):
         xh, bh = (t.numpy() for t in streamer.fetch(slot))
         fc_ev[slot].synchronize()
+        # a chain whose hand-off wait expired (info = -1) was not advanced: fail loudly
+        check_handoff(info_host[slot])
         tot = int(fc_host[slot].sum())
         if tot > fc_seen[0]:
             bad = np.nonzero(fc_host[slot].numpy())[0]
             print(f"WARNING: sweeps {ii}..{nxt - 1}: {tot - fc_seen[0]} b draws hit a non-positive-definite "
-                  f"Sigma (previous b kept; the reference's LinAlgError branch, pulsar_gibbs.py:507-516); "
-                  f"systems so far: {bad[:8].tolist()}{' ...' if bad.size > 8 else ''}")
+                  f"Sigma; those chains KEEP their previous b -- unlike the reference, whose LinAlgError "
+                  f"branch (pulsar_gibbs.py:507-516) redraws b from a QR/SVD of Sigma with the wrong "
+                  f"covariance (SURVEY Appendix A.7); systems so far: {bad[:8].tolist()}"
+                  f"{' ...' if bad.size > 8 else ''}")
             fc_seen[0] = tot
         last = nxt - 1
         save = last % save_every == 0 and last > 0
@@ -200,6 +200,7 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
         runner.run(n, x_rec=xr, b_rec=br, record_b_chains=bk)
         with torch.cuda.stream(ctx.stream):
             fc_host[slot].copy_(runner.fail_count, non_blocking=True)
+            info_host[slot].copy_(runner.info, non_blocking=True)
             fc_ev[slot].record(ctx.stream)
         streamer.submit(slot, n)
         if pending is not None:
@@ -389,7 +390,7 @@ class PulsarBlockGibbs(object):
             raise NotImplementedError("ECORR phi is not 10**(2 log10_ecorr) per epoch")
         bounds = []
         for p in self.params:
-            lo, hi = _parse_uniform_bounds(p)
+            lo, hi = uniform_bounds(p)
             bounds += [(lo, hi)] * (p.size or 1)
         emin = np.array([bounds[j][0] for j in eind])
         emax = np.array([bounds[j][1] for j in eind])
@@ -476,7 +477,7 @@ class PulsarBlockGibbs(object):
         wl = []
         bounds = {}
         for p in self.params:
-            lo, hi = _parse_uniform_bounds(p)
+            lo, hi = uniform_bounds(p)
             for n in ([p.name] if not p.size else [f"{p.name}_{i}" for i in range(p.size)]):
                 bounds[n] = (lo, hi)
         for j, k, mk in zip(wind, kinds, masks):
@@ -644,14 +645,14 @@ class PulsarBlockGibbs(object):
             return np.array(self.red_sig.get_phi(self.map_params(x)))[::2]
         lnphi = powerlaw_loglinear(phi_of)
         by_index = [p for p in self.params for _ in range(p.size or 1)]
-        bounds = (_parse_uniform_bounds(by_index[ia]), _parse_uniform_bounds(by_index[ig]))
+        bounds = (uniform_bounds(by_index[ia]), uniform_bounds(by_index[ig]))
         self._red_info = (ia, ig, lnphi, bounds)
         return self._red_info
 
     def _param_bounds(self):
         lo, hi = [], []
         for p in self.params:
-            a, b = _parse_uniform_bounds(p)
+            a, b = uniform_bounds(p)
             lo += [a] * (p.size or 1)
             hi += [b] * (p.size or 1)
         return np.array(lo), np.array(hi)

@@ -87,8 +87,21 @@ def fourier_basis(toas_s, n_f, Tspan):
 
 
 def powerlaw_phi(f, Tspan, log10_A, gamma):
+    """enterprise's powerlaw PSD times df.  Far outside any prior (a Metropolis proposal such as
+    the reference's PTA jumps of 0.05 len(hind) x 10, pta_gibbs.py:290-295, reaching log10_A ~ 45,
+    gamma ~ -40) the direct product overflows to inf x 0 = NaN, and the reference's
+    get_lnlikelihood -- which it evaluates BEFORE the prior rejects the point (:298) -- dies in
+    cho_factor; those entries are evaluated in log space instead (same value wherever the direct
+    form is finite and nonzero)."""
     df = 1.0 / Tspan
-    return (10.0 ** log10_A) ** 2 / 12.0 / np.pi ** 2 * FYR ** (gamma - 3) * f ** (-gamma) * df
+    with np.errstate(over="ignore", invalid="ignore", under="ignore"):
+        phi = (10.0 ** log10_A) ** 2 / 12.0 / np.pi ** 2 * FYR ** (gamma - 3) * f ** (-gamma) * df
+    bad = ~(np.isfinite(phi) & (phi > 0))
+    if np.any(bad):
+        lphi = (2.0 * np.log(10.0) * log10_A - np.log(12.0 * np.pi ** 2) + (gamma - 3) * np.log(FYR)
+                - gamma * np.log(f) + np.log(df))
+        phi = np.where(bad, np.exp(np.minimum(lphi, 700.0)), phi)
+    return phi
 
 
 class FourierGP:
@@ -459,6 +472,10 @@ def array_pta(kind="curn_red", n_f=30, n_psr=None, gw_prior=(-9.0, -4.0), red_pr
 
     kind = 'curn'      common 'gw_crn' free spectrum only,
            'curn_red'  + per-pulsar 'red_noise' free spectrum on the same basis,
+           'curn_plred' + per-pulsar power-law 'red_noise' (log10_A Uniform(-20, -11), gamma
+                       Uniform(0, 7): model_definition.py's red_var block / enterprise's
+                       powerlaw) on the same basis -- what PTABlockGibbs' default
+                       redsample='mh' samples (pta_gibbs.py:278-340),
            'indep'     BASELINE configs[2]: no common process; every pulsar carries its
                        own 'gw' free spectrum ``{psr}_gw_log10_rho`` on its own T_span
                        (config 1's model for each of the 45 pulsars: signals white, gw,
@@ -487,9 +504,15 @@ def array_pta(kind="curn_red", n_f=30, n_psr=None, gw_prior=(-9.0, -4.0), red_pr
         if kind == "curn_red":
             rp = Uniform(f"{n}_red_noise_log10_rho", red_prior[0], red_prior[1], size=n_f)
             sigs.append(FourierGP(n, "red_noise", toas, Tspan, n_f, "spectrum", [rp]))
+        elif kind == "curn_plred":
+            la = Uniform(f"{n}_red_noise_log10_A", -20.0, -11.0)
+            ga = Uniform(f"{n}_red_noise_gamma", 0.0, 7.0)
+            sigs.append(FourierGP(n, "red_noise", toas, Tspan, n_f, "powerlaw", [la, ga]))
+        elif kind != "curn":
+            raise ValueError(f"unknown array kind {kind!r}")
         sigs.append(MeasurementNoise(n, err))
         r = _simulate_residuals(rng, gw.get_basis(), gw.freqs, Tspan, tm.get_basis(), err,
-                                log10_A, gamma, red=(-14.5, 3.0) if kind == "curn_red" else None)
+                                log10_A, gamma, red=(-14.5, 3.0) if kind in ("curn_red", "curn_plred") else None)
         models.append(PulsarModel(n, toas, r, sigs))
     return PTA(models)
 

@@ -307,6 +307,72 @@ def pta_long(ref, out, kind, niter=20000, seed=21, red_psr=(0,)):
     print("pta long:", kind, out, g.chain.shape)
 
 
+def pta_hyper_mh(ref, out, kind="curn_plred", niter=8, warm=100, acl=20, n_psr=None, nlike=4):
+    """PTABlockGibbs with the reference's DEFAULT redsample='mh' (pta_gibbs.py:278-340): per-pulsar
+    red-noise hyper-parameters by single-parameter Metropolis on the summed marginalised likelihood
+    get_lnlikelihood (:577-621), inside sample()'s order (:664-704), driven with the reference's own
+    methods as pta_run does.  Sweep 0's warm-up branch (iters=100, :283-315) ends in np.cov /
+    np.linalg.svd / acor of short_chain[100:], which is EMPTY for iters=100: numpy's SVD of the NaN
+    covariance raises LinAlgError, so the reference cannot pass sweep 0 on its own default path
+    (acor is absent here besides).  Its 100 MH steps are pinned through the steady-state branch
+    (iters=None) with aclength_hyper = warm -- the same loop body, draws and acceptance -- and
+    aclength_hyper = acl afterwards.  Every draw is captured (choice of scale, choice of parameter,
+    randn jump, rand acceptance; CURN uniforms; b normals), plus x after each hyper block and the
+    reference's get_lnlikelihood at a few states."""
+    pta = synthetic.array_pta(kind=kind, n_psr=n_psr, seed=0)
+    N = pta.get_ndiag({})
+    R = pta.get_residuals()
+    TNT, d = [], []
+    for i, T in enumerate(pta.get_basis()):          # as update_b computes them (pta_gibbs.py:523-526)
+        TNT.append(T.T @ (T / N[i][:, None]))
+        d.append(T.T @ (R[i] / N[i]))
+    np.random.seed(15)
+    g = _quiet(ref.PTABlockGibbs, pta, hypersample="conditional", redsample="mh")
+    x0 = np.concatenate([p.sample().flatten() for p in g.params])
+    hind = g.get_hyper_param_indices()
+    names = list(g.param_names)
+    chain, hyper_in, hyper_out, bhist = [], [], [], []
+    xnew = x0.copy()
+    with Capture() as cap:
+        np.random.seed(16)
+        for ii in range(niter):
+            chain.append(xnew.copy())
+            bhist.append(np.concatenate(g._b))
+            if ii == 0:
+                g._b = g.update_b(x0)
+            g.TNT, g.d = [], []
+            g.aclength_hyper = warm if ii == 0 else acl
+            hyper_in.append(xnew.copy())
+            xnew = g.update_hyper_params(xnew, iters=None)
+            hyper_out.append(xnew.copy())
+            xnew = g.update_rho_params(xnew)
+            if np.all(xnew != chain[ii][-1]):
+                g._b = g.update_b(xnew)
+    log = cap.log
+    kinds = np.array([k for k, _ in log])
+    vals = [v for _, v in log]
+    # the reference's summed marginalised likelihood at a few states (no draws consumed)
+    lstates = [hyper_in[0], hyper_out[0]] + hyper_out[1:nlike - 1]
+    lnl = []
+    for xs in lstates:
+        g.TNT, g.d = [], []
+        lnl.append(g.get_lnlikelihood(xs))
+    np.savez_compressed(out, x0=x0, chain=np.stack(chain), bhist=np.stack(bhist), b_final=np.concatenate(g._b),
+                        x_final=xnew, TNT=np.concatenate([t.ravel() for t in TNT]), d=np.concatenate(d),
+                        off=np.concatenate([[0], np.cumsum([len(v) for v in d])]), n_psr=len(pta.pulsars),
+                        hyper_in=np.stack(hyper_in), hyper_out=np.stack(hyper_out), kinds=kinds,
+                        vals=np.concatenate([np.atleast_1d(v).ravel() for v in vals]),
+                        lens=np.array([np.atleast_1d(v).size for v in vals]),
+                        warm=warm, aclength=acl, hind=hind, rind=g.get_rho_param_indices(),
+                        gwid=np.stack([np.asarray(gw) for gw in g.gwid]), m=np.array([len(b) for b in g._b]),
+                        rhomin_gw=g.rhomin_gw, rhomax_gw=g.rhomax_gw, lnl_states=np.stack(lstates),
+                        lnl=np.array(lnl), param_names=np.array(names), kind=kind,
+                        pmin=np.array([p.pmin for p in g.params for _ in range(p.size or 1)]),
+                        pmax=np.array([p.pmax for p in g.params for _ in range(p.size or 1)]))
+    print("pta hyper mh:", kind, out, len(log), "accepted moves:",
+          int(sum(np.sum(a != b) for a, b in zip(hyper_in, hyper_out))))
+
+
 def likelihoods(ref, out):
     """White-noise and fully-marginalised likelihoods (pulsar_gibbs.py:523-546, 569-610)."""
     pta = synthetic.single_pulsar_pta("J1713+0747", seed=0, efac_vary=True, n_backends=3)
@@ -559,6 +625,10 @@ def main(root):
         if f"--only-pta-long-{kind}" in sys.argv:
             pta_long(PT, os.path.join(HERE, f"pta_long_{kind}.npz"), kind)
             return
+    if "--only-pta-mh" in sys.argv:
+        pta_hyper_mh(PT, os.path.join(HERE, "pta_plred_mh.npz"), "curn_plred")
+        pta_hyper_mh(PT, os.path.join(HERE, "pta_red_mh.npz"), "curn_red", n_psr=6, niter=6, acl=30)
+        return
     if "--only-red" in sys.argv:
         red_likelihood(PB, os.path.join(HERE, "red_lnlike_j1713.npz"))
         return
@@ -568,6 +638,8 @@ def main(root):
     pta_run(PT, os.path.join(HERE, "pta_curn.npz"), "curn", niter=12)
     pta_run(PT, os.path.join(HERE, "pta_curn_red.npz"), "curn_red", niter=12)
     pta_sample_check(PT, os.path.join(HERE, "pta_sample_small.npz"))
+    pta_hyper_mh(PT, os.path.join(HERE, "pta_plred_mh.npz"), "curn_plred")
+    pta_hyper_mh(PT, os.path.join(HERE, "pta_red_mh.npz"), "curn_red", n_psr=6, niter=6, acl=30)
     white_mh(PB, os.path.join(HERE, "white_mh_j1713.npz"))
     red_likelihood(PB, os.path.join(HERE, "red_lnlike_j1713.npz"))
     ecorr_mh(PB, os.path.join(HERE, "ecorr_mh_j1713.npz"))

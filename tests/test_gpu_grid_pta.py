@@ -116,9 +116,13 @@ def test_grid_cdf_kernels_exact(ctx, kind, grid_exact, request):
         assert np.array_equal(x.cpu().numpy()[0], r["x_curn"]), ii
 
 
-@pytest.mark.parametrize("kind", ["curn", "curn_red"])
-def test_pta_engine_matches_reference_chain(ctx, kind):
-    """PTAChains (45 pulsars) fed the reference's rotated normals and uniforms."""
+@pytest.mark.parametrize("kind,mode", [("curn", "exact"), ("curn", "sum"), ("curn_red", "exact")])
+def test_pta_engine_matches_reference_chain(ctx, kind, mode):
+    """PTAChains (45 pulsars) fed the reference's rotated normals and uniforms.  mode 'sum' is
+    the production CURN path (PTABlockGibbs' curn_mode='auto' without per-pulsar red noise, the
+    benched line and the one a pulsar-sharded run all-reduces for): gs_tau_sum_fx_b ->
+    gs_fx_to_double -> gs_rho_curn_sum must pick the reference's grid index on every sweep, so
+    the recorded x chain equals the reference's exactly and the gate matches each sweep."""
     from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
     from pulsar_timing_gibbsspec_amd import synthetic
     g = golden(f"pta_{kind}.npz")
@@ -136,7 +140,7 @@ def test_pta_engine_matches_reference_chain(ctx, kind):
     hind = g["hind"]
     red_col = hind.reshape(len(T), -1) if kind == "curn_red" else None
     eng = PTAChains(model, g["x0"].size, g["rind"], red_col, (float(g["rhomin_gw"]), float(g["rhomax_gw"])),
-                    (float(g["rhomin_red"]), float(g["rhomax_red"])), 1, g["x0"])
+                    (float(g["rhomin_red"]), float(g["rhomax_red"])), 1, g["x0"], curn_mode=mode)
     xr = torch.zeros(len(rec), 1, g["x0"].size, dtype=torch.float64, device="cuda")
     for ii, r in enumerate(rec):
         eng.sweep(x_rec=xr[ii], z0=dev(r["z0"]) if ii == 0 else None,
@@ -145,6 +149,7 @@ def test_pta_engine_matches_reference_chain(ctx, kind):
                   u_curn=dev(r["u_curn"][None]))
         assert bool(eng.gate.cpu()[0]) == r["gate"], ii
     assert np.array_equal(xr.cpu().numpy()[:, 0], g["chain"])
+    eng.check_fx()
     b = eng.b.cpu().numpy()
     # final b per pulsar vs the reference draw with an exact mean (1e-9); the
     # reference's own fp64 SVD mean is off by up to ~3e-8 on these systems
@@ -289,6 +294,82 @@ def test_curn_sum_kernel_matches_reference(ctx):
                    "gs_rho_curn_sum")
         assert np.array_equal(idx.cpu().numpy(), r["idx_curn"] % 1000), ii
         assert np.array_equal(x.cpu().numpy()[0], r["x_curn"]), ii
+
+
+def test_curn_sum_fixed_point_matches_reference(ctx):
+    """The production CURN kernels open loop on every fixture sweep's recorded tau: the exact
+    fixed-point digits (gs_tau_sum_fx, the quantity a pulsar-sharded run all-reduces) ->
+    gs_fx_to_double -> gs_rho_curn_sum give the reference's grid index (pta_gibbs.py:181-214)
+    and the sums equal the exactly rounded sum of the tau (math.fsum) to 1 ulp; the in-kernel
+    variant from b (gs_tau_sum_fx_b) gives the same digits as tau -> gs_tau_sum_fx."""
+    import math
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import grid3
+    g = golden("pta_curn.npz")
+    _, bhist, _, _, _, rec = pta_replay(g, "curn")
+    P, n_f = rec[0]["tau"].shape
+    Gg = grid3(float(g["rhomin_gw"]), float(g["rhomax_gw"]))
+    e0 = int(np.floor(np.log2(float(g["rhomin_gw"])))) - 64
+    n_param = g["x0"].size
+    K = Keep()
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for ii, r in enumerate(rec):
+        acc = torch.zeros(3, n_f, 1, dtype=torch.int64, device="cuda")
+        _lib.check(ctx.lib.gs_tau_sum_fx(ctx.handle, P, 1, n_f, K(r["tau"][:, :, None]), e0, _lib.ptr(acc),
+                                         _lib.ptr(ovf)), "gs_tau_sum_fx")
+        S = torch.zeros(n_f, 1, dtype=torch.float64, device="cuda")
+        _lib.check(ctx.lib.gs_fx_to_double(ctx.handle, n_f, e0, _lib.ptr(acc), _lib.ptr(S)), "gs_fx_to_double")
+        Sh = S.cpu().numpy()[:, 0]
+        want = np.array([math.fsum(r["tau"][:, k]) for k in range(n_f)])
+        assert np.all(np.abs(Sh - want) <= np.spacing(want)), ii
+        x = dev(g["chain"][ii][None])
+        idx = torch.zeros(n_f, dtype=torch.int32, device="cuda")
+        _lib.check(ctx.lib.gs_rho_curn_sum(ctx.handle, P, 1, n_f, _lib.ptr(S), 1000, _lib.ptr(Gg),
+                                           K(r["u_curn"][None]), 0, 0, _lib.ptr(x), n_param,
+                                           K(g["rind"].astype(np.int32), torch.int32), _lib.ptr(idx)),
+                   "gs_rho_curn_sum")
+        assert np.array_equal(idx.cpu().numpy(), r["idx_curn"] % 1000), ii
+        assert np.array_equal(x.cpu().numpy()[0], r["x_curn"]), ii
+    assert int(ovf.item()) == 0
+    # gs_tau_sum_fx_b straight from b (the engine's fused pass) == tau -> gs_tau_sum_fx
+    m = g["m"]
+    ldb = int(m.max())
+    off = np.concatenate([[0], np.cumsum(m)])
+    fidx = np.stack([np.asarray(gw, np.int32) for gw in g["gwid"]])
+    for ii in (1, len(rec) - 1):
+        bb = np.zeros((P, ldb))
+        for p in range(P):
+            bb[p, :m[p]] = bhist[ii][off[p]:off[p + 1]]
+        tau = np.stack([O.tau_full(bb[p, :m[p]], g["gwid"][p]) for p in range(P)])
+        a1 = torch.zeros(3, n_f, 1, dtype=torch.int64, device="cuda")
+        a2 = torch.zeros_like(a1)
+        _lib.check(ctx.lib.gs_tau_sum_fx(ctx.handle, P, 1, n_f, K(tau[:, :, None]), e0, _lib.ptr(a1), None),
+                   "gs_tau_sum_fx")
+        _lib.check(ctx.lib.gs_tau_sum_fx_b(ctx.handle, P, 1, 2 * n_f, ldb, K(fidx, torch.int32), K(bb), e0,
+                                           _lib.ptr(a2), None), "gs_tau_sum_fx_b")
+        assert torch.equal(a1, a2), ii
+
+
+def test_curn_sum_overflow_raises(ctx):
+    """A tau outside the fixed-point window (here b = 1e30) must not feed a silently truncated S
+    into the CURN draw: PTAChains.check_fx raises."""
+    from pulsar_timing_gibbsspec_amd import synthetic
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
+    pta = synthetic.array_pta(kind="curn", n_psr=3, seed=2)
+    T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
+    names = pta.param_names
+    rind = [i for i, n in enumerate(names) if "rho" in n and "gw" in n]
+    gwid = [np.arange(t.shape[1] - 60, t.shape[1]) for t in T]
+    fixed = [np.full(t.shape[1] - 60, 1e-40) for t in T]
+    x0 = np.random.default_rng(0).uniform(-9, -4, (4, len(names)))
+    eng = PTAChains(DeviceModel(ctx, T, N, R, gwid, fixed), len(names), rind, None, (1e-18, 1e-8), (1e-18, 1e-8),
+                    4, x0, curn_mode="sum")
+    eng.sweep()
+    eng.check_fx()
+    eng.b.fill_(1e30)
+    eng.sweep()
+    with pytest.raises(RuntimeError, match="fixed-point window"):
+        eng.check_fx()
 
 
 def test_curn_sum_sharded_engine_matches_unsharded():

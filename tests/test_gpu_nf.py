@@ -141,3 +141,49 @@ def test_big_nf_non_pd_keeps_b(ctx):
     b, info = b.cpu().numpy(), info.cpu().numpy()
     assert info[0] > 0 and info[1] == 0
     assert np.array_equal(b[0], prev[0]) and np.all(np.isfinite(b[1])) and not np.array_equal(b[1], prev[1])
+
+
+@pytest.mark.parametrize("sched", [0, 1])
+def test_sweep_nmx64_4096_chains_falls_back_to_4_wave(ctx, sched):
+    """NF = 60 with a 64-column timing model at 4096 chains: the 12-wave hand-off workgroup would
+    need 168 KB of LDS (> 160 KB), so the launcher must run the 4-wave shape even when the cost
+    model (sched 0) or GS_OPT_SWEEP_SCHED = 1 asks for hand-off workgroups.  Same
+    draws: bit for bit the chains of GS_OPT_SWEEP_SCHED = 2; chains 0 and 4095 equal the oracle's
+    Cholesky loop on the injected normals / uniforms (1e-9) and every draw is the exact draw."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import FreeSpectrumChains
+    model, T, N, r = _model(ctx, 30, 64)
+    assert model.NMX == 64
+    m = T.shape[1]
+    C, S = 4096, 4
+    rng = np.random.default_rng(5)
+    x0 = rng.uniform(-9, -5, (C, 30))
+    z = np.zeros((S + 1, C, model.ldb))
+    z[:, :, :m] = rng.standard_normal((S + 1, C, m))
+    U = rng.random((S, C, 30))
+    zd0, zd, Ud = dev(z[0]), dev(z[1:]), dev(U)
+    out = []
+    prev = ctx.get_option(_lib.OPT_SWEEP_SCHED)
+    try:
+        for sc in (sched, 2):
+            ctx.set_option(_lib.OPT_SWEEP_SCHED, sc)
+            run = FreeSpectrumChains(model, 1e-18, 1e-8, C, x0)
+            xr, br = run.run(S, z0_inj=zd0, z_inj=zd, u_inj=Ud)
+            run.check_info()
+            out.append([t.cpu().numpy() for t in (xr, br, run.x, run.b, run.info)])
+    finally:
+        ctx.set_option(_lib.OPT_SWEEP_SCHED, prev)
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    assert not out[0][-1].any()
+    xr, br = out[0][0], out[0][1]
+    TNT, d = O.tnt(T, N, r)
+    order = O.chol_order(m, np.arange(60))
+    tl = exact_tnt(T, N, r)
+    for c in (0, C - 1):
+        want_x, _, _ = O.sweep_single(TNT, d, np.arange(60), x0[c], 1e-18, 1e-8, z[:, c, :m], U[:, c], S,
+                                      lambda x: O.phiinv_single(x, 64), draw="chol", order=order)
+        assert normwise_rel(xr[:, c], want_x) < 1e-9, c
+        for j in range(1, S):
+            bx = exact_chol_draw_pre(tl, O.phiinv_single(xr[j, c], 64), z[j, c, :m], order)
+            assert normwise_rel(br[j, c, :m], bx) < 1e-9, (c, j)

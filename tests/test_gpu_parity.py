@@ -432,3 +432,51 @@ def test_sweep_handoff_workgroups_equal_one_chain_per_wave(ctx, model, replay, C
     for a, b in zip(*out):
         assert np.array_equal(a, b)
     assert not out[0][-1].any()
+
+
+def test_sweep_handoff_timeout_fails_loudly(ctx, model, replay):
+    """A hand-off that never arrives (GS_OPT_DEBUG_HANDOFF: workgroup 0's first trio does not
+    publish its first third) must not be read: the extra chain (chain 12 of workgroup 0) ends with
+    info = -1, its state is not advanced (x_state keeps x0, no stale row), every other chain is
+    the one-chain-per-wave run's bit for bit, and FreeSpectrumChains.check_info() raises."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import FreeSpectrumChains
+    C, S = 32, 9
+    x0 = np.random.default_rng(4).uniform(-9, -5, (C, 30))
+    prev = ctx.get_option(_lib.OPT_SWEEP_SCHED)
+    try:
+        ctx.set_option(_lib.OPT_SWEEP_SCHED, 2)
+        ref = FreeSpectrumChains(model, replay["rhomin"], replay["rhomax"], C, x0)
+        ref.run(S)
+        ctx.set_option(_lib.OPT_SWEEP_SCHED, 1)
+        ctx.set_option(_lib.OPT_DEBUG_HANDOFF, 1)
+        run = FreeSpectrumChains(model, replay["rhomin"], replay["rhomax"], C, x0)
+        run.run(S)
+    finally:
+        ctx.set_option(_lib.OPT_DEBUG_HANDOFF, 0)
+        ctx.set_option(_lib.OPT_SWEEP_SCHED, prev)
+    info = run.info.cpu().numpy()
+    assert info[12] == -1
+    assert not np.delete(info, 12).any()
+    x = run.x.cpu().numpy()
+    assert np.array_equal(x[12], x0[12])                       # never advanced from a stale slot
+    keep = np.delete(np.arange(C), 12)
+    assert np.array_equal(x[keep], ref.x.cpu().numpy()[keep])
+    assert np.array_equal(run.b.cpu().numpy()[keep], ref.b.cpu().numpy()[keep])
+    with pytest.raises(RuntimeError, match="hand-off"):
+        run.check_info()
+    ref.check_info()
+
+
+def test_fail_counts_scopes_nest(ctx):
+    """engine.fail_counts restores the attachment it replaced: an inner engine's
+    scope inside an outer one leaves the outer counter attached."""
+    from pulsar_timing_gibbsspec_amd.engine import fail_counts
+    a = torch.zeros(4, dtype=torch.int32, device=ctx.device)
+    b = torch.zeros(4, dtype=torch.int32, device=ctx.device)
+    assert getattr(ctx, "_fail_counts_attached", None) is None
+    with fail_counts(ctx, a):
+        with fail_counts(ctx, b):
+            assert ctx._fail_counts_attached is b
+        assert ctx._fail_counts_attached is a
+    assert ctx._fail_counts_attached is None

@@ -1,0 +1,189 @@
+"""PTABlockGibbs(redsample='mh') -- the reference's default PTA red-noise block
+(pta_gibbs.py:278-340, get_lnlikelihood :577-621, sweep order :689-704) -- against the
+reference's own captured runs (tests/golden/make_golden.py pta_hyper_mh): 45 pulsars with
+power-law red noise + CURN (pta_plred_mh.npz) and 6 pulsars with red free spectra sampled by
+the same Metropolis block (pta_red_mh.npz).
+
+* MH decisions bit for bit: every sweep's block started from the reference's x and fed its
+  draws (scale, parameter, randn, rand) ends exactly at the reference's x;
+* the summed marginalised likelihood within 1e-9 relative of the reference's get_lnlikelihood;
+* the whole sweep (first b draw, warm-up block, CURN draw with the new red phi, gate, gated b
+  draw) fed every captured draw (normals rotated onto the Cholesky draw) reproduces the
+  reference's chain exactly.
+Needs an MI355X."""
+import numpy as np
+import pytest
+
+from oracle import gibbs_oracle as O
+from tests.conftest import golden
+from tests.parity_data import normwise_rel, pta_blocks
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+FIXTURES = [("pta_plred_mh.npz", "curn_plred", None), ("pta_red_mh.npz", "curn_red", 6)]
+
+
+def dev(a):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64).cuda()
+
+
+def _setup(fname, kind, n_psr):
+    from pulsar_timing_gibbsspec_amd import PTABlockGibbs, synthetic
+    g = golden(fname)
+    pta = synthetic.array_pta(kind=kind, n_psr=n_psr, seed=0)
+    gb = PTABlockGibbs(pta, hypersample="conditional", redsample="mh", nchains=1, seed=3)
+    assert np.array_equal(gb.get_hyper_param_indices(), g["hind"])
+    return g, pta, gb
+
+
+class DrawLog:
+    """Walk the captured draw log in the reference's call order."""
+
+    def __init__(self, g):
+        self.kinds, self.vals, self.lens = g["kinds"], g["vals"], g["lens"]
+        self.offs = np.concatenate([[0], np.cumsum(self.lens)])
+        self.k = 0
+        self.hind = g["hind"]
+
+    def peek(self):
+        return self.kinds[self.k] if self.k < len(self.kinds) else None
+
+    def take(self, kind):
+        assert self.kinds[self.k] == kind, (self.k, self.kinds[self.k], kind)
+        v = self.vals[self.offs[self.k]:self.offs[self.k + 1]]
+        self.k += 1
+        return v
+
+    def mh(self, nsteps):
+        from pulsar_timing_gibbsspec_amd.pta_hyper import mh_injection
+        rows, self.k = mh_injection(self.kinds, self.vals, self.lens, self.hind, self.k, nsteps)
+        return rows
+
+
+@pytest.mark.parametrize("fname,kind,n_psr", FIXTURES)
+def test_hyper_mh_decisions_match_reference(fname, kind, n_psr):
+    """Open loop per sweep: the device block from the reference's x with its draws lands on the
+    reference's x exactly (every accept / reject decision and every proposed value)."""
+    g, pta, gb = _setup(fname, kind, n_psr)
+    eng = gb._new_engine(g["x0"])
+    log = DrawLog(g)
+    niter = g["chain"].shape[0]
+    P = int(g["n_psr"])
+    n_acc = 0
+    for ii in range(niter):
+        if ii == 0:
+            for _ in range(P):
+                log.take("randn")
+        n = int(g["warm"]) if ii == 0 else int(g["aclength"])
+        rows = log.mh(n)
+        eng.x.copy_(dev(g["hyper_in"][ii][None]))
+        eng.hyper_block(n, inj=dev(rows[:, None, :]))
+        got = eng.x.cpu().numpy()[0]
+        assert np.array_equal(got, g["hyper_out"][ii]), (ii, np.nonzero(got != g["hyper_out"][ii]))
+        n_acc += int(eng.hyper.n_acc.cpu()[0])
+        log.take("uniform")
+        if log.peek() == "randn":               # the gated b draw
+            for _ in range(P):
+                log.take("randn")
+    assert log.k == len(log.kinds)
+    assert n_acc > 10                       # the fixture exercises both outcomes
+    assert n_acc < (int(g["warm"]) + (niter - 1) * int(g["aclength"]))
+
+
+@pytest.mark.parametrize("fname,kind,n_psr", FIXTURES)
+def test_lnlikelihood_matches_reference(fname, kind, n_psr):
+    g, pta, gb = _setup(fname, kind, n_psr)
+    for xs, want in zip(g["lnl_states"], g["lnl"]):
+        got = gb.get_lnlikelihood(xs)
+        assert abs(got - want) <= 1e-9 * abs(want), (got, want)
+
+
+@pytest.mark.parametrize("fname,kind,n_psr", FIXTURES)
+def test_hyper_mh_sweep_matches_reference_chain(fname, kind, n_psr):
+    """Closed loop: PTAChains with the hyper block fed every captured draw reproduces the
+    reference's chain (x exactly; the gate each sweep) and the final b per pulsar to 1e-9 of the
+    exact-mean draw."""
+    from tests.parity_data import exact_mean_draw
+    g, pta, gb = _setup(fname, kind, n_psr)
+    TNT, d = pta_blocks(g)
+    P = int(g["n_psr"])
+    m = g["m"]
+    gwid = [np.asarray(v) for v in g["gwid"]]
+    orders = [O.chol_order(int(m[p]), gwid[p]) for p in range(P)]
+    eng = gb._new_engine(g["x0"])
+    eng.hyper_warmup = int(g["warm"])
+    eng.hyper_acl = int(g["aclength"])
+    ldb = eng.model.ldb
+    log = DrawLog(g)
+    chain = g["chain"]
+    niter = chain.shape[0]
+
+    def phiinv(x):
+        return pta.get_phiinv(gb.map_params(x))
+
+    def normals(x):
+        ph = phiinv(x)
+        z = np.zeros((P, ldb))
+        zr = []
+        for p in range(P):
+            zz = log.take("randn")
+            zr.append(zz)
+            z[p, :m[p]] = O.rotate_normals(TNT[p], ph[p], zz, orders[p])
+        return z, ph, zr
+
+    xr = torch.zeros(niter, 1, g["x0"].size, dtype=torch.float64, device="cuda")
+    last = None
+    for ii in range(niter):
+        z0 = None
+        if ii == 0:
+            z0, _, _ = normals(g["x0"])
+        rows = log.mh(int(g["warm"]) if ii == 0 else int(g["aclength"]))
+        u = log.take("uniform")
+        x_after = chain[ii + 1] if ii + 1 < niter else g["x_final"]
+        gate = log.peek() == "randn"
+        z = None
+        if gate:
+            z, ph, zr = normals(x_after)
+            last = (x_after, ph, zr)
+        eng.sweep(x_rec=xr[ii], z0=dev(z0) if z0 is not None else None, z=dev(z) if z is not None else None,
+                  u_curn=dev(u[None]), mh_inj=dev(rows[:, None, :]))
+        assert bool(eng.gate.cpu()[0]) == gate, ii
+    assert log.k == len(log.kinds)
+    assert np.array_equal(xr.cpu().numpy()[:, 0], chain)
+    assert np.array_equal(eng.x.cpu().numpy()[0], g["x_final"])
+    b = eng.b.cpu().numpy()
+    x_last, ph, zr = last
+    for p in range(P):
+        zc = O.rotate_normals(TNT[p], ph[p], zr[p], orders[p])
+        bx = exact_mean_draw(TNT[p], d[p], ph[p], zc)
+        assert normwise_rel(b[p, :m[p]], bx) < 1e-9, p
+    assert not eng.info.cpu().numpy().any()
+
+
+def test_pta_block_gibbs_mh_sample(tmp_path):
+    """The drop-in with the reference's defaults (redsample='mh'), device Philox: sample() runs the
+    warm-up, estimates aclength_hyper, keeps every red parameter inside its prior, writes
+    chain.txt, and resume continues bit for bit from gibbs_state.npz."""
+    from pulsar_timing_gibbsspec_amd import PTABlockGibbs, synthetic
+    pta = synthetic.array_pta(kind="curn_plred", n_psr=5, seed=3)
+
+    def new():
+        return PTABlockGibbs(pta, nchains=8, seed=11)
+    x0 = np.concatenate([np.atleast_1d(p.sample()).ravel() for p in new().params])
+    full = new()
+    chain = full.sample(x0, outdir=str(tmp_path / "a"), niter=230)
+    assert full.aclength_hyper >= 1
+    hind = full.get_hyper_param_indices()
+    names = np.array(full.param_names)[hind]
+    red = full.chains[:, :, hind]
+    la = red[:, :, ["log10_A" in n for n in names]]
+    ga = red[:, :, ["gamma" in n for n in names]]
+    assert la.min() >= -20 and la.max() <= -11 and ga.min() >= 0 and ga.max() <= 7
+    assert 0 < float(np.mean(full.hyper_acceptance)) < 1
+    assert np.loadtxt(tmp_path / "a" / "chain.txt").shape == (201, chain.shape[1])
+    part = new()
+    part.sample(x0, outdir=str(tmp_path / "b"), niter=150)
+    res = new()
+    c2 = res.sample(x0, outdir=str(tmp_path / "b"), niter=230, resume=True)
+    assert np.array_equal(c2, chain) and np.array_equal(res.chains, full.chains)
