@@ -62,13 +62,13 @@ def pmc_traffic(S, C):
     return d["bytes_per_launch"]
 
 
-def ess_fraction(x_rec, max_chains=256):
+def ess_fraction(x_rec, max_chains=256, burn_frac=0.2):
     """Min over the bins of the ESS per chain-sweep of log10 rho (mean over up to ``max_chains``
-    chains of 1 / IAT on the post-burn-in rows, first 20 % dropped)."""
+    chains of 1 / IAT on the post-burn-in rows, the first ``burn_frac`` dropped)."""
     from pulsar_timing_gibbsspec_amd.diagnostics import iat
     xr = x_rec[:, :max_chains]                      # (K, C, n_f)
     K, C, nf = xr.shape
-    burn = K // 5
+    burn = int(K * burn_frac)
     return float(min(np.mean([1.0 / max(iat(xr[burn:, c, k]), 1.0) for c in range(C)]) for k in range(nf)))
 
 
@@ -138,12 +138,14 @@ def valu_roof(plain, transc):
 
 
 # minimal lane operations per unit: red grid point h e^-h (pta_gibbs.py:265-266) = gw + rho,
-# 1/a, tau y, e^-h, h e^-h, the running sum and the searchsorted compare; CURN term of the pdf
-# product (pta_gibbs.py:192-205) = one Horner FMA each for the product D(rho) = prod (rho + irn)
-# and the ratio numerator N(rho) (no per-term division or log; the kernel groups 4 pulsars and
-# spends 2.5); CURN-from-sums grid point = one FMA (c_g - S w_g), the row max, e^x, the running
-# sum and the compare.
-GRID_MIN_OPS = {"red": (5, 2), "curn_term": (2, 0), "curn_sum": (4, 1)}
+# 1/a, tau y, e^-h, h e^-h, the running sum and the searchsorted compare -- k_rho_red_cert runs
+# them in f32 with two points per packed v_pk_* instruction, so its 5 plain ops cost 2.5 issue
+# slots per point (4 cycles each) beside the 2 unpacked transcendentals (8 cycles each): 26
+# cycles per wave-point; CURN term of the pdf product (pta_gibbs.py:192-205) = one Horner FMA
+# each for the product D(rho) = prod (rho + irn) and the ratio numerator N(rho) (no per-term
+# division or log; the kernel groups 4 pulsars and spends 2.5); CURN-from-sums grid point = one
+# FMA (c_g - S w_g), the row max, e^x, the running sum and the compare.
+GRID_MIN_OPS = {"red": (2.5, 2), "curn_term": (2, 0), "curn_sum": (4, 1)}
 
 
 def cpu_line(kind, seconds):
@@ -156,7 +158,30 @@ def cpu_line(kind, seconds):
         return {"value": None, "unit": "iters/s", "kind": "port", "error": str(exc)[-500:]}
 
 
-def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain"):
+def pta_ess(eng_factory, rind, ce, burn, sweeps, dev):
+    """ESS per chain-sweep (worst bin of the common log10 rho) of a PTA engine: an untimed run of
+    ``ce`` chains from the bench's start, ``burn`` sweeps dropped, then ``sweeps`` recorded."""
+    eng = eng_factory(ce)
+    ri = torch.as_tensor(np.asarray(rind), dtype=torch.long, device=dev)
+    xe = torch.empty(sweeps, ce, len(rind), dtype=torch.float64, device=dev)
+    for _ in range(burn):
+        eng.sweep()
+    for i in range(sweeps):
+        eng.sweep()
+        xe[i] = eng.x.index_select(1, ri)
+    return ess_fraction(xe.cpu().numpy(), burn_frac=0.0)
+
+
+def cpu_calibration():
+    """The committed reference-vs-port CPU speed ratios (tools/calibrate_cpu_baseline.py, run in
+    the build container where the reference is importable), or None."""
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", "cpu_calibration.json")))
+    except (OSError, ValueError):
+        return None
+
+
+def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500, ess_sweeps=2000):
     """configs[3]: PTAChains over the 45 simulated pulsars.  shard='chain': C chains per
     GPU, no collective (weak).  shard='pulsar' (N > 1): every rank runs the same C chains
     over its pulsar block (balanced by m^3) and exchanges per sweep over RCCL -- the
@@ -189,8 +214,11 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain"):
     else:
         model = DeviceModel(ctx, T, N, R, gwid, fixed)
         x0 = np.random.default_rng(rank).uniform(-9, -4, (C, len(names)))
-        eng = PTAChains(model, len(names), rind, red_col, (1e-18, 1e-8), (1e-20, 1e-8), C, x0,
-                        chain_base=rank * C, curn_mode=curn_mode)
+
+        def make(nc):
+            return PTAChains(model, len(names), rind, red_col, (1e-18, 1e-8), (1e-20, 1e-8), nc, x0[:nc],
+                             chain_base=rank * C, curn_mode=curn_mode)
+        eng = make(C)
     rec = torch.empty(K, C, len(names), dtype=torch.float64, device=dev)
     for _ in range(max(1, W)):
         eng.sweep(x_rec=rec[0])
@@ -201,14 +229,24 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain"):
     el = timed_region(world, dev, run)
     if eng.info.cpu().numpy().any():
         raise RuntimeError("non-PD Sigma in the PTA bench")
+    if curn_mode == "sum":
+        eng.check_fx()
     total_chains = C if sharded else C * world
-    out = dict(value=total_chains * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+    value = total_chains * K / el
+    out = dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
                chains_per_gpu=C, n_psr=len(T), n_param=len(names), n_gpus=world,
                scaling="strong" if sharded else "weak",
                sharding=("pulsars over %d GPUs (RCCL %s per sweep)" %
                          (world, "all-reduce of the tau sums" if curn_mode == "sum" else "all-gather of [tau | x_red]"))
-               if sharded else "chains (no collective)",
-               ess_per_s=ess_min_bin(rec[:, :, rind].cpu().numpy(), el, total_chains))
+               if sharded else "chains (no collective)")
+    if not sharded and ess_sweeps > 0:
+        # ESS from a separate untimed run as for the headline: burn-in, then >= 2000 recorded sweeps
+        ce = min(C, 256)
+        frac = pta_ess(make, rind, ce, ess_burn, ess_sweeps, dev)
+        out["ess_per_s"] = value * frac
+        out["ess"] = {"per_chain_sweep_min_bin": frac, "burn_in": ess_burn, "sweeps": ess_sweeps, "chains": ce,
+                      "note": "ess_per_s = value x the worst common-rho bin's mean ESS per chain-sweep (1/IAT) of a "
+                              "separate untimed run from the same start, burn-in dropped"}
     # roofline of the dominant kernels, each HIP-event timed alone on the context stream
     lib, h, m = ctx.lib, ctx.handle, eng.model
     st = ctx.stream
@@ -237,7 +275,8 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain"):
             op_mix_ceiling_f64_wave=(gp["red_evals_per_s"] / 1e9) if gp else None,
             note="grid-point evaluations ratio*exp(-ratio/2)*ln10 (pta_gibbs.py:265-266): P x n_f x C x 1000 "
                  "per launch (certified f32 pass, f64 redo of unproven rows); peak = hardware VALU issue rate "
-                 "/ the minimal op count per point (5 plain at 4 cycles + rcp and exp at 8 per wave64)")
+                 "/ the minimal op count per point in packed f32 (5 plain ops = 2.5 v_pk_* slots at 4 cycles + "
+                 "rcp and exp at 8 per wave64: 26 cycles)")
         if not sharded:
             check(lib, lib.gs_phi_from_x(h, C, eng.PG * n_f, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.red_col_g),
                                          _lib.ptr(eng.irn)))
@@ -596,6 +635,8 @@ def main():
     ap.add_argument("--sweeps-per-launch", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="seconds per CPU-baseline process")
+    ap.add_argument("--cpu-ess", type=int, default=1, help="measure the CPU port's ESS per sweep (single-process "
+                    "runs of 500 + 10000 (J1713) / 2000 (PTA) sweeps beside the GPU work)")
     ap.add_argument("--bcast", type=int, default=None, help="GS_OPT_BCAST (0 readlane, 1 LDS, 2 batched, 3 tile)")
     ap.add_argument("--host-stream", type=int, default=1,
                     help="also time the headline with every recorded row streamed to pinned host memory (1/0)")
@@ -647,6 +688,15 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     cpu = not args.no_cpu_baseline and world == 1 and rank == 0   # rank 0 at N = 1 only
+    # the CPU port's ESS per sweep: one single-process run per chain-mixing config, started now so
+    # it runs beside the GPU work (numpy only, one thread each); the throughput processes of
+    # cpu_baseline run at the very end, after these have finished, so nothing competes with them
+    ess_procs = {}
+    if cpu and args.cpu_ess:
+        from oracle.cpu_baseline import ess_start
+        ess_procs = {"single": ess_start("single", 500, 10000)}
+        for kind in [k for k in args.pta.split(",") if k in ("curn", "curn_red")]:
+            ess_procs[kind] = ess_start(kind, 500, 2000)
 
     from pulsar_timing_gibbsspec_amd import _lib, synthetic
     from pulsar_timing_gibbsspec_amd.engine import DeviceModel, FreeSpectrumChains, HistoryStreamer
@@ -764,14 +814,13 @@ def main():
                          "executed_tflops": exe, "executed_frac": exe / FP64_PEAK_TFLOPS},
             "with_host_stream": host,
         }
-        if cpu:
-            out["cpu_baseline"] = cpu_line("single", args.cpu_seconds)
     sec = {}
+    cpu_kinds = {}
 
     def add(name, d, kind=None):
         if rank == 0:
-            if cpu and kind:
-                d["cpu_baseline"] = cpu_line(kind, args.cpu_seconds)
+            if kind:
+                cpu_kinds[name] = kind
             sec[name] = d
 
     if args.indep:
@@ -800,6 +849,28 @@ def main():
         d["config"] = ("configs[4]: 200 synthetic pulsars x 10^4 TOAs x 100 frequencies (m=216), "
                        "white-noise MH (20 steps) + per-chain TNT recompute every sweep, chain-sharded")
         add("config5", d, "config5")
+    if rank == 0 and cpu:
+        from oracle.cpu_baseline import ess_collect
+        ess_cpu = {k: ess_collect(p) for k, p in ess_procs.items()}
+        calib = cpu_calibration()
+
+        def baseline(kind):
+            b = cpu_line(kind, args.cpu_seconds)
+            e = ess_cpu.get(kind)
+            if e is not None:
+                b["ess"] = e
+                if b.get("value") and "ess_per_sweep" in e:
+                    b["ess_per_s"] = b["value"] * e["ess_per_sweep"]
+            c = (calib or {}).get("ratios", {}).get(kind)
+            if c and b.get("value"):
+                b["reference_equivalent"] = {
+                    "value": b["value"] * c["ref_over_port"], "ref_over_port": c["ref_over_port"],
+                    "note": "the port's host rate scaled by the reference/port speed ratio measured single-threaded "
+                            "in the build container (profiles/cpu_calibration.json, tools/calibrate_cpu_baseline.py)"}
+            return b
+        out["cpu_baseline"] = baseline("single")
+        for name, kind in cpu_kinds.items():
+            sec[name]["cpu_baseline"] = baseline(kind)
     if rank == 0:
         out["secondary"] = sec
         print(json.dumps(out), flush=True)

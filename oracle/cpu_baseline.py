@@ -33,7 +33,7 @@ def _loop(step, seconds):
             return it, el
 
 
-def single(seconds):
+def single():
     """configs[0]/[1]: J1713 single chain (PulsarBlockGibbs.sample, pulsar_gibbs.py:656-698)."""
     import numpy as np
     from oracle import gibbs_oracle as O
@@ -52,10 +52,10 @@ def single(seconds):
         tau = O.tau_half(st["b"], gwid)
         st["x"] = 0.5 * np.log10(O.rho_analytic(tau, rng.random(30), 1e-18, 1e-8))
         st["b"] = O.bdraw_svd(TNT, d, O.phiinv_single(st["x"], n_tm), rng.standard_normal(T.shape[1]), fallback=True)
-    return _loop(step, seconds), "J1713 single-chain sweeps (oracle restatement of pulsar_gibbs.py:656-698)"
+    return step, lambda: st["x"], "J1713 single-chain sweeps (oracle restatement of pulsar_gibbs.py:656-698)"
 
 
-def indep(seconds):
+def indep():
     """configs[2]: one sweep of every one of the 45 pulsars' PulsarBlockGibbs loops (each
     pulsar its own free spectrum, pulsar_gibbs.py:656-698) = one array sweep."""
     import numpy as np
@@ -76,10 +76,10 @@ def indep(seconds):
                 bs[p] = O.bdraw_svd(TNT, d, O.phiinv_single(xs[p], m - 60), rng.standard_normal(m), fallback=True)
             xs[p] = 0.5 * np.log10(O.rho_analytic(O.tau_half(bs[p], gwid), rng.random(30), 1e-18, 1e-8))
             bs[p] = O.bdraw_svd(TNT, d, O.phiinv_single(xs[p], m - 60), rng.standard_normal(m), fallback=True)
-    return _loop(step, seconds), "45-pulsar array sweeps (each pulsar's PulsarBlockGibbs loop, pulsar_gibbs.py:656-698)"
+    return step, lambda: xs[0], "45-pulsar array sweeps (each pulsar's PulsarBlockGibbs loop, pulsar_gibbs.py:656-698)"
 
 
-def pta(kind, seconds):
+def pta(kind):
     """configs[3]: PTABlockGibbs.sample (pta_gibbs.py:664-704), SVD draws, 45 pulsars."""
     import numpy as np
     from oracle import gibbs_oracle as O
@@ -117,10 +117,10 @@ def pta(kind, seconds):
         rr, _ = O.rho_grid_cdf_curn(taus, irn, rng.random(30), 1e-18, 1e-8)
         x[rind] = 0.5 * np.log10(rr)
         st["b"] = draw(x)
-    return _loop(step, seconds), f"45-pulsar {kind} sweeps (oracle restatement of pta_gibbs.py:664-704)"
+    return step, lambda: st["x"][rind], f"45-pulsar {kind} sweeps (oracle restatement of pta_gibbs.py:664-704)"
 
 
-def config5(seconds):
+def config5():
     """configs[4]: one pulsar's sweep (10^4 TOAs, m = 216, 20 white MH steps, each
     recomputing r - T b and the white likelihood as pulsar_gibbs.py:523-546 does); the
     rate is reported per 200-pulsar array sweep (x 1/200)."""
@@ -159,12 +159,11 @@ def config5(seconds):
         x[gw] = 0.5 * np.log10(O.rho_analytic(O.tau_half(b, np.arange(2 * gw.size)), rng.random(gw.size),
                                               d["rhomin"], d["rhomax"]))
         st["x"] = x
-    (it, el) = _loop(step, seconds)
-    return (it / 200.0, el), ("single-pulsar sweeps (10^4 TOAs, m=216, 20 white MH steps; pulsar_gibbs.py:656-698 + "
-                              ":373-404) scaled to the 200-pulsar array")
+    return step, lambda: st["x"][gw], ("single-pulsar sweeps (10^4 TOAs, m=216, 20 white MH steps; "
+                                       "pulsar_gibbs.py:656-698 + :373-404) scaled to the 200-pulsar array")
 
 
-def _ecorr(seconds, white, aclength=10):
+def _ecorr(white, aclength=10):
     """the ECORR sweep (notebook order), optionally with the white MH block."""
     import numpy as np
     from oracle import gibbs_oracle as O
@@ -221,19 +220,48 @@ def _ecorr(seconds, white, aclength=10):
         x[gw] = 0.5 * np.log10(O.rho_analytic(O.tau_half(b, gwid), rng.random(gw.size), 1e-18, 1e-8))
         st["x"], st["b"] = x, O.bdraw_svd(TNT, dd, 1.0 / phi(x), rng.standard_normal(m), fallback=True)
     what = "white + ECORR" if white else "ECORR"
-    return _loop(step, seconds), (f"single-chain {what} sweeps (m={m}, {ne} epochs, {aclength} MH steps per block, "
-                                  "oracle restatement of the notebook sampler)")
+    return step, lambda: st["x"][gw], (f"single-chain {what} sweeps (m={m}, {ne} epochs, {aclength} MH steps per "
+                                       "block, oracle restatement of the notebook sampler)")
 
 
 KINDS = {
     "single": single,
     "indep": indep,
-    "curn": lambda s: pta("curn", s),
-    "curn_red": lambda s: pta("curn_red", s),
+    "curn": lambda: pta("curn"),
+    "curn_red": lambda: pta("curn_red"),
     "config5": config5,
-    "ecorr": lambda s: _ecorr(s, False),
-    "ecorr_white": lambda s: _ecorr(s, True),
+    "ecorr": lambda: _ecorr(False),
+    "ecorr_white": lambda: _ecorr(True),
 }
+# rates are reported per unit of the BASELINE metric: config5's single-pulsar sweep is 1/200 of an
+# array sweep
+PER_SWEEP = {"config5": 1.0 / 200.0}
+
+
+def rate(kind, seconds):
+    """(iterations, seconds, what) of one single-thread process running loop ``kind``."""
+    step, _, what = KINDS[kind]()
+    it, el = _loop(step, seconds)
+    return it * PER_SWEEP.get(kind, 1.0), el, what
+
+
+def ess_per_sweep(kind, burn, sweeps):
+    """The port's ESS per sweep of log10 rho (worst bin, 1/IAT with diagnostics.iat = Sokal's
+    window) from ONE single-process run of ``burn`` + ``sweeps`` sweeps -- with the host rate it
+    gives the CPU's ESS/s (north_star compares ESS/s)."""
+    import numpy as np
+    from pulsar_timing_gibbsspec_amd.diagnostics import iat
+    step, get_x, what = KINDS[kind]()
+    for _ in range(burn):
+        step()
+    rows = np.empty((sweeps, len(get_x())))
+    t0 = time.perf_counter()
+    for i in range(sweeps):
+        step()
+        rows[i] = get_x()
+    el = time.perf_counter() - t0
+    frac = float(min(1.0 / max(iat(rows[:, k]), 1.0) for k in range(rows.shape[1])))
+    return dict(ess_per_sweep=frac, burn_in=burn, sweeps=sweeps, seconds=el, what=what)
 
 
 def host_cores():
@@ -282,9 +310,32 @@ def aggregate(kind, seconds, cores=None):
                        f"value = sum of their rates (numpy/OpenBLAS, OPENBLAS_NUM_THREADS=1 each)")
 
 
+def ess_start(kind, burn, sweeps):
+    """Start the single-process ESS run of ``kind`` in the background (numpy only, one thread);
+    ``ess_collect`` waits for it.  bench.py runs these beside the GPU work."""
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1", MKL_NUM_THREADS="1",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    return subprocess.Popen([sys.executable, "-m", "oracle.cpu_baseline", kind, "ess", str(burn), str(sweeps)],
+                            cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+
+
+def ess_collect(proc, timeout=900):
+    try:
+        o, e = proc.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        proc.kill()
+        return {"error": "timed out"}
+    if proc.returncode != 0:
+        return {"error": e.strip().splitlines()[-1][:300] if e.strip() else f"exit {proc.returncode}"}
+    return json.loads(o.strip().splitlines()[-1])
+
+
 def main():
-    kind, seconds = sys.argv[1], float(sys.argv[2])
-    (it, el), what = KINDS[kind](seconds)
+    kind = sys.argv[1]
+    if len(sys.argv) > 2 and sys.argv[2] == "ess":
+        print(json.dumps(ess_per_sweep(kind, int(sys.argv[3]), int(sys.argv[4]))))
+        return
+    it, el, what = rate(kind, float(sys.argv[2]))
     print(json.dumps(dict(it=it, el=el, what=what)))
 
 

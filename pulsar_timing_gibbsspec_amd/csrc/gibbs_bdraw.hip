@@ -564,7 +564,8 @@ __global__ __launch_bounds__(64, 2) void k_hyper_mh(HyperMhArgs A) {
       z = v1;
     }
     const int col = A.hcol[j], p = A.hpsr[j];
-    const double xq = xs[col] + (z * sig) * sc;
+    // q[par] += randn * sigmas * scale, rounded as numpy does (no fma contraction)
+    const double xq = __dadd_rn(xs[col], __dmul_rn(__dmul_rn(z, sig), sc));
     bool accepted = false;
     if (xq >= A.hlo[j] && xq <= A.hhi[j]) {  // uniform prior: -inf outside (:298, :624-628)
       double red;
@@ -776,7 +777,8 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
         // rho|b analytic (pulsar_gibbs.py:208-216, 236)
         const double partner = __shfl_xor(bF, 1);
         const double be = (lane & 1) ? partner : bF, bo = (lane & 1) ? bF : partner;
-        const double tau = (be * be + bo * bo) / 2;
+        // tau = (b_sin^2 + b_cos^2) / 2 rounded as numpy (pulsar_gibbs.py:208-209): no fma contraction
+        const double tau = __dadd_rn(__dmul_rn(be, be), __dmul_rn(bo, bo)) / 2;
         double U;
         if (A.u_inj) {
           U = act ? A.u_inj[rec * NFR + kf] : 0.5;
@@ -897,7 +899,7 @@ __global__ void k_rho_analytic(RhoArgs A) {
   const int p = (int)(sys / A.n_chain), c = (int)(sys % A.n_chain);
   const double bs = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k]];
   const double bc = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k + 1]];
-  const double tau = (bs * bs + bc * bc) / 2;
+  const double tau = __dadd_rn(__dmul_rn(bs, bs), __dmul_rn(bc, bc)) / 2;  // numpy's rounding
   double U;
   if (A.u) {
     U = A.u[sys * NFR + k];

@@ -33,8 +33,9 @@ __global__ void k_tau(TauArgs A) {
   const int64_t sys = (int64_t)p * A.n_chain + c;
   const double bs = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k]];
   const double bc = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k + 1]];
-  const double s2 = bs * bs, c2 = bc * bc;
-  A.tau[t] = A.half ? (s2 + c2) / 2 : s2 + c2;
+  // b_sin^2 + b_cos^2 rounded as numpy (pta_gibbs.py:194-195): no fma contraction
+  const double s2c2 = __dadd_rn(__dmul_rn(bs, bs), __dmul_rn(bc, bc));
+  A.tau[t] = A.half ? s2c2 / 2 : s2c2;
 }
 
 // ------------------------------------------------------------ a6: common CDF
@@ -212,7 +213,7 @@ __global__ __launch_bounds__(256) void k_tau_sum_fx_b(TauArgs A, int e0, long lo
     const int64_t sys = (int64_t)p * A.n_chain + c;
     const double bs = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k]];
     const double bc = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k + 1]];
-    ok &= fx_add(bs * bs + bc * bc, e0, d0, d1, d2);
+    ok &= fx_add(__dadd_rn(__dmul_rn(bs, bs), __dmul_rn(bc, bc)), e0, d0, d1, d2);  // numpy's tau rounding
   }
   acc[t] = d0;
   acc[nrow + t] = d1;

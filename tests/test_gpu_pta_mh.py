@@ -154,10 +154,14 @@ def test_hyper_mh_sweep_matches_reference_chain(fname, kind, n_psr):
     assert np.array_equal(eng.x.cpu().numpy()[0], g["x_final"])
     b = eng.b.cpu().numpy()
     x_last, ph, zr = last
+    off = np.concatenate([[0], np.cumsum(m)])
     for p in range(P):
-        zc = O.rotate_normals(TNT[p], ph[p], zr[p], orders[p])
-        bx = exact_mean_draw(TNT[p], d[p], ph[p], zc)
+        # the reference's draw with its mean computed exactly (its own fp64 SVD mean is off by up
+        # to ~3e-8 on these systems, tests/test_oracle_golden.py::test_reference_svd_mean_error)
+        bx = exact_mean_draw(TNT[p], d[p], ph[p], zr[p])
         assert normwise_rel(b[p, :m[p]], bx) < 1e-9, p
+        bref = g["b_final"][off[p]:off[p + 1]]
+        assert normwise_rel(b[p, :m[p]], bref) <= normwise_rel(bref, bx) + 1e-9, p
     assert not eng.info.cpu().numpy().any()
 
 
