@@ -172,6 +172,9 @@ def pta_ess(eng_factory, rind, ce, burn, sweeps, dev):
     return ess_fraction(xe.cpu().numpy(), burn_frac=0.0)
 
 
+HYPER_ACL = 20     # aclength_hyper of the curn_plred line (as configs[4] fixes aclength_white = 20)
+
+
 def cpu_calibration():
     """The committed reference-vs-port CPU speed ratios (tools/calibrate_cpu_baseline.py, run in
     the build container where the reference is importable), or None."""
@@ -201,6 +204,15 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
     fixed = [np.full(t.shape[1] - 60, 1e-40) for t in T]
     red_col = hind.reshape(len(T), -1) if kind == "curn_red" else None
     sharded = shard == "pulsar" and world > 1
+    hyper = None
+    if kind == "curn_plred":
+        # the reference's default redsample='mh' on per-pulsar power-law red noise (pta_gibbs.py:278-340):
+        # chain-sharded only, aclength_hyper fixed (its warm-up's acor cannot run, pta_hyper)
+        from pulsar_timing_gibbsspec_amd.pta_hyper import HyperSpec
+        hidx = np.array([i for i, n in enumerate(names) if "red" in n and ("log10_A" in n or "gamma" in n)])
+        hyper = HyperSpec(pta, pta.params, [s for s in (pta.signals[k] for k in pta.signals) if "red" in s.name],
+                          hidx, np.zeros(len(names)), 30, dev)
+        sharded = False
     if sharded:
         blocks = balanced_blocks(np.array([t.shape[1] ** 3 for t in T], float), world)
         lo, hi = blocks[rank]
@@ -213,11 +225,15 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
                         P_global=len(T), psr_lo=lo, curn_mode=curn_mode, **ex)
     else:
         model = DeviceModel(ctx, T, N, R, gwid, fixed)
-        x0 = np.random.default_rng(rank).uniform(-9, -4, (C, len(names)))
+        rng = np.random.default_rng(rank)
+        x0 = rng.uniform(-9, -4, (C, len(names)))
+        if hyper is not None:
+            x0[:, hyper.hind] = rng.uniform(hyper.hlo_host, hyper.hhi_host, (C, hyper.n_h))
 
         def make(nc):
             return PTAChains(model, len(names), rind, red_col, (1e-18, 1e-8), (1e-20, 1e-8), nc, x0[:nc],
-                             chain_base=rank * C, curn_mode=curn_mode)
+                             chain_base=rank * C, curn_mode=curn_mode, hyper=hyper,
+                             hyper_acl=HYPER_ACL if hyper is not None else None)
         eng = make(C)
     rec = torch.empty(K, C, len(names), dtype=torch.float64, device=dev)
     for _ in range(max(1, W)):
@@ -261,7 +277,27 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
                                     "flop per chain (SURVEY 8d)")}
     gp = grid_peak()
     n_f = eng.n_f
-    if kind == "curn_red":
+    if hyper is not None:
+        hm = eng.hyper
+        eng._update_irn()
+        ms_seed = event_ms(st, lambda: (eng._gate_phiinv(with_gate=False, out=eng.phiinv_h, gate=eng._gate_h),
+                                        hm.seed(eng.phiinv_h)), 5)
+        x_save = eng.x.clone()
+        ms_mh = event_ms(st, lambda: hm.steps(eng.x, HYPER_ACL, eng.it, eng.chain_base), 3)
+        eng.x.copy_(x_save)
+        nf = 60
+        fl = nf ** 3 / 3 + nf ** 2 / 2 + nf / 6          # one NF x NF Schur-block factorisation
+        kernels["k_hyper_mh"] = dict(
+            kernel_avg_ms=ms_mh, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
+            achieved=HYPER_ACL * C * fl / (ms_mh * 1e-3) / 1e12, alg_per_launch=HYPER_ACL * C * fl,
+            note=f"{HYPER_ACL} single-parameter MH steps per chain (pta_gibbs.py:319-340), each one pulsar's "
+                 "marginalised likelihood (NF x NF Schur block Cholesky, NF^3/3 + NF^2/2 + NF/6 flop; the "
+                 "reference re-evaluates all 45 pulsars' full m x m systems per step)")
+        kernels["seed_lnlike"] = dict(
+            kernel_avg_ms=ms_seed, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
+            achieved=len(T) * C * fl / (ms_seed * 1e-3) / 1e12, alg_per_launch=len(T) * C * fl,
+            note="lnL_p of every (pulsar, chain) at the block's start (phiinv + gs_lnlike_marg)")
+    elif kind == "curn_red":
         check(lib, lib.gs_phi_from_x(h, C, n_f, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.gw_col),
                                      _lib.ptr(eng.gwphi)))
         ms_r = event_ms(st, lambda: check(lib, lib.gs_rho_red(
@@ -643,8 +679,9 @@ def main():
     ap.add_argument("--indep", type=int, default=1, help="measure BASELINE configs[2] (45 independent pulsars)")
     ap.add_argument("--indep-chains", type=int, default=256, help="chains per pulsar for configs[2]")
     ap.add_argument("--indep-steps", type=int, default=500)
-    ap.add_argument("--pta", default="curn_red,curn", help="secondary PTA configs measured in the same run "
-                    "(comma list of curn_red, curn; or none). curn uses the sufficient-statistic draw")
+    ap.add_argument("--pta", default="curn_red,curn,curn_plred", help="secondary PTA configs measured in the "
+                    "same run (comma list of curn_red, curn, curn_plred; or none). curn uses the sufficient-statistic "
+                    "draw; curn_plred the red-noise Metropolis block (redsample='mh')")
     ap.add_argument("--pta-chains", type=int, default=2048,
                     help="chains per GPU for the PTA lines (measured: 256 -> 1024 -> 2048 -> 4096 chains give "
                          "CURN + red 3.0e5 -> 3.8e5 -> 3.9e5 -> 4.0e5 chain-it/s: saturated at 2048)")
@@ -695,8 +732,10 @@ def main():
     if cpu and args.cpu_ess:
         from oracle.cpu_baseline import ess_start
         ess_procs = {"single": ess_start("single", 500, 10000)}
-        for kind in [k for k in args.pta.split(",") if k in ("curn", "curn_red")]:
-            ess_procs[kind] = ess_start(kind, 500, 2000)
+        for kind in [k for k in args.pta.split(",") if k in ("curn", "curn_red", "curn_plred")]:
+            # (the MH line's CPU sweep is ~5 it/s: a shorter run, 100 + 400 sweeps)
+            ess_procs[kind] = ess_start(kind, 500 if kind != "curn_plred" else 100, 2000 if kind != "curn_plred"
+                                        else 400)
 
     from pulsar_timing_gibbsspec_amd import _lib, synthetic
     from pulsar_timing_gibbsspec_amd.engine import DeviceModel, FreeSpectrumChains, HistoryStreamer
@@ -832,8 +871,11 @@ def main():
         d = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, shard="chain")
         d["config"] = (f"configs[3]: 45-pulsar CURN{' + per-pulsar red' if kind == 'curn_red' else ''} free "
                        f"spectrum, common draw {'from the tau sums' if kind == 'curn' else 'exact product'}")
+        if kind == "curn_plred":
+            d["config"] = ("configs[3] with the reference's default redsample='mh': 45-pulsar CURN free spectrum + "
+                           f"per-pulsar power-law red noise by {HYPER_ACL} Metropolis steps per sweep")
         add(kind, d, kind)
-        if world > 1:
+        if world > 1 and kind != "curn_plred":
             d = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, shard="pulsar")
             d["config"] = f"configs[3] {kind}, pulsars sharded over the ranks with the per-sweep RCCL exchange"
             add(kind + "_pulsar_sharded", d)

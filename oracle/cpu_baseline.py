@@ -120,6 +120,64 @@ def pta(kind):
     return step, lambda: st["x"][rind], f"45-pulsar {kind} sweeps (oracle restatement of pta_gibbs.py:664-704)"
 
 
+def pta_mh(aclength=20):
+    """configs[3] with the reference's default redsample='mh' (pta_gibbs.py:278-340, 664-704):
+    per sweep ``aclength`` single-parameter Metropolis steps over every pulsar's power-law
+    (log10_A, gamma), each re-evaluating the SUMMED marginalised likelihood of all 45 pulsars
+    (get_lnlikelihood :577-621, Cholesky per pulsar, TNT reset and recomputed each sweep), then the
+    CURN grid draw with the power-law irn and the SVD b draws."""
+    import numpy as np
+    from oracle import gibbs_oracle as O
+    from pulsar_timing_gibbsspec_amd import synthetic
+    from pulsar_timing_gibbsspec_amd.plumbing import uniform_bounds
+    p_ = synthetic.array_pta(kind="curn_plred", seed=0)
+    T, N, R = p_.get_basis(), p_.get_ndiag({}), p_.get_residuals()
+    P = len(T)
+    names = p_.param_names
+    by_name = {q.name: q for q in p_.params}
+    rind = np.array([i for i, n in enumerate(names) if "rho" in n and "gw" in n])
+    hind = np.array([i for i, n in enumerate(names) if "red" in n and ("log10_A" in n or "gamma" in n)])
+    lo = np.array([uniform_bounds(by_name[names[i]])[0] for i in hind])
+    hi = np.array([uniform_bounds(by_name[names[i]])[1] for i in hind])
+    red_sigs = [s for s in (p_.signals[k] for k in p_.signals) if "red" in s.name]
+    rng = np.random.default_rng(os.getpid())
+    x = rng.uniform(-9, -4, len(names))
+    x[hind] = rng.uniform(lo, hi)
+    m = [t.shape[1] for t in T]
+    gw = [np.arange(mm - 60, mm) for mm in m]
+    st = dict(x=x)
+
+    def phis(x):
+        return p_.get_phi(p_.map_params(x))
+
+    def draw(x, TD):
+        return [O.bdraw_svd(TD[p][0], TD[p][1], 1.0 / ph, rng.standard_normal(m[p]), fallback=True)
+                for p, ph in enumerate(phis(x))]
+
+    def lnprior(x):
+        v = x[hind]
+        return 0.0 if np.all((v >= lo) & (v <= hi)) else -np.inf
+    st["b"] = draw(x, [O.tnt(T[p], N[p], R[p]) for p in range(P)])
+
+    def step():
+        x, b = st["x"], st["b"]
+        TD = [O.tnt(T[p], N[p], R[p]) for p in range(P)]      # reset + recompute (pta_gibbs.py:672-673)
+
+        def lnlike(xx):
+            return sum(O.lnlike_fullmarg(R[p], N[p], TD[p][0], TD[p][1], 1.0 / ph, float(np.sum(np.log(ph))))
+                       for p, ph in enumerate(phis(xx)))
+        steps = [(rng.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]), rng.choice(hind),
+                  rng.standard_normal(), rng.random()) for _ in range(aclength)]
+        x = O.white_mh(x, hind, steps, lnlike, lnprior)
+        taus = np.stack([O.tau_full(b[p], gw[p]) for p in range(P)])
+        irn = np.stack([np.asarray(s.get_phi(p_.map_params(x)), float)[::2] for s in red_sigs])
+        rr, _ = O.rho_grid_cdf_curn(taus, irn, rng.random(30), 1e-18, 1e-8)
+        x[rind] = 0.5 * np.log10(rr)
+        st["x"], st["b"] = x, draw(x, TD)
+    return step, lambda: st["x"][rind], (f"45-pulsar CURN + power-law red sweeps with {aclength} red MH steps "
+                                         "(oracle restatement of pta_gibbs.py:278-340, 577-621, 664-704)")
+
+
 def config5():
     """configs[4]: one pulsar's sweep (10^4 TOAs, m = 216, 20 white MH steps, each
     recomputing r - T b and the white likelihood as pulsar_gibbs.py:523-546 does); the
@@ -229,6 +287,7 @@ KINDS = {
     "indep": indep,
     "curn": lambda: pta("curn"),
     "curn_red": lambda: pta("curn_red"),
+    "curn_plred": pta_mh,
     "config5": config5,
     "ecorr": lambda: _ecorr(False),
     "ecorr_white": lambda: _ecorr(True),

@@ -565,7 +565,7 @@ __global__ __launch_bounds__(64, 2) void k_hyper_mh(HyperMhArgs A) {
     }
     const int col = A.hcol[j], p = A.hpsr[j];
     // q[par] += randn * sigmas * scale, rounded as numpy does (no fma contraction)
-    const double xq = __dadd_rn(xs[col], __dmul_rn(__dmul_rn(z, sig), sc));
+    const double xq = gs_add_rn(xs[col], gs_mul_rn(gs_mul_rn(z, sig), sc));
     bool accepted = false;
     if (xq >= A.hlo[j] && xq <= A.hhi[j]) {  // uniform prior: -inf outside (:298, :624-628)
       double red;
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(64, 2) void k_hyper_mh(HyperMhArgs A) {
         const int ca = A.pl_col[2 * p], cg = A.pl_col[2 * p + 1];
         const double la = ca == col ? xq : xs[ca], ga = cg == col ? xq : xs[cg];
         const double* L = A.lnphi + (int64_t)p * 3 * n_f;
-        red = exp(__dadd_rn(__dadd_rn(__dmul_rn(L[n_f + kf], la), L[kf]), __dmul_rn(L[2 * n_f + kf], ga)));
+        red = exp(gs_add_rn(gs_add_rn(gs_mul_rn(L[n_f + kf], la), L[kf]), gs_mul_rn(L[2 * n_f + kf], ga)));
       }
       const double phinv = act ? 1.0 / (gw + red) : 1.0;
       const double* mb = A.model + (int64_t)p * A.mstride;
@@ -778,7 +778,7 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
         const double partner = __shfl_xor(bF, 1);
         const double be = (lane & 1) ? partner : bF, bo = (lane & 1) ? bF : partner;
         // tau = (b_sin^2 + b_cos^2) / 2 rounded as numpy (pulsar_gibbs.py:208-209): no fma contraction
-        const double tau = __dadd_rn(__dmul_rn(be, be), __dmul_rn(bo, bo)) / 2;
+        const double tau = gs_add_rn(gs_mul_rn(be, be), gs_mul_rn(bo, bo)) / 2;
         double U;
         if (A.u_inj) {
           U = act ? A.u_inj[rec * NFR + kf] : 0.5;
@@ -899,7 +899,7 @@ __global__ void k_rho_analytic(RhoArgs A) {
   const int p = (int)(sys / A.n_chain), c = (int)(sys % A.n_chain);
   const double bs = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k]];
   const double bc = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k + 1]];
-  const double tau = __dadd_rn(__dmul_rn(bs, bs), __dmul_rn(bc, bc)) / 2;  // numpy's rounding
+  const double tau = gs_add_rn(gs_mul_rn(bs, bs), gs_mul_rn(bc, bc)) / 2;  // numpy's rounding
   double U;
   if (A.u) {
     U = A.u[sys * NFR + k];

@@ -241,6 +241,20 @@ __device__ __forceinline__ void gs_normal2(gs_u4 c, gs_key k, double& n1, double
   n2 = r * s;
 }
 
+// ---------------------------------------------------------------- separately rounded ops
+// a * b and a + b each rounded to nearest, never fused into an fma with a neighbouring operation:
+// the reference's numpy arithmetic (tau = b_s^2 + b_c^2, q = x + z sigma scale, ...).  HIP's
+// __dmul_rn / __dadd_rn are plain `*` / `+` here and still contract under -ffp-contract=fast; the
+// operations carry the no-contract flag only when the pragma is in their own scope.
+__device__ __forceinline__ double gs_mul_rn(double a, double b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ double gs_add_rn(double a, double b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+
 // ---------------------------------------------------------------- Metropolis jump scale
 // scale = np.random.choice([0.1, 0.5, 1, 3, 10], p=[.1, .15, .5, .15, .1]) of every one-parameter
 // MH block of the reference (pulsar_gibbs.py:377-381, 430-433; pta_gibbs.py:290-293): numpy's

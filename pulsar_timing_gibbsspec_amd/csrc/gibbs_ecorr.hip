@@ -543,7 +543,7 @@ __device__ __forceinline__ void ecorr_propose_one(const EcorrMhArgs& A, int c, i
   // the likelihood kernels read only the ECORR columns of xq
   for (int j = 0; j < A.n_e; ++j) qr[A.ecol[j]] = xr[A.ecol[j]];
   const int col = A.ecol[p];
-  const double qv = __dadd_rn(xr[col], __dmul_rn(__dmul_rn(z, 0.05 * A.n_e), sc));  // numpy's rounding (no fma)
+  const double qv = gs_add_rn(xr[col], gs_mul_rn(gs_mul_rn(z, 0.05 * A.n_e), sc));  // numpy's rounding (no fma)
   qr[col] = qv;
   double* pr = A.prop + (int64_t)c * 4;
   pr[0] = (double)col;

@@ -34,7 +34,7 @@ __global__ void k_tau(TauArgs A) {
   const double bs = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k]];
   const double bc = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k + 1]];
   // b_sin^2 + b_cos^2 rounded as numpy (pta_gibbs.py:194-195): no fma contraction
-  const double s2c2 = __dadd_rn(__dmul_rn(bs, bs), __dmul_rn(bc, bc));
+  const double s2c2 = gs_add_rn(gs_mul_rn(bs, bs), gs_mul_rn(bc, bc));
   A.tau[t] = A.half ? s2c2 / 2 : s2c2;
 }
 
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void k_tau_sum_fx_b(TauArgs A, int e0, long lo
     const int64_t sys = (int64_t)p * A.n_chain + c;
     const double bs = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k]];
     const double bc = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k + 1]];
-    ok &= fx_add(__dadd_rn(__dmul_rn(bs, bs), __dmul_rn(bc, bc)), e0, d0, d1, d2);  // numpy's tau rounding
+    ok &= fx_add(gs_add_rn(gs_mul_rn(bs, bs), gs_mul_rn(bc, bc)), e0, d0, d1, d2);  // numpy's tau rounding
   }
   acc[t] = d0;
   acc[nrow + t] = d1;
@@ -940,7 +940,7 @@ __global__ void k_phi_powerlaw(int n_psr, int n_chain, int n_f, const double* x,
   const double* xc = x + (int64_t)c * ldx;
   const double la = xc[pl_col[2 * p]], ga = xc[pl_col[2 * p + 1]];
   const double* L = lnphi + (int64_t)p * 3 * n_f;
-  out[t] = exp(__dadd_rn(__dadd_rn(__dmul_rn(L[n_f + k], la), L[k]), __dmul_rn(L[2 * n_f + k], ga)));
+  out[t] = exp(gs_add_rn(gs_add_rn(gs_mul_rn(L[n_f + k], la), L[k]), gs_mul_rn(L[2 * n_f + k], ga)));
 }
 
 // ------------------------------------------------------------ PTA record / gate / phiinv

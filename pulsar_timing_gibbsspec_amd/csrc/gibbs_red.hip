@@ -40,7 +40,7 @@ struct RedFreq {
 
 __device__ __forceinline__ double lnirn(const RedFreq& F, int j, double la, double ga) {
   // (a_k la + c_k) + g_k ga, rounded step by step (no contraction), as the oracle computes it
-  return __dadd_rn(__dadd_rn(__dmul_rn(F.a[j], la), F.c[j]), __dmul_rn(F.g[j], ga));
+  return gs_add_rn(gs_add_rn(gs_mul_rn(F.a[j], la), F.c[j]), gs_mul_rn(F.g[j], ga));
 }
 
 __device__ __forceinline__ double red_lnlike(const RedFreq& F, double la, double ga) {

@@ -121,7 +121,7 @@ __global__ __launch_bounds__(64 * MH_WPB) void k_white_mh(WhiteMhArgs A) {
     }
     // q[par] += randn * sigmas * scale  (:383)
     const double xo = xs[w];
-    const double xq = __dadd_rn(xo, __dmul_rn(__dmul_rn(z, sig), sc));  // numpy's rounding (no fma)
+    const double xq = gs_add_rn(xo, gs_mul_rn(gs_mul_rn(z, sig), sc));  // numpy's rounding (no fma)
     if (A.q_rec && lane < nw)
       A.q_rec[((int64_t)st * n_sys + sys) * GS_WHITE_MAX_W + lane] = (lane == w) ? xq : xs[lane];
     // Uniform prior: -inf outside [pmin, pmax] -> diff = -inf, rejected (:613-617, :398)
