@@ -72,7 +72,8 @@ enum {
                          pdfs equal to ~1e-15 relative); 0 (default) = as 2, except gs_rho_red:
                          every point in f32 with a per-row error certificate, rows whose index
                          the certificate cannot prove redone in f64 (indices of exact
-                         arithmetic, as 2's) */
+                         arithmetic, as 2's), 16 lanes per row; 3 = as 0 with the round-3
+                         certified kernel (64 lanes per row, one compare per point) */
   GS_OPT_BREC_CHAINS = 5, /* gs_sweep_freespec b_rec: 0 (default) = every system, row
                          sweep * n_psr * n_chain + p * n_chain + c; K > 0 = chains c < K of
                          each pulsar only, compact rows (sweep * n_psr + p) * K + c (the

@@ -261,7 +261,7 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
       ctx->psr_base = value;
       return 0;
     case GS_OPT_GRID_EXACT:
-      if (value < 0 || value > 2) return fail_arg(3, "GS_OPT_GRID_EXACT must be 0, 1 or 2");
+      if (value < 0 || value > 3) return fail_arg(3, "GS_OPT_GRID_EXACT must be 0, 1, 2 or 3");
       ctx->grid_exact = value;
       return 0;
     case GS_OPT_BREC_CHAINS:

@@ -12,6 +12,8 @@
 // chains (coalesced).  The grid rho_g = 10**linspace(...), log rho_g and
 // 0.5*log10 rho_g are computed on the host with numpy and passed in
 // (grid3 = [rho | log rho | 0.5 log10 rho]), bit-identical to the reference's.
+#include <cstdlib>
+
 #include "gibbs_common.h"
 #include "gibbs_internal.h"
 #include "gibbs_gridpt.h"
@@ -881,6 +883,212 @@ __global__ __launch_bounds__(256) void k_rho_red_cert(GridArgs A, int32_t* n_fal
   if (n_fallback && lane == 0 && nfb) atomicAdd(n_fallback, nfb);
 }
 
+// ------------------------------------------------------------ a7 default: certified draw, 16 lanes per row
+// k_rho_red_cert's arithmetic and certificate with the row spread over ONE DPP row of 16 lanes
+// instead of the whole wave: row group g = lane >> 4 walks row 4 it + g of the wave's 64 rows, lane
+// l = lane & 15 owning grid points [64 l, 64 l + 64) (ngrid <= 1024).  Per point the same packed
+// f32 work; per row four times fewer instructions than the 64-lane walk -- the prefix over lanes is
+// a 4-step DPP row_shr scan, the total a row_newbcast:15 -- and the searchsorted count needs no
+// compare per point: a lane whose last (first) value is below (not below) a threshold contributes
+// all (none) of its points, and the one lane that straddles it writes its 64 running sums to LDS,
+// where the row group counts them 4 per lane.  Two straddling lanes (rounding can in principle
+// break the lane-level order) or an unproven row take the f64 redo of k_rho_red_cert, wave-wide.
+// Certificate: the same first-order bound with 64 + 4 additions per prefix (k_rho_red_cert: 16 +
+// 6), D = eps (170 T + 18 w + 12 xm T) + 2e-35 (the 80 T term rescaled: 2 (12 + 68 + 3) < 170).
+constexpr int RQ_P = 64;  // grid points per lane (16 lanes per row)
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {  // row-local DPP move, 0 from outside the row
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float row_scan16(float x) {  // inclusive prefix over each 16-lane row
+  x += dpp_f32<0x111>(x);                                // row_shr:1
+  x += dpp_f32<0x112>(x);                                // row_shr:2
+  x += dpp_f32<0x114>(x);                                // row_shr:4
+  x += dpp_f32<0x118>(x);                                // row_shr:8
+  return x;
+}
+__device__ __forceinline__ float row_last(float x) {  // lane 15 of each row to the whole row
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x15f, 0xf, 0xf, false));  // row_newbcast:15
+}
+// the 16-bit field of row group g of a wave mask
+__device__ __forceinline__ unsigned grp_bits(unsigned long long m, int g) { return (unsigned)(m >> (16 * g)) & 0xffffu; }
+
+__global__ __launch_bounds__(256) void k_rho_red_cert16(GridArgs A, int32_t* n_fallback) {
+  __shared__ double tb[64];                 // the f64 redo's exp table
+  __shared__ float slot[4][4][2][RQ_P + 2];  // [wave][row group][lo, hi]: a straddling lane's sums + threshold
+  __shared__ gs_f2 rgs[16 * RQ_P / 2];        // the scaled f32 grid, shared by the workgroup's rows
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane >> 4, l = lane & 15;
+  const int S = -ilogb(A.grid3[0]);  // rho_min 2^S in [1, 2)
+  if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
+  // off-grid slots: a = inf -> y = 0 -> t = 0 and E = 2^xm, finite (xm <= 100 below): pdf' exactly 0
+  for (int q = threadIdx.x; q < 16 * RQ_P; q += 256)
+    reinterpret_cast<float*>(rgs)[q] = q < A.ngrid ? (float)ldexp(A.grid3[q], S) : __builtin_inff();
+  __syncthreads();
+  const int64_t nrow = (int64_t)A.n_psr * A.n_f * A.n_chain;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
+  if (r0 >= nrow) return;
+  const int64_t r = r0 + lane;
+  const bool rok = r < nrow;
+  const int64_t rr = rok ? r : r0;
+  const int c = (int)(rr % A.n_chain);
+  const int k = (int)((rr / A.n_chain) % A.n_f);
+  const int p = (int)(rr / ((int64_t)A.n_chain * A.n_f));
+  double u;
+  if (A.u) {
+    u = A.u[((int64_t)c * A.n_psr + p) * A.n_f + k];
+  } else {
+    double u2;
+    gs_uniform2(gs_counter(k, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, p + A.psr_base, GS_EV_RED), A.key, u, u2);
+  }
+  const double tau = A.tau[rr];
+  const double gw = A.irn[(int64_t)k * A.n_chain + c];
+  const gs_f2* rgl = rgs + RQ_P / 2 * l;  // this lane's points, read per pair from LDS (no 64 VGPRs)
+  // valid points of this lane, and the valid-count split for the lane-level counts
+  const int nval = min(max(A.ngrid - RQ_P * l, 0), RQ_P);
+  const int L0 = A.ngrid / RQ_P, R0 = A.ngrid % RQ_P;  // lanes < L0 full, lane L0 holds R0
+  const int nr = (int)min((int64_t)64, nrow - r0);
+  const double sc = 1.4426950408889634 * 0.5 * ldexp(1.0, S);
+  const float rgmax32 = (float)ldexp(A.grid3[A.ngrid - 1], S);
+  float* myslot_lo = slot[wave][g][0];
+  float* myslot_hi = slot[wave][g][1];
+  int myidx = 0, nfb = 0;
+  for (int it = 0; 4 * it < nr; ++it) {
+    const int src = min(4 * it + g, nr - 1);  // this row group's row (a short last batch repeats one)
+    const double taui = __shfl(tau, src), gwi = __shfl(gw, src), ui = __shfl(u, src);
+    int e;
+    const double thm = frexp(0.5 * taui, &e);
+    const float tl = (float)thm * 1.44269504f;
+    const float tl2 = (float)(taui * sc);
+    const float gw32 = (float)ldexp(gwi, S);
+    // the row's smallest exponent x (at rho_max), capped at 100 so an off-grid slot's 2^xm stays
+    // finite; every on-grid e = xm - x is still <= 0 (a row with x > 226 everywhere underflows to
+    // T = 0 and takes the f64 redo)
+    const float xm = fminf(tl2 * __builtin_amdgcn_rcpf(gw32 + rgmax32), 100.0f);
+    const gs_f2 gw2 = {gw32, gw32}, tlv = {tl, tl}, ntl2v = {-tl2, -tl2}, xm2 = {xm, xm};
+    float cum[RQ_P];
+    float loc = 0.0f;
+    gs_f2 w2 = {0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < RQ_P; j += 2) {
+      const gs_f2 a = gw2 + rgl[j / 2];
+      const gs_f2 y = {__builtin_amdgcn_rcpf(a[0]), __builtin_amdgcn_rcpf(a[1])};
+      const gs_f2 t = tlv * y;
+      const gs_f2 ex = __builtin_elementwise_fma(ntl2v, y, xm2);
+      const gs_f2 E = {__builtin_amdgcn_exp2f(ex[0]), __builtin_amdgcn_exp2f(ex[1])};
+      const gs_f2 pdf = t * E;
+      w2 = __builtin_elementwise_fma(pdf, -ex, w2);
+      loc += pdf[0];
+      cum[j] = loc;
+      loc += pdf[1];
+      cum[j + 1] = loc;
+    }
+    const float incl = row_scan16(loc);
+    const float excl = dpp_f32<0x111>(incl);  // row_shr:1: the previous lane's prefix, 0 on lane 0
+    const float T = row_last(incl);
+    const float wsum = fmaf(xm, T, row_last(row_scan16(w2[0] + w2[1])));  // sum pdf' x over the row
+    const bool okrow = T > 1e-33f && T < 3e38f && wsum < 3e38f;         // uniform per row group
+    const float D = 5.9604645e-08f * (170.0f * T + 18.0f * wsum + 12.0f * xm * T) + 2e-35f;
+    const float uT = (float)ui * T;
+    const float tlo = (uT - 2.0f * D) - excl, thr = (uT + 2.0f * D) - excl;
+    // lane classes for each threshold: all points below / none below / straddling
+    const bool lo_all = cum[RQ_P - 1] < tlo, lo_none = !(cum[0] < tlo);
+    const bool hi_all = cum[RQ_P - 1] < thr, hi_none = !(cum[0] < thr);
+    const bool lo_str = !lo_all && !lo_none, hi_str = !hi_all && !hi_none;
+    const unsigned long long m_lo_all = __ballot(lo_all), m_hi_all = __ballot(hi_all);
+    const unsigned long long m_lo_str = __ballot(lo_str), m_hi_str = __ballot(hi_str);
+    const unsigned long long m_ok = __ballot(okrow);
+    // the straddling lanes leave their sums (and their local threshold) for the row group
+    if (lo_str) {
+#pragma unroll
+      for (int j = 0; j < RQ_P; ++j) myslot_lo[j] = cum[j];
+      myslot_lo[RQ_P] = tlo;
+      myslot_lo[RQ_P + 1] = __int_as_float(nval);
+    }
+    if (hi_str) {
+#pragma unroll
+      for (int j = 0; j < RQ_P; ++j) myslot_hi[j] = cum[j];
+      myslot_hi[RQ_P] = thr;
+      myslot_hi[RQ_P + 1] = __int_as_float(nval);
+    }
+    wave_lds_sync();
+    // the row group counts the straddler's points below its threshold, 4 per lane
+    unsigned long long m_lo_in[4], m_hi_in[4];
+    {
+      const float t_lo = myslot_lo[RQ_P], t_hi = myslot_hi[RQ_P];
+      const int nv_lo = __float_as_int(myslot_lo[RQ_P + 1]), nv_hi = __float_as_int(myslot_hi[RQ_P + 1]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = 4 * l + q;
+        m_lo_in[q] = __ballot(j < nv_lo && myslot_lo[j] < t_lo);
+        m_hi_in[q] = __ballot(j < nv_hi && myslot_hi[j] < t_hi);
+      }
+    }
+    wave_lds_sync();  // the slots are rewritten next iteration
+    unsigned fb = 0;  // row groups whose row takes the f64 redo
+    int idx_g[4];
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const unsigned fl_all = grp_bits(m_lo_all, gg), fh_all = grp_bits(m_hi_all, gg);
+      const unsigned fl_str = grp_bits(m_lo_str, gg), fh_str = grp_bits(m_hi_str, gg);
+      const unsigned full = (1u << L0) - 1u;  // lanes with RQ_P valid points
+      int clo = RQ_P * __builtin_popcount(fl_all & full) + (((fl_all >> L0) & 1u) ? R0 : 0);
+      int chi = RQ_P * __builtin_popcount(fh_all & full) + (((fh_all >> L0) & 1u) ? R0 : 0);
+      if (fl_str) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) clo += __builtin_popcount(grp_bits(m_lo_in[q], gg));
+      }
+      if (fh_str) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) chi += __builtin_popcount(grp_bits(m_hi_in[q], gg));
+      }
+      const bool proven = grp_bits(m_ok, gg) != 0 && __builtin_popcount(fl_str) <= 1 &&
+                          __builtin_popcount(fh_str) <= 1 && clo == chi;
+      idx_g[gg] = clo - 1;
+      if (!proven && 4 * it + gg < nr) fb |= 1u << gg;
+    }
+    // unproven rows: k_rho_red_cert's f64 redo, the whole wave on one row (~2 % of rows)
+    while (fb) {
+      const int gg = __builtin_ctz(fb);
+      fb &= fb - 1;
+      ++nfb;
+      const int rrow = 4 * it + gg;
+      const double tr = rdlane(tau, rrow), gr = rdlane(gw, rrow), ur = rdlane(u, rrow);
+      double rgd[RW_G], cumd[RW_G];
+#pragma unroll
+      for (int j = 0; j < RW_G; ++j) {
+        const int gi = RW_G * lane + j;
+        rgd[j] = gi < A.ngrid ? A.grid3[gi] : 1e60;
+      }
+      const double locd = red_lane_cumsum<RW_G>(0.5 * tr, gr, rgd, tb, cumd);
+      double incd = locd;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double v = __shfl_up(incd, o);
+        if (lane >= o) incd += v;
+      }
+      const double total = rdlane(incd, 63);
+      const double thd = ur * total - (incd - locd);
+      int cnt = 0;
+#pragma unroll
+      for (int j = 0; j < RW_G; ++j) cnt += __popcll(__ballot(cumd[j] < thd && RW_G * lane + j < A.ngrid));
+      idx_g[gg] = cnt - 1;
+    }
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      int id = idx_g[gg];
+      if (id < 0) id += A.ngrid;
+      myidx = (lane == 4 * it + gg) ? id : myidx;
+    }
+  }
+  if (rok) {
+    if (A.idx_out) A.idx_out[r] = myidx;
+    A.x[(int64_t)c * A.ldx + A.xcol[p * A.n_f + k]] = A.grid3[2 * A.ngrid + myidx];
+  }
+  if (n_fallback && lane == 0 && nfb) atomicAdd(n_fallback, nfb);
+}
+
 // ------------------------------------------------------------ a4: Gumbel-max
 // rows r = k * n_chain + c (one pulsar, systems = chains); tau half-convention.
 // logpdf = log tau - logaddexp(log irn, log rho) - exp(...); argmax(logpdf + G),
@@ -1077,7 +1285,9 @@ int launch_rho_red(hipStream_t s, const GridArgs& a) {
   if (n == 0) return 0;
   if (a.exact == 1)
     hipLaunchKernelGGL(k_rho_red<true>, grid1(n, 64), dim3(64), 0, s, a);
-  else if (a.ngrid <= 64 * RW_G && a.exact == 0)
+  else if (a.ngrid <= 16 * RQ_P && a.exact == 0)
+    hipLaunchKernelGGL(k_rho_red_cert16, grid1(n, 256), dim3(256), 0, s, a, a.n_fallback);
+  else if (a.ngrid <= 64 * RW_G && (a.exact == 0 || a.exact == 3))
     hipLaunchKernelGGL(k_rho_red_cert, grid1(n, 256), dim3(256), 0, s, a, a.n_fallback);
   else if (a.ngrid <= 64 * RW_G)
     hipLaunchKernelGGL(k_rho_red_wave, grid1(n, 256), dim3(256), 0, s, a);

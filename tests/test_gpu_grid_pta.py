@@ -508,9 +508,9 @@ def test_red_grid_certified_f32_matches_exact(ctx, request):
         u[c, p, k] = cdf[j]
     G = grid3(lo, hi)
     xcol = torch.arange(P * n_f, dtype=torch.int32, device="cuda")
-    out = {}
+    out, nfbs = {}, {}
     fb = torch.zeros(1, dtype=torch.int32, device="cuda")
-    for mode in (1, 2, 0):
+    for mode in (1, 2, 3, 0):
         _lib.check(ctx.lib.gs_ctx_set_option(ctx.handle, _lib.OPT_GRID_EXACT, mode), "set_option")
         x = torch.zeros(C, P * n_f, dtype=torch.float64, device="cuda")
         idx = torch.zeros(P * n_f * C, dtype=torch.int32, device="cuda")
@@ -522,11 +522,13 @@ def test_red_grid_certified_f32_matches_exact(ctx, request):
         finally:
             _lib.check(ctx.lib.gs_ctx_set_grid_fallback_counter(ctx.handle, None), "counter")
         out[mode] = idx.cpu().numpy()
-        if mode != 0:
-            fb.zero_()
-    nfb = int(fb)
+        nfbs[mode] = int(fb)
+        fb.zero_()
+    nfb = nfbs[0]
     advset = {(p * n_f + k) * C + c for p, k, c in adv}   # row r = (p * n_f + k) * C + c
+    # mode 0 = 16 lanes per row (k_rho_red_cert16), 3 = the round-3 64-lane certified kernel
     assert np.array_equal(out[0], out[2]), int(np.sum(out[0] != out[2]))
+    assert np.array_equal(out[3], out[2]), int(np.sum(out[3] != out[2]))
     keep = np.ones(out[0].size, bool)
     keep[list(advset)] = False
     bad = np.nonzero((out[0] != out[1]) & keep)[0]
@@ -543,9 +545,10 @@ def test_red_grid_certified_f32_matches_exact(ctx, request):
                              u=float(u[c_, p_, k_]), cdf=cdf[max(0, j0 - 1):j0 + 2].tolist(),
                              tau=float(tau[p_, k_, c_]), gw=float(gw[k_, c_])))
         pytest.fail(f"{bad.size} rows differ (fallbacks {nfb}): {info}")
-    # the adversarial rows, and ~1 % of the others (u within the certificate's margin of one of
-    # ~1000 cdf values)
-    assert len(adv) <= nfb < 0.03 * out[0].size, nfb
+    # the adversarial rows, and ~1-2 % of the others (u within the certificate's margin of one of
+    # ~1000 cdf values; the 16-lane kernel's 64-term lane sums double the margin)
+    assert len(adv) <= nfbs[3] < 0.03 * out[0].size, nfbs[3]
+    assert len(adv) <= nfb < 0.05 * out[0].size, nfb
 
 
 @pytest.mark.parametrize("with_red", [True, False])
