@@ -916,15 +916,20 @@ __device__ __forceinline__ unsigned grp_bits(unsigned long long m, int g) { retu
 
 __global__ __launch_bounds__(256) void k_rho_red_cert16(GridArgs A, int32_t* n_fallback) {
   __shared__ double tb[64];                 // the f64 redo's exp table
-  __shared__ float slot[4][4][2][RQ_P + 2];  // [wave][row group][lo, hi]: a straddling lane's sums + threshold
+  __shared__ __attribute__((aligned(16))) float slot[4][4][2][RQ_P + 4];  // [wave][group][lo, hi]: sums, threshold, count
   __shared__ gs_f2 rgs[16 * RQ_P / 2];        // the scaled f32 grid, shared by the workgroup's rows
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4, l = lane & 15;
   const int S = -ilogb(A.grid3[0]);  // rho_min 2^S in [1, 2)
   if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
   // off-grid slots: a = inf -> y = 0 -> t = 0 and E = 2^xm, finite (xm <= 100 below): pdf' exactly 0
-  for (int q = threadIdx.x; q < 16 * RQ_P; q += 256)
-    reinterpret_cast<float*>(rgs)[q] = q < A.ngrid ? (float)ldexp(A.grid3[q], S) : __builtin_inff();
+  // pair-major (rgs[pair * 16 + lane]): the 16 lanes of a row read 16 consecutive 8-byte words
+  // per point pair -- bank-conflict free (lane-major, 256 bytes apart, was a 16-way conflict)
+  for (int q = threadIdx.x; q < 16 * RQ_P; q += 256) {
+    const int ln = q / RQ_P, jj = q % RQ_P;  // grid point q = 64 ln + jj
+    reinterpret_cast<float*>(rgs)[((jj / 2) * 16 + ln) * 2 + (jj & 1)] =
+        q < A.ngrid ? (float)ldexp(A.grid3[q], S) : __builtin_inff();
+  }
   __syncthreads();
   const int64_t nrow = (int64_t)A.n_psr * A.n_f * A.n_chain;
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
@@ -944,7 +949,7 @@ __global__ __launch_bounds__(256) void k_rho_red_cert16(GridArgs A, int32_t* n_f
   }
   const double tau = A.tau[rr];
   const double gw = A.irn[(int64_t)k * A.n_chain + c];
-  const gs_f2* rgl = rgs + RQ_P / 2 * l;  // this lane's points, read per pair from LDS (no 64 VGPRs)
+  const gs_f2* rgl = rgs + l;  // this lane's point pairs at rgl[16 jp], read from LDS (no 64 VGPRs)
   // valid points of this lane, and the valid-count split for the lane-level counts
   const int nval = min(max(A.ngrid - RQ_P * l, 0), RQ_P);
   const int L0 = A.ngrid / RQ_P, R0 = A.ngrid % RQ_P;  // lanes < L0 full, lane L0 holds R0
@@ -972,7 +977,7 @@ __global__ __launch_bounds__(256) void k_rho_red_cert16(GridArgs A, int32_t* n_f
     gs_f2 w2 = {0.0f, 0.0f};
 #pragma unroll
     for (int j = 0; j < RQ_P; j += 2) {
-      const gs_f2 a = gw2 + rgl[j / 2];
+      const gs_f2 a = gw2 + rgl[16 * (j / 2)];
       const gs_f2 y = {__builtin_amdgcn_rcpf(a[0]), __builtin_amdgcn_rcpf(a[1])};
       const gs_f2 t = tlv * y;
       const gs_f2 ex = __builtin_elementwise_fma(ntl2v, y, xm2);
@@ -1000,29 +1005,33 @@ __global__ __launch_bounds__(256) void k_rho_red_cert16(GridArgs A, int32_t* n_f
     const unsigned long long m_lo_str = __ballot(lo_str), m_hi_str = __ballot(hi_str);
     const unsigned long long m_ok = __ballot(okrow);
     // the straddling lanes leave their sums (and their local threshold) for the row group
+    typedef float gs_f4 __attribute__((ext_vector_type(4)));
     if (lo_str) {
 #pragma unroll
-      for (int j = 0; j < RQ_P; ++j) myslot_lo[j] = cum[j];
-      myslot_lo[RQ_P] = tlo;
-      myslot_lo[RQ_P + 1] = __int_as_float(nval);
+      for (int j = 0; j < RQ_P; j += 4)
+        *reinterpret_cast<gs_f4*>(myslot_lo + j) = gs_f4{cum[j], cum[j + 1], cum[j + 2], cum[j + 3]};
+      *reinterpret_cast<gs_f2*>(myslot_lo + RQ_P) = gs_f2{tlo, __int_as_float(nval)};
     }
     if (hi_str) {
 #pragma unroll
-      for (int j = 0; j < RQ_P; ++j) myslot_hi[j] = cum[j];
-      myslot_hi[RQ_P] = thr;
-      myslot_hi[RQ_P + 1] = __int_as_float(nval);
+      for (int j = 0; j < RQ_P; j += 4)
+        *reinterpret_cast<gs_f4*>(myslot_hi + j) = gs_f4{cum[j], cum[j + 1], cum[j + 2], cum[j + 3]};
+      *reinterpret_cast<gs_f2*>(myslot_hi + RQ_P) = gs_f2{thr, __int_as_float(nval)};
     }
     wave_lds_sync();
     // the row group counts the straddler's points below its threshold, 4 per lane
     unsigned long long m_lo_in[4], m_hi_in[4];
     {
-      const float t_lo = myslot_lo[RQ_P], t_hi = myslot_hi[RQ_P];
-      const int nv_lo = __float_as_int(myslot_lo[RQ_P + 1]), nv_hi = __float_as_int(myslot_hi[RQ_P + 1]);
+      const gs_f2 tl_lo = *reinterpret_cast<const gs_f2*>(myslot_lo + RQ_P);
+      const gs_f2 tl_hi = *reinterpret_cast<const gs_f2*>(myslot_hi + RQ_P);
+      const int nv_lo = __float_as_int(tl_lo[1]), nv_hi = __float_as_int(tl_hi[1]);
+      const gs_f4 vlo = *reinterpret_cast<const gs_f4*>(myslot_lo + 4 * l);
+      const gs_f4 vhi = *reinterpret_cast<const gs_f4*>(myslot_hi + 4 * l);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int j = 4 * l + q;
-        m_lo_in[q] = __ballot(j < nv_lo && myslot_lo[j] < t_lo);
-        m_hi_in[q] = __ballot(j < nv_hi && myslot_hi[j] < t_hi);
+        m_lo_in[q] = __ballot(j < nv_lo && vlo[q] < tl_lo[0]);
+        m_hi_in[q] = __ballot(j < nv_hi && vhi[q] < tl_hi[0]);
       }
     }
     wave_lds_sync();  // the slots are rewritten next iteration

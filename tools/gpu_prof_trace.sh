@@ -15,7 +15,7 @@ cd $GRAFT_REPO_ROOT
 tr=$(find $out/prof -name '*kernel_trace.csv' | head -1)
 st=$(find $out/prof -name '*kernel_stats.csv' | head -1)
 cp $st $out/kernel_stats.csv
-for k in "k_sweep_freespec<" k_sweep_freespec_rm k_bdraw_tiled "k_bdraw<" k_rho_red_cert k_rho_red_wave k_rho_curn_fast k_rho_curn_sum_wave k_white_syrk k_ecorr_prefix; do
+for k in "k_sweep_freespec<" k_sweep_freespec_rm k_bdraw_tiled "k_bdraw<" k_rho_red_cert16 "k_rho_red_cert(" k_rho_red_wave k_hyper_mh k_lnlike_marg k_rho_curn_fast k_rho_curn_sum_wave k_white_syrk k_ecorr_prefix; do
   python tools/launch_stats.py $tr $k
 done > $out/launch_stats.log
 grep mean $out/launch_stats.log
