@@ -886,15 +886,31 @@ __global__ __launch_bounds__(256) void k_rho_red_cert(GridArgs A, int32_t* n_fal
 // ------------------------------------------------------------ a7 default: certified draw, 16 lanes per row
 // k_rho_red_cert's arithmetic and certificate with the row spread over ONE DPP row of 16 lanes
 // instead of the whole wave: row group g = lane >> 4 walks row 4 it + g of the wave's 64 rows, lane
-// l = lane & 15 owning grid points [64 l, 64 l + 64) (ngrid <= 1024).  Per point the same packed
-// f32 work; per row four times fewer instructions than the 64-lane walk -- the prefix over lanes is
-// a 4-step DPP row_shr scan, the total a row_newbcast:15 -- and the searchsorted count needs no
-// compare per point: a lane whose last (first) value is below (not below) a threshold contributes
-// all (none) of its points, and the one lane that straddles it writes its 64 running sums to LDS,
-// where the row group counts them 4 per lane.  Two straddling lanes (rounding can in principle
-// break the lane-level order) or an unproven row take the f64 redo of k_rho_red_cert, wave-wide.
-// Certificate: the same first-order bound with 64 + 4 additions per prefix (k_rho_red_cert: 16 +
-// 6), D = eps (170 T + 18 w + 12 xm T) + 2e-35 (the 80 T term rescaled: 2 (12 + 68 + 3) < 170).
+// l = lane & 15 owning grid points [64 l, 64 l + 64) (ngrid <= 1024).
+//
+// Pass 1 keeps no per-point state: each lane sums its 64 pdf' = y E (the row constant tl of
+// k_rho_red_cert cancels in cdf / total and is dropped) in four packed accumulators, and the lane
+// totals are prefixed by a 4-step DPP row_shr scan (total: row_newbcast:15).  The searchsorted
+// count is then taken at lane level: a lane whose last prefix is below a threshold contributes all
+// of its points, one whose first prefix is not below contributes none, and the ONE lane that
+// straddles it is recomputed by the whole row group, 4 points per lane (same f32 ops), prefixed by
+// a second row scan and compared.  The counts are summed over the row by an integer DPP scan (lo
+// and hi thresholds packed in one word).  Two straddling lanes (rounding can in principle break the
+// lane-level order) or an unproven row take the f64 redo of k_rho_red_cert, wave-wide.
+//
+// Certificate: every prefix used (lane ends, first points, recomputed points, the total) is a sum
+// of the exact prefix's terms with <= 24 roundings on any term's path (8 per accumulator + 3 to
+// combine, 4 in the lane scan, 1 for the first point or 3 + 4 + 2 for a recomputed point), and
+// pdf' = y E carries (8 + 5.6 x + 4.9 xm) eps (k_rho_red_cert's list without tl's 3 and one
+// product), 3 roundings in the thresholds: D = eps (72 T + 18 w + 12 xm T) + 2e-35 (2 (8 + 24 +
+// 3) < 72).  The lane-level classes are sound with each value D-accurate on its own: an "all"
+// lane's points are truly below (C_j <= C_last <= end + D < uT - D), a "none" lane's truly not
+// below, and the straddler's points are counted from D-accurate values, so the counts at uT -+ 2D
+// bracket the exact count, and equal counts prove it.
+// Measured (configs[3] rows near the posterior, 2048 chains, tools/ab_red_grid.py): 0.75 ms per
+// launch with 1.34 % of rows redone in f64 (round-3 k_rho_red_cert: 1.22 ms, 1.45 %; the first
+// 16-lane version, which kept the 64 running sums per lane and counted per group on the SALU:
+// 1.12 ms, 2.6 %), indices equal to the f64 kernel's on every row.
 constexpr int RQ_P = 64;  // grid points per lane (16 lanes per row)
 
 template <int CTRL>
@@ -908,27 +924,64 @@ __device__ __forceinline__ float row_scan16(float x) {  // inclusive prefix over
   x += dpp_f32<0x118>(x);                                // row_shr:8
   return x;
 }
+__device__ __forceinline__ int row_scan16_i(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+  return x;
+}
 __device__ __forceinline__ float row_last(float x) {  // lane 15 of each row to the whole row
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x15f, 0xf, 0xf, false));  // row_newbcast:15
 }
-// the 16-bit field of row group g of a wave mask
-__device__ __forceinline__ unsigned grp_bits(unsigned long long m, int g) { return (unsigned)(m >> (16 * g)) & 0xffffu; }
+__device__ __forceinline__ int row_last_i(int x) { return __builtin_amdgcn_mov_dpp(x, 0x15f, 0xf, 0xf, false); }
+
+typedef float gs_f4 __attribute__((ext_vector_type(4)));
+
+// Points 64 s + 4 l + q (q < 4) of row group g's lane s, recomputed by lane l: their prefixes
+// within lane s's range, and the number below thresholds lo / hi among the nv valid ones.
+struct StrCount {
+  int lo, hi;
+};
+__device__ __forceinline__ StrCount red_straddler(const gs_f4* rlin4, int s, int l, int g, float excl, float gw32,
+                                                  float ntl2, float xm, int ngrid, float tlo, float thr) {
+  const gs_f4 rq = rlin4[16 * s + l];
+  float P[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float y = __builtin_amdgcn_rcpf(gw32 + rq[q]);
+    P[q] = y * __builtin_amdgcn_exp2f(fmaf(ntl2, y, xm));
+  }
+  const float q1 = P[0] + P[1], q2 = q1 + P[2], q3 = q2 + P[3];
+  const float ex16 = dpp_f32<0x111>(row_scan16(q3));
+  const float base = __shfl(excl, 16 * g + s) + ex16;
+  const float c[4] = {base + P[0], base + q1, base + q2, base + q3};
+  const int nv = min(max(ngrid - RQ_P * s - 4 * l, 0), 4);
+  StrCount r = {0, 0};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    r.lo += (q < nv && c[q] < tlo) ? 1 : 0;
+    r.hi += (q < nv && c[q] < thr) ? 1 : 0;
+  }
+  return r;
+}
 
 __global__ __launch_bounds__(256) void k_rho_red_cert16(GridArgs A, int32_t* n_fallback) {
-  __shared__ double tb[64];                 // the f64 redo's exp table
-  __shared__ __attribute__((aligned(16))) float slot[4][4][2][RQ_P + 4];  // [wave][group][lo, hi]: sums, threshold, count
-  __shared__ gs_f2 rgs[16 * RQ_P / 2];        // the scaled f32 grid, shared by the workgroup's rows
+  __shared__ double tb[64];          // the f64 redo's exp table
+  __shared__ gs_f2 rgs[16 * RQ_P / 2];  // the scaled f32 grid, pair-major, for pass 1
+  __shared__ gs_f4 rlin4[16 * RQ_P / 4];  // the same grid in point order, for the straddler recompute
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4, l = lane & 15;
   const int S = -ilogb(A.grid3[0]);  // rho_min 2^S in [1, 2)
   if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
-  // off-grid slots: a = inf -> y = 0 -> t = 0 and E = 2^xm, finite (xm <= 100 below): pdf' exactly 0
-  // pair-major (rgs[pair * 16 + lane]): the 16 lanes of a row read 16 consecutive 8-byte words
-  // per point pair -- bank-conflict free (lane-major, 256 bytes apart, was a 16-way conflict)
+  // off-grid slots: a = inf -> y = 0 -> E = 2^xm, finite (xm <= 100 below): pdf' exactly 0.
+  // Pair-major (rgs[pair * 16 + lane]): the 16 lanes of a row read 16 consecutive 8-byte words per
+  // point pair, bank-conflict free.
   for (int q = threadIdx.x; q < 16 * RQ_P; q += 256) {
     const int ln = q / RQ_P, jj = q % RQ_P;  // grid point q = 64 ln + jj
-    reinterpret_cast<float*>(rgs)[((jj / 2) * 16 + ln) * 2 + (jj & 1)] =
-        q < A.ngrid ? (float)ldexp(A.grid3[q], S) : __builtin_inff();
+    const float v = q < A.ngrid ? (float)ldexp(A.grid3[q], S) : __builtin_inff();
+    reinterpret_cast<float*>(rgs)[((jj / 2) * 16 + ln) * 2 + (jj & 1)] = v;
+    reinterpret_cast<float*>(rlin4)[q] = v;
   }
   __syncthreads();
   const int64_t nrow = (int64_t)A.n_psr * A.n_f * A.n_chain;
@@ -949,118 +1002,79 @@ __global__ __launch_bounds__(256) void k_rho_red_cert16(GridArgs A, int32_t* n_f
   }
   const double tau = A.tau[rr];
   const double gw = A.irn[(int64_t)k * A.n_chain + c];
-  const gs_f2* rgl = rgs + l;  // this lane's point pairs at rgl[16 jp], read from LDS (no 64 VGPRs)
-  // valid points of this lane, and the valid-count split for the lane-level counts
-  const int nval = min(max(A.ngrid - RQ_P * l, 0), RQ_P);
-  const int L0 = A.ngrid / RQ_P, R0 = A.ngrid % RQ_P;  // lanes < L0 full, lane L0 holds R0
+  const gs_f2* rgl = rgs + l;  // this lane's point pairs at rgl[16 jp]
+  const int nval = min(max(A.ngrid - RQ_P * l, 0), RQ_P);  // valid points of this lane
   const int nr = (int)min((int64_t)64, nrow - r0);
   const double sc = 1.4426950408889634 * 0.5 * ldexp(1.0, S);
   const float rgmax32 = (float)ldexp(A.grid3[A.ngrid - 1], S);
-  float* myslot_lo = slot[wave][g][0];
-  float* myslot_hi = slot[wave][g][1];
   int myidx = 0, nfb = 0;
   for (int it = 0; 4 * it < nr; ++it) {
     const int src = min(4 * it + g, nr - 1);  // this row group's row (a short last batch repeats one)
     const double taui = __shfl(tau, src), gwi = __shfl(gw, src), ui = __shfl(u, src);
-    int e;
-    const double thm = frexp(0.5 * taui, &e);
-    const float tl = (float)thm * 1.44269504f;
     const float tl2 = (float)(taui * sc);
     const float gw32 = (float)ldexp(gwi, S);
     // the row's smallest exponent x (at rho_max), capped at 100 so an off-grid slot's 2^xm stays
     // finite; every on-grid e = xm - x is still <= 0 (a row with x > 226 everywhere underflows to
     // T = 0 and takes the f64 redo)
     const float xm = fminf(tl2 * __builtin_amdgcn_rcpf(gw32 + rgmax32), 100.0f);
-    const gs_f2 gw2 = {gw32, gw32}, tlv = {tl, tl}, ntl2v = {-tl2, -tl2}, xm2 = {xm, xm};
-    float cum[RQ_P];
-    float loc = 0.0f;
-    gs_f2 w2 = {0.0f, 0.0f};
+    const gs_f2 gw2 = {gw32, gw32}, ntl2v = {-tl2, -tl2}, xm2 = {xm, xm};
+    // pass 1: a = gw' + rho', y = 1/a, e = xm - tl2 y (one FMA), E = 2^e, pdf' = y E; the lane's
+    // sum of pdf' and of pdf' e (so that sum pdf' x = xm T - sum pdf' e)
+    gs_f2 acc[4] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
+    gs_f2 wacc[2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
+    float p0 = 0.0f;
 #pragma unroll
-    for (int j = 0; j < RQ_P; j += 2) {
-      const gs_f2 a = gw2 + rgl[16 * (j / 2)];
+    for (int jp = 0; jp < RQ_P / 2; ++jp) {
+      const gs_f2 a = gw2 + rgl[16 * jp];
       const gs_f2 y = {__builtin_amdgcn_rcpf(a[0]), __builtin_amdgcn_rcpf(a[1])};
-      const gs_f2 t = tlv * y;
       const gs_f2 ex = __builtin_elementwise_fma(ntl2v, y, xm2);
       const gs_f2 E = {__builtin_amdgcn_exp2f(ex[0]), __builtin_amdgcn_exp2f(ex[1])};
-      const gs_f2 pdf = t * E;
-      w2 = __builtin_elementwise_fma(pdf, -ex, w2);
-      loc += pdf[0];
-      cum[j] = loc;
-      loc += pdf[1];
-      cum[j + 1] = loc;
+      const gs_f2 P = y * E;
+      if (jp == 0) p0 = P[0];
+      acc[jp & 3] += P;
+      wacc[jp & 1] = __builtin_elementwise_fma(P, ex, wacc[jp & 1]);
     }
-    const float incl = row_scan16(loc);
+    const gs_f2 s2 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    const gs_f2 w2 = wacc[0] + wacc[1];
+    const float incl = row_scan16(s2[0] + s2[1]);
     const float excl = dpp_f32<0x111>(incl);  // row_shr:1: the previous lane's prefix, 0 on lane 0
     const float T = row_last(incl);
-    const float wsum = fmaf(xm, T, row_last(row_scan16(w2[0] + w2[1])));  // sum pdf' x over the row
-    const bool okrow = T > 1e-33f && T < 3e38f && wsum < 3e38f;         // uniform per row group
-    const float D = 5.9604645e-08f * (170.0f * T + 18.0f * wsum + 12.0f * xm * T) + 2e-35f;
+    const float wsum = fmaf(xm, T, -row_last(row_scan16(w2[0] + w2[1])));  // sum pdf' x over the row
+    const bool okrow = T > 1e-33f && T < 3e38f && wsum < 3e38f;          // uniform per row group
+    const float D = 5.9604645e-08f * (72.0f * T + 18.0f * wsum + 12.0f * xm * T) + 2e-35f;
     const float uT = (float)ui * T;
-    const float tlo = (uT - 2.0f * D) - excl, thr = (uT + 2.0f * D) - excl;
-    // lane classes for each threshold: all points below / none below / straddling
-    const bool lo_all = cum[RQ_P - 1] < tlo, lo_none = !(cum[0] < tlo);
-    const bool hi_all = cum[RQ_P - 1] < thr, hi_none = !(cum[0] < thr);
-    const bool lo_str = !lo_all && !lo_none, hi_str = !hi_all && !hi_none;
-    const unsigned long long m_lo_all = __ballot(lo_all), m_hi_all = __ballot(hi_all);
-    const unsigned long long m_lo_str = __ballot(lo_str), m_hi_str = __ballot(hi_str);
-    const unsigned long long m_ok = __ballot(okrow);
-    // the straddling lanes leave their sums (and their local threshold) for the row group
-    typedef float gs_f4 __attribute__((ext_vector_type(4)));
-    if (lo_str) {
-#pragma unroll
-      for (int j = 0; j < RQ_P; j += 4)
-        *reinterpret_cast<gs_f4*>(myslot_lo + j) = gs_f4{cum[j], cum[j + 1], cum[j + 2], cum[j + 3]};
-      *reinterpret_cast<gs_f2*>(myslot_lo + RQ_P) = gs_f2{tlo, __int_as_float(nval)};
+    const float tlo = uT - 2.0f * D, thr = uT + 2.0f * D;
+    // lane classes for each threshold: all points below / none below / straddling (lanes past the
+    // grid: none)
+    const float c0 = excl + p0;
+    const bool has = nval > 0;
+    const bool lo_all = has && incl < tlo, hi_all = has && incl < thr;
+    const bool lo_str = has && !lo_all && c0 < tlo, hi_str = has && !hi_all && c0 < thr;
+    const unsigned long long m_lo = __ballot(lo_str), m_hi = __ballot(hi_str);
+    const unsigned f_lo = (unsigned)(m_lo >> (16 * g)) & 0xffffu, f_hi = (unsigned)(m_hi >> (16 * g)) & 0xffffu;
+    const int s_lo = f_lo ? __builtin_ctz(f_lo) : -1, s_hi = f_hi ? __builtin_ctz(f_hi) : -1;
+    int cl = lo_all ? nval : 0, ch = hi_all ? nval : 0;
+    // pass A: the lo straddler (else the hi one); pass B: a hi straddler in another lane
+    const int sA = s_lo >= 0 ? s_lo : s_hi;
+    if (__ballot(sA >= 0)) {
+      const StrCount n = red_straddler(rlin4, max(sA, 0), l, g, excl, gw32, -tl2, xm, A.ngrid, tlo, thr);
+      cl += (sA >= 0 && sA == s_lo) ? n.lo : 0;
+      ch += (sA >= 0 && sA == s_hi) ? n.hi : 0;
     }
-    if (hi_str) {
-#pragma unroll
-      for (int j = 0; j < RQ_P; j += 4)
-        *reinterpret_cast<gs_f4*>(myslot_hi + j) = gs_f4{cum[j], cum[j + 1], cum[j + 2], cum[j + 3]};
-      *reinterpret_cast<gs_f2*>(myslot_hi + RQ_P) = gs_f2{thr, __int_as_float(nval)};
+    const bool needB = s_hi >= 0 && s_lo >= 0 && s_hi != s_lo;
+    if (__ballot(needB)) {
+      const StrCount n = red_straddler(rlin4, max(s_hi, 0), l, g, excl, gw32, -tl2, xm, A.ngrid, tlo, thr);
+      ch += needB ? n.hi : 0;
     }
-    wave_lds_sync();
-    // the row group counts the straddler's points below its threshold, 4 per lane
-    unsigned long long m_lo_in[4], m_hi_in[4];
-    {
-      const gs_f2 tl_lo = *reinterpret_cast<const gs_f2*>(myslot_lo + RQ_P);
-      const gs_f2 tl_hi = *reinterpret_cast<const gs_f2*>(myslot_hi + RQ_P);
-      const int nv_lo = __float_as_int(tl_lo[1]), nv_hi = __float_as_int(tl_hi[1]);
-      const gs_f4 vlo = *reinterpret_cast<const gs_f4*>(myslot_lo + 4 * l);
-      const gs_f4 vhi = *reinterpret_cast<const gs_f4*>(myslot_hi + 4 * l);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = 4 * l + q;
-        m_lo_in[q] = __ballot(j < nv_lo && vlo[q] < tl_lo[0]);
-        m_hi_in[q] = __ballot(j < nv_hi && vhi[q] < tl_hi[0]);
-      }
-    }
-    wave_lds_sync();  // the slots are rewritten next iteration
-    unsigned fb = 0;  // row groups whose row takes the f64 redo
-    int idx_g[4];
-#pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      const unsigned fl_all = grp_bits(m_lo_all, gg), fh_all = grp_bits(m_hi_all, gg);
-      const unsigned fl_str = grp_bits(m_lo_str, gg), fh_str = grp_bits(m_hi_str, gg);
-      const unsigned full = (1u << L0) - 1u;  // lanes with RQ_P valid points
-      int clo = RQ_P * __builtin_popcount(fl_all & full) + (((fl_all >> L0) & 1u) ? R0 : 0);
-      int chi = RQ_P * __builtin_popcount(fh_all & full) + (((fh_all >> L0) & 1u) ? R0 : 0);
-      if (fl_str) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) clo += __builtin_popcount(grp_bits(m_lo_in[q], gg));
-      }
-      if (fh_str) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) chi += __builtin_popcount(grp_bits(m_hi_in[q], gg));
-      }
-      const bool proven = grp_bits(m_ok, gg) != 0 && __builtin_popcount(fl_str) <= 1 &&
-                          __builtin_popcount(fh_str) <= 1 && clo == chi;
-      idx_g[gg] = clo - 1;
-      if (!proven && 4 * it + gg < nr) fb |= 1u << gg;
-    }
-    // unproven rows: k_rho_red_cert's f64 redo, the whole wave on one row (~2 % of rows)
-    while (fb) {
-      const int gg = __builtin_ctz(fb);
-      fb &= fb - 1;
+    const int tot = row_last_i(row_scan16_i(cl | (ch << 16)));
+    const int clo = tot & 0xffff, chi = tot >> 16;
+    const bool proven = okrow && __builtin_popcount(f_lo) <= 1 && __builtin_popcount(f_hi) <= 1 && clo == chi;
+    int idx = clo - 1;
+    // unproven rows: k_rho_red_cert's f64 redo, the whole wave on one row (~1 % of rows)
+    unsigned long long fbm = __ballot(!proven && l == 0 && 4 * it + g < nr);
+    while (fbm) {
+      const int gg = __builtin_ctzll(fbm) >> 4;
+      fbm &= fbm - 1;
       ++nfb;
       const int rrow = 4 * it + gg;
       const double tr = rdlane(tau, rrow), gr = rdlane(gw, rrow), ur = rdlane(u, rrow);
@@ -1082,14 +1096,11 @@ __global__ __launch_bounds__(256) void k_rho_red_cert16(GridArgs A, int32_t* n_f
       int cnt = 0;
 #pragma unroll
       for (int j = 0; j < RW_G; ++j) cnt += __popcll(__ballot(cumd[j] < thd && RW_G * lane + j < A.ngrid));
-      idx_g[gg] = cnt - 1;
+      idx = (g == gg) ? cnt - 1 : idx;
     }
-#pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      int id = idx_g[gg];
-      if (id < 0) id += A.ngrid;
-      myidx = (lane == 4 * it + gg) ? id : myidx;
-    }
+    if (idx < 0) idx += A.ngrid;
+    const int mine = __shfl(idx, 16 * (lane & 3));  // row 4 it + gg lives in row group gg
+    myidx = ((lane >> 2) == it) ? mine : myidx;
   }
   if (rok) {
     if (A.idx_out) A.idx_out[r] = myidx;
