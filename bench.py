@@ -138,7 +138,7 @@ def valu_roof(plain, transc):
 
 
 # minimal lane operations per unit: red grid point h e^-h (pta_gibbs.py:265-266) = gw + rho,
-# 1/a, tau y, e^-h, h e^-h, the running sum and the searchsorted compare -- k_rho_red_cert runs
+# 1/a, tau y, e^-h, h e^-h, the running sum and the searchsorted compare -- k_rho_red_cert16 runs
 # them in f32 with two points per packed v_pk_* instruction, so its 5 plain ops cost 2.5 issue
 # slots per point (4 cycles each) beside the 2 unpacked transcendentals (8 cycles each): 26
 # cycles per wave-point; CURN term of the pdf product (pta_gibbs.py:192-205) = one Horner FMA
@@ -279,6 +279,12 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
     n_f = eng.n_f
     if hyper is not None:
         hm = eng.hyper
+        # lnL_p comes with the gated b draw (gs_ctx_set_bdraw_lnl, inside k_bdraw above); the chains
+        # whose gate stayed shut are filled by gs_lnlike_marg_gated; a full re-seed is timed for reference
+        ms_fill = event_ms(st, lambda: check(lib, lib.gs_lnlike_marg_gated(
+            h, m.P, C, m.NF, m.NMX, _lib.ptr(m.model), _lib.ptr(m.nm_dev), _lib.ptr(eng.phiinv_F),
+            _lib.ptr(eng.gate), _lib.ptr(hm.lnl_p), None)), 5)
+        gate_shut = float((eng.gate == 0).float().mean().item())
         eng._update_irn()
         ms_seed = event_ms(st, lambda: (eng._gate_phiinv(with_gate=False, out=eng.phiinv_h, gate=eng._gate_h),
                                         hm.seed(eng.phiinv_h)), 5)
@@ -293,26 +299,41 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
             note=f"{HYPER_ACL} single-parameter MH steps per chain (pta_gibbs.py:319-340), each one pulsar's "
                  "marginalised likelihood (NF x NF Schur block Cholesky, NF^3/3 + NF^2/2 + NF/6 flop; the "
                  "reference re-evaluates all 45 pulsars' full m x m systems per step)")
-        kernels["seed_lnlike"] = dict(
-            kernel_avg_ms=ms_seed, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
-            achieved=len(T) * C * fl / (ms_seed * 1e-3) / 1e12, alg_per_launch=len(T) * C * fl,
-            note="lnL_p of every (pulsar, chain) at the block's start (phiinv + gs_lnlike_marg)")
+        kernels["lnlike_gated_fill"] = dict(
+            kernel_avg_ms=ms_fill, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
+            achieved=len(T) * C * gate_shut * fl / (ms_fill * 1e-3) / 1e12,
+            alg_per_launch=len(T) * C * gate_shut * fl, gate_shut_frac=gate_shut,
+            full_reseed_ms=ms_seed,
+            note="lnL_p of the (pulsar, chain) systems whose b draw the gate skipped (gs_lnlike_marg_gated); "
+                 "the drawn ones come out of k_bdraw (gs_ctx_set_bdraw_lnl). full_reseed_ms: phiinv + "
+                 "gs_lnlike_marg over every system, the round-4 (r04e) per-sweep seed")
     elif kind == "curn_red":
         check(lib, lib.gs_phi_from_x(h, C, n_f, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.gw_col),
                                      _lib.ptr(eng.gwphi)))
         ms_r = event_ms(st, lambda: check(lib, lib.gs_rho_red(
             h, eng.P, C, n_f, _lib.ptr(eng.tau), _lib.ptr(eng.gwphi), eng.ngrid, _lib.ptr(eng.grid_red), None,
             eng.it, eng.chain_base, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.red_col), None)), 5)
+        # the rows the certified f32 pass could not prove and redid in f64 (one untimed launch)
+        nfb = torch.zeros(1, dtype=torch.int32, device=eng.x.device)
+        check(lib, lib.gs_ctx_set_grid_fallback_counter(h, _lib.ptr(nfb)))
+        try:
+            check(lib, lib.gs_rho_red(h, eng.P, C, n_f, _lib.ptr(eng.tau), _lib.ptr(eng.gwphi), eng.ngrid,
+                                      _lib.ptr(eng.grid_red), None, eng.it, eng.chain_base, _lib.ptr(eng.x),
+                                      eng.n_param, _lib.ptr(eng.red_col), None))
+            torch.cuda.synchronize()
+        finally:
+            check(lib, lib.gs_ctx_set_grid_fallback_counter(h, None))
         ev = eng.P * n_f * C * eng.ngrid
-        kernels["k_rho_red_cert"] = dict(
+        kernels["k_rho_red_cert16"] = dict(
             kernel_avg_ms=ms_r, bound="valu", unit="Geval/s", achieved=ev / (ms_r * 1e-3) / 1e9,
             alg_per_launch=ev, peak=valu_roof(*GRID_MIN_OPS["red"]) / 1e9,
             min_ops_per_unit=dict(zip(("plain", "transcendental"), GRID_MIN_OPS["red"])),
             op_mix_ceiling_f64_wave=(gp["red_evals_per_s"] / 1e9) if gp else None,
+            f64_redo_rows_frac=int(nfb.item()) / (eng.P * n_f * C),
             note="grid-point evaluations ratio*exp(-ratio/2)*ln10 (pta_gibbs.py:265-266): P x n_f x C x 1000 "
-                 "per launch (certified f32 pass, f64 redo of unproven rows); peak = hardware VALU issue rate "
-                 "/ the minimal op count per point in packed f32 (5 plain ops = 2.5 v_pk_* slots at 4 cycles + "
-                 "rcp and exp at 8 per wave64: 26 cycles)")
+                 "per launch (certified f32 pass, f64 redo of unproven rows: f64_redo_rows_frac); peak = "
+                 "hardware VALU issue rate / the minimal op count per point in packed f32 (5 plain ops = 2.5 "
+                 "v_pk_* slots at 4 cycles + rcp and exp at 8 per wave64: 26 cycles)")
         if not sharded:
             check(lib, lib.gs_phi_from_x(h, C, eng.PG * n_f, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.red_col_g),
                                          _lib.ptr(eng.irn)))

@@ -68,7 +68,9 @@ SIGNATURES = {
     "gs_counter_add": (_I, [_P, _P, _I64]),
     "gs_ctx_set_fail_counts": (_I, [_P, _P]),
     "gs_ctx_set_grid_fallback_counter": (_I, [_P, _P]),
+    "gs_ctx_set_bdraw_lnl": (_I, [_P, _P, _P]),
     "gs_lnlike_marg": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P]),
+    "gs_lnlike_marg_gated": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "gs_rho_curn_sum": (_I, [_P, _I, _I, _I, _P, _I, _P, _P, _I64, _I64, _P, _I, _P, _P]),
     "gs_rho_gumbel": (_I, [_P, _I, _I, _P, _P, _I, _P, _P, _I64, _I64, _P, _I, _P, _P]),
     "gs_phi_from_x": (_I, [_P, _I, _I, _P, _I, _P, _P]),

@@ -21,6 +21,8 @@ struct gs_ctx {
   const int64_t* sweep_dev = nullptr;  // gs_ctx_set_sweep_counter
   int32_t* fail_counts = nullptr;      // gs_ctx_set_fail_counts
   int32_t* grid_fallback = nullptr;    // gs_ctx_set_grid_fallback_counter
+  double* bdraw_lnl = nullptr;         // gs_ctx_set_bdraw_lnl
+  const double* bdraw_lnl_model = nullptr;
   double* ws = nullptr;  // tile workspace of the large-NF b-draw (grown on demand)
   size_t ws_bytes = 0;
 };
@@ -320,6 +322,14 @@ int gs_ctx_set_grid_fallback_counter(gs_ctx* ctx, int32_t* counter) {
   return 0;
 }
 
+int gs_ctx_set_bdraw_lnl(gs_ctx* ctx, double* lnl, const double* model) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if ((lnl == nullptr) != (model == nullptr)) return fail_arg(3, "lnl and model go together (both or neither)");
+  ctx->bdraw_lnl = lnl;
+  ctx->bdraw_lnl_model = model;
+  return 0;
+}
+
 int gs_counter_add(gs_ctx* ctx, int64_t* counter, int64_t inc) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (!counter) return fail_arg(2, "counter is NULL");
@@ -428,6 +438,7 @@ static int bdraw_impl(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
     return fail_arg(5, "NMX must be in 0..128 (0..64 with NF > 64)");
   if (ldb < NF + 1) return fail_arg(6, "ldb too small");
   if (!model || !fidx || !midx || !nm || !phiinv_F || !b) return fail_arg(7, "NULL array");
+  if (ctx->bdraw_lnl) return fail_arg(1, "the likelihood output (gs_ctx_set_bdraw_lnl) comes with gs_bdraw_tiled only");
   if (n_psr == 0 || n_chain == 0) return 0;
   if (big) {
     const size_t need = (size_t)n_psr * n_chain * big_ws_doubles_per_sys(NF) * sizeof(double);
@@ -442,6 +453,7 @@ static int bdraw_impl(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.phiinv_F = phiinv_F; a.z = z;
   a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = ctx->bcast; a.psr_base = ctx->psr_base;
   a.fail_count = ctx->fail_counts;
+  a.lnl = nullptr; a.lnl_model = nullptr; a.lnl_mstride = 0;
   a.model_per_sys = per_sys;
   a.mask_per_sys = ctx->x_per_sys;
   a.phi_per_chain = ctx->phi_per_chain;
@@ -492,6 +504,7 @@ int gs_bdraw_tiled(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb
   a.phiinv_F = phiinv_F; a.z = z;
   a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = 3;  /* tile variant */ a.psr_base = ctx->psr_base;
   a.fail_count = ctx->fail_counts;
+  a.lnl = ctx->bdraw_lnl; a.lnl_model = ctx->bdraw_lnl_model; a.lnl_mstride = model_stride_doubles(NF, NMX);
   a.model_per_sys = 0;
   a.mask_per_sys = ctx->x_per_sys;
   a.phi_per_chain = ctx->phi_per_chain;
@@ -629,7 +642,23 @@ int gs_lnlike_marg(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const d
   a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.model_per_sys = model_per_sys ? 1 : 0;
   a.model_global = NMX > 64;
   a.mstride = model_stride_doubles(NF, NMX); a.model = model; a.nm = nm; a.phiinv_F = phiinv_F;
-  a.lnl = lnl; a.info = info;
+  a.lnl = lnl; a.info = info; a.skip = nullptr;
+  return launch_rc(launch_lnlike_marg(ctx->stream, a), "k_lnlike_marg");
+}
+
+int gs_lnlike_marg_gated(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const double* model, const int32_t* nm,
+                         const double* phiinv_F, const int32_t* gate, double* lnl, int32_t* info) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
+  if (!nf_supported(NF)) return fail_arg(4, "NF must be even and <= 64");
+  if (NMX < 0 || NMX > GS_NMX_WIDE) return fail_arg(5, "NMX must be in 0..128");
+  if (!model || !nm || !phiinv_F || !gate || !lnl) return fail_arg(6, "NULL array");
+  if (n_psr == 0 || n_chain == 0) return 0;
+  LnlArgs a;
+  a.n_psr = n_psr; a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.model_per_sys = 0;
+  a.model_global = NMX > 64;
+  a.mstride = model_stride_doubles(NF, NMX); a.model = model; a.nm = nm; a.phiinv_F = phiinv_F;
+  a.lnl = lnl; a.info = info; a.skip = gate;
   return launch_rc(launch_lnlike_marg(ctx->stream, a), "k_lnlike_marg");
 }
 

@@ -202,15 +202,19 @@ __device__ __forceinline__ int bdraw_wave(const ModelLds& M, int NMX, int nM, in
 // One b|rho draw with the variant BC (tile MFMA or lane-row broadcast).  NFC > 0: the
 // fixed-NF instantiations (20 / 40 / 60, every variant); NFC == 0: any even NF < 16 NTC at
 // run time (tile variant only).
-template <int NFC, int NTC, int BC, bool PR = false, typename ModelT>
+// LNLD (tile variant only): also leave gs_lnlike_marg's y and pivots in scr (lnl_terms).
+template <int NFC, int NTC, int BC, bool PR = false, bool LNLD = false, typename ModelT>
 __device__ __forceinline__ int bdraw_sys(const ModelT& M, int NMX, int nM, int lane, double phinv,
                                          double zF, double zM, double& bF, double& bM, double* scr, int NF) {
+  constexpr int L = LNLD ? 2 : 0;
   if constexpr (NFC == 0)
-    return bdraw_tile_n<NTC, false, PR>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
+    return bdraw_tile_n<NTC, L, PR>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
   else if constexpr (BC == GS_BCAST_TILE)
-    return bdraw_tile<NFC, false, PR>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
-  else
+    return bdraw_tile<NFC, L, PR>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
+  else {
+    static_assert(!LNLD, "the likelihood terms come with the tile variant only");
     return bdraw_wave<NFC, BC>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr);
+  }
 }
 
 // Copy a pulsar's model block into LDS (whole workgroup), 16 bytes per lane and access: model
@@ -356,8 +360,10 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
 #ifndef GS_BDRAW_TILED
 #define GS_BDRAW_TILED 0
 #endif
-// one (pulsar p, chain c) system of k_bdraw
-template <int NFC, int NTC, int BC, typename ModelT>
+// one (pulsar p, chain c) system of k_bdraw.  LNLD: also lnl[sys] = gs_lnlike_marg's value at the
+// same phiinv (bit-identical: the same factorisation and accumulation, the model constants from the
+// row-major block A.lnl_model) -- the PTA hyper block's lnL_p seed for the next sweep.
+template <int NFC, int NTC, int BC, bool LNLD = false, typename ModelT>
 __device__ __forceinline__ void bdraw_item(const BdrawArgs& A, const ModelT& M, int p, int c, int NF, int nM, int fi,
                                            int mi, double* scr, int lane) {
   const int64_t sys = (int64_t)p * A.n_chain + c;
@@ -372,7 +378,7 @@ __device__ __forceinline__ void bdraw_item(const BdrawArgs& A, const ModelT& M, 
                zM);
   }
   double bF = 0.0, bM = 0.0;
-  const int fail = bdraw_sys<NFC, NTC, BC, GS_BDRAW_PR>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
+  const int fail = bdraw_sys<NFC, NTC, BC, GS_BDRAW_PR, LNLD>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
   if (!fail) {  // non-PD Sigma: the previous b stays (wave-uniform)
     if (lane < NF) A.b[sys * A.ldb + fi] = bF;
     if (lane < nM) A.b[sys * A.ldb + mi] = bM;
@@ -380,6 +386,17 @@ __device__ __forceinline__ void bdraw_item(const BdrawArgs& A, const ModelT& M, 
     A.fail_count[sys] += 1;
   }
   if (A.info && lane == 0) A.info[sys] = fail;
+  if constexpr (LNLD) {
+    double yy, lp;
+    lnl_terms(scr, lane, NF, yy, lp);
+    double lph = lane < NF ? log(phinv) : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lph += __shfl_xor(lph, o);
+    if (lane == 0) {
+      const double* aux = A.lnl_model + (int64_t)p * A.lnl_mstride + model_aux_offset(NF, A.NMX);
+      A.lnl[sys] = fail ? -__builtin_inf() : 0.5 * (aux[1] + yy - 2.0 * aux[0] - lp) + 0.5 * lph;
+    }
+  }
 }
 
 template <int NFC, int NTC, int WPB, int BC>
@@ -445,7 +462,7 @@ __global__ void k_model_tile(const double* __restrict__ model, int64_t mstride, 
 // k_bdraw on precomputed tiled blocks: each workgroup DMA-stages its pulsar's tile-layout block
 // (30.8 KB at NF = 60, nm = 16, against 40.5 KB row-major) for GS_BDRAW_LOOP chain groups, and
 // the draw loads its tiles lane-linearly (tile variant only).
-template <int NFC, int NTC, int WPB, bool FX>
+template <int NFC, int NTC, int WPB, bool FX, bool LNLD>
 __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_bdraw_tiled(BdrawArgs A) {
   extern __shared__ double lds[];
   const int NF = NFC ? NFC : A.NF;
@@ -464,7 +481,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
   for (int r = 0; r < GS_BDRAW_LOOP; ++r) {
     const int c = (g0 + r) * WPB + wave;
     if (c >= A.n_chain) break;
-    bdraw_item<NFC, NTC, GS_BCAST_TILE>(A, M, p, c, NF, nM, fi, mi, scr, lane);
+    bdraw_item<NFC, NTC, GS_BCAST_TILE, LNLD>(A, M, p, c, NF, nM, fi, mi, scr, lane);
   }
 }
 
@@ -474,23 +491,16 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
 // with the prefix: d^T Sigma^-1 d = |e|^2 + |y|^2, log det Sigma = 2 sum log diag L_M +
 // log det S; |y|^2 and log det S come out of the augmented tile factorisation.  The
 // model constants -1/2 (log det N + r^T N^-1 r) - 1/2 sum_M log phi_M are the caller's.
+// A shared model block is staged once per workgroup for GS_BDRAW_LOOP chain groups (as k_bdraw):
+// staging it for every WPB chains cost more than the factorisations (0.61 ms per configs[3]-shaped
+// launch, 92k systems; r04).
 template <int NFC, int NTC, int WPB>
-__global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
-  extern __shared__ double lds[];
+__device__ __forceinline__ void lnlike_item(const LnlArgs& A, const double* mb, int p, int c, double* scr, int lane) {
   const int NF = NFC ? NFC : A.NF;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nb = (A.n_chain + WPB - 1) / WPB;
-  const int p = blockIdx.x / nb;
-  const int c = (blockIdx.x % nb) * WPB + wave;
-  const bool in_lds = !A.model_per_sys && !A.model_global;
-  if (in_lds) stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
-  if (c >= A.n_chain) return;
   const int64_t sys = (int64_t)p * A.n_chain + c;
-  const double* mb = in_lds ? lds : A.model + (A.model_per_sys ? sys : (int64_t)p) * A.mstride;
   const ModelLds M = model_view(mb, NF, A.NMX);
   const double phinv = lane < NF ? A.phiinv_F[sys * NF + lane] : 1.0;
   double yy = 0.0, ldS = 0.0;
-  double* scr = lds + (in_lds ? A.mstride : 0) + wave * gs_tile_scr(NF);
   int fail;
   if constexpr (NFC == 0)
     fail = bdraw_tile_n<NTC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr, NF);
@@ -504,6 +514,63 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
   if (lane == 0) {
     A.lnl[sys] = fail ? -__builtin_inf() : 0.5 * (ee + yy - 2.0 * lm - ldS) + 0.5 * lph;
     if (A.info) A.info[sys] = fail;
+  }
+}
+
+template <int NFC, int NTC, int WPB>
+__global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
+  extern __shared__ double lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nb = (A.n_chain + WPB - 1) / WPB;
+  const bool in_lds = !A.model_per_sys && !A.model_global;
+  double* scr = lds + (in_lds ? A.mstride : 0) + wave * gs_tile_scr(NFC ? NFC : A.NF);
+  if (!in_lds) {
+    const int p = blockIdx.x / nb;
+    const int c = (blockIdx.x % nb) * WPB + wave;
+    if (c >= A.n_chain || (A.skip && A.skip[c])) return;
+    const int64_t sys = (int64_t)p * A.n_chain + c;
+    lnlike_item<NFC, NTC, WPB>(A, A.model + (A.model_per_sys ? sys : (int64_t)p) * A.mstride, p, c, scr, lane);
+    return;
+  }
+  const int nbl = (nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP;
+  const int p = blockIdx.x / nbl;
+  const int g0 = (blockIdx.x % nbl) * GS_BDRAW_LOOP;
+  constexpr int PER = GS_BDRAW_LOOP * WPB;  // chains per workgroup
+  __shared__ int sel[PER];
+  if (A.skip) {
+    // gs_lnlike_marg_gated: workgroup j of pulsar p takes the chains of rank [PER j, PER j + PER)
+    // among those with skip[c] == 0 (a block-wide ballot scan of skip), so the model is staged only
+    // by workgroups with work and every wave of them draws.  Workgroups past the count return.
+    __shared__ int wcnt[WPB];
+    __shared__ int base_s;
+    const int want0 = (blockIdx.x % nbl) * PER;
+    if (threadIdx.x < PER) sel[threadIdx.x] = -1;
+    if (threadIdx.x == 0) base_s = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < A.n_chain; c0 += 64 * WPB) {
+      const int c = c0 + (int)threadIdx.x;
+      const bool todo = c < A.n_chain && A.skip[c] == 0;
+      const unsigned long long m = __ballot(todo);
+      if (lane == 0) wcnt[wave] = __popcll(m);
+      __syncthreads();
+      int rank = base_s;
+      for (int w = 0; w < wave; ++w) rank += wcnt[w];
+      rank += __popcll(m & ((1ull << lane) - 1ull));
+      if (todo && rank >= want0 && rank < want0 + PER) sel[rank - want0] = c;
+      __syncthreads();
+      if (threadIdx.x == 0)
+        for (int w = 0; w < WPB; ++w) base_s += wcnt[w];
+      __syncthreads();
+      if (base_s >= want0 + PER) break;
+    }
+    if (sel[0] < 0) return;
+  }
+  stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+#pragma unroll 1
+  for (int r = 0; r < GS_BDRAW_LOOP; ++r) {
+    const int c = A.skip ? sel[r * WPB + wave] : (g0 + r) * WPB + wave;
+    if (c < 0 || c >= A.n_chain) break;
+    lnlike_item<NFC, NTC, WPB>(A, lds, p, c, scr, lane);
   }
 }
 
@@ -980,7 +1047,8 @@ int dispatch_nf_bdraw(int NF, int bc, dim3 grid, size_t lds, hipStream_t s, cons
 int launch_lnlike_marg(hipStream_t s, const LnlArgs& a) {
   constexpr int WPB = GS_SWEEP_WPB;
   const int nb = (a.n_chain + WPB - 1) / WPB;
-  dim3 grid((unsigned)(a.n_psr * nb));
+  const bool in_lds = !a.model_per_sys && !a.model_global;
+  dim3 grid((unsigned)(a.n_psr * (in_lds ? (nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP : nb)));
   const size_t lds = ((size_t)(a.model_per_sys || a.model_global ? 0 : a.mstride) + gs_tile_scr(a.NF) * WPB) *
                      sizeof(double);
   // a shared model block staged in LDS: above 64 KB (e.g. NF = 60 with NMX > 31) the launch needs
@@ -1129,15 +1197,20 @@ int launch_bdraw_tiled(hipStream_t s, const BdrawArgs& a) {
   dim3 grid((unsigned)(a.n_psr * ((nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP)));
   const size_t lds = ((size_t)a.mstride + (size_t)gs_tile_scr(a.NF) * WPB) * sizeof(double);
   const int NF = a.NF;
-#define GS_TL_LAUNCH(NFC, NTC)                                                                   \
-  if (fx) {                                                                                     \
-    if (lds > 65536 && set_lds(k_bdraw_tiled<NFC, NTC, WPB, true>, lds)) return 2;             \
-    hipLaunchKernelGGL((k_bdraw_tiled<NFC, NTC, WPB, true>), grid, dim3(64 * WPB), lds, s, a);  \
-  } else {                                                                                      \
-    if (lds > 65536 && set_lds(k_bdraw_tiled<NFC, NTC, WPB, false>, lds)) return 2;            \
-    hipLaunchKernelGGL((k_bdraw_tiled<NFC, NTC, WPB, false>), grid, dim3(64 * WPB), lds, s, a); \
-  }                                                                                             \
-  return 0;
+#define GS_TL_K(NFC, NTC, FX, LD)                                                               \
+  {                                                                                             \
+    if (lds > 65536 && set_lds(k_bdraw_tiled<NFC, NTC, WPB, FX, LD>, lds)) return 2;            \
+    hipLaunchKernelGGL((k_bdraw_tiled<NFC, NTC, WPB, FX, LD>), grid, dim3(64 * WPB), lds, s, a); \
+    return 0;                                                                                   \
+  }
+#define GS_TL_LAUNCH(NFC, NTC)                 \
+  if (fx) {                                    \
+    if (a.lnl) GS_TL_K(NFC, NTC, true, true)   \
+    GS_TL_K(NFC, NTC, true, false)             \
+  } else {                                     \
+    if (a.lnl) GS_TL_K(NFC, NTC, false, true)  \
+    GS_TL_K(NFC, NTC, false, false)            \
+  }
   const bool fx = model_tiled_fix(a.NMX);
   switch (NF) {
     case 20: GS_TL_LAUNCH(20, 0)
@@ -1154,6 +1227,7 @@ int launch_bdraw_tiled(hipStream_t s, const BdrawArgs& a) {
     default: GS_TL_LAUNCH(0, 5)
   }
 #undef GS_TL_LAUNCH
+#undef GS_TL_K
 }
 
 int launch_rho_analytic(hipStream_t s, const RhoArgs& a) {

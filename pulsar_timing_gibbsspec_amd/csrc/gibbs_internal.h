@@ -86,6 +86,7 @@ struct LnlArgs {
   const double* phiinv_F;
   double* lnl;
   int32_t* info;
+  const int32_t* skip;  // chains c with skip[c] != 0 are left as they are (gs_lnlike_marg_gated), or NULL
 };
 int launch_lnlike_marg(hipStream_t s, const LnlArgs& a);
 
@@ -116,6 +117,9 @@ struct BdrawArgs {
   double* b;
   int32_t* info;
   int32_t* fail_count;  // gs_ctx_set_fail_counts: failed draws per system (b kept), or NULL
+  double* lnl;             // gs_ctx_set_bdraw_lnl: lnL of each drawn system (k_bdraw_tiled), or NULL
+  const double* lnl_model;  // ... with the model constants from these row-major blocks
+  int64_t lnl_mstride;
   gs_key key;
 };
 

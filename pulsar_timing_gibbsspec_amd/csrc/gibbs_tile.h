@@ -564,7 +564,25 @@ struct model_is_tiled<ModelTiled> {
 // stored straight to bext[mrow[row]] (rows < 64 still return in bM, one per lane).
 // PR: the issue-priority raises of GS_DIAG_PRIO / GS_SOLVE_PRIO (the persistent fused sweep
 // only: in the short-lived k_bdraw waves at 3 waves/SIMD they cost 25 %).
-template <int NT, int CPC, bool LNL, bool WIDE = false, bool PR = false, typename ModelT>
+// The likelihood terms of a factorised system from the wave's LDS scratch: lane l < NF holds y_l
+// (U^T y = dF) at tb[128 + l] and the pivot^-1/2 of column l at tb[l] (bdraw_tile_core, LNL != 0);
+// |y|^2 = sum y_l^2 and log det S = sum -2 log(pivot^-1/2), one term per lane, wave-summed in one
+// fixed order.  The draw (after its solves) and the likelihood mode run the same code: bit-identical.
+__device__ __forceinline__ void lnl_terms(const double* tb, int lane, int NF, double& yy, double& lp) {
+  const double y = lane < NF ? tb[128 + lane] : 0.0;
+  yy = y * y;
+  lp = lane < NF ? -2.0 * log(tb[lane]) : 0.0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    yy += __shfl_xor(yy, o);
+    lp += __shfl_xor(lp, o);
+  }
+}
+
+// LNL: 0 the draw; 1 the likelihood terms only (bF = |y|^2, bM = log det S, no solves); 2 the draw,
+// leaving y and the pivots in the scratch for the caller's lnl_terms (tb is not touched after the
+// factorisation on the draw's non-WIDE path).
+template <int NT, int CPC, int LNL, bool WIDE = false, bool PR = false, typename ModelT>
 __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM, int lane, double phinv,
                                                double zF, double zM, double& bF, double& bM,
                                                double* __restrict__ scr, const int nf_rt, double zMa = 0.0,
@@ -661,8 +679,6 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
   double ycol[NT];
   gs_d4 yrow[NT];
   int fail = 0;
-  double lpiv = 0.0;   // LNL: sum over this lane's column of log pivot
-  double yyacc = 0.0;  // LNL: sum of y_K^2 over this lane's rows 4s+q (K < NT-1)
   double ylast = 0.0;  // AUG: y of the last tile row, column layout
 #pragma unroll
   for (int K = 0; K < NT; ++K) {
@@ -690,7 +706,6 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
     // first bad pivot of this tile (columns c of row group 0)
     const unsigned long long badm = __ballot(!(rsd > 0.0 && rsd < __builtin_inf())) & 0xffffull;
     if (!fail && badm) fail = 16 * K + __ffsll((long long)badm);
-    if constexpr (LNL) lpiv += (16 * K + c < NF) ? -2.0 * log(rsd) : 0.0;
     gs_d4 V;  // U_KK^-1
 #pragma unroll
     for (int s = 0; s < 4; ++s) V[s] = B[s] * rsd;
@@ -701,15 +716,6 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
     for (int J = K + 1; J < NT; ++J) {
       const gs_d4 z = {0.0, 0.0, 0.0, 0.0};
       t[tix(K, J, NT)] = mfma_tn(z, V, t[tix(K, J, NT)]);
-    }
-    if constexpr (LNL) {
-      // |y_K|^2: y_K = column CP of U_K,last (rows 4s+q in row group q, any column)
-      if (K + 1 < NT)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const double yv = newbcast(t[tix(K, NT - 1, NT)][s], CP);
-          yyacc = fma(yv, yv, yyacc);
-        }
     }
     // the backward solve wants U_KK^-T: transpose in place while the MFMAs run
     if constexpr (AUG) t[tix(K, K, NT)] = transpose(V, tb, q, c);
@@ -757,20 +763,20 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
 
   GS_PH(3)
   if constexpr (LNL) {
-    static_assert(AUG, "the likelihood mode reads y off the augmented factorisation");
-    // rows of y_0..y_{NT-2}: lane (q, 0) holds rows 4s+q of each (sum over the 4 row
-    // groups); y_last in column layout (sum over the 16 columns of row group 0)
-    double yy = (c == 0) ? yyacc : 0.0;
-    yy += (q == 0) ? ylast * ylast : 0.0;
-    double lp = (q == 0) ? lpiv : 0.0;
+    static_assert(AUG && !WIDE, "the likelihood terms read y off the augmented factorisation");
+    // y (column layout, row group 0) and the diagonal of each U_KK^-1 (= pivot^-1/2 exactly: the
+    // eliminated B is unit upper), held by the lanes with q == c & 3 in register c >> 2
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      yy += __shfl_xor(yy, o);
-      lp += __shfl_xor(lp, o);
+    for (int K = 0; K < NT; ++K) {
+      const int i = 16 * K + c;
+      if (q == 0 && i < NF) tb[128 + i] = ycol[K];
+      if (q == (c & 3) && i < NF) tb[i] = d4_get(t[tix(K, K, NT)], c >> 2);
     }
-    bF = yy;
-    bM = lp;
-    return fail;
+    lds_fence();
+    if constexpr (LNL == 1) {
+      lnl_terms(tb, lane, NF, bF, bM);
+      return fail;
+    }
   }
   if constexpr (PR && GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_SOLVE_PRIO);
   // ---- backward: U x = y + zF   (x_K = U_KK^-1 (w_K - sum_{J>K} U_KJ x_J))
@@ -861,7 +867,7 @@ __device__ __forceinline__ int bdraw_tile_core(const ModelT& M, int NMX, int nM,
 }
 
 // Fixed NF (the tuned 20 / 40 / 60 instantiations); NF % 16 != 0.
-template <int NF, bool LNL = false, bool PR = false, typename ModelT>
+template <int NF, int LNL = 0, bool PR = false, typename ModelT>
 __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int lane, double phinv,
                                           double zF, double zM, double& bF, double& bM,
                                           double* __restrict__ scr) {
@@ -871,7 +877,7 @@ __device__ __forceinline__ int bdraw_tile(const ModelT& M, int NMX, int nM, int 
 }
 
 // Any even NF with NF / 16 + 1 == NT (NF <= 64: one lane per free-spectrum column).
-template <int NT, bool LNL = false, bool PR = false, typename ModelT>
+template <int NT, int LNL = 0, bool PR = false, typename ModelT>
 __device__ __forceinline__ int bdraw_tile_n(const ModelT& M, int NMX, int nM, int lane, double phinv,
                                             double zF, double zM, double& bF, double& bM,
                                             double* __restrict__ scr, int NF) {
@@ -884,5 +890,5 @@ __device__ __forceinline__ int bdraw_tile_wide(const ModelT& M, int NMX, int nM,
                                                double zF, double zM, double zMa, double& bF, double& bM,
                                                double* __restrict__ scr, int NF, double* bext,
                                                const int32_t* mrow) {
-  return bdraw_tile_core<NT, -1, false, true>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF, zMa, bext, mrow);
+  return bdraw_tile_core<NT, -1, 0, true>(M, NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF, zMa, bext, mrow);
 }

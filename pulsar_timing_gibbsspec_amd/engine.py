@@ -515,12 +515,26 @@ class PTAChains:
         tiled = (m.model_tiled is not None and self.ctx.get_option(_lib.OPT_BCAST) == 3
                  and os.environ.get("GS_PTA_TILED", "1") != "0")        # A/B knob
         fn, name = (lib.gs_bdraw_tiled, "gs_bdraw_tiled") if tiled else (lib.gs_bdraw, "gs_bdraw")
+        # the red MH block's lnL_p seed as a by-product of the draw (gs_ctx_set_bdraw_lnl): the draw
+        # factorises every (pulsar, chain) system at the phiinv the next block starts from; the chains
+        # a gated draw skips get gs_lnlike_marg_gated (pta_gibbs.py:689-704 order)
+        lnl = self.hyper is not None and tiled and not self.phi_shared
+        if lnl:
+            check(lib.gs_ctx_set_bdraw_lnl(h, ptr(self.hyper.lnl_p), ptr(m.model)), "gs_ctx_set_bdraw_lnl")
         try:
             check(fn(h, m.P, self.C, m.NF, m.NMX, m.ldb, ptr(m.model_tiled if tiled else m.model), ptr(m.fidx),
                      ptr(m.midx), ptr(m.nm_dev), ptr(self.phiinv_F), ptr(z), self.it, event, self.chain_base,
                      ptr(mask), ptr(self.b), ptr(self.info)), name)
         finally:
             self.ctx.set_option(_lib.OPT_PHI_PER_CHAIN, prev)
+            if lnl:
+                check(lib.gs_ctx_set_bdraw_lnl(h, None, None), "gs_ctx_set_bdraw_lnl")
+        if lnl:
+            if mask is not None:
+                check(lib.gs_lnlike_marg_gated(h, m.P, self.C, m.NF, m.NMX, ptr(m.model), ptr(m.nm_dev),
+                                               ptr(self.phiinv_F), ptr(mask), ptr(self.hyper.lnl_p), None),
+                      "gs_lnlike_marg_gated")
+            self.hyper.fresh = True
 
     def _gate_phiinv(self, with_gate, out=None, gate=None):
         out = self.phiinv_F if out is None else out
@@ -544,15 +558,18 @@ class PTAChains:
             check(self.ctx.lib.gs_phi_from_x(self.ctx.handle, self.C, self.PG * self.n_f, ptr(self.x), self.n_param,
                                              ptr(self.red_col_g), ptr(self.irn)), "gs_phi_from_x")
 
-    def hyper_block(self, nsteps, inj=None, q_rec=None):
+    def hyper_block(self, nsteps, inj=None, q_rec=None, seed=True):
         """The red hyper-parameter Metropolis block (pta_gibbs.py:278-340) for every chain:
-        lnL_p of every (pulsar, chain) seeded at the current x, then nsteps steps in place."""
+        lnL_p of every (pulsar, chain) seeded at the current x (seed=False: lnl_p is already that,
+        from the last b draw), then nsteps steps in place."""
         h = self.hyper
-        if self.hyper_pl:
-            self._update_irn()
-        self._gate_phiinv(with_gate=False, out=self.phiinv_h, gate=self._gate_h)
-        h.seed(self.phiinv_h)
+        if seed:
+            if self.hyper_pl:
+                self._update_irn()
+            self._gate_phiinv(with_gate=False, out=self.phiinv_h, gate=self._gate_h)
+            h.seed(self.phiinv_h)
         h.steps(self.x, nsteps, self.it, self.chain_base, inj=inj, q_rec=q_rec)
+        h.fresh = False
 
     def sweep_begin(self, x_rec=None, z0=None, u_red=None, mh_inj=None):
         """Record, [first draw], [hyper MH], tau and the local red draws.  Returns the local
@@ -573,13 +590,13 @@ class PTAChains:
                 q_rec = torch.empty(n, self.C, 3, dtype=torch.float64, device=self.ctx.device) \
                     if self.hyper_acl is None else None
                 x_start = self.x[0].cpu().numpy() if q_rec is not None else None
-                self.hyper_block(n, inj=mh_inj, q_rec=q_rec)
+                self.hyper_block(n, inj=mh_inj, q_rec=q_rec, seed=not self.hyper.fresh)
                 if q_rec is not None:                          # aclength_hyper from the warm-up (:311-315)
                     from .pta_hyper import hyper_aclength
                     self.hyper_short_chain = self.hyper_spec.short_chain(x_start, q_rec[:, 0].cpu().numpy())
                     self.hyper_acl = hyper_aclength(self.hyper_short_chain)
             else:
-                self.hyper_block(self.hyper_acl, inj=mh_inj)
+                self.hyper_block(self.hyper_acl, inj=mh_inj, seed=not self.hyper.fresh)
         if self.curn_mode == "sum":                            # sufficient statistic S_k
             # tau and its fixed-point digits in one pass over b (tau itself is not needed)
             check(lib.gs_tau_sum_fx_b(h, self.P, self.C, m.NF, m.ldb, ptr(m.fidx), ptr(self.b), self.fx_e0,

@@ -137,6 +137,7 @@ class HyperMH:
         self.n_acc = torch.zeros(self.C, dtype=torch.int32, device=dev)
         self.acc_total = torch.zeros(self.C, dtype=torch.int64, device=dev)
         self.steps_total = 0
+        self.fresh = False      # lnl_p holds lnL_p at the current x (set by the engine's b draw)
 
     def seed(self, phiinv_F):
         """lnl_p[p * C + c] = phi-dependent lnL of system (p, c) at the phiinv rows given."""

@@ -191,3 +191,45 @@ def test_pta_block_gibbs_mh_sample(tmp_path):
     res = new()
     c2 = res.sample(x0, outdir=str(tmp_path / "b"), niter=230, resume=True)
     assert np.array_equal(c2, chain) and np.array_equal(res.chains, full.chains)
+
+
+def test_bdraw_lnl_is_lnlike_marg_bit_for_bit():
+    """The red block's lnL_p seed comes out of the gated b draw (gs_ctx_set_bdraw_lnl) and, for the
+    chains whose gate stayed shut, gs_lnlike_marg_gated: both equal gs_lnlike_marg at the same
+    phiinv exactly, drawn chains are the only ones the draw writes, shut chains the only ones the
+    fill writes."""
+    from pulsar_timing_gibbsspec_amd import PTABlockGibbs, _lib, synthetic
+    from pulsar_timing_gibbsspec_amd._lib import check, ptr
+    pta = synthetic.array_pta(kind="curn_plred", n_psr=6, seed=3)
+    gb = PTABlockGibbs(pta, nchains=64, seed=11)
+    x0 = np.concatenate([np.atleast_1d(p.sample()).ravel() for p in gb.params])
+    eng = gb._new_engine(x0)
+    for _ in range(3):
+        eng.sweep()
+    assert eng.hyper.fresh
+    m, C, lib, h = eng.model, eng.C, eng.ctx.lib, eng.ctx.handle
+    want = torch.empty(m.P * C, dtype=torch.float64, device="cuda")
+    check(lib.gs_lnlike_marg(h, m.P, C, m.NF, m.NMX, ptr(m.model), 0, ptr(m.nm_dev), ptr(eng.phiinv_F), ptr(want),
+                             None), "gs_lnlike_marg")
+    assert torch.isfinite(want).all()
+    assert torch.equal(eng.hyper.lnl_p, want)
+    # a mixed gate: the draw writes the open chains' systems, the fill the shut ones'
+    gate = torch.tensor([(c % 3) != 0 for c in range(C)], dtype=torch.int32, device="cuda")
+    sys_open = gate.repeat(m.P).bool()
+    eng.hyper.lnl_p.fill_(float("nan"))
+    eng._bdraw(None, _lib.EV_B, gate)      # attaches the lnl output, then fills the shut chains
+    assert torch.equal(eng.hyper.lnl_p, want)
+    eng.hyper.lnl_p.fill_(float("nan"))
+    check(lib.gs_lnlike_marg_gated(h, m.P, C, m.NF, m.NMX, ptr(m.model), ptr(m.nm_dev), ptr(eng.phiinv_F),
+                                   ptr(gate), ptr(eng.hyper.lnl_p), None), "gs_lnlike_marg_gated")
+    got = eng.hyper.lnl_p
+    assert torch.isnan(got[sys_open]).all()
+    assert torch.equal(got[~sys_open], want[~sys_open])
+    # the plain draws refuse to run while the output is attached
+    check(lib.gs_ctx_set_bdraw_lnl(h, ptr(got), ptr(m.model)), "attach")
+    try:
+        rc = lib.gs_bdraw(h, m.P, C, m.NF, m.NMX, m.ldb, ptr(m.model), ptr(m.fidx), ptr(m.midx), ptr(m.nm_dev),
+                          ptr(eng.phiinv_F), None, 0, _lib.EV_B, 0, None, ptr(eng.b), None)
+        assert rc != 0
+    finally:
+        check(lib.gs_ctx_set_bdraw_lnl(h, None, None), "detach")
