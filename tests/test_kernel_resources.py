@@ -31,15 +31,19 @@ def one(res, frag):
 HOT = [
     ("k_bdrawILi60ELi0ELi4ELi3E", 3, 2),           # PTA / CURN b|rho (configs[3]); 4 chain groups
                                                    # per workgroup: 2 spills, measured faster (r03h)
-    ("k_bdraw_tiledILi60ELi0ELi4ELb1E", 3, 0),     # PTA b|rho on register-tile model copies (nm <= 16)
-    ("k_bdraw_tiledILi60ELi0ELi4ELb0E", 3, 0),     # ... nm > 16 (configs[3]: row-major fixed block)
+    ("k_bdraw_tiledILi60ELi0ELi4ELb1ELb0E", 3, 0),  # PTA b|rho on register-tile model copies (nm <= 16)
+    ("k_bdraw_tiledILi60ELi0ELi4ELb0ELb0E", 3, 0),  # ... nm > 16 (configs[3]: row-major fixed block)
+    ("k_bdraw_tiledILi60ELi0ELi4ELb1ELb1E", 3, 0),  # ... with the red MH block's lnL_p (round 4)
+    ("k_bdraw_tiledILi60ELi0ELi4ELb0ELb1E", 3, 0),
+    ("k_lnlike_margILi60ELi0ELi4EE", 3, 0),         # lnL_p fill of shut gates / full seed
     ("k_sweep_freespec_rmILi60ELi0ELi4ELi3E", 3, 16),  # configs[2] (nm up to 17)
     ("k_sweep_freespecILi60ELi0ELi4ELi3E", 3, 16),
     ("k_sweep_freespecILi60ELi0ELi12ELi3E", 3, 40),    # 12-wave hand-off workgroups (the headline's
     ("k_sweep_freespec_rmILi60ELi0ELi12ELi3E", 3, 40),  # 4096 chains): 38 spills outside the body  # headline fused sweep (configs[1], [2]): 3 waves,
                                                     # 13 spills outside the inner body (round 3)
     ("k_rho_red_waveE", 4, 0),                     # CURN + red grid CDF (f64 wave kernel)
-    ("k_rho_red_certE", 4, 0),                     # CURN + red grid CDF (default: certified f32)
+    ("k_rho_red_certE", 4, 0),                     # CURN + red grid CDF (round-3 certified f32)
+    ("k_rho_red_cert16E", 3, 0),                   # ... the default since round 4 (16 lanes per row)
     ("k_rho_curn_fastE", 3, 0),                    # 0.60 -> 0.53 ms at 3 waves/SIMD (round 3)
     ("k_rho_curn_sum_waveILi16EE", 2, 0),
     ("k_white_syrkILi14EE", 2, 0),                 # configs[4] per-chain TNT (m = 216)
