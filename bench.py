@@ -105,8 +105,13 @@ def timed_region(world, dev, fn):
     return el
 
 
-def event_ms(stream, fn, reps):
-    """Average HIP-event time of fn() on ``stream`` (the context stream the C-ABI launches on)."""
+def event_ms(stream, fn, reps, warm=10):
+    """Average HIP-event time of fn() on ``stream`` (the context stream the C-ABI launches on),
+    after `warm` untimed calls: the clock ramps back up over ~10 ms of sustained load after the
+    small ESS launches (rocprof r04f: the red grid kernel at 0.84 ms right after them, 0.745 in the
+    sweeps)."""
+    for _ in range(warm):
+        fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(reps):
