@@ -284,12 +284,6 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
     n_f = eng.n_f
     if hyper is not None:
         hm = eng.hyper
-        # lnL_p comes with the gated b draw (gs_ctx_set_bdraw_lnl, inside k_bdraw above); the chains
-        # whose gate stayed shut are filled by gs_lnlike_marg_gated; a full re-seed is timed for reference
-        ms_fill = event_ms(st, lambda: check(lib, lib.gs_lnlike_marg_gated(
-            h, m.P, C, m.NF, m.NMX, _lib.ptr(m.model), _lib.ptr(m.nm_dev), _lib.ptr(eng.phiinv_F),
-            _lib.ptr(eng.gate), _lib.ptr(hm.lnl_p), None)), 5)
-        gate_shut = float((eng.gate == 0).float().mean().item())
         eng._update_irn()
         ms_seed = event_ms(st, lambda: (eng._gate_phiinv(with_gate=False, out=eng.phiinv_h, gate=eng._gate_h),
                                         hm.seed(eng.phiinv_h)), 5)
@@ -304,14 +298,11 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
             note=f"{HYPER_ACL} single-parameter MH steps per chain (pta_gibbs.py:319-340), each one pulsar's "
                  "marginalised likelihood (NF x NF Schur block Cholesky, NF^3/3 + NF^2/2 + NF/6 flop; the "
                  "reference re-evaluates all 45 pulsars' full m x m systems per step)")
-        kernels["lnlike_gated_fill"] = dict(
-            kernel_avg_ms=ms_fill, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
-            achieved=len(T) * C * gate_shut * fl / (ms_fill * 1e-3) / 1e12,
-            alg_per_launch=len(T) * C * gate_shut * fl, gate_shut_frac=gate_shut,
-            full_reseed_ms=ms_seed,
-            note="lnL_p of the (pulsar, chain) systems whose b draw the gate skipped (gs_lnlike_marg_gated); "
-                 "the drawn ones come out of k_bdraw (gs_ctx_set_bdraw_lnl). full_reseed_ms: phiinv + "
-                 "gs_lnlike_marg over every system, the round-4 (r04e) per-sweep seed")
+        kernels["k_bdraw"]["note"] += ("; with redsample='mh' the launch also writes lnL_p of every system "
+                                       "(gs_ctx_set_bdraw_lnl: the red block's seed, likelihood mode for the "
+                                       "systems the gate skips); the separate re-seed it replaces (phiinv + "
+                                       "gs_lnlike_marg over every system) measures full_reseed_ms")
+        kernels["k_bdraw"]["full_reseed_ms"] = ms_seed
     elif kind == "curn_red":
         check(lib, lib.gs_phi_from_x(h, C, n_f, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.gw_col),
                                      _lib.ptr(eng.gwphi)))

@@ -153,9 +153,10 @@ int gs_counter_add(gs_ctx* ctx, int64_t* counter, int64_t inc);
    redo in f64 (GS_OPT_GRID_EXACT = 0). */
 int gs_ctx_set_grid_fallback_counter(gs_ctx* ctx, int32_t* counter);
 /* Likelihood by-product of the b draw (NULL, NULL detaches): while attached, gs_bdraw_tiled also
-   writes lnl[p * n_chain + c] for every system it draws -- gs_lnlike_marg's value at the same
-   phiinv_F, bit for bit (the same factorisation; the model constants aux[2] from the row-major
-   gs_prefix blocks `model`, one per pulsar).  The PTA red-noise Metropolis block starts from these
+   writes lnl[p * n_chain + c] for every system -- gs_lnlike_marg's value at the same phiinv_F, bit
+   for bit (the same factorisation; the model constants aux[2] from the row-major gs_prefix blocks
+   `model`, one per pulsar); a system whose chain_mask entry is 0 keeps its b and still gets its
+   lnl (the likelihood-mode factorisation on the already staged block).  The PTA red-noise Metropolis block starts from these
    (pta_gibbs.py:689-704: the gated draw at the end of a sweep factorises exactly the systems the
    next sweep's block starts from), instead of re-factorising every (pulsar, chain).  gs_bdraw /
    gs_bdraw_sys refuse to run while it is attached. */
@@ -304,7 +305,9 @@ int gs_rho_curn(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau,
 int gs_lnlike_marg(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const double* model,
                    int model_per_sys, const int32_t* nm, const double* phiinv_F, double* lnl, int32_t* info);
 /* gs_lnlike_marg (shared model blocks) for the chains a gated b draw skipped: only systems of
-   chains c with gate[c] == 0 are evaluated; the others keep their lnl (and info). */
+   chains c with gate[c] == 0 are evaluated; the others keep their lnl (and info).  Ranks the
+   chains with a workgroup ballot scan so only workgroups with work stage a model block (for a
+   b draw without the lnl output, e.g. the row-major gs_bdraw path). */
 int gs_lnlike_marg_gated(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, const double* model, const int32_t* nm,
                          const double* phiinv_F, const int32_t* gate, double* lnl, int32_t* info);
 

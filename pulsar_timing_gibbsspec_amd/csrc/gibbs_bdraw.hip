@@ -360,15 +360,43 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
 #ifndef GS_BDRAW_TILED
 #define GS_BDRAW_TILED 0
 #endif
+// lnl[sys] of k_lnlike_marg from the two factorisation terms (gs_ctx_set_bdraw_lnl)
+__device__ __forceinline__ void bdraw_lnl_store(const BdrawArgs& A, int p, int64_t sys, int NF, int lane, double phinv,
+                                                int fail, double yy, double lp) {
+  double lph = lane < NF ? log(phinv) : 0.0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lph += __shfl_xor(lph, o);
+  if (lane == 0) {
+    const double* aux = A.lnl_model + (int64_t)p * A.lnl_mstride + model_aux_offset(NF, A.NMX);
+    A.lnl[sys] = fail ? -__builtin_inf() : 0.5 * (aux[1] + yy - 2.0 * aux[0] - lp) + 0.5 * lph;
+  }
+}
+
 // one (pulsar p, chain c) system of k_bdraw.  LNLD: also lnl[sys] = gs_lnlike_marg's value at the
 // same phiinv (bit-identical: the same factorisation and accumulation, the model constants from the
-// row-major block A.lnl_model) -- the PTA hyper block's lnL_p seed for the next sweep.
+// row-major block A.lnl_model) -- the PTA hyper block's lnL_p seed for the next sweep -- for the
+// systems the gate skips as well (likelihood mode on the already staged block: no second launch).
 template <int NFC, int NTC, int BC, bool LNLD = false, typename ModelT>
 __device__ __forceinline__ void bdraw_item(const BdrawArgs& A, const ModelT& M, int p, int c, int NF, int nM, int fi,
                                            int mi, double* scr, int lane) {
   const int64_t sys = (int64_t)p * A.n_chain + c;
-  if (A.chain_mask && A.chain_mask[A.mask_per_sys ? sys : (int64_t)c] == 0) return;  // gate closed: keep b
+  const bool shut = A.chain_mask && A.chain_mask[A.mask_per_sys ? sys : (int64_t)c] == 0;  // gate closed: keep b
+  if constexpr (!LNLD) {
+    if (shut) return;
+  }
   const double phinv = lane < NF ? A.phiinv_F[(A.phi_per_chain ? (int64_t)c : sys) * NF + lane] : 0.0;
+  if constexpr (LNLD) {
+    if (shut) {  // no draw, but the lnL at this phiinv all the same (likelihood mode: no solves)
+      double yy = 0.0, lp = 0.0;
+      int fail;
+      if constexpr (NFC == 0)
+        fail = bdraw_tile_n<NTC, 1, GS_BDRAW_PR>(M, A.NMX, nM, lane, phinv, 0.0, 0.0, yy, lp, scr, NF);
+      else
+        fail = bdraw_tile<NFC, 1, GS_BDRAW_PR>(M, A.NMX, nM, lane, phinv, 0.0, 0.0, yy, lp, scr);
+      bdraw_lnl_store(A, p, sys, NF, lane, phinv, fail, yy, lp);
+      return;
+    }
+  }
   double zF = 0.0, zM = 0.0;
   if (A.z) {
     zF = lane < NF ? A.z[sys * A.ldb + fi] : 0.0;
@@ -389,13 +417,7 @@ __device__ __forceinline__ void bdraw_item(const BdrawArgs& A, const ModelT& M, 
   if constexpr (LNLD) {
     double yy, lp;
     lnl_terms(scr, lane, NF, yy, lp);
-    double lph = lane < NF ? log(phinv) : 0.0;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) lph += __shfl_xor(lph, o);
-    if (lane == 0) {
-      const double* aux = A.lnl_model + (int64_t)p * A.lnl_mstride + model_aux_offset(NF, A.NMX);
-      A.lnl[sys] = fail ? -__builtin_inf() : 0.5 * (aux[1] + yy - 2.0 * aux[0] - lp) + 0.5 * lph;
-    }
+    bdraw_lnl_store(A, p, sys, NF, lane, phinv, fail, yy, lp);
   }
 }
 

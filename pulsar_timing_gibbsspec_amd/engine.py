@@ -516,8 +516,9 @@ class PTAChains:
                  and os.environ.get("GS_PTA_TILED", "1") != "0")        # A/B knob
         fn, name = (lib.gs_bdraw_tiled, "gs_bdraw_tiled") if tiled else (lib.gs_bdraw, "gs_bdraw")
         # the red MH block's lnL_p seed as a by-product of the draw (gs_ctx_set_bdraw_lnl): the draw
-        # factorises every (pulsar, chain) system at the phiinv the next block starts from; the chains
-        # a gated draw skips get gs_lnlike_marg_gated (pta_gibbs.py:689-704 order)
+        # factorises every (pulsar, chain) system at the phiinv the next block starts from, and the
+        # systems a gated draw skips get the likelihood-mode factorisation in the same launch
+        # (pta_gibbs.py:689-704 order)
         lnl = self.hyper is not None and tiled and not self.phi_shared
         if lnl:
             check(lib.gs_ctx_set_bdraw_lnl(h, ptr(self.hyper.lnl_p), ptr(m.model)), "gs_ctx_set_bdraw_lnl")
@@ -530,10 +531,6 @@ class PTAChains:
             if lnl:
                 check(lib.gs_ctx_set_bdraw_lnl(h, None, None), "gs_ctx_set_bdraw_lnl")
         if lnl:
-            if mask is not None:
-                check(lib.gs_lnlike_marg_gated(h, m.P, self.C, m.NF, m.NMX, ptr(m.model), ptr(m.nm_dev),
-                                               ptr(self.phiinv_F), ptr(mask), ptr(self.hyper.lnl_p), None),
-                      "gs_lnlike_marg_gated")
             self.hyper.fresh = True
 
     def _gate_phiinv(self, with_gate, out=None, gate=None):

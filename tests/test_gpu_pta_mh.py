@@ -194,10 +194,9 @@ def test_pta_block_gibbs_mh_sample(tmp_path):
 
 
 def test_bdraw_lnl_is_lnlike_marg_bit_for_bit():
-    """The red block's lnL_p seed comes out of the gated b draw (gs_ctx_set_bdraw_lnl) and, for the
-    chains whose gate stayed shut, gs_lnlike_marg_gated: both equal gs_lnlike_marg at the same
-    phiinv exactly, drawn chains are the only ones the draw writes, shut chains the only ones the
-    fill writes."""
+    """The red block's lnL_p seed comes out of the gated b draw (gs_ctx_set_bdraw_lnl), for the
+    chains whose gate stayed shut too (likelihood mode, b kept); gs_lnlike_marg_gated fills exactly
+    the shut chains.  Every value equals gs_lnlike_marg at the same phiinv bit for bit."""
     from pulsar_timing_gibbsspec_amd import PTABlockGibbs, _lib, synthetic
     from pulsar_timing_gibbsspec_amd._lib import check, ptr
     pta = synthetic.array_pta(kind="curn_plred", n_psr=6, seed=3)
@@ -217,8 +216,11 @@ def test_bdraw_lnl_is_lnlike_marg_bit_for_bit():
     gate = torch.tensor([(c % 3) != 0 for c in range(C)], dtype=torch.int32, device="cuda")
     sys_open = gate.repeat(m.P).bool()
     eng.hyper.lnl_p.fill_(float("nan"))
-    eng._bdraw(None, _lib.EV_B, gate)      # attaches the lnl output, then fills the shut chains
+    b0 = eng.b.clone()
+    eng._bdraw(None, _lib.EV_B, gate)      # the lnl output: drawn systems and (likelihood mode) shut ones
     assert torch.equal(eng.hyper.lnl_p, want)
+    assert torch.equal(eng.b[~sys_open], b0[~sys_open])          # shut gates keep their b
+    assert not torch.equal(eng.b[sys_open], b0[sys_open])
     eng.hyper.lnl_p.fill_(float("nan"))
     check(lib.gs_lnlike_marg_gated(h, m.P, C, m.NF, m.NMX, ptr(m.model), ptr(m.nm_dev), ptr(eng.phiinv_F),
                                    ptr(gate), ptr(eng.hyper.lnl_p), None), "gs_lnlike_marg_gated")
