@@ -334,7 +334,8 @@ int gs_tau_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, 
 int gs_tau_sum_fx(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* tau, int e0, int64_t* acc,
                   int32_t* ovf);
 int gs_fx_to_double(gs_ctx* ctx, int64_t n, int e0, const int64_t* acc, double* S);
-/* gs_tau followed by gs_tau_sum_fx in one pass over b (tau never stored): the same digits. */
+/* gs_tau followed by gs_tau_sum_fx in one pass over b (tau never stored): the same digits.
+   NF <= 64 (one lane per free-spectrum column; a workgroup per chain). */
 int gs_tau_sum_fx_b(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const int32_t* fidx, const double* b,
                     int e0, int64_t* acc, int32_t* ovf);
 int gs_rho_curn_sum(gs_ctx* ctx, int n_psr, int n_chain, int n_f, const double* S, int ngrid,

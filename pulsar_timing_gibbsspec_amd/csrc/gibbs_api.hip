@@ -686,7 +686,7 @@ int gs_tau_sum_fx_b(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const 
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_psr < 0 || n_chain < 0) return fail_arg(2, "negative batch");
   if (n_psr >= (1 << 15)) return fail_arg(2, "n_psr >= 32768 (int64 digit headroom)");
-  if (NF <= 0 || (NF & 1)) return fail_arg(4, "NF must be even");
+  if (NF <= 0 || NF > 64 || (NF & 1)) return fail_arg(4, "NF must be even and <= 64");
   if (ldb < NF) return fail_arg(5, "ldb < NF");
   if (!fidx || !b || !acc) return fail_arg(6, "NULL array");
   if (e0 < -1000 || e0 > 800) return fail_arg(8, "e0 out of range");

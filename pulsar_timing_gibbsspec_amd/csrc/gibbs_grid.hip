@@ -203,24 +203,37 @@ __device__ __forceinline__ bool fx_add(double v, int e0, long long& d0, long lon
   return sh + 53 <= 3 * FX_BITS;
 }
 
+// One workgroup per chain, its 4 waves taking every 4th pulsar: lane j < NF reads b column
+// fidx[p][j] of system (p, c) (a b row's free-spectrum columns: one coalesced read per wave and
+// pulsar), the even lane 2k forms tau_k = b_sin^2 + b_cos^2 with its neighbour's value and adds its
+// digits; the four waves' digits are summed in LDS.  (Round 3 ran one thread per (k, c) row over
+// all pulsars: 960 waves of 600-byte-strided gathers, 0.038 ms per configs[3] sweep.)
 __global__ __launch_bounds__(256) void k_tau_sum_fx_b(TauArgs A, int e0, long long* acc, int* ovf) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ long long dsum[3][4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = blockIdx.x;
   const int NFR = A.NF / 2;
   const int64_t nrow = (int64_t)NFR * A.n_chain;
-  if (t >= nrow) return;
-  const int c = (int)(t % A.n_chain), k = (int)(t / A.n_chain);
+  const bool act = lane < A.NF;
   long long d0 = 0, d1 = 0, d2 = 0;
   bool ok = true;
-  for (int p = 0; p < A.n_psr; ++p) {
+#pragma unroll 4
+  for (int p = wave; p < A.n_psr; p += 4) {
     const int64_t sys = (int64_t)p * A.n_chain + c;
-    const double bs = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k]];
-    const double bc = A.b[sys * A.ldb + A.fidx[p * A.NF + 2 * k + 1]];
-    ok &= fx_add(gs_add_rn(gs_mul_rn(bs, bs), gs_mul_rn(bc, bc)), e0, d0, d1, d2);  // numpy's tau rounding
+    const double bv = act ? A.b[sys * A.ldb + A.fidx[p * A.NF + lane]] : 0.0;
+    const double bc = __shfl_xor(bv, 1);
+    if (act && !(lane & 1)) ok &= fx_add(gs_add_rn(gs_mul_rn(bv, bv), gs_mul_rn(bc, bc)), e0, d0, d1, d2);  // numpy's tau rounding
   }
-  acc[t] = d0;
-  acc[nrow + t] = d1;
-  acc[2 * nrow + t] = d2;
+  dsum[0][wave][lane] = d0;
+  dsum[1][wave][lane] = d1;
+  dsum[2][wave][lane] = d2;
   if (!ok && ovf) *ovf = 1;
+  __syncthreads();
+  if (wave == 0 && act && !(lane & 1)) {
+    const int64_t t = (int64_t)(lane >> 1) * A.n_chain + c;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) acc[i * nrow + t] = dsum[i][0][lane] + dsum[i][1][lane] + dsum[i][2][lane] + dsum[i][3][lane];
+  }
 }
 
 __global__ __launch_bounds__(256) void k_fx_to_double(int64_t nrow, int e0, const long long* acc, double* S) {
@@ -1272,9 +1285,9 @@ int launch_tau_sum_fx(hipStream_t s, int n_psr, int64_t nrow, const double* tau,
 }
 
 int launch_tau_sum_fx_b(hipStream_t s, const TauArgs& a, int e0, long long* acc, int* ovf) {
-  const int64_t n = (int64_t)(a.NF / 2) * a.n_chain;
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(k_tau_sum_fx_b, grid1(n, 256), dim3(256), 0, s, a, e0, acc, ovf);
+  if ((int64_t)(a.NF / 2) * a.n_chain == 0) return 0;
+  if (a.NF > 64) return 1;  // one lane per free-spectrum column
+  hipLaunchKernelGGL(k_tau_sum_fx_b, dim3((unsigned)a.n_chain), dim3(256), 0, s, a, e0, acc, ovf);
   return 0;
 }
 
