@@ -276,7 +276,9 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
     bflop = C * float(np.sum(mm ** 3 / 3 + mm ** 2 / 2 + mm / 6 + 3 * mm ** 2))
     kernels = {"k_bdraw": dict(kernel_avg_ms=ms_b, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
                                achieved=bflop / (ms_b * 1e-3) / 1e12, alg_per_launch=bflop,
-                               traffic=(_ecorr_traffic(m.P * C, "pmc_traffic_curn.json") if kind == "curn" else None),
+                               traffic=_ecorr_traffic(m.P * C, {"curn": "pmc_traffic_curn.json",
+                                                                "curn_red": "pmc_traffic_red_bdraw.json"}[kind])
+                               if kind in ("curn", "curn_red") else None,
                                name="k_bdraw_tiled" if m.model_tiled is not None else "k_bdraw",
                                note="b|rho of every (pulsar, chain) system: sum_p m^3/3 + m^2/2 + m/6 + 3 m^2 "
                                     "flop per chain (SURVEY 8d)")}
@@ -326,8 +328,12 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
             min_ops_per_unit=dict(zip(("plain", "transcendental"), GRID_MIN_OPS["red"])),
             op_mix_ceiling_f64_wave=(gp["red_evals_per_s"] / 1e9) if gp else None,
             f64_redo_rows_frac=int(nfb.item()) / (eng.P * n_f * C),
+            traffic=_ecorr_traffic(C, "pmc_traffic_red.json"),
+            alg_bytes_per_launch=eng.P * n_f * C * 24,
             note="grid-point evaluations ratio*exp(-ratio/2)*ln10 (pta_gibbs.py:265-266): P x n_f x C x 1000 "
-                 "per launch (certified f32 pass, f64 redo of unproven rows: f64_redo_rows_frac); peak = "
+                 "per launch (certified f32 pass, f64 redo of unproven rows: f64_redo_rows_frac); traffic: PMC "
+                 "FETCH_SIZE x2 + WRITE_SIZE per launch (tools/gpu_pmc_red.sh; algorithmic 24 B per row: tau, "
+                 "irn and the x write) -- ~60 GB/s, far from the HBM roof; peak = "
                  "hardware VALU issue rate / the minimal op count per point in packed f32 (5 plain ops = 2.5 "
                  "v_pk_* slots at 4 cycles + rcp and exp at 8 per wave64: 26 cycles)")
         if not sharded:
@@ -703,6 +709,8 @@ def main():
                     help="chains per GPU for the PTA lines (measured: 256 -> 1024 -> 2048 -> 4096 chains give "
                          "CURN + red 3.0e5 -> 3.8e5 -> 3.9e5 -> 4.0e5 chain-it/s: saturated at 2048)")
     ap.add_argument("--pta-steps", type=int, default=200)
+    ap.add_argument("--pta-ess-sweeps", type=int, default=2000,
+                    help="untimed sweeps of each PTA line's ESS run after a 500-sweep burn-in (0: no ESS)")
     ap.add_argument("--config5", type=int, default=1, help="measure BASELINE configs[4] too (1/0)")
     ap.add_argument("--ecorr", type=int, default=1, help="measure the basis-ECORR path (SURVEY 8f-4) too (1/0)")
     ap.add_argument("--ecorr-chains", type=int, default=4096)
@@ -885,7 +893,8 @@ def main():
                        f"{args.indep_chains} chains per pulsar, one fused launch per 100 sweeps")
         add("indep", d, "indep")
     for kind in [k for k in args.pta.split(",") if k and k != "none"]:
-        d = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, shard="chain")
+        d = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, shard="chain",
+                      ess_sweeps=args.pta_ess_sweeps)
         d["config"] = (f"configs[3]: 45-pulsar CURN{' + per-pulsar red' if kind == 'curn_red' else ''} free "
                        f"spectrum, common draw {'from the tau sums' if kind == 'curn' else 'exact product'}")
         if kind == "curn_plred":
