@@ -235,3 +235,29 @@ def test_bdraw_lnl_is_lnlike_marg_bit_for_bit():
         assert rc != 0
     finally:
         check(lib.gs_ctx_set_bdraw_lnl(h, None, None), "detach")
+
+
+@pytest.mark.parametrize("C,shut_frac", [(600, 0.2), (600, 0.97), (257, 0.5)])
+def test_lnlike_gated_compaction(C, shut_frac):
+    """gs_lnlike_marg_gated ranks the shut chains with a workgroup ballot scan over chunks of 256
+    chains: with several chunks, nearly all or about half shut, the shut systems get exactly
+    gs_lnlike_marg's values and the open ones are untouched."""
+    from pulsar_timing_gibbsspec_amd import PTABlockGibbs, synthetic
+    from pulsar_timing_gibbsspec_amd._lib import check, ptr
+    pta = synthetic.array_pta(kind="curn_plred", n_psr=3, seed=4)
+    gb = PTABlockGibbs(pta, nchains=C, seed=2)
+    x0 = np.concatenate([np.atleast_1d(p.sample()).ravel() for p in gb.params])
+    eng = gb._new_engine(x0)
+    eng.sweep()
+    m, lib, h = eng.model, eng.ctx.lib, eng.ctx.handle
+    want = torch.empty(m.P * C, dtype=torch.float64, device="cuda")
+    check(lib.gs_lnlike_marg(h, m.P, C, m.NF, m.NMX, ptr(m.model), 0, ptr(m.nm_dev), ptr(eng.phiinv_F), ptr(want),
+                             None), "gs_lnlike_marg")
+    rng = np.random.default_rng(C)
+    gate = torch.as_tensor((rng.random(C) >= shut_frac).astype(np.int32), device="cuda")
+    got = torch.full_like(want, float("nan"))
+    check(lib.gs_lnlike_marg_gated(h, m.P, C, m.NF, m.NMX, ptr(m.model), ptr(m.nm_dev), ptr(eng.phiinv_F),
+                                   ptr(gate), ptr(got), None), "gs_lnlike_marg_gated")
+    sys_open = gate.repeat(m.P).bool()
+    assert torch.isnan(got[sys_open]).all()
+    assert torch.equal(got[~sys_open], want[~sys_open])
