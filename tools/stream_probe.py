@@ -49,6 +49,18 @@ def main():
     out["copy_ms"] = timed(lambda n: [hx.copy_(xr, non_blocking=True) for _ in range(n)])
     out["copy_GBps"] = xr.numel() * 8 / out["copy_ms"] / 1e6
 
+    # the same copy split over K streams (chunks of sweeps): several copy engines at once?
+    sides = [torch.cuda.Stream(device=dev) for _ in range(4)]
+
+    def split_copy(n, K):
+        step = S // K
+        for _ in range(n):
+            for i in range(K):
+                with torch.cuda.stream(sides[i]):
+                    hx[i * step:(i + 1) * step].copy_(xr[i * step:(i + 1) * step], non_blocking=True)
+    for K in (2, 4):
+        out[f"copy_split{K}_ms"] = timed(lambda n: split_copy(n, K))
+
     streamer = HistoryStreamer(ctx, [(S, C, 30)])
 
     def streamed(n):
