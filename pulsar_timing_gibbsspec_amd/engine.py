@@ -536,10 +536,14 @@ class PTAChains:
     def _gate_phiinv(self, with_gate, out=None, gate=None):
         out = self.phiinv_F if out is None else out
         gate = self.gate if gate is None else gate
-        if self.hyper_pl:       # power-law red: phi = 10^(2 x_gw) + irn (irn current with x)
+        if self.hyper_pl or self.red_cond:
+            # phi = 10^(2 x_gw) + irn, irn current with x: the power-law red phi, or the red free
+            # spectrum's 10^(2 x_red) that gs_phi_from_x already formed for the common draw (the
+            # same pow: the same bits as recomputing it per (pulsar, bin) here)
+            irn = self.irn[self.psr_lo:self.psr_lo + self.P]
             check(self.ctx.lib.gs_pta_gate_phiinv_irn(
                 self.ctx.handle, self.P, self.C, self.n_f, self.n_param, ptr(self.x),
-                ptr(self.xlast) if with_gate else None, ptr(self.gw_col), ptr(self.irn), ptr(out),
+                ptr(self.xlast) if with_gate else None, ptr(self.gw_col), ptr(irn), ptr(out),
                 ptr(gate)), "gs_pta_gate_phiinv_irn")
             return
         check(self.ctx.lib.gs_pta_gate_phiinv(
@@ -576,7 +580,7 @@ class PTAChains:
         check(lib.gs_pta_record(h, self.C, self.n_param, ptr(self.x), ptr(x_rec), ptr(self.xlast)),
               "gs_pta_record")
         if ii == 0 or self.redraw_b:                           # pta_gibbs.py:669-670
-            if self.hyper_pl:
+            if self.hyper_pl or self.red_cond:
                 self._update_irn()
             self._gate_phiinv(with_gate=False)
             self._bdraw(z0, _lib.EV_B0, None)
