@@ -453,7 +453,7 @@ static int bdraw_impl(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.phiinv_F = phiinv_F; a.z = z;
   a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = ctx->bcast; a.psr_base = ctx->psr_base;
   a.fail_count = ctx->fail_counts;
-  a.lnl = nullptr; a.lnl_model = nullptr; a.lnl_mstride = 0;
+  a.lnl = nullptr; a.lnl_model = nullptr; a.lnl_mstride = 0; a.persist = 0;
   a.model_per_sys = per_sys;
   a.mask_per_sys = ctx->x_per_sys;
   a.phi_per_chain = ctx->phi_per_chain;
@@ -505,6 +505,7 @@ int gs_bdraw_tiled(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb
   a.b = b; a.info = info; a.key = key_of(ctx); a.bcast = 3;  /* tile variant */ a.psr_base = ctx->psr_base;
   a.fail_count = ctx->fail_counts;
   a.lnl = ctx->bdraw_lnl; a.lnl_model = ctx->bdraw_lnl_model; a.lnl_mstride = model_stride_doubles(NF, NMX);
+  a.persist = 0;
   a.model_per_sys = 0;
   a.mask_per_sys = ctx->x_per_sys;
   a.phi_per_chain = ctx->phi_per_chain;

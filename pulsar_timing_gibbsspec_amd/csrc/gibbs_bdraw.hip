@@ -490,6 +490,31 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
   const int NF = NFC ? NFC : A.NF;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nb = (A.n_chain + WPB - 1) / WPB;
+  double* scr = lds + A.mstride + wave * gs_tile_scr(NF);
+  const ModelTiled M = model_tiled_view<FX>(lds, NF, A.NMX);
+  if (A.persist) {
+    // one round of workgroups (A.persist = CUs x resident workgroups per CU), workgroup w taking the
+    // (pulsar, chain group) items [w n / G, (w + 1) n / G) in pulsar-major order: every workgroup
+    // draws the same number of groups, restaging the model only where its range crosses a pulsar
+    const int64_t n_items = (int64_t)A.n_psr * nb;
+    const int64_t lo = (int64_t)blockIdx.x * n_items / A.persist, hi = (int64_t)(blockIdx.x + 1) * n_items / A.persist;
+    int cur = -1, nM = 0, fi = 0, mi = 0;
+#pragma unroll 1
+    for (int64_t it = lo; it < hi; ++it) {
+      const int p = (int)(it / nb), grp = (int)(it % nb);
+      if (p != cur) {  // uniform over the workgroup
+        if (cur >= 0) __syncthreads();  // every wave is done with the previous block
+        stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+        cur = p;
+        nM = A.nm[p];
+        fi = lane < NF ? A.fidx[p * NF + lane] : 0;
+        mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
+      }
+      const int c = grp * WPB + wave;
+      if (c < A.n_chain) bdraw_item<NFC, NTC, GS_BCAST_TILE, LNLD>(A, M, p, c, NF, nM, fi, mi, scr, lane);
+    }
+    return;
+  }
   const int nbl = (nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP;
   const int p = blockIdx.x / nbl;
   const int g0 = (blockIdx.x % nbl) * GS_BDRAW_LOOP;
@@ -497,8 +522,6 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
   const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
   const int mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
   stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
-  const ModelTiled M = model_tiled_view<FX>(lds, NF, A.NMX);
-  double* scr = lds + A.mstride + wave * gs_tile_scr(NF);
 #pragma unroll 1
   for (int r = 0; r < GS_BDRAW_LOOP; ++r) {
     const int c = (g0 + r) * WPB + wave;
@@ -1213,17 +1236,26 @@ int launch_model_tile(hipStream_t s, const double* model, int n_psr, int NF, int
   return 0;
 }
 
-int launch_bdraw_tiled(hipStream_t s, const BdrawArgs& a) {
+int launch_bdraw_tiled(hipStream_t s, const BdrawArgs& a0) {
   constexpr int WPB = GS_BDRAW_WPB;
+  BdrawArgs a = a0;
   const int nb = (a.n_chain + WPB - 1) / WPB;
-  dim3 grid((unsigned)(a.n_psr * ((nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP)));
+  const int64_t nwg = (int64_t)a.n_psr * ((nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP);
   const size_t lds = ((size_t)a.mstride + (size_t)gs_tile_scr(a.NF) * WPB) * sizeof(double);
   const int NF = a.NF;
-#define GS_TL_K(NFC, NTC, FX, LD)                                                               \
-  {                                                                                             \
-    if (lds > 65536 && set_lds(k_bdraw_tiled<NFC, NTC, WPB, FX, LD>, lds)) return 2;            \
-    hipLaunchKernelGGL((k_bdraw_tiled<NFC, NTC, WPB, FX, LD>), grid, dim3(64 * WPB), lds, s, a); \
-    return 0;                                                                                   \
+  static const int persist_env = getenv("GS_BDRAW_PERSIST") ? atoi(getenv("GS_BDRAW_PERSIST")) : 1;
+  // persistent shape: one round of resident workgroups when the classic grid needs more than one
+#define GS_TL_K(NFC, NTC, FX, LD)                                                                 \
+  {                                                                                               \
+    auto kern = k_bdraw_tiled<NFC, NTC, WPB, FX, LD>;                                             \
+    if (lds > 65536 && set_lds(kern, lds)) return 2;                                              \
+    int per_cu = 0;                                                                               \
+    if (persist_env && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WPB, lds) == hipSuccess && \
+        per_cu > 0 && nwg > (int64_t)per_cu * device_cus())                                       \
+      a.persist = per_cu * device_cus();                                                          \
+    dim3 grid((unsigned)(a.persist ? a.persist : nwg));                                           \
+    hipLaunchKernelGGL(kern, grid, dim3(64 * WPB), lds, s, a);                                    \
+    return 0;                                                                                     \
   }
 #define GS_TL_LAUNCH(NFC, NTC)                 \
   if (fx) {                                    \

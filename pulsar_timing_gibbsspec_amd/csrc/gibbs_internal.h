@@ -120,6 +120,7 @@ struct BdrawArgs {
   double* lnl;             // gs_ctx_set_bdraw_lnl: lnL of each drawn system (k_bdraw_tiled), or NULL
   const double* lnl_model;  // ... with the model constants from these row-major blocks
   int64_t lnl_mstride;
+  int persist;  // k_bdraw_tiled: 0 = one workgroup per 16 chains of a pulsar, G = G persistent workgroups
   gs_key key;
 };
 
