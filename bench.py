@@ -351,9 +351,18 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
                 note="(grid point, pulsar) terms of the common pdf product (pta_gibbs.py:192-205): "
                      "P x n_f x C x 1000 per launch; peak = hardware f64 VALU issue rate / 2 FMAs per term")
     else:
-        ms_s = event_ms(st, lambda: check(lib, lib.gs_rho_curn_sum(
-            h, eng.PG, C, n_f, _lib.ptr(eng.S), eng.ngrid, _lib.ptr(eng.grid_gw), None, eng.it, eng.chain_base,
-            _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.gw_col), None)), 5)
+        def curn_sum():
+            check(lib, lib.gs_rho_curn_sum(h, eng.PG, C, n_f, _lib.ptr(eng.S), eng.ngrid, _lib.ptr(eng.grid_gw), None,
+                                           eng.it, eng.chain_base, _lib.ptr(eng.x), eng.n_param, _lib.ptr(eng.gw_col),
+                                           None))
+        nfb = torch.zeros(1, dtype=torch.int32, device=eng.x.device)
+        check(lib, lib.gs_ctx_set_grid_fallback_counter(h, _lib.ptr(nfb)))
+        try:
+            curn_sum()
+            torch.cuda.synchronize()
+        finally:
+            check(lib, lib.gs_ctx_set_grid_fallback_counter(h, None))
+        ms_s = event_ms(st, curn_sum, 5)
         ev = n_f * C * eng.ngrid
         kernels["k_rho_curn_sum"] = dict(kernel_avg_ms=ms_s, bound="valu", unit="Geval/s",
                                          achieved=ev / (ms_s * 1e-3) / 1e9, alg_per_launch=ev,
@@ -362,9 +371,11 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
                                                                    GRID_MIN_OPS["curn_sum"])),
                                          op_mix_ceiling=(gp.get("curn_sum_evals_per_s", gp["red_evals_per_s"]) / 1e9)
                                          if gp else None,
-                                         note="n_f x C x 1000 grid points of the common pdf from the tau sums; "
-                                              "peak = hardware VALU issue rate / the minimal op count per point "
-                                              "(4 plain at 4 cycles + one exp at 8 per wave64)")
+                                         f64_redo_rows_frac=int(nfb.item()) / (n_f * C),
+                                         note="n_f x C x 1000 grid points of the common pdf from the tau sums "
+                                              "(certified f32 pass, f64 redo of unproven rows); peak = hardware "
+                                              "VALU issue rate / the minimal op count per point (4 plain at 4 "
+                                              "cycles + one exp at 8 per wave64)")
     for k in kernels.values():
         k["frac"] = (k["achieved"] / k["peak"]) if k.get("peak") else None
     dom = max(kernels, key=lambda k: kernels[k]["kernel_avg_ms"])

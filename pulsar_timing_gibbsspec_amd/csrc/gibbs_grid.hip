@@ -336,6 +336,40 @@ constexpr int CSW_G = 16;
 #define GS_CSW_RPW 16
 #endif
 
+// One row of k_rho_curn_sum_wave, wave-wide: lane l holds points [16 l, 16 l + 16) as cg, wg
+// (valid: the 16 ballot masks of the on-grid points); returns searchsorted(cdf / total, u) - 1 (-1
+// before wrapping).  Shared with k_rho_curn_sum_cert16's f64 redo of unproven rows.
+__device__ __forceinline__ int curn_sum_row_f64(double nS, double ui, const double* cg, const double* wg,
+                                                const unsigned long long* valid, const double* tb, int lane) {
+  double lp[CSW_G];
+  double mx = -__builtin_inf();
+#pragma unroll
+  for (int j = 0; j < CSW_G; ++j) {
+    lp[j] = fma(nS, wg[j], cg[j]);
+    mx = fmax(mx, lp[j]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+  double loc = 0.0;
+#pragma unroll
+  for (int j = 0; j < CSW_G; ++j) {
+    loc += exp_neg_t64(lp[j] - mx, tb);
+    lp[j] = loc;
+  }
+  double incl = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  const double total = rdlane(incl, 63);
+  const double thr = ui * total - (incl - loc);
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < CSW_G; ++j) cnt += __popcll(__ballot(lp[j] < thr) & valid[j]);
+  return cnt - 1;
+}
+
 template <int RPW>
 __global__ __launch_bounds__(256) void k_rho_curn_sum_wave(GridArgs A) {
   __shared__ double tb[64];
@@ -372,34 +406,7 @@ __global__ __launch_bounds__(256) void k_rho_curn_sum_wave(GridArgs A) {
   const int nr = (int)min((int64_t)RPW, nrow - r0);
   int myidx = 0;
   for (int i = 0; i < nr; ++i) {
-    const double nS = -rdlane(S, i), ui = rdlane(u, i);
-    double lp[CSW_G];
-    double mx = -__builtin_inf();
-#pragma unroll
-    for (int j = 0; j < CSW_G; ++j) {
-      lp[j] = fma(nS, wg[j], cg[j]);
-      mx = fmax(mx, lp[j]);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
-    double loc = 0.0;
-#pragma unroll
-    for (int j = 0; j < CSW_G; ++j) {
-      loc += exp_neg_t64(lp[j] - mx, tb);
-      lp[j] = loc;
-    }
-    double incl = loc;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const double v = __shfl_up(incl, o);
-      if (lane >= o) incl += v;
-    }
-    const double total = rdlane(incl, 63);
-    const double thr = ui * total - (incl - loc);
-    int cnt = 0;
-#pragma unroll
-    for (int j = 0; j < CSW_G; ++j) cnt += __popcll(__ballot(lp[j] < thr) & valid[j]);
-    int idx = cnt - 1;
+    int idx = curn_sum_row_f64(-rdlane(S, i), rdlane(u, i), cg, wg, valid, tb, lane);
     if (idx < 0) idx += A.ngrid;
     myidx = (lane == i) ? idx : myidx;
   }
@@ -1122,6 +1129,189 @@ __global__ __launch_bounds__(256) void k_rho_red_cert16(GridArgs A, int32_t* n_f
   if (n_fallback && lane == 0 && nfb) atomicAdd(n_fallback, nfb);
 }
 
+// ------------------------------------------------------------ a6' default: certified CURN-from-sums draw
+// k_rho_curn_sum_wave's draw (log pdf_g = -P log rho_g - S w_g, w_g = 1/(2 rho_g), pta_gibbs.py:181-214
+// with irn = 0) in f32 with k_rho_red_cert16's row layout, certificate shape and lane-level counts:
+// 16 lanes per row, lane l owning grid points [64 l, 64 l + 64), unproven rows redone with the f64
+// wave arithmetic (curn_sum_row_f64), so the default mode returns GS_OPT_GRID_EXACT = 2's index on
+// every row.
+//
+// The exponent is taken relative to a reference point m near the row's mode (rho* = S / (2 P); any
+// m is correct, a near one keeps the terms small): in log2 units e_g = -t1 - t2 with
+// t1 = P' (log rho_g - log rho_m), t2 = S' (w_g - w_m), P' = P log2e, S' = S log2e.  The grid's
+// log rho and w are held as f32 (hi, lo) pairs (~48 bits), so each difference is two f32
+// subtractions and an add, relatively accurate to ~2 eps plus 2^-48 of the values, and t1, t2 have
+// opposite signs (log rho rises, w falls along the grid): X_g = |t1 - t2| = |t1| + |t2|.  Per point
+// the exponent's error is below 6.1 eps X_g + 2^-46 (P' L + S' w_m) (L = max |log rho|), so pdf'_g =
+// 2^e_g carries eps (2 + 4.3 X_g) + 2^-46 (P' L + S' w_m) relative; with the 24 roundings of any
+// prefix (k_rho_red_cert16's sums) every value used is within
+//   D = eps (56 T + 9 W) + 2^-44 (P' L + S' w_m) T + 2e-35,   W = sum_g pdf'_g X_g,
+// a margin of ~2 on every term.  Off-grid slots hold log rho = 1e30, so 2^e is exactly 0 there
+// (S' w_m < 2^80 by the fixed-point window of S, far below P' 1e30).
+__device__ __forceinline__ StrCount cs_straddler(const gs_f4* pts, int s, int l, int g, float excl, gs_f4 ref,
+                                                 float Pp, float Sp, int ngrid, float tlo, float thr) {
+  float P[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const gs_f4 t = pts[RQ_P * s + 4 * l + q];
+    const float dl = (t[0] - ref[0]) + (t[1] - ref[1]);
+    const float dw = (t[2] - ref[2]) + (t[3] - ref[3]);
+    P[q] = __builtin_amdgcn_exp2f(-(Pp * dl) - (Sp * dw));
+  }
+  const float q1 = P[0] + P[1], q2 = q1 + P[2], q3 = q2 + P[3];
+  const float ex16 = dpp_f32<0x111>(row_scan16(q3));
+  const float base = __shfl(excl, 16 * g + s) + ex16;
+  const float c[4] = {base + P[0], base + q1, base + q2, base + q3};
+  const int nv = min(max(ngrid - RQ_P * s - 4 * l, 0), 4);
+  StrCount r = {0, 0};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    r.lo += (q < nv && c[q] < tlo) ? 1 : 0;
+    r.hi += (q < nv && c[q] < thr) ? 1 : 0;
+  }
+  return r;
+}
+
+// 8 point pairs per unrolled step at 3 waves/SIMD: a full unroll hoists all 256 table loads (391 VGPRs)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_rho_curn_sum_cert16(GridArgs A, int32_t* n_fallback) {
+  __shared__ double tb[64];                   // the f64 redo's exp table
+  __shared__ gs_f2 tab2[4][16 * RQ_P / 2];    // (log rho hi, lo, w hi, lo), pair-major for pass 1
+  __shared__ gs_f4 pts[16 * RQ_P];            // the same per point, in order (straddler, reference)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane >> 4, l = lane & 15;
+  const int n = A.ngrid;
+  if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
+  for (int q = threadIdx.x; q < 16 * RQ_P; q += 256) {
+    const bool on = q < n;
+    const int qq = on ? q : n - 1;
+    const double lr = A.grid3[n + qq], w = 0.5 / A.grid3[qq];
+    const float lh = (float)lr, wh = (float)w;
+    const gs_f4 v = {on ? lh : 1e30f, on ? (float)(lr - (double)lh) : 0.0f, wh, (float)(w - (double)wh)};
+    pts[q] = v;
+    const int ln = q / RQ_P, jj = q % RQ_P, o = ((jj / 2) * 16 + ln) * 2 + (jj & 1);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) reinterpret_cast<float*>(tab2[t])[o] = v[t];
+  }
+  __syncthreads();
+  const int64_t nrow = (int64_t)A.n_f * A.n_chain;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
+  if (r0 >= nrow) return;
+  const int64_t r = r0 + lane;
+  const bool rok = r < nrow;
+  const int64_t rr = rok ? r : r0;
+  const int c = (int)(rr % A.n_chain), k = (int)(rr / A.n_chain);
+  double u;
+  if (A.u) {
+    u = A.u[(int64_t)c * A.n_f + k];
+  } else {
+    double u2;
+    gs_uniform2(gs_counter(k, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, 0, GS_EV_CURN), A.key, u, u2);
+  }
+  const double Srow = A.tau[rr];
+  const double P = (double)A.n_psr;
+  const float Pp = (float)(P * 1.4426950408889634);
+  const double lr0 = A.grid3[n], lrn = A.grid3[2 * n - 1];
+  const float L = (float)fmax(fabs(lr0), fabs(lrn));
+  const float ih = n > 1 ? (float)((n - 1) / (lrn - lr0)) : 0.0f;  // grid points per unit log rho
+  const int nval = min(max(n - RQ_P * l, 0), RQ_P);
+  const int nr = (int)min((int64_t)64, nrow - r0);
+  const gs_f2* t0 = tab2[0] + l;
+  const gs_f2* t1p = tab2[1] + l;
+  const gs_f2* t2p = tab2[2] + l;
+  const gs_f2* t3p = tab2[3] + l;
+  int myidx = 0, nfb = 0;
+  for (int it = 0; 4 * it < nr; ++it) {
+    const int src = min(4 * it + g, nr - 1);
+    const double S = __shfl(Srow, src), ui = __shfl(u, src);
+    const float Sp = (float)(S * 1.4426950408889634);
+    // the reference point: the grid point nearest the continuous mode rho* = S / (2 P), clamped
+    const float lm = __builtin_amdgcn_logf((float)(S / (2.0 * P))) * 0.69314718f;  // ln rho*
+    float mf = (lm - (float)lr0) * ih + 0.5f;
+    mf = (mf == mf) ? fminf(fmaxf(mf, 0.0f), (float)(n - 1)) : 0.0f;
+    const int m = (int)mf;
+    const gs_f4 ref = pts[m];
+    const gs_f2 r0h = {ref[0], ref[0]}, r0l = {ref[1], ref[1]}, r1h = {ref[2], ref[2]}, r1l = {ref[3], ref[3]};
+    const gs_f2 Pp2 = {Pp, Pp}, Sp2 = {Sp, Sp};
+    gs_f2 acc[4] = {{0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}, {0.0f, 0.0f}};
+    gs_f2 wacc[2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
+    float p0 = 0.0f;
+#pragma unroll 8
+    for (int jp = 0; jp < RQ_P / 2; ++jp) {
+      const gs_f2 dl = (t0[16 * jp] - r0h) + (t1p[16 * jp] - r0l);
+      const gs_f2 dw = (t2p[16 * jp] - r1h) + (t3p[16 * jp] - r1l);
+      const gs_f2 a = Pp2 * dl, b = Sp2 * dw;
+      const gs_f2 e = -a - b;
+      const gs_f2 E = {__builtin_amdgcn_exp2f(e[0]), __builtin_amdgcn_exp2f(e[1])};
+      const gs_f2 d = a - b;
+      const gs_f2 X = {__builtin_fabsf(d[0]), __builtin_fabsf(d[1])};
+      if (jp == 0) p0 = E[0];
+      acc[jp & 3] += E;
+      wacc[jp & 1] = __builtin_elementwise_fma(E, X, wacc[jp & 1]);
+    }
+    const gs_f2 s2 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    const gs_f2 w2 = wacc[0] + wacc[1];
+    const float incl = row_scan16(s2[0] + s2[1]);
+    const float excl = dpp_f32<0x111>(incl);
+    const float T = row_last(incl);
+    const float W = row_last(row_scan16(w2[0] + w2[1]));
+    const float swm = Sp * ref[2];  // S' w_m
+    const bool okrow = T > 1e-33f && T < 3e38f && W < 3e38f && swm < 1e30f;
+    const float D = 5.9604645e-08f * (56.0f * T + 9.0f * W) + 5.684342e-14f * (Pp * L + swm) * T + 2e-35f;
+    const float uT = (float)ui * T;
+    const float tlo = uT - 2.0f * D, thr = uT + 2.0f * D;
+    const float c0 = excl + p0;
+    const bool has = nval > 0;
+    const bool lo_all = has && incl < tlo, hi_all = has && incl < thr;
+    const bool lo_str = has && !lo_all && c0 < tlo, hi_str = has && !hi_all && c0 < thr;
+    const unsigned long long m_lo = __ballot(lo_str), m_hi = __ballot(hi_str);
+    const unsigned f_lo = (unsigned)(m_lo >> (16 * g)) & 0xffffu, f_hi = (unsigned)(m_hi >> (16 * g)) & 0xffffu;
+    const int s_lo = f_lo ? __builtin_ctz(f_lo) : -1, s_hi = f_hi ? __builtin_ctz(f_hi) : -1;
+    int cl = lo_all ? nval : 0, ch = hi_all ? nval : 0;
+    const int sA = s_lo >= 0 ? s_lo : s_hi;
+    if (__ballot(sA >= 0)) {
+      const StrCount nn = cs_straddler(pts, max(sA, 0), l, g, excl, ref, Pp, Sp, n, tlo, thr);
+      cl += (sA >= 0 && sA == s_lo) ? nn.lo : 0;
+      ch += (sA >= 0 && sA == s_hi) ? nn.hi : 0;
+    }
+    const bool needB = s_hi >= 0 && s_lo >= 0 && s_hi != s_lo;
+    if (__ballot(needB)) {
+      const StrCount nn = cs_straddler(pts, max(s_hi, 0), l, g, excl, ref, Pp, Sp, n, tlo, thr);
+      ch += needB ? nn.hi : 0;
+    }
+    const int tot = row_last_i(row_scan16_i(cl | (ch << 16)));
+    const int clo = tot & 0xffff, chi = tot >> 16;
+    const bool proven = okrow && __builtin_popcount(f_lo) <= 1 && __builtin_popcount(f_hi) <= 1 && clo == chi;
+    int idx = clo - 1;
+    unsigned long long fbm = __ballot(!proven && l == 0 && 4 * it + g < nr);
+    while (fbm) {  // unproven rows: k_rho_curn_sum_wave's f64 arithmetic, the whole wave on one row
+      const int gg = __builtin_ctzll(fbm) >> 4;
+      fbm &= fbm - 1;
+      ++nfb;
+      const int rrow = 4 * it + gg;
+      double cg[CSW_G], wg[CSW_G];
+      unsigned long long valid[CSW_G];
+#pragma unroll
+      for (int j = 0; j < CSW_G; ++j) {
+        const int gi = CSW_G * lane + j;
+        const bool ok = gi < n;
+        cg[j] = ok ? -P * A.grid3[n + gi] : -1e300;
+        wg[j] = ok ? 0.5 / A.grid3[gi] : 0.0;
+        valid[j] = __ballot(ok);
+      }
+      const int id = curn_sum_row_f64(-rdlane(Srow, rrow), rdlane(u, rrow), cg, wg, valid, tb, lane);
+      idx = (g == gg) ? id : idx;
+    }
+    if (idx < 0) idx += n;
+    const int mine = __shfl(idx, 16 * (lane & 3));
+    myidx = ((lane >> 2) == it) ? mine : myidx;
+  }
+  if (rok) {
+    if (A.idx_out) A.idx_out[r] = myidx;
+    A.x[(int64_t)c * A.ldx + A.xcol[k]] = A.grid3[2 * n + myidx];
+  }
+  if (n_fallback && lane == 0 && nfb) atomicAdd(n_fallback, nfb);
+}
+
 // ------------------------------------------------------------ a4: Gumbel-max
 // rows r = k * n_chain + c (one pulsar, systems = chains); tau half-convention.
 // logpdf = log tau - logaddexp(log irn, log rho) - exp(...); argmax(logpdf + G),
@@ -1306,7 +1496,9 @@ int launch_tau_sum(hipStream_t s, int n_psr, int64_t nrow, const double* tau, do
 int launch_rho_curn_sum(hipStream_t s, const GridArgs& a) {
   const int64_t n = (int64_t)a.n_f * a.n_chain;
   if (n == 0) return 0;
-  if (a.ngrid <= 64 * CSW_G)
+  if (a.ngrid <= 16 * RQ_P && a.exact == 0)
+    hipLaunchKernelGGL(k_rho_curn_sum_cert16, grid1(n, 256), dim3(256), 0, s, a, a.n_fallback);
+  else if (a.ngrid <= 64 * CSW_G)
     hipLaunchKernelGGL(k_rho_curn_sum_wave<GS_CSW_RPW>, grid1(n, 4 * GS_CSW_RPW), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(k_rho_curn_sum, grid1(n, 4), dim3(256), 0, s, a);

@@ -661,3 +661,52 @@ def test_bdraw_tiled_equals_row_major(ctx, phi_shared, masked, nf, small_nm):
     if masked:                                              # gated systems keep b
         keep = np.tile(mask.cpu().numpy() == 0, model.P)
         assert keep.any() and np.all(b1[keep] == 7.0)
+
+
+@pytest.mark.parametrize("ngrid", [1000, 1024, 333, 64, 1])
+def test_curn_sum_certified_f32_matches_f64(ctx, request, ngrid):
+    """The default CURN-from-sums draw (k_rho_curn_sum_cert16: f32 points relative to the row's
+    mode + per-row error certificate, f64 redo of unproven rows) against the f64 wave kernel
+    (GS_OPT_GRID_EXACT = 2) on 15k rows whose mode spans the grid and beyond it on both sides,
+    with adversarial rows (u placed exactly on an f64 cdf value): the same index on every row, the
+    adversarial ones among the few redone in f64."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import grid3
+    request.addfinalizer(lambda: ctx.lib.gs_ctx_set_option(ctx.handle, _lib.OPT_GRID_EXACT, 0))
+    rng = np.random.default_rng(ngrid)
+    P, n_f, C = 45, 30, 512
+    lo, hi = 1e-18, 1e-8
+    rho_true = 10 ** rng.uniform(-21, -5, (n_f, C))
+    S = 2 * rho_true * rng.gamma(P, 1.0, (n_f, C))
+    S[0, :8] = 0.0                                   # no data: pdf ~ rho^-P, the left edge
+    u = rng.random((C, n_f))
+    G = grid3(lo, hi, n=ngrid)
+    rho = 10 ** np.linspace(np.log10(lo), np.log10(hi), ngrid)
+    adv = list(zip(rng.integers(0, n_f, 40), rng.integers(8, C, 40)))
+    for k, c in adv:
+        lp = -P * np.log(rho) - S[k, c] / (2 * rho)
+        cdf = np.cumsum(np.exp(lp - lp.max()))
+        cdf /= cdf[-1]
+        u[c, k] = cdf[int(rng.integers(0, ngrid))]
+    xcol = torch.arange(n_f, dtype=torch.int32, device="cuda")
+    fb = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out, nfb = {}, {}
+    for mode in (2, 0):
+        _lib.check(ctx.lib.gs_ctx_set_option(ctx.handle, _lib.OPT_GRID_EXACT, mode), "set_option")
+        x = torch.zeros(C, n_f, dtype=torch.float64, device="cuda")
+        idx = torch.full((n_f * C,), -7, dtype=torch.int32, device="cuda")
+        K = Keep()
+        fb.zero_()
+        _lib.check(ctx.lib.gs_ctx_set_grid_fallback_counter(ctx.handle, _lib.ptr(fb)), "counter")
+        try:
+            _lib.check(ctx.lib.gs_rho_curn_sum(ctx.handle, P, C, n_f, K(S), ngrid, _lib.ptr(G), K(u), 0, 0,
+                                               _lib.ptr(x), n_f, _lib.ptr(xcol), _lib.ptr(idx)), "gs_rho_curn_sum")
+        finally:
+            _lib.check(ctx.lib.gs_ctx_set_grid_fallback_counter(ctx.handle, None), "counter")
+        out[mode] = (idx.cpu().numpy(), x.cpu().numpy())
+        nfb[mode] = int(fb)
+    assert out[0][0].min() >= 0 and out[0][0].max() < ngrid
+    assert np.array_equal(out[0][0], out[2][0]), int(np.sum(out[0][0] != out[2][0]))
+    assert np.array_equal(out[0][1], out[2][1])
+    if ngrid > 1:
+        assert nfb[0] < 0.03 * out[0][0].size, nfb[0]
