@@ -1172,7 +1172,13 @@ __device__ __forceinline__ StrCount cs_straddler(const gs_f4* pts, int s, int l,
   return r;
 }
 
-// 8 point pairs per unrolled step at 3 waves/SIMD: a full unroll hoists all 256 table loads (391 VGPRs)
+// 8 point pairs per unrolled step at 3 waves/SIMD: a full unroll hoists all 256 table loads (391 VGPRs).
+// CS_RPW rows per wave (4 at a time): the CURN line's 30 x 2048 rows are 960 waves at 64 (under one
+// per SIMD: 0.060 ms), 3840 at 16 (0.0435 ms; 8: 0.0465, 32: 0.0458; f64 wave kernel 0.078).
+#ifndef GS_CS_RPW
+#define GS_CS_RPW 16
+#endif
+constexpr int CS_RPW = GS_CS_RPW;
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_rho_curn_sum_cert16(GridArgs A, int32_t* n_fallback) {
   __shared__ double tb[64];                   // the f64 redo's exp table
   __shared__ gs_f2 tab2[4][16 * RQ_P / 2];    // (log rho hi, lo, w hi, lo), pair-major for pass 1
@@ -1194,10 +1200,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   }
   __syncthreads();
   const int64_t nrow = (int64_t)A.n_f * A.n_chain;
-  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * CS_RPW;
   if (r0 >= nrow) return;
   const int64_t r = r0 + lane;
-  const bool rok = r < nrow;
+  const bool rok = lane < CS_RPW && r < nrow;
   const int64_t rr = rok ? r : r0;
   const int c = (int)(rr % A.n_chain), k = (int)(rr / A.n_chain);
   double u;
@@ -1214,7 +1220,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   const float L = (float)fmax(fabs(lr0), fabs(lrn));
   const float ih = n > 1 ? (float)((n - 1) / (lrn - lr0)) : 0.0f;  // grid points per unit log rho
   const int nval = min(max(n - RQ_P * l, 0), RQ_P);
-  const int nr = (int)min((int64_t)64, nrow - r0);
+  const int nr = (int)min((int64_t)CS_RPW, nrow - r0);
   const gs_f2* t0 = tab2[0] + l;
   const gs_f2* t1p = tab2[1] + l;
   const gs_f2* t2p = tab2[2] + l;
@@ -1497,7 +1503,7 @@ int launch_rho_curn_sum(hipStream_t s, const GridArgs& a) {
   const int64_t n = (int64_t)a.n_f * a.n_chain;
   if (n == 0) return 0;
   if (a.ngrid <= 16 * RQ_P && a.exact == 0)
-    hipLaunchKernelGGL(k_rho_curn_sum_cert16, grid1(n, 256), dim3(256), 0, s, a, a.n_fallback);
+    hipLaunchKernelGGL(k_rho_curn_sum_cert16, grid1(n, 4 * CS_RPW), dim3(256), 0, s, a, a.n_fallback);
   else if (a.ngrid <= 64 * CSW_G)
     hipLaunchKernelGGL(k_rho_curn_sum_wave<GS_CSW_RPW>, grid1(n, 4 * GS_CSW_RPW), dim3(256), 0, s, a);
   else
