@@ -14,4 +14,4 @@ echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -s KILL 170 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $R/bench.py $ARGS > $OUT/write.log 2>&1; rc=$?
 echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd $R && SWEEPS=1 CHAINS=2048 GRID=2764800 HEAD_LAUNCHES=6 python tools/pmc_traffic.py $OUT "k_rho_red_cert16" $OUT/pmc_traffic_red.json && \
-  SWEEPS=1 CHAINS=92160 GRID=1474560 HEAD_LAUNCHES=6 python tools/pmc_traffic.py $OUT "k_bdraw_tiled<60" $OUT/pmc_traffic_red_bdraw.json
+  SWEEPS=1 CHAINS=92160 GRID=196608 HEAD_LAUNCHES=6 python tools/pmc_traffic.py $OUT "k_bdraw_tiled<60" $OUT/pmc_traffic_red_bdraw.json
