@@ -524,6 +524,21 @@ def _ecorr_traffic(C, fname="pmc_traffic_ecorr.json"):
     return d.get("bytes_per_launch") if d.get("chains") == C else None
 
 
+def chain_ess(eng, cols, burn=300, sweeps=1000, max_chains=256):
+    """ESS per chain-sweep of the worst log10_rho bin from the engine's own chains continued past
+    the timed region (untimed): ``burn`` more sweeps dropped, then ``sweeps`` recorded (x columns
+    ``cols`` of the first max_chains chains)."""
+    for _ in range(burn):
+        eng.sweep()
+    idx = torch.as_tensor(cols, dtype=torch.long, device=eng.x.device)
+    ce = min(max_chains, eng.x.shape[0])
+    xe = torch.empty(sweeps, ce, len(cols), dtype=torch.float64, device=eng.x.device)
+    for i in range(sweeps):
+        eng.sweep()
+        xe[i] = eng.x[:ce].index_select(1, idx)
+    return ess_fraction(xe.cpu().numpy(), burn_frac=0.0), ce
+
+
 def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
     """SURVEY 8f-4 with white noise sampled too (the notebook's J1713 configuration): per sweep
     white MH (aclength steps) -> per-chain TNT (gs_white_tnt) -> per-chain ECORR operands ->
@@ -571,6 +586,7 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
         el = float(t.item())
     if int(em.binfo.abs().sum()) or int(em.pinfo.abs().sum()):
         raise RuntimeError("non-PD system in the white + ECORR bench")
+    ess_frac, ess_c = chain_ess(eng, gw)
     # dominant kernel: gs_ecorr_prefix in likelihood mode on per-chain operands, timed alone
     stream = ctx.stream
     eng._phiinv(False)
@@ -591,7 +607,11 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
     nb = em.ldbx // 16
     alg_bytes = C * 8 * (ne * em.ldbx + 256 * nb * (nb + 1) // 2 + ne + NF + 5)
     traffic = _ecorr_traffic(C, "pmc_traffic_ecorr_white.json")
-    return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+    value = C * world * K / el
+    return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+                ess_per_s=value * ess_frac,
+                ess={"per_chain_sweep_min_bin": ess_frac, "burn_in": 300, "sweeps": 1000, "chains": ess_c,
+                     "note": "the bench's chains continued untimed: 300 more sweeps dropped, 1000 recorded"},
                 chains_per_gpu=C, m=m, n_epoch=ne, aclength_white=aclength, aclength_ecorr=aclength,
                 roofline={"bound": "mfma", "kernel": "k_ecorr_prefix<likelihood mode, per-chain operands>",
                           "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -646,6 +666,7 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
         el = float(t.item())
     if int(em.binfo.abs().sum()) or int(em.pinfo.abs().sum()):
         raise RuntimeError("non-PD system in the ECORR bench")
+    ess_frac, ess_c = chain_ess(eng, gw)
     # dominant kernel: gs_ecorr_prefix in likelihood mode (one launch per Metropolis step:
     # epoch Schur complement + fixed-prior prefix + F-block factorisation), timed alone
     stream = ctx.stream
@@ -663,7 +684,11 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
     # update + the (NF+1)-augmented Cholesky of the free-spectrum block
     flops = C * (ne * (mR + 1) * (mR + 2) + nM * (NF + 1) * (NF + 2) + (NF + 1) ** 3 // 3)
     tflops = flops / (k_ms * 1e-3) / 1e12
-    return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+    value = C * world * K / el
+    return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+                ess_per_s=value * ess_frac,
+                ess={"per_chain_sweep_min_bin": ess_frac, "burn_in": 300, "sweeps": 1000, "chains": ess_c,
+                     "note": "the bench's chains continued untimed: 300 more sweeps dropped, 1000 recorded"},
                 chains_per_gpu=C, m=m, n_epoch=ne, m_R=mR, aclength=aclength,
                 roofline={"bound": "mfma", "kernel": ("k_ecorr_prefix<likelihood mode>" if em.fused and em.fused_lnl
                                                       else "k_ecorr_schur + k_prefix + k_lnlike_marg"),
