@@ -739,7 +739,7 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
   extern __shared__ double lds[];
   const int NF = NFC ? NFC : A.NF;
   const int NFR = NF / 2;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave-uniform (SGPR)
   // tile variant: the model block in the register-tile layout (stage_model_tiled); the lane-row
   // broadcast variants read the row-major block
   constexpr bool TL = GS_SWEEP_TILED && (BC == GS_BCAST_TILE || NFC == 0);
