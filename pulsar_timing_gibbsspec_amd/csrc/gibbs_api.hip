@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void k_tnt(const gs_tnt_desc* desc, int nb, co
   const int bi = blockIdx.y / nb, bj = blockIdx.y % nb;
   const int m = (int)D.m;
   if (bi * 16 >= m || bj * 16 >= m) return;
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = gs_wave_id(), l = threadIdx.x & 63;
   const int i = l & 15, k = l >> 4;
   const int ci = bi * 16 + i, cj = bj * 16 + i;
   const double* Tp = T + D.T_off;
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void k_tnr(const gs_tnt_desc* desc, const doub
                                              const double* Nv, const double* r, double* d) {
   __shared__ double red[2][4][64];
   const gs_tnt_desc D = desc[blockIdx.x];
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = gs_wave_id(), l = threadIdx.x & 63;
   const int m = (int)D.m;
   const int j = blockIdx.y * 64 + l;
   double hi = 0.0, lo = 0.0;

@@ -228,7 +228,7 @@ typedef __attribute__((address_space(3))) void* gs_lds_vptr;
 __device__ __forceinline__ void stage_model(double* lds, const double* g, int64_t n) {
   const int n2 = (int)(n >> 1);
 #if GS_STAGE_GLDS
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   for (int base = wave * 64; base < n2; base += nw * 64) {
     if (base + lane < n2)
       __builtin_amdgcn_global_load_lds((const void*)(g + 2 * (base + lane)), (gs_lds_vptr)(lds + 2 * base), 16, 0,
@@ -303,7 +303,7 @@ template <int NTC, int WPB>
 __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
   extern __shared__ double lds[];
   const int NF = A.NF;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int nb = (A.n_chain + WPB - 1) / WPB;
   const int p = blockIdx.x / nb;
   const int c = (blockIdx.x % nb) * WPB + wave;
@@ -425,7 +425,7 @@ template <int NFC, int NTC, int WPB, int BC>
 __global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_bdraw(BdrawArgs A) {
   extern __shared__ double lds[];
   const int NF = NFC ? NFC : A.NF;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int nb = (A.n_chain + WPB - 1) / WPB;
   if (A.model_per_sys) {
     // per-system models (white-noise runs, TNT differs per chain): read from global memory (L2)
@@ -488,7 +488,7 @@ template <int NFC, int NTC, int WPB, bool FX, bool LNLD>
 __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_bdraw_tiled(BdrawArgs A) {
   extern __shared__ double lds[];
   const int NF = NFC ? NFC : A.NF;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int nb = (A.n_chain + WPB - 1) / WPB;
   double* scr = lds + A.mstride + wave * gs_tile_scr(NF);
   const ModelTiled M = model_tiled_view<FX>(lds, NF, A.NMX);
@@ -565,7 +565,7 @@ __device__ __forceinline__ void lnlike_item(const LnlArgs& A, const double* mb, 
 template <int NFC, int NTC, int WPB>
 __global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
   extern __shared__ double lds[];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int nb = (A.n_chain + WPB - 1) / WPB;
   const bool in_lds = !A.model_per_sys && !A.model_global;
   double* scr = lds + (in_lds ? A.mstride : 0) + wave * gs_tile_scr(NFC ? NFC : A.NF);
@@ -739,7 +739,7 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
   extern __shared__ double lds[];
   const int NF = NFC ? NFC : A.NF;
   const int NFR = NF / 2;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave-uniform (SGPR)
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   // tile variant: the model block in the register-tile layout (stage_model_tiled); the lane-row
   // broadcast variants read the row-major block
   constexpr bool TL = GS_SWEEP_TILED && (BC == GS_BCAST_TILE || NFC == 0);

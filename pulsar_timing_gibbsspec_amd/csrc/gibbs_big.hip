@@ -49,7 +49,7 @@ template <int CP>
 __global__ __launch_bounds__(64 * BIG_WPB) void k_bdraw_big(BdrawArgs A, double* wsp, int64_t ws_stride) {
   using namespace gtile;
   extern __shared__ double lds[];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int q = lane >> 4, c = lane & 15;
   const int64_t n_sys = (int64_t)A.n_psr * A.n_chain;
   const int64_t sys = (int64_t)blockIdx.x * BIG_WPB + wave;

@@ -24,6 +24,12 @@ __host__ __device__ constexpr int gs_tile_scr(int NF) {
 // Lanes of one wavefront exchanging data through LDS: wavefront-scope release/acquire
 // fences around the wave barrier (a bare wave barrier does not order the LDS accesses
 // for the compiler backend).
+// The wave's index in its workgroup as a wave-uniform SGPR value.  `threadIdx.x >> 6` is uniform
+// too, but the compiler's divergence analysis does not know it, so everything derived from it
+// (chain, system, pointers) would sit in VGPRs: the 12-wave fused sweep spilled 37 VGPRs that way,
+// 6 with this (r04).
+__device__ __forceinline__ int gs_wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

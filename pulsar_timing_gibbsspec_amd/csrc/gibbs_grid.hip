@@ -52,7 +52,7 @@ __global__ void k_tau(TauArgs A) {
 #endif
 __global__ __launch_bounds__(64 * GS_CURN_WPB) void k_rho_curn(GridArgs A) {
   extern __shared__ double sh[];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * GS_CURN_WPB + wave;
   const int64_t nrow = (int64_t)A.n_f * A.n_chain;
   if (r >= nrow) return;  // whole wavefront exits together (no block barrier below)
@@ -210,7 +210,7 @@ __device__ __forceinline__ bool fx_add(double v, int e0, long long& d0, long lon
 // all pulsars: 960 waves of 600-byte-strided gathers, 0.038 ms per configs[3] sweep.)
 __global__ __launch_bounds__(256) void k_tau_sum_fx_b(TauArgs A, int e0, long long* acc, int* ovf) {
   __shared__ long long dsum[3][4][64];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int c = blockIdx.x;
   const int NFR = A.NF / 2;
   const int64_t nrow = (int64_t)NFR * A.n_chain;
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256) void k_fx_to_double(int64_t nrow, int e0, cons
 constexpr int CS_MAXG = 32;  // grid points per lane (ngrid <= 2048)
 
 __global__ __launch_bounds__(256) void k_rho_curn_sum(GridArgs A) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + wave;
   const int64_t nrow = (int64_t)A.n_f * A.n_chain;
   if (r >= nrow) return;
@@ -373,7 +373,7 @@ __device__ __forceinline__ int curn_sum_row_f64(double nS, double ui, const doub
 template <int RPW>
 __global__ __launch_bounds__(256) void k_rho_curn_sum_wave(GridArgs A) {
   __shared__ double tb[64];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
   __syncthreads();
   const int64_t nrow = (int64_t)A.n_f * A.n_chain;
@@ -441,7 +441,7 @@ constexpr int CF_RN = 2;     // groups between rescalings: (2 rho_min)^(CF_K CF_
 #define GS_CF_MINW 3
 #endif
 __global__ __launch_bounds__(256, GS_CF_MINW) void k_rho_curn_fast(GridArgs A) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + wave;
   const int64_t nrow = (int64_t)A.n_f * A.n_chain;
   if (r >= nrow) return;
@@ -674,7 +674,7 @@ typedef float gs_f2 __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(256) void k_rho_red_wave(GridArgs A) {
   __shared__ double tb[64];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
   __syncthreads();
   const int64_t nrow = (int64_t)A.n_psr * A.n_f * A.n_chain;
@@ -766,7 +766,7 @@ __global__ __launch_bounds__(256) void k_rho_red_wave(GridArgs A) {
 // ~ 1000 x 4 D / T, about 1 % of rows (measured 1.3 % on rows spanning 16 decades of tau).
 __global__ __launch_bounds__(256) void k_rho_red_cert(GridArgs A, int32_t* n_fallback) {
   __shared__ double tb[64];  // the f64 redo's exp table
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
   __syncthreads();
   const int64_t nrow = (int64_t)A.n_psr * A.n_f * A.n_chain;
@@ -990,7 +990,7 @@ __global__ __launch_bounds__(256) void k_rho_red_cert16(GridArgs A, int32_t* n_f
   __shared__ double tb[64];          // the f64 redo's exp table
   __shared__ gs_f2 rgs[16 * RQ_P / 2];  // the scaled f32 grid, pair-major, for pass 1
   __shared__ gs_f4 rlin4[16 * RQ_P / 4];  // the same grid in point order, for the straddler recompute
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int g = lane >> 4, l = lane & 15;
   const int S = -ilogb(A.grid3[0]);  // rho_min 2^S in [1, 2)
   if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
@@ -1183,7 +1183,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   __shared__ double tb[64];                   // the f64 redo's exp table
   __shared__ gs_f2 tab2[4][16 * RQ_P / 2];    // (log rho hi, lo, w hi, lo), pair-major for pass 1
   __shared__ gs_f4 pts[16 * RQ_P];            // the same per point, in order (straddler, reference)
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int g = lane >> 4, l = lane & 15;
   const int n = A.ngrid;
   if (threadIdx.x < 64) tb[threadIdx.x] = GS_EXP2_64[threadIdx.x];

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void k_tnr_dd(const gs_tnt_desc* desc, const d
                                                 const double* r, double* d, double* d_lo) {
   __shared__ double red[2][4][64];
   const gs_tnt_desc D = desc[blockIdx.x];
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = gs_wave_id(), l = threadIdx.x & 63;
   const int m = (int)D.m;
   const int j = blockIdx.y * 64 + l;
   gs_dot2 acc;

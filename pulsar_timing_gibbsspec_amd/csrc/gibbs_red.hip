@@ -58,7 +58,7 @@ __device__ __forceinline__ double red_lnlike(const RedFreq& F, double la, double
 }
 
 __global__ __launch_bounds__(256) void k_red_mh(RedMhArgs A) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * 4 + wave;
   if (c >= A.n_chain) return;  // whole wavefront exits together
   double* xc = A.x + c * A.ldx;

@@ -51,7 +51,7 @@ constexpr int MH_WPB = 4;
 __global__ __launch_bounds__(64 * MH_WPB) void k_white_mh(WhiteMhArgs A) {
   __shared__ double sb[MH_WPB][4][GS_WHITE_MAX_BK + 1];  // ef2, t2, tn, S per backend
   __shared__ double sx[MH_WPB][GS_WHITE_MAX_W];         // current white parameter values
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int p = blockIdx.y;
   const int c = blockIdx.x * MH_WPB + wave;
   if (c >= A.n_chain) return;  // no workgroup barriers below
@@ -191,7 +191,7 @@ typedef double gs_d4_t __attribute__((ext_vector_type(4)));
 // ceil(n_chain / 16)), 4 waves per workgroup (consecutive TOA tiles).
 __global__ __launch_bounds__(256) void k_white_resid_mfma(WhiteResidArgs A) {
   const gs_tnt_desc D = A.tdesc[blockIdx.y];
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 15, k = l >> 4;
+  const int w = gs_wave_id(), l = threadIdx.x & 63, i = l & 15, k = l >> 4;
   const int64_t t0 = ((int64_t)blockIdx.x * 4 + w) * 16;
   if (t0 >= D.n_toa) return;  // wave-uniform, no barriers
   const int p = blockIdx.y;
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void k_white_tnt(WhiteTntArgs A) {
   const int m = (int)D.m;
   if (bi * 16 >= m) return;
   stage_white(A, W, A.x_per_sys ? sys : (int64_t)c, sb[0], sb[1], sb[2]);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = gs_wave_id(), l = threadIdx.x & 63;
   const int i = l & 15, k = l >> 4;
   const int ci = bi * 16 + i, cj = bj * 16 + i;
   const double* Tp = A.T + D.T_off;
@@ -585,7 +585,7 @@ __global__ __launch_bounds__(256) void k_white_tnr(WhiteTntArgs A) {
   const gs_tnt_desc D = A.tdesc[p];
   const gs_white_desc W = A.wdesc[p];
   stage_white(A, W, A.x_per_sys ? sys : (int64_t)c, sb[0], sb[1], sb[2]);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = gs_wave_id(), l = threadIdx.x & 63;
   const int m = (int)D.m;
   const int j = blockIdx.y * 64 + l;
   double s = 0.0;
