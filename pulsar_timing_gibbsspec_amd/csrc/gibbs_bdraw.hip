@@ -311,7 +311,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
   const int64_t sys = (int64_t)p * A.n_chain + c;
   if (A.chain_mask && A.chain_mask[A.mask_per_sys ? sys : (int64_t)c] == 0) return;
   const ModelLds M = model_view(A.model + (A.model_per_sys ? sys : (int64_t)p) * A.mstride, NF, A.NMX);
-  const int nM = A.nm[p];
+  const int nM = __builtin_amdgcn_readfirstlane(A.nm[p]);  // uniform: SGPR
   const int32_t* mrow = A.midx + (int64_t)p * A.NMX;
   const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
   const int mi = lane < nM ? mrow[lane] : 0;
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_bdraw(Bdraw
     const int p = blockIdx.x / nb;
     const int c = (blockIdx.x % nb) * WPB + wave;
     if (c >= A.n_chain) return;
-    const int nM = A.nm[p];
+    const int nM = __builtin_amdgcn_readfirstlane(A.nm[p]);  // uniform: SGPR
     const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
     const int mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
     const int64_t sys = (int64_t)p * A.n_chain + c;
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_bdraw(Bdraw
   const int nbl = (nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP;
   const int p = blockIdx.x / nbl;
   const int g0 = (blockIdx.x % nbl) * GS_BDRAW_LOOP;
-  const int nM = A.nm[p];
+  const int nM = __builtin_amdgcn_readfirstlane(A.nm[p]);  // uniform: SGPR
   const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
   const int mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
   constexpr bool TL = GS_BDRAW_TILED && (BC == GS_BCAST_TILE || NFC == 0);
@@ -506,7 +506,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
         if (cur >= 0) __syncthreads();  // every wave is done with the previous block
         stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
         cur = p;
-        nM = A.nm[p];
+        nM = __builtin_amdgcn_readfirstlane(A.nm[p]);
         fi = lane < NF ? A.fidx[p * NF + lane] : 0;
         mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
       }
@@ -518,7 +518,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
   const int nbl = (nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP;
   const int p = blockIdx.x / nbl;
   const int g0 = (blockIdx.x % nbl) * GS_BDRAW_LOOP;
-  const int nM = A.nm[p];
+  const int nM = __builtin_amdgcn_readfirstlane(A.nm[p]);  // uniform: SGPR
   const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
   const int mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
   stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
@@ -755,7 +755,7 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
   const int p = blockIdx.x / nb;
   const int cblk = (blockIdx.x % nb) * CPB;
   const int c_own = cblk + wave;
-  const int nM = A.nm[p];
+  const int nM = __builtin_amdgcn_readfirstlane(A.nm[p]);  // uniform: SGPR
   int64_t mlds;
   if constexpr (BAL) {  // hand-off flags (the staging's barrier orders this before any use)
     if (threadIdx.x < NTRIO)

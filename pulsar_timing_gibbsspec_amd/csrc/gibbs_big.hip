@@ -57,7 +57,7 @@ __global__ __launch_bounds__(64 * BIG_WPB) void k_bdraw_big(BdrawArgs A, double*
   const int p = (int)(sys / A.n_chain), ch = (int)(sys % A.n_chain);
   if (A.chain_mask && A.chain_mask[A.mask_per_sys ? sys : (int64_t)ch] == 0) return;  // gate closed
   const int NF = A.NF, NMX = A.NMX, NT = NF / 16 + 1, LD = NF + 1;
-  const int nM = A.nm[p];
+  const int nM = __builtin_amdgcn_readfirstlane(A.nm[p]);  // uniform: SGPR
   double* ws = wsp + sys * ws_stride;
   double* scr = lds + wave * BIG_SCR;
   double* tb = scr;
