@@ -86,6 +86,17 @@ __device__ __forceinline__ ModelTiled model_tiled_view(const double* base, int N
   }
   return m;
 }
+// The view of a block staged with the pulsar's own layout (FX: the batch's NMX <= 16, all tiled);
+// returns the NMX the tile core indexes the block with.
+template <bool FX>
+__device__ __forceinline__ ModelTiled model_tiled_view_psr(const double* base, int NF, int NMX, int nM, int& NMXe) {
+  if (FX) {
+    NMXe = NMX;
+    return model_tiled_view<true>(base, NF, NMX);
+  }
+  NMXe = model_tiled_layout(NMX, nM);
+  return model_tiled_fix(NMXe) ? model_tiled_view<true>(base, NF, NMXe) : model_tiled_view<false>(base, NF, NMX);
+}
 
 __device__ __forceinline__ ModelLds model_view(const double* base, int NF, int NMX) {
   ModelLds m;
@@ -250,11 +261,14 @@ __device__ __forceinline__ void stage_model(double* lds, const double* g, int64_
 #ifndef GS_SWEEP_TILED
 #define GS_SWEEP_TILED 1
 #endif
+// NMX: the batch's fixed-column count (the row-major block's strides); the LDS layout is the
+// pulsar's own, model_tiled_layout(NMX, nM).
 __device__ void stage_model_tiled(double* __restrict__ L, const double* __restrict__ g, int NF, int NMX, int nM) {
-  const int NT = model_tiled_nt(NF), LD = NF + 1, nP = model_tiled_np(NMX);
-  const bool fixt = model_tiled_fix(NMX);
+  const int NML = model_tiled_layout(NMX, nM);
+  const int NT = model_tiled_nt(NF), LD = NF + 1, nP = model_tiled_np(NML);
+  const bool fixt = model_tiled_fix(NML);
   const int oG = (int)model_tiled_g_offset(NF), n = (int)model_tiled_doubles(NF, NMX);
-  const int oR = fixt ? (int)model_tiled_r_offset(NF, NMX) : n, oH = fixt ? (int)model_tiled_h_offset(NF, NMX) : n;
+  const int oR = fixt ? (int)model_tiled_r_offset(NF, NML) : n, oH = fixt ? (int)model_tiled_h_offset(NF, NML) : n;
   const double* S0 = g;  // NF x (NF + 1), column NF = dF
   const double* G = g + NF * LD + NF;
   const double* h = G + NMX * LD;
@@ -288,7 +302,7 @@ __device__ void stage_model_tiled(double* __restrict__ L, const double* __restri
       if (row < nM && mm < nM) v = R[row * NMX + mm];
     } else {
       const int k = idx - oH;
-      if (k < NMX) v = h[k];
+      if (k < NML) v = h[k];
     }
     L[idx] = v;
   }
@@ -378,7 +392,8 @@ __device__ __forceinline__ void bdraw_lnl_store(const BdrawArgs& A, int p, int64
 // systems the gate skips as well (likelihood mode on the already staged block: no second launch).
 template <int NFC, int NTC, int BC, bool LNLD = false, typename ModelT>
 __device__ __forceinline__ void bdraw_item(const BdrawArgs& A, const ModelT& M, int p, int c, int NF, int nM, int fi,
-                                           int mi, double* scr, int lane) {
+                                           int mi, double* scr, int lane, int NMXe = -1) {
+  if (NMXe < 0) NMXe = A.NMX;  // the NMX the block is indexed with (model_tiled_view_psr)
   const int64_t sys = (int64_t)p * A.n_chain + c;
   const bool shut = A.chain_mask && A.chain_mask[A.mask_per_sys ? sys : (int64_t)c] == 0;  // gate closed: keep b
   if constexpr (!LNLD) {
@@ -390,9 +405,9 @@ __device__ __forceinline__ void bdraw_item(const BdrawArgs& A, const ModelT& M, 
       double yy = 0.0, lp = 0.0;
       int fail;
       if constexpr (NFC == 0)
-        fail = bdraw_tile_n<NTC, 1, GS_BDRAW_PR>(M, A.NMX, nM, lane, phinv, 0.0, 0.0, yy, lp, scr, NF);
+        fail = bdraw_tile_n<NTC, 1, GS_BDRAW_PR>(M, NMXe, nM, lane, phinv, 0.0, 0.0, yy, lp, scr, NF);
       else
-        fail = bdraw_tile<NFC, 1, GS_BDRAW_PR>(M, A.NMX, nM, lane, phinv, 0.0, 0.0, yy, lp, scr);
+        fail = bdraw_tile<NFC, 1, GS_BDRAW_PR>(M, NMXe, nM, lane, phinv, 0.0, 0.0, yy, lp, scr);
       bdraw_lnl_store(A, p, sys, NF, lane, phinv, fail, yy, lp);
       return;
     }
@@ -406,7 +421,7 @@ __device__ __forceinline__ void bdraw_item(const BdrawArgs& A, const ModelT& M, 
                zM);
   }
   double bF = 0.0, bM = 0.0;
-  const int fail = bdraw_sys<NFC, NTC, BC, GS_BDRAW_PR, LNLD>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
+  const int fail = bdraw_sys<NFC, NTC, BC, GS_BDRAW_PR, LNLD>(M, NMXe, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
   if (!fail) {  // non-PD Sigma: the previous b stays (wave-uniform)
     if (lane < NF) A.b[sys * A.ldb + fi] = bF;
     if (lane < nM) A.b[sys * A.ldb + mi] = bM;
@@ -451,13 +466,11 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_bdraw(Bdraw
   using ModelT = typename std::conditional<TL, ModelTiled, ModelLds>::type;
   ModelT M;
   int64_t mlds;
+  int NMXe = A.NMX;
   if constexpr (TL) {
     stage_model_tiled(lds, A.model + (int64_t)p * A.mstride, NF, A.NMX, nM);
     mlds = model_tiled_doubles(NF, A.NMX);
-    if (model_tiled_fix(A.NMX))
-      M = model_tiled_view<true>(lds, NF, A.NMX);
-    else
-      M = model_tiled_view<false>(lds, NF, A.NMX);
+    M = model_tiled_view_psr<false>(lds, NF, A.NMX, nM, NMXe);
   } else {
     stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
     mlds = A.mstride;
@@ -468,7 +481,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_bdraw(Bdraw
   for (int r = 0; r < GS_BDRAW_LOOP; ++r) {
     const int c = (g0 + r) * WPB + wave;
     if (c >= A.n_chain) break;
-    bdraw_item<NFC, NTC, BC>(A, M, p, c, NF, nM, fi, mi, scr, lane);
+    bdraw_item<NFC, NTC, BC>(A, M, p, c, NF, nM, fi, mi, scr, lane, NMXe);
   }
 }
 
@@ -491,14 +504,14 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
   const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int nb = (A.n_chain + WPB - 1) / WPB;
   double* scr = lds + A.mstride + wave * gs_tile_scr(NF);
-  const ModelTiled M = model_tiled_view<FX>(lds, NF, A.NMX);
   if (A.persist) {
     // one round of workgroups (A.persist = CUs x resident workgroups per CU), workgroup w taking the
     // (pulsar, chain group) items [w n / G, (w + 1) n / G) in pulsar-major order: every workgroup
     // draws the same number of groups, restaging the model only where its range crosses a pulsar
     const int64_t n_items = (int64_t)A.n_psr * nb;
     const int64_t lo = (int64_t)blockIdx.x * n_items / A.persist, hi = (int64_t)(blockIdx.x + 1) * n_items / A.persist;
-    int cur = -1, nM = 0, fi = 0, mi = 0;
+    int cur = -1, nM = 0, fi = 0, mi = 0, NMXe = A.NMX;
+    ModelTiled M;
 #pragma unroll 1
     for (int64_t it = lo; it < hi; ++it) {
       const int p = (int)(it / nb), grp = (int)(it % nb);
@@ -509,9 +522,10 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
         nM = __builtin_amdgcn_readfirstlane(A.nm[p]);
         fi = lane < NF ? A.fidx[p * NF + lane] : 0;
         mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
+        M = model_tiled_view_psr<FX>(lds, NF, A.NMX, nM, NMXe);
       }
       const int c = grp * WPB + wave;
-      if (c < A.n_chain) bdraw_item<NFC, NTC, GS_BCAST_TILE, LNLD>(A, M, p, c, NF, nM, fi, mi, scr, lane);
+      if (c < A.n_chain) bdraw_item<NFC, NTC, GS_BCAST_TILE, LNLD>(A, M, p, c, NF, nM, fi, mi, scr, lane, NMXe);
     }
     return;
   }
@@ -522,11 +536,13 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
   const int fi = lane < NF ? A.fidx[p * NF + lane] : 0;
   const int mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
   stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+  int NMXe;
+  const ModelTiled M = model_tiled_view_psr<FX>(lds, NF, A.NMX, nM, NMXe);
 #pragma unroll 1
   for (int r = 0; r < GS_BDRAW_LOOP; ++r) {
     const int c = (g0 + r) * WPB + wave;
     if (c >= A.n_chain) break;
-    bdraw_item<NFC, NTC, GS_BCAST_TILE, LNLD>(A, M, p, c, NF, nM, fi, mi, scr, lane);
+    bdraw_item<NFC, NTC, GS_BCAST_TILE, LNLD>(A, M, p, c, NF, nM, fi, mi, scr, lane, NMXe);
   }
 }
 
@@ -772,8 +788,9 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
   if (c_own >= A.n_chain) return;  // (then no extra chain either: 12 + e > wave)
   using ModelT = typename std::conditional<TL, ModelTiled, ModelLds>::type;
   ModelT M;
+  int NMXe = A.NMX;  // the NMX the staged block is indexed with (its own layout, model_tiled_view_psr)
   if constexpr (TL) {
-    M = model_tiled_view<FX>(lds, NF, A.NMX);
+    M = model_tiled_view_psr<FX>(lds, NF, A.NMX, nM, NMXe);
   } else {
     M = model_view(lds, NF, A.NMX);
   }
@@ -957,7 +974,7 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
       // previous b waits in the wave's LDS save slot, not in 4 VGPRs across the draw.
       bsave[lane] = bF;
       bsave[64 + lane] = bM;
-      const int f = bdraw_sys<NFC, NTC, BC, true>(M, A.NMX, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
+      const int f = bdraw_sys<NFC, NTC, BC, true>(M, NMXe, nM, lane, phinv, zF, zM, bF, bM, scr, NF);
       if (f) {
         gtile::lds_fence();
         bF = bsave[lane];

@@ -53,10 +53,18 @@ __host__ __device__ inline int64_t model_tiled_h_offset(int NF, int NMX) {
 // block past the LDS budget of 3 workgroups per CU (nm = 17 in configs[2]/[3]: 43 KB tiled vs
 // 30 KB S' + row-major G/h/R).
 __host__ __device__ inline bool model_tiled_fix(int NMX) { return NMX <= 16; }
+// The fixed-block layout of ONE pulsar's block in a batch with NMX columns at most: a pulsar with
+// nM <= 16 takes the tiled fixed block of a 16-column model even when NMX > 16 (configs[2]/[3]: 43
+// of the 45 pulsars have nM <= 16, two have 17), so only the pulsars that need it read G and R
+// row-major.  The block size covers both layouts.
+__host__ __device__ inline int model_tiled_layout(int NMX, int nM) { return NMX <= 16 ? NMX : (nM <= 16 ? 16 : NMX); }
 __host__ __device__ inline int64_t model_tiled_doubles(int NF, int NMX) {
-  if (model_tiled_fix(NMX)) return model_tiled_h_offset(NF, NMX) + ((NMX + 1) & ~1);
+  const int nf = NMX <= 16 ? NMX : 16;
+  const int64_t fix = model_tiled_h_offset(NF, nf) + ((nf + 1) & ~1);
+  if (model_tiled_fix(NMX)) return fix;
   const int64_t n = model_tiled_g_offset(NF) + (int64_t)NMX * (NF + 1) + NMX + (int64_t)NMX * NMX;
-  return (n + 1) & ~int64_t(1);
+  const int64_t rm = (n + 1) & ~int64_t(1);
+  return rm > fix ? rm : fix;
 }
 
 // gs_prefix / gs_prefix_sys / gs_prefix_dd (gibbs_prefix.hip)
