@@ -69,11 +69,12 @@ enum {
   GS_OPT_GRID_EXACT = 4, /* grid conditionals: 1 = numpy's operation order (sequential product
                          of per-pulsar pdfs, sequential cumsum: bit-identical pdfs); 2 = the f64
                          wave kernels (log-space product, one rcp per four ratios, short exp:
-                         pdfs equal to ~1e-15 relative); 0 (default) = as 2, except gs_rho_red:
-                         every point in f32 with a per-row error certificate, rows whose index
-                         the certificate cannot prove redone in f64 (indices of exact
-                         arithmetic, as 2's), 16 lanes per row; 3 = as 0 with the round-3
-                         certified kernel (64 lanes per row, one compare per point) */
+                         pdfs equal to ~1e-15 relative); 0 (default) = as 2, except gs_rho_red
+                         and gs_rho_curn_sum (ngrid <= 1024): every point in f32 with a per-row
+                         error certificate, rows whose index the certificate cannot prove redone
+                         with 2's f64 arithmetic (indices of exact arithmetic, as 2's), 16 lanes
+                         per row; 3 = as 0 with the round-3 certified red kernel (64 lanes per
+                         row, one compare per point) and 2's CURN-from-sums kernel */
   GS_OPT_BREC_CHAINS = 5, /* gs_sweep_freespec b_rec: 0 (default) = every system, row
                          sweep * n_psr * n_chain + p * n_chain + c; K > 0 = chains c < K of
                          each pulsar only, compact rows (sweep * n_psr + p) * K + c (the
@@ -156,8 +157,8 @@ int gs_ctx_set_grid_fallback_counter(gs_ctx* ctx, int32_t* counter);
    writes lnl[p * n_chain + c] for every system -- gs_lnlike_marg's value at the same phiinv_F, bit
    for bit (the same factorisation; the model constants aux[2] from the row-major gs_prefix blocks
    `model`, one per pulsar); a system whose chain_mask entry is 0 keeps its b and still gets its
-   lnl (the likelihood-mode factorisation on the already staged block).  The PTA red-noise Metropolis block starts from these
-   (pta_gibbs.py:689-704: the gated draw at the end of a sweep factorises exactly the systems the
+   lnl (the likelihood-mode factorisation on the already staged block).  The PTA red-noise
+   Metropolis block starts from these (pta_gibbs.py:689-704: the gated draw at the end of a sweep factorises exactly the systems the
    next sweep's block starts from), instead of re-factorising every (pulsar, chain).  gs_bdraw /
    gs_bdraw_sys refuse to run while it is attached. */
 int gs_ctx_set_bdraw_lnl(gs_ctx* ctx, double* lnl, const double* model);
