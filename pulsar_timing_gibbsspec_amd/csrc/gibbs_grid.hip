@@ -512,13 +512,19 @@ __global__ __launch_bounds__(256, GS_CF_MINW) void k_rho_curn_fast(GridArgs A) {
     }
   }
   constexpr double LN2 = 0.693147180559945309417232121458176568;
-  double lp[CF_MAXG];
+  // pdf_g = 2^-ex / dd e^(-N / 2D): with y = 1 / dd = fr 2^e (frexp, exact), pdf_g = fr e^(lp_g) and
+  // lp_g = (e - ex) ln2 - nn y / 2 -- no log per point (round 3 took -log dd: ~25 more f64 ops)
+  double lp[CF_MAXG], fr[CF_MAXG];
   double mx = -__builtin_inf();
 #pragma unroll
   for (int j = 0; j < CF_MAXG; ++j) {
     lp[j] = -__builtin_inf();
+    fr[j] = 0.0;
     if (j < G && g0 + j < A.ngrid) {
-      lp[j] = -(gs_log_pos(dd[j]) + ex * LN2) - 0.5 * (nn[j] * rcp_nr2(dd[j]));
+      const double y = rcp_nr2(dd[j]);
+      int e;
+      fr[j] = frexp(y, &e);
+      lp[j] = fma((double)(e - ex), LN2, -0.5 * (nn[j] * y));
       mx = fmax(mx, lp[j]);
     }
   }
@@ -528,7 +534,7 @@ __global__ __launch_bounds__(256, GS_CF_MINW) void k_rho_curn_fast(GridArgs A) {
 #pragma unroll
   for (int j = 0; j < CF_MAXG; ++j) {
     if (j < G) {
-      loc += gs_exp_neg(lp[j] - mx);
+      loc += fr[j] * gs_exp_neg(lp[j] - mx);
       lp[j] = loc;
     }
   }
@@ -547,10 +553,12 @@ __global__ __launch_bounds__(256, GS_CF_MINW) void k_rho_curn_fast(GridArgs A) {
     double u2;
     gs_uniform2(gs_counter(k, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, 0, GS_EV_CURN), A.key, u, u2);
   }
+  // searchsorted(cdf / total, u): cdf < u total - (the lane offset), no division per point
+  const double thr = u * total - off;
   int cnt = 0;
 #pragma unroll
   for (int j = 0; j < CF_MAXG; ++j)
-    if (j < G && g0 + j < A.ngrid) cnt += ((off + lp[j]) / total < u) ? 1 : 0;
+    if (j < G && g0 + j < A.ngrid) cnt += (lp[j] < thr) ? 1 : 0;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
   if (lane == 0) {
