@@ -426,7 +426,7 @@ __global__ __launch_bounds__(256) void k_rho_curn_sum_wave(GridArgs A) {
 // so lane q computes group q's once per row and every grid point evaluates them by Horner
 // (CF_K + CF_K - 1 FMAs), then N <- N D_grp + D N_grp, D <- D D_grp: 2 CF_K + 2 f64 ops per
 // (point, group), 2.5 per (point, pulsar) at CF_K = 4 instead of 4 (add, two multiplies and an
-// FMA per pulsar).  D and N are rescaled together every CF_RN groups by one power of two per
+// FMA per pulsar).  D and N are rescaled together every RN groups by one power of two per
 // lane (the lane's 16 neighbouring grid points keep D within a few decades of each other).  One
 // log, one division and one exp per grid point at the end.  pdf rounding differs from numpy's
 // by ~1e-15 relative, so the index can only differ when u falls that close to a cdf value
@@ -434,13 +434,38 @@ __global__ __launch_bounds__(256) void k_rho_curn_sum_wave(GridArgs A) {
 // rows).  One wavefront per row, lane l owns grid points [l G, (l+1) G), wave scan of the lane
 // sums.
 constexpr int CF_MAXG = 16;  // grid points per lane (ngrid <= 1024)
-constexpr int CF_K = 4;      // pulsars per coefficient group
-constexpr int CF_RN = 2;     // groups between rescalings: (2 rho_min)^(CF_K CF_RN) must stay normal
 
 #ifndef GS_CF_MINW
 #define GS_CF_MINW 3
 #endif
+// Group coefficients handed from lane q to the whole wave through the wave's LDS slot (one
+// broadcast ds_read per coefficient pair, LDS pipe) instead of two v_readlane_b32 per coefficient
+// (VALU: ~9 issue cycles each on MI355X, tools/probe/mfma_probe.hip -- 18 per group, a fifth of
+// the group's VALU time at CF_K = 4).
+#ifndef GS_CF_LDS
+#define GS_CF_LDS 1
+#endif
+// CF_K = 5 for pulsar counts where it needs fewer groups x ops (45 = 9 x 5: 108 f64 ops per grid
+// point instead of 12 groups x 10 = 120), else 4; GS_CF_AUTOK=0 keeps 4.
+#ifndef GS_CF_AUTOK
+#define GS_CF_AUTOK 1
+#endif
+// The tail's exp by Tang's 64-entry table (exp_neg_t64, 12 f64 instructions + one LDS read) instead
+// of gs_exp_neg's degree-11 polynomial (17, and 2 v_mov_b32 per f64 coefficient at this pressure)
+#ifndef GS_CF_TEXP
+#define GS_CF_TEXP 1
+#endif
+template <int CF_K>
 __global__ __launch_bounds__(256, GS_CF_MINW) void k_rho_curn_fast(GridArgs A) {
+  constexpr int CS = 2 * CF_K + 2;  // LDS doubles per group (even: pairs stay 16-byte aligned)
+#if GS_CF_LDS
+  __shared__ __attribute__((aligned(16))) double cfl[4][64 * CS];
+#endif
+#if GS_CF_TEXP
+  __shared__ double etb[64];
+  if (threadIdx.x < 64) etb[threadIdx.x] = GS_EXP2_64[threadIdx.x];
+  __syncthreads();
+#endif
   const int wave = gs_wave_id(), lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + wave;
   const int64_t nrow = (int64_t)A.n_f * A.n_chain;
@@ -449,17 +474,25 @@ __global__ __launch_bounds__(256, GS_CF_MINW) void k_rho_curn_fast(GridArgs A) {
   const int G = (A.ngrid + 63) / 64;
   const int g0 = lane * G;
   double rg[CF_MAXG], dd[CF_MAXG], nn[CF_MAXG];
+  double rmin = 1e300;
 #pragma unroll
   for (int j = 0; j < CF_MAXG; ++j) {
     const int g = min(g0 + j, A.ngrid - 1);
     rg[j] = A.grid3[g];
+    rmin = fmin(rmin, rg[j]);
     dd[j] = 1.0;
     nn[j] = 0.0;
   }
+  // D and N are rescaled every RN groups: (2 rho_min)^(CF_K RN) must stay normal.  RN = 2 (one
+  // rescale per 2 CF_K pulsars) for rho_min >= 1e-30 (CF_K = 5; 1e-38 at CF_K = 4: every prior
+  // box of the reference's examples), else every group (rho_min down to ~1e-61).
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) rmin = fmin(rmin, __shfl_xor(rmin, o));
+  const int RN = __builtin_amdgcn_readfirstlane((int)(rmin >= (CF_K == 4 ? 1e-38 : 1e-30)) + 1);
   int ex = 0;  // the lane's common binary exponent of dd (and nn)
   const int P = A.n_psr;
-  // 64 groups (256 pulsars) at a time: lane q builds group q's coefficients from its pulsars'
-  // (tau, irn), ascending powers: D_grp = sum_e pc[e] rho^e, N_grp = sum_e qc[e] rho^e
+  // 64 groups (64 CF_K pulsars) at a time: lane q builds group q's coefficients from its
+  // pulsars' (tau, irn), ascending powers: D_grp = sum_e pc[e] rho^e, N_grp = sum_e qc[e] rho^e
   for (int p0 = 0; p0 < P; p0 += 64 * CF_K) {
     const int ng = min(64, (P - p0 + CF_K - 1) / CF_K);
     double pc[CF_K + 1], qc[CF_K];
@@ -482,12 +515,37 @@ __global__ __launch_bounds__(256, GS_CF_MINW) void k_rho_curn_fast(GridArgs A) {
         }
       }
     }
+#if GS_CF_LDS
+    double* cw = cfl[wave];
+    if (lane < ng) {
+#pragma unroll
+      for (int e = 0; e <= CF_K; ++e) cw[lane * CS + e] = pc[e];
+#pragma unroll
+      for (int e = 0; e < CF_K; ++e) cw[lane * CS + CF_K + 1 + e] = qc[e];
+    }
+    wave_lds_sync();
+#endif
     for (int q = 0; q < ng; ++q) {
       double a[CF_K + 1], b[CF_K];
+#if GS_CF_LDS
+      const double2* cq = reinterpret_cast<const double2*>(cw + q * CS);
+      double co[CS];
+#pragma unroll
+      for (int e = 0; e < CS / 2; ++e) {
+        const double2 v = cq[e];
+        co[2 * e] = v.x;
+        co[2 * e + 1] = v.y;
+      }
+#pragma unroll
+      for (int e = 0; e <= CF_K; ++e) a[e] = co[e];
+#pragma unroll
+      for (int e = 0; e < CF_K; ++e) b[e] = co[CF_K + 1 + e];
+#else
 #pragma unroll
       for (int e = 0; e <= CF_K; ++e) a[e] = rdlane(pc[e], q);
 #pragma unroll
       for (int e = 0; e < CF_K; ++e) b[e] = rdlane(qc[e], q);
+#endif
 #pragma unroll
       for (int j = 0; j < CF_MAXG; ++j) {
         const double x = rg[j];
@@ -497,10 +555,12 @@ __global__ __launch_bounds__(256, GS_CF_MINW) void k_rho_curn_fast(GridArgs A) {
         double qn = fma(b[CF_K - 1], x, b[CF_K - 2]);
 #pragma unroll
         for (int e = CF_K - 3; e >= 0; --e) qn = fma(qn, x, b[e]);
-        nn[j] = fma(nn[j], pd, dd[j] * qn);
+        // N pd (a multiply into N's own register) + D qn (v_fmac onto it): no register copy
+        // per point (fma(N, pd, D qn) tied the v_fmac to the D qn temporary: one v_mov_b64 more)
+        nn[j] = fma(dd[j], qn, nn[j] * pd);
         dd[j] *= pd;
       }
-      if ((q % CF_RN) == CF_RN - 1 || q == ng - 1) {
+      if ((q % RN) == RN - 1 || q == ng - 1) {
         const int e = __builtin_amdgcn_frexp_exp(dd[0]);
         ex += e;
 #pragma unroll
@@ -510,6 +570,9 @@ __global__ __launch_bounds__(256, GS_CF_MINW) void k_rho_curn_fast(GridArgs A) {
         }
       }
     }
+#if GS_CF_LDS
+    wave_lds_sync();  // the next 64-group block rewrites the slot
+#endif
   }
   constexpr double LN2 = 0.693147180559945309417232121458176568;
   // pdf_g = 2^-ex / dd e^(-N / 2D): with y = 1 / dd = fr 2^e (frexp, exact), pdf_g = fr e^(lp_g) and
@@ -534,7 +597,11 @@ __global__ __launch_bounds__(256, GS_CF_MINW) void k_rho_curn_fast(GridArgs A) {
 #pragma unroll
   for (int j = 0; j < CF_MAXG; ++j) {
     if (j < G) {
+#if GS_CF_TEXP
+      loc += fr[j] * exp_neg_t64s(lp[j] - mx, etb);
+#else
       loc += fr[j] * gs_exp_neg(lp[j] - mx);
+#endif
       lp[j] = loc;
     }
   }
@@ -1469,7 +1536,12 @@ int launch_rho_curn(hipStream_t s, const GridArgs& a) {
   const int64_t n = (int64_t)a.n_f * a.n_chain;
   if (n == 0) return 0;
   if (a.exact != 1 && a.ngrid <= 64 * CF_MAXG) {
-    hipLaunchKernelGGL(k_rho_curn_fast, grid1(n, 4), dim3(256), 0, s, a);
+    // CF_K = 5 where ceil(P / 5) groups of 12 ops beat ceil(P / 4) groups of 10 per grid point
+    const int p4 = (a.n_psr + 3) / 4 * 10, p5 = (a.n_psr + 4) / 5 * 12;
+    if (GS_CF_AUTOK && p5 < p4)
+      hipLaunchKernelGGL(k_rho_curn_fast<5>, grid1(n, 4), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(k_rho_curn_fast<4>, grid1(n, 4), dim3(256), 0, s, a);
     return 0;
   }
   const size_t lds = (size_t)GS_CURN_WPB * a.ngrid * sizeof(double);

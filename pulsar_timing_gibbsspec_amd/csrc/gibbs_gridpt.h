@@ -43,6 +43,31 @@ __device__ __forceinline__ double exp_neg_t64(double x, const double* __restrict
   return fma(T, em1, T) * __hiloint2double(((ni >> 6) + 1023) << 20, 0);
 }
 
+// f64 constant held in an SGPR pair (two s_mov_b32, scalar issue) for a VOP3 operand: gfx950's
+// VOP3 f64 ops take no literal, and under VGPR pressure the compiler rematerialises each use as
+// two v_mov_b32 (VALU issue)
+__device__ __forceinline__ double gs_sconst(double v) {
+  asm("" : "+s"(v));
+  return v;
+}
+
+// exp_neg_t64 with its coefficients in SGPRs (the same arithmetic, bit-identical results)
+__device__ __forceinline__ double exp_neg_t64s(double x, const double* __restrict__ tb) {
+  x = fmax(x, -708.0);
+  const double t = fma(x, gs_sconst(0x1.71547652b82fep+6), gs_sconst(0x1.8p52));
+  const double n = t - gs_sconst(0x1.8p52);
+  double r = fma(n, gs_sconst(-0x1.62e42fefa39efp-7), x);
+  r = fma(n, gs_sconst(-0x1.abc9e3b39803fp-62), r);
+  double q = fma(r, gs_sconst(0x1.1111111111111p-7), gs_sconst(0x1.5555555555555p-5));
+  q = fma(r, q, gs_sconst(0x1.5555555555555p-3));
+  q = fma(r, q, 0.5);
+  q = fma(r, q, 1.0);
+  const double em1 = r * q;
+  const int ni = (int)(unsigned)__double_as_longlong(t);
+  const double T = tb[ni & 63];
+  return fma(T, em1, T) * __hiloint2double(((ni >> 6) + 1023) << 20, 0);
+}
+
 // One lane's G consecutive grid points of one row: h = (tau/2) / (gw + rho_g) with four
 // reciprocals from one (R = 1/(a0 a1 a2 a3), 1/(a0 a1) = a2 a3 R, 1/a0 = a1 / (a0 a1), ...: one
 // v_rcp_f64 + Newton steps per four points), pdf' = h exp(-h); cum[j] = the lane's running

@@ -44,7 +44,8 @@ HOT = [
     ("k_rho_red_waveE", 4, 0),                     # CURN + red grid CDF (f64 wave kernel)
     ("k_rho_red_certE", 4, 0),                     # CURN + red grid CDF (round-3 certified f32)
     ("k_rho_red_cert16E", 3, 0),                   # ... the default since round 4 (16 lanes per row)
-    ("k_rho_curn_fastE", 3, 0),                    # 0.60 -> 0.53 ms at 3 waves/SIMD (round 3)
+    ("k_rho_curn_fastILi5EE", 3, 0),               # 0.60 -> 0.53 ms at 3 waves/SIMD (round 3); CF_K = 5
+    ("k_rho_curn_fastILi4EE", 3, 0),               # (configs[3]'s 45 pulsars) and 4, coefficients via LDS
     ("k_rho_curn_sum_waveILi16EE", 2, 0),
     ("k_white_syrkILi14EE", 2, 0),                 # configs[4] per-chain TNT (m = 216)
     ("k_tntEPK", 4, 0),                            # TNT / d, compensated block sums
