@@ -672,71 +672,90 @@ __global__ __launch_bounds__(64, 2) void k_hyper_mh(HyperMhArgs A) {
   const double sig = 0.05 * A.n_h;  // sigmas = 0.05 * len(hind)
   const long long chain = A.chain_base + c;
   const long long sw = gs_sweep(A.sweep, A.sweep_dev);
+  // The proposals do not depend on the chain state: lane l draws step s0 + l's (scale, parameter,
+  // normal, log u) for 64 steps at once into the wave's step table (3 Philox blocks per lane in
+  // parallel instead of 3 wave-uniform blocks on the critical path of every step).
+  double* stab = scr + gs_tile_scr(NF);
   int nacc = 0;
-  for (int st = 0; st < A.nsteps; ++st) {
-    double sc, z, u;
-    int j;
-    if (A.inj) {
-      const double* q = A.inj + ((int64_t)st * A.n_chain + c) * 4;
-      sc = q[0];
-      j = (int)q[1];
-      z = q[2];
-      u = q[3];
-    } else {
-      double u1, u2, v1, v2, u4;
-      gs_uniform2(gs_counter(3u * st, sw, chain, 0, GS_EV_HYPER), A.key, u1, u2);
-      gs_normal2(gs_counter(3u * st + 1, sw, chain, 0, GS_EV_HYPER), A.key, v1, v2);
-      gs_uniform2(gs_counter(3u * st + 2, sw, chain, 0, GS_EV_HYPER), A.key, u, u4);
-      sc = gs_mh_scale(u1);
-      j = min((int)(u2 * A.n_h), A.n_h - 1);
-      z = v1;
-    }
-    const int col = A.hcol[j], p = A.hpsr[j];
-    // q[par] += randn * sigmas * scale, rounded as numpy does (no fma contraction)
-    const double xq = gs_add_rn(xs[col], gs_mul_rn(gs_mul_rn(z, sig), sc));
-    bool accepted = false;
-    if (xq >= A.hlo[j] && xq <= A.hhi[j]) {  // uniform prior: -inf outside (:298, :624-628)
-      double red;
-      if (A.red_kind == 0) {  // free spectrum: phi_red = 10^(2 rho_red)
-        const int rc = A.red_col[p * n_f + kf];
-        red = pow(10.0, 2.0 * (rc == col ? xq : xs[rc]));
-      } else {                // power law: log phi_red = (a log10_A + c) + g gamma
-        const int ca = A.pl_col[2 * p], cg = A.pl_col[2 * p + 1];
-        const double la = ca == col ? xq : xs[ca], ga = cg == col ? xq : xs[cg];
-        const double* L = A.lnphi + (int64_t)p * 3 * n_f;
-        red = exp(gs_add_rn(gs_add_rn(gs_mul_rn(L[n_f + kf], la), L[kf]), gs_mul_rn(L[2 * n_f + kf], ga)));
+  for (int s0 = 0; s0 < A.nsteps; s0 += 64) {
+    const int ns = min(64, A.nsteps - s0);
+    if (lane < ns) {
+      const int st = s0 + lane;
+      double sc, z, u;
+      int j;
+      if (A.inj) {
+        const double* q = A.inj + ((int64_t)st * A.n_chain + c) * 4;
+        sc = q[0];
+        j = (int)q[1];
+        z = q[2];
+        u = q[3];
+      } else {
+        double u1, u2, v1, v2, u4;
+        gs_uniform2(gs_counter(3u * st, sw, chain, 0, GS_EV_HYPER), A.key, u1, u2);
+        gs_normal2(gs_counter(3u * st + 1, sw, chain, 0, GS_EV_HYPER), A.key, v1, v2);
+        gs_uniform2(gs_counter(3u * st + 2, sw, chain, 0, GS_EV_HYPER), A.key, u, u4);
+        sc = gs_mh_scale(u1);
+        j = min((int)(u2 * A.n_h), A.n_h - 1);
+        z = v1;
       }
-      const double phinv = act ? 1.0 / (gw + red) : 1.0;
-      const double* mb = A.model + (int64_t)p * A.mstride;
-      const ModelLds M = model_view(mb, NF, A.NMX);
-      double yy = 0.0, ldS = 0.0;
-      int fail;
-      if constexpr (NFC == 0)
-        fail = bdraw_tile_n<NTC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr, NF);
-      else
-        fail = bdraw_tile<NFC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr);
-      double lph = act ? log(phinv) : 0.0;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) lph += __shfl_xor(lph, o);
-      const int64_t ao = model_aux_offset(NF, A.NMX);
-      const double L1 = fail ? -__builtin_inf() : 0.5 * (mb[ao + 1] + yy - 2.0 * mb[ao] - ldS) + 0.5 * lph;
-      const double diff = L1 - Ls[p];
-      if (diff > log(u)) {
-        accepted = true;
-        ++nacc;
-        if (lane == 0) {
-          xs[col] = xq;
-          Ls[p] = L1;
+      stab[4 * lane] = sc;
+      stab[4 * lane + 1] = (double)j;
+      stab[4 * lane + 2] = z;
+      stab[4 * lane + 3] = log(u);
+    }
+    wave_lds_sync();
+    for (int i = 0; i < ns; ++i) {
+      const int st = s0 + i;
+      const double sc = stab[4 * i], z = stab[4 * i + 2], lu = stab[4 * i + 3];
+      const int j = __builtin_amdgcn_readfirstlane((int)stab[4 * i + 1]);
+      const int col = A.hcol[j], p = A.hpsr[j];
+      // q[par] += randn * sigmas * scale, rounded as numpy does (no fma contraction)
+      const double xq = gs_add_rn(xs[col], gs_mul_rn(gs_mul_rn(z, sig), sc));
+      bool accepted = false;
+      if (xq >= A.hlo[j] && xq <= A.hhi[j]) {  // uniform prior: -inf outside (:298, :624-628)
+        double red;
+        if (A.red_kind == 0) {  // free spectrum: phi_red = 10^(2 rho_red)
+          const int rc = A.red_col[p * n_f + kf];
+          red = pow(10.0, 2.0 * (rc == col ? xq : xs[rc]));
+        } else {                // power law: log phi_red = (a log10_A + c) + g gamma
+          const int ca = A.pl_col[2 * p], cg = A.pl_col[2 * p + 1];
+          const double la = ca == col ? xq : xs[ca], ga = cg == col ? xq : xs[cg];
+          const double* L = A.lnphi + (int64_t)p * 3 * n_f;
+          red = exp(gs_add_rn(gs_add_rn(gs_mul_rn(L[n_f + kf], la), L[kf]), gs_mul_rn(L[2 * n_f + kf], ga)));
         }
+        const double phinv = act ? 1.0 / (gw + red) : 1.0;
+        const double* mb = A.model + (int64_t)p * A.mstride;
+        const ModelLds M = model_view(mb, NF, A.NMX);
+        double yy = 0.0, ldS = 0.0;
+        int fail;
+        if constexpr (NFC == 0)
+          fail = bdraw_tile_n<NTC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr, NF);
+        else
+          fail = bdraw_tile<NFC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr);
+        double lph = act ? log(phinv) : 0.0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) lph += __shfl_xor(lph, o);
+        const int64_t ao = model_aux_offset(NF, A.NMX);
+        const double L1 = fail ? -__builtin_inf() : 0.5 * (mb[ao + 1] + yy - 2.0 * mb[ao] - ldS) + 0.5 * lph;
+        const double diff = L1 - Ls[p];
+        if (diff > lu) {
+          accepted = true;
+          ++nacc;
+          if (lane == 0) {
+            xs[col] = xq;
+            Ls[p] = L1;
+          }
+        }
+        wave_lds_sync();
       }
-      wave_lds_sync();
+      if (A.q_rec && lane == 0) {
+        double* qr = A.q_rec + ((int64_t)st * A.n_chain + c) * 3;
+        qr[0] = (double)j;
+        qr[1] = xq;
+        qr[2] = accepted ? 1.0 : 0.0;
+      }
     }
-    if (A.q_rec && lane == 0) {
-      double* qr = A.q_rec + ((int64_t)st * A.n_chain + c) * 3;
-      qr[0] = (double)j;
-      qr[1] = xq;
-      qr[2] = accepted ? 1.0 : 0.0;
-    }
+    wave_lds_sync();  // the next 64 steps rewrite the table
   }
   for (int i = lane; i < A.ldx; i += 64) xg[i] = xs[i];
   for (int p = lane; p < A.n_psr; p += 64) A.lnl_p[(int64_t)p * A.n_chain + c] = Ls[p];
@@ -1138,7 +1157,8 @@ int launch_lnlike_marg(hipStream_t s, const LnlArgs& a) {
 
 int launch_hyper_mh(hipStream_t s, const HyperMhArgs& a) {
   if (a.n_chain == 0) return 0;
-  const size_t lds = ((size_t)((a.ldx + a.n_psr + 1) & ~1) + gs_tile_scr(a.NF)) * sizeof(double);
+  // x row, lnL_p, tile scratch, the 64-step proposal table
+  const size_t lds = ((size_t)((a.ldx + a.n_psr + 1) & ~1) + gs_tile_scr(a.NF) + 4 * 64) * sizeof(double);
   dim3 grid((unsigned)a.n_chain);
 #define GS_HY_LAUNCH(NFC, NTC)                                                   \
   if (lds > 65536 && set_lds(k_hyper_mh<NFC, NTC>, lds)) return 2;               \

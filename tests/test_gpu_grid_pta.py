@@ -581,20 +581,22 @@ def test_red_grid_certified_grid_sizes(ctx, request, ngrid):
     assert np.array_equal(out[0][1], out[2][1])
 
 
-@pytest.mark.parametrize("with_red", [True, False])
-def test_curn_fast_matches_numpy_order_on_random_rows(ctx, request, with_red):
+@pytest.mark.parametrize("with_red,P,lo", [(True, 45, 1e-18), (False, 45, 1e-18), (True, 12, 1e-18),
+                                            (True, 45, 1e-34)])
+def test_curn_fast_matches_numpy_order_on_random_rows(ctx, request, with_red, P, lo):
     """The default CURN draw (k_rho_curn_fast: grouped-polynomial N / D product, log-space pdf)
-    against numpy's operation order (GS_OPT_GRID_EXACT = 1) on 7680 random rows of 45 pulsars
+    against numpy's operation order (GS_OPT_GRID_EXACT = 1) on random rows of P pulsars
     whose tau follows each row's own rho (ratio / 2 ~ Exp(1) at rho_true, so the product over
     pulsars stays representable as in a real chain), with and without per-pulsar red noise
     spanning 9 decades: the same index on every row (pdfs agree to ~1e-15 relative, so a row could
-    only differ if u fell that close to a cdf value)."""
+    only differ if u fell that close to a cdf value).  P = 45 takes 5-pulsar coefficient groups,
+    P = 12 4-pulsar groups; a grid down to rho = 1e-34 (< 1e-30) rescales after every group."""
     from pulsar_timing_gibbsspec_amd import _lib
     from pulsar_timing_gibbsspec_amd.engine import grid3
     request.addfinalizer(lambda: ctx.lib.gs_ctx_set_option(ctx.handle, _lib.OPT_GRID_EXACT, 0))
-    rng = np.random.default_rng(5 + with_red)
-    P, n_f, C = 45, 30, 256
-    lo, hi = 1e-18, 1e-8
+    rng = np.random.default_rng(5 + with_red + P)
+    n_f, C = 30, 256
+    hi = 1e-8
     rho_true = 10 ** rng.uniform(-16, -9, (1, n_f, C))
     irn = 10 ** rng.uniform(-18, -9, (P, n_f, C)) if with_red else np.zeros((P, n_f, C))
     tau = (irn + rho_true) * rng.exponential(2.0, (P, n_f, C))
@@ -614,7 +616,7 @@ def test_curn_fast_matches_numpy_order_on_random_rows(ctx, request, with_red):
     bad = np.nonzero(out[0] != out[1])[0]
     assert bad.size == 0, (bad.size, bad[:8].tolist(), out[0][bad[:8]].tolist(), out[1][bad[:8]].tolist())
     # the draws are spread over the grid, not piled on one end
-    assert len(np.unique(out[1])) > 200
+    assert len(np.unique(out[1])) > 150
 
 
 @pytest.mark.parametrize("phi_shared,masked,nf,small_nm", [(False, False, 60, False), (True, True, 60, False),
