@@ -136,6 +136,20 @@ def grid_peak():
 SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 
+def simd_issue(launch_s, draws, valu=1459, mfma=64, valu_cycles=4.5):
+    """The headline kernel against the SIMD's issue capacity: on MI355X an f64 MFMA (64 cycles) does
+    not overlap the SIMD's VALU (tools/probe/mfma_probe.hip, profiles/r04o/mfma_probe.txt), so a draw
+    costs at least its VALU issue cycles + 64 per f64 MFMA.  Per-draw instruction counts from the SQ
+    counters of profiles/r03t (SQ_INSTS_VALU / SQ_INSTS_MFMA per draw); ~4.5 SIMD cycles per VALU
+    instruction (f64 FMA ~5, 32-bit ~2.5, profiles/valu_rate.json)."""
+    cyc = launch_s * 2.4e9 * 1024 / draws
+    need = valu * valu_cycles + mfma * 64
+    return {"simd_cycles_per_draw": cyc, "valu_per_draw": valu, "mfma_per_draw": mfma,
+            "issue_cycles_per_draw": need, "frac": need / cyc,
+            "note": "fraction of the SIMD time a draw's instructions need to issue (MFMA and VALU serialise "
+                    "on MI355X); the rest is dependency wait nobody fills"}
+
+
 def valu_roof(plain, transc):
     """Units/s the whole chip can issue when one unit needs `plain` 4-cycle and `transc` 8-cycle
     lane operations (the grid kernels' stated minimal op counts)."""
@@ -911,7 +925,8 @@ def main():
                          "alg_flops_per_launch": alg_flops_launch,
                          "note": "achieved = SURVEY 8d's algorithmic flops (dense m=76 potrf + 3 solves); the kernel "
                                  "executes fewer (executed_*: NF=60 Schur block after the fixed-prior prefix)",
-                         "executed_tflops": exe, "executed_frac": exe / FP64_PEAK_TFLOPS},
+                         "executed_tflops": exe, "executed_frac": exe / FP64_PEAK_TFLOPS,
+                         "simd_issue": simd_issue(launch_s, C * S)},
             "with_host_stream": host,
         }
     sec = {}
