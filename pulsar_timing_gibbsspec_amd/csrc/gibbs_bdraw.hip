@@ -651,20 +651,40 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_lnlike_marg(LnlArgs A) {
 // randn * (0.05 len(hind)) * scale; accept if diff > log(rand).  Philox event GS_EV_HYPER,
 // slots 3 s .. 3 s + 2 of step s: (u_scale, u_par), (Box-Muller pair), (u_acc, -).
 
+// GS_HY_W = 2: two waves per chain, wave w taking the steps whose pulsar p has p % 2 == w (a step
+// changes only pulsar p's parameters and lnL_p, so the two subsequences are independent and each
+// keeps the reference's step order): 4096 waves for 2048 chains instead of 2048, at <= 168 VGPRs
+// (7 spilled).  Measured (power-law MH line, tools/gpu_ab_mh.sh ALT=w2): the launch alone 0.148 ->
+// 0.144 ms, the sweep 1.154 -> 1.172 ms -- off by default.
+#ifndef GS_HY_W
+#define GS_HY_W 1
+#endif
+__device__ __forceinline__ void hy_sync() {
+  if constexpr (GS_HY_W == 1)
+    wave_lds_sync();
+  else
+    __syncthreads();
+}
+
 template <int NFC, int NTC>
-__global__ __launch_bounds__(64, 2) void k_hyper_mh(HyperMhArgs A) {
+__global__ __launch_bounds__(64 * GS_HY_W, GS_HY_W == 1 ? 2 : 3) void k_hyper_mh(HyperMhArgs A) {
   extern __shared__ double lds[];
   const int NF = NFC ? NFC : A.NF;
   const int n_f = NF / 2;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wv = GS_HY_W == 1 ? 0 : gs_wave_id();
   const int c = blockIdx.x;
   double* xs = lds;              // the chain's x row
   double* Ls = lds + A.ldx;      // lnL_p of every pulsar at x
-  double* scr = lds + ((A.ldx + A.n_psr + 1) & ~1);
+  // The proposals do not depend on the chain state: lane l draws step s0 + l's (scale, parameter,
+  // normal, log u) for 64 steps at once into the chain's step table (3 Philox blocks per lane in
+  // parallel instead of 3 wave-uniform blocks on the critical path of every step).
+  double* stab = lds + ((A.ldx + A.n_psr + 1) & ~1);
+  double* scr = stab + 4 * 64 + wv * gs_tile_scr(NF);
   double* xg = A.x + (int64_t)c * A.ldx;
-  for (int i = lane; i < A.ldx; i += 64) xs[i] = xg[i];
-  for (int p = lane; p < A.n_psr; p += 64) Ls[p] = A.lnl_p[(int64_t)p * A.n_chain + c];
-  wave_lds_sync();
+  for (int i = threadIdx.x; i < A.ldx; i += 64 * GS_HY_W) xs[i] = xg[i];
+  for (int p = threadIdx.x; p < A.n_psr; p += 64 * GS_HY_W) Ls[p] = A.lnl_p[(int64_t)p * A.n_chain + c];
+  hy_sync();
   const bool act = lane < NF;
   const int kf = act ? (lane >> 1) : 0;
   // the common spectrum is fixed during the block (only red parameters move)
@@ -672,14 +692,10 @@ __global__ __launch_bounds__(64, 2) void k_hyper_mh(HyperMhArgs A) {
   const double sig = 0.05 * A.n_h;  // sigmas = 0.05 * len(hind)
   const long long chain = A.chain_base + c;
   const long long sw = gs_sweep(A.sweep, A.sweep_dev);
-  // The proposals do not depend on the chain state: lane l draws step s0 + l's (scale, parameter,
-  // normal, log u) for 64 steps at once into the wave's step table (3 Philox blocks per lane in
-  // parallel instead of 3 wave-uniform blocks on the critical path of every step).
-  double* stab = scr + gs_tile_scr(NF);
   int nacc = 0;
   for (int s0 = 0; s0 < A.nsteps; s0 += 64) {
     const int ns = min(64, A.nsteps - s0);
-    if (lane < ns) {
+    if (wv == 0 && lane < ns) {
       const int st = s0 + lane;
       double sc, z, u;
       int j;
@@ -703,12 +719,13 @@ __global__ __launch_bounds__(64, 2) void k_hyper_mh(HyperMhArgs A) {
       stab[4 * lane + 2] = z;
       stab[4 * lane + 3] = log(u);
     }
-    wave_lds_sync();
+    hy_sync();
     for (int i = 0; i < ns; ++i) {
       const int st = s0 + i;
-      const double sc = stab[4 * i], z = stab[4 * i + 2], lu = stab[4 * i + 3];
       const int j = __builtin_amdgcn_readfirstlane((int)stab[4 * i + 1]);
       const int col = A.hcol[j], p = A.hpsr[j];
+      if (GS_HY_W > 1 && p % GS_HY_W != wv) continue;  // the other wave's pulsar
+      const double sc = stab[4 * i], z = stab[4 * i + 2], lu = stab[4 * i + 3];
       // q[par] += randn * sigmas * scale, rounded as numpy does (no fma contraction)
       const double xq = gs_add_rn(xs[col], gs_mul_rn(gs_mul_rn(z, sig), sc));
       bool accepted = false;
@@ -755,11 +772,18 @@ __global__ __launch_bounds__(64, 2) void k_hyper_mh(HyperMhArgs A) {
         qr[2] = accepted ? 1.0 : 0.0;
       }
     }
-    wave_lds_sync();  // the next 64 steps rewrite the table
+    hy_sync();  // the next 64 steps rewrite the table
   }
-  for (int i = lane; i < A.ldx; i += 64) xg[i] = xs[i];
-  for (int p = lane; p < A.n_psr; p += 64) A.lnl_p[(int64_t)p * A.n_chain + c] = Ls[p];
-  if (A.n_acc && lane == 0) A.n_acc[c] = nacc;
+  for (int i = threadIdx.x; i < A.ldx; i += 64 * GS_HY_W) xg[i] = xs[i];
+  for (int p = threadIdx.x; p < A.n_psr; p += 64 * GS_HY_W) A.lnl_p[(int64_t)p * A.n_chain + c] = Ls[p];
+  if constexpr (GS_HY_W > 1) {
+    __shared__ int nac[GS_HY_W];
+    if (lane == 0) nac[wv] = nacc;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int w = 1; w < GS_HY_W; ++w) nacc += nac[w];
+  }
+  if (A.n_acc && threadIdx.x == 0) A.n_acc[c] = nacc;
 }
 
 // ------------------------------------------------------------ fused sweep
@@ -1157,12 +1181,12 @@ int launch_lnlike_marg(hipStream_t s, const LnlArgs& a) {
 
 int launch_hyper_mh(hipStream_t s, const HyperMhArgs& a) {
   if (a.n_chain == 0) return 0;
-  // x row, lnL_p, tile scratch, the 64-step proposal table
-  const size_t lds = ((size_t)((a.ldx + a.n_psr + 1) & ~1) + gs_tile_scr(a.NF) + 4 * 64) * sizeof(double);
+  // x row, lnL_p, the 64-step proposal table, each wave's tile scratch
+  const size_t lds = ((size_t)((a.ldx + a.n_psr + 1) & ~1) + 4 * 64 + GS_HY_W * gs_tile_scr(a.NF)) * sizeof(double);
   dim3 grid((unsigned)a.n_chain);
 #define GS_HY_LAUNCH(NFC, NTC)                                                   \
   if (lds > 65536 && set_lds(k_hyper_mh<NFC, NTC>, lds)) return 2;               \
-  hipLaunchKernelGGL((k_hyper_mh<NFC, NTC>), grid, dim3(64), lds, s, a);         \
+  hipLaunchKernelGGL((k_hyper_mh<NFC, NTC>), grid, dim3(64 * GS_HY_W), lds, s, a); \
   return 0;
   switch (a.NF) {
     case 20: GS_HY_LAUNCH(20, 0)

@@ -4,7 +4,8 @@ set -u
 mkdir -p gpurun_out/mh
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_pta_mh.py > gpurun_out/mh/tests.txt 2>&1 || { tail -30 gpurun_out/mh/tests.txt; exit 1; }
 tail -2 gpurun_out/mh/tests.txt
-for L in default old default old; do
+ALT=${ALT:-old}
+for L in default $ALT default $ALT; do
   if [ $L = default ]; then unset GS_LIB_PATH; else export GS_LIB_PATH=$PWD/pulsar_timing_gibbsspec_amd/libpulsar_gibbs_$L.so; fi
   timeout -k 10 300 python bench.py --no-cpu-baseline --steps 3 --warmup 1 --indep 0 --config5 0 --ecorr 0 --pta curn_plred --pta-ess-sweeps 0 --ess-sweeps 100 --cpu-ess 0 > gpurun_out/mh/b_$L.json 2> gpurun_out/mh/b_$L.err || exit 1
   python -c "
