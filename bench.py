@@ -225,23 +225,29 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
     sharded = shard == "pulsar" and world > 1
     hyper = None
     if kind == "curn_plred":
-        # the reference's default redsample='mh' on per-pulsar power-law red noise (pta_gibbs.py:278-340):
-        # chain-sharded only, aclength_hyper fixed (its warm-up's acor cannot run, pta_hyper)
+        # the reference's default redsample='mh' on per-pulsar power-law red noise (pta_gibbs.py:278-340),
+        # aclength_hyper fixed (its warm-up's acor cannot run, pta_hyper); pulsar-sharded, every rank
+        # applies its own pulsars' steps of the common step table and the (log10_A, gamma) values
+        # travel in the [tau | x_red] all-gather (no other collective)
         from pulsar_timing_gibbsspec_amd.pta_hyper import HyperSpec
         hidx = np.array([i for i, n in enumerate(names) if "red" in n and ("log10_A" in n or "gamma" in n)])
         hyper = HyperSpec(pta, pta.params, [s for s in (pta.signals[k] for k in pta.signals) if "red" in s.name],
                           hidx, np.zeros(len(names)), 30, dev)
-        sharded = False
     if sharded:
         blocks = balanced_blocks(np.array([t.shape[1] ** 3 for t in T], float), world)
         lo, hi = blocks[rank]
         model = DeviceModel(ctx, T[lo:hi], N[lo:hi], R[lo:hi], gwid[lo:hi], fixed[lo:hi])
-        x0 = np.random.default_rng(0).uniform(-9, -4, (C, len(names)))
+        rng = np.random.default_rng(0)
+        x0 = rng.uniform(-9, -4, (C, len(names)))
+        if hyper is not None:
+            x0[:, hyper.hind] = rng.uniform(hyper.hlo_host, hyper.hhi_host, (C, hyper.n_h))
         ex = dict(allreduce=TauSumAllReduce()) if curn_mode == "sum" else \
             dict(gather=PulsarAllGather([np.arange(a, b) for a, b in blocks],
-                                        ((2 if red_col is not None else 1), 30, C), device=dev))
+                                        ((2 if (red_col is not None or hyper is not None) else 1), 30, C),
+                                        device=dev))
         eng = PTAChains(model, len(names), rind, red_col, (1e-18, 1e-8), (1e-20, 1e-8), C, x0,
-                        P_global=len(T), psr_lo=lo, curn_mode=curn_mode, **ex)
+                        P_global=len(T), psr_lo=lo, curn_mode=curn_mode, hyper=hyper,
+                        hyper_acl=HYPER_ACL if hyper is not None else None, **ex)
     else:
         model = DeviceModel(ctx, T, N, R, gwid, fixed)
         rng = np.random.default_rng(rank)
@@ -308,9 +314,12 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
         eng.x.copy_(x_save)
         nf = 60
         fl = nf ** 3 / 3 + nf ** 2 / 2 + nf / 6          # one NF x NF Schur-block factorisation
+        # a pulsar-sharded rank evaluates only the steps of its own pulsars (expected share)
+        own = float(np.mean((hm.hpsr >= 0).cpu().numpy()))
         kernels["k_hyper_mh"] = dict(
             kernel_avg_ms=ms_mh, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
-            achieved=HYPER_ACL * C * fl / (ms_mh * 1e-3) / 1e12, alg_per_launch=HYPER_ACL * C * fl,
+            achieved=own * HYPER_ACL * C * fl / (ms_mh * 1e-3) / 1e12, alg_per_launch=own * HYPER_ACL * C * fl,
+            own_step_share=own,
             note=f"{HYPER_ACL} single-parameter MH steps per chain (pta_gibbs.py:319-340), each one pulsar's "
                  "marginalised likelihood (NF x NF Schur block Cholesky, NF^3/3 + NF^2/2 + NF/6 flop; the "
                  "reference re-evaluates all 45 pulsars' full m x m systems per step)")
@@ -952,7 +961,7 @@ def main():
             d["config"] = ("configs[3] with the reference's default redsample='mh': 45-pulsar CURN free spectrum + "
                            f"per-pulsar power-law red noise by {HYPER_ACL} Metropolis steps per sweep")
         add(kind, d, kind)
-        if world > 1 and kind != "curn_plred":
+        if world > 1:
             d = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, shard="pulsar")
             d["config"] = f"configs[3] {kind}, pulsars sharded over the ranks with the per-sweep RCCL exchange"
             add(kind + "_pulsar_sharded", d)

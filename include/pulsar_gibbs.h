@@ -421,7 +421,10 @@ int gs_pta_gate_phiinv_irn(gs_ctx* ctx, int n_psr, int n_chain, int n_f, int n_p
  *   marginalised likelihood.  Parameter j belongs to pulsar hpsr[j], so only that pulsar's term
  *   is re-evaluated: lnl_p [n_psr x n_chain] holds every pulsar's phi-dependent lnL at x (seed it
  *   with gs_lnlike_marg on the phiinv of x) and is updated in place.  A proposal outside [hlo[j],
- *   hhi[j]] (uniform prior) is rejected without a likelihood.  Red phi of pulsar p: red_kind 0 =
+ *   hhi[j]] (uniform prior) is rejected without a likelihood.  hpsr[j] = -1: parameter j belongs to
+ *   a pulsar this call does not hold (pulsar-sharded run: every rank draws the same steps from the
+ *   chain-level Philox counters and applies those of its own pulsars); its steps are skipped.
+ *   Red phi of pulsar p: red_kind 0 =
  *   free spectrum 10**(2 x[red_col[p][k]]) (red_col [n_psr x n_f]); 1 = power law (pl_col,
  *   lnphi as above).  phi = 10**(2 x[gw_col[k]]) + red (the common spectrum is held fixed in the
  *   block).  inj [nsteps x n_chain x 4] = (scale, j, randn, rand) per step, or NULL (Philox event

@@ -284,6 +284,36 @@ def lnlike_fullmarg(r, Nvec, TNT, d, phiinv, logdet_phi):
     return ll + 0.5 * (np.dot(d, ev) - logdet_sigma - logdet_phi)
 
 
+def lnlike_phi_batch(pf, phi_F, chunk=2048):
+    """The phi-dependent part of one pulsar's marginalised likelihood (pta_gibbs.py:596-619, the
+    term of pulsar ii in get_lnlikelihood) for a batch of free-spectrum phi rows phi_F (B x NF,
+    the prefix_factor pf's F order), the fixed-prior columns' phi held fixed:
+    1/2 (d^T Sigma^-1 d - log det Sigma - log det phi) = 1/2 (|L_S^-1 dF|^2 - log det(S0 + diag(1/phi_F))
+    - sum log phi_F) + const, since log det Sigma = log det A_MM + log det(S0 + D_F) and
+    d^T Sigma^-1 d = |L_M^-1 d_M|^2 + dF^T (S0 + D_F)^-1 dF.  The dropped constant (log det N, r^T N^-1 r,
+    the A_MM terms, the timing-model phi) does not depend on phi_F.  -inf where S0 + D_F is not PD."""
+    phi_F = np.atleast_2d(np.asarray(phi_F, float))
+    S0, dF = pf["S0"], pf["dF"]
+    nF = S0.shape[0]
+    out = np.empty(phi_F.shape[0])
+    for a in range(0, phi_F.shape[0], chunk):
+        ph = phi_F[a:a + chunk]
+        S = np.broadcast_to(S0, (ph.shape[0], nF, nF)).copy()
+        S[:, np.arange(nF), np.arange(nF)] += 1.0 / ph
+        try:
+            L = np.linalg.cholesky(S)
+        except np.linalg.LinAlgError:           # some row is not PD: row by row
+            out[a:a + chunk] = ([lnlike_phi_batch(pf, r[None])[0] for r in ph] if ph.shape[0] > 1
+                                else -np.inf)
+            continue
+        y = np.empty((ph.shape[0], nF))
+        for i in range(nF):                     # forward substitution, vectorised over the batch
+            y[:, i] = (dF[i] - np.einsum("bj,bj->b", L[:, i, :i], y[:, :i])) / L[:, i, i]
+        ld = 2.0 * np.sum(np.log(L[:, np.arange(nF), np.arange(nF)]), axis=1)
+        out[a:a + chunk] = 0.5 * (np.sum(y * y, axis=1) - ld - np.sum(np.log(ph), axis=1))
+    return out
+
+
 # ============================================================== Philox4x32-10 (a9)
 PHILOX_M0, PHILOX_M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
 PHILOX_W0, PHILOX_W1 = np.uint32(0x9E3779B9), np.uint32(0xBB67AE85)

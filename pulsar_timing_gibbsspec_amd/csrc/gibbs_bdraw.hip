@@ -702,7 +702,7 @@ __global__ __launch_bounds__(64 * GS_HY_W, GS_HY_W == 1 ? 2 : 3) void k_hyper_mh
       if (A.inj) {
         const double* q = A.inj + ((int64_t)st * A.n_chain + c) * 4;
         sc = q[0];
-        j = (int)q[1];
+        j = min(max((int)q[1], 0), A.n_h - 1);  // the host validates; never index out of range
         z = q[2];
         u = q[3];
       } else {
@@ -724,6 +724,7 @@ __global__ __launch_bounds__(64 * GS_HY_W, GS_HY_W == 1 ? 2 : 3) void k_hyper_mh
       const int st = s0 + i;
       const int j = __builtin_amdgcn_readfirstlane((int)stab[4 * i + 1]);
       const int col = A.hcol[j], p = A.hpsr[j];
+      if (p < 0) continue;  // a pulsar of another rank (pulsar-sharded run): its steps are applied there
       if (GS_HY_W > 1 && p % GS_HY_W != wv) continue;  // the other wave's pulsar
       const double sc = stab[4 * i], z = stab[4 * i + 2], lu = stab[4 * i + 3];
       // q[par] += randn * sigmas * scale, rounded as numpy does (no fma contraction)

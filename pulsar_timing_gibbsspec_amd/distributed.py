@@ -108,6 +108,20 @@ class TauSumAllReduce:
         return partial
 
 
+def allreduce_sum(t, group=None):
+    """Sum of a small tensor over the ranks of ``group`` (host-side bookkeeping, not the data path:
+    the red MH warm-up records, acceptance counts).  gloo reduces on the host, so a device tensor is
+    staged through host memory there; RCCL reduces it in place."""
+    if not (dist.is_available() and dist.is_initialized()):
+        raise RuntimeError("a pulsar-sharded engine needs torch.distributed initialised for this reduction")
+    if dist.get_backend(group) == "nccl" or t.device.type == "cpu":
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        return t
+    h = t.cpu()
+    dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+    return h.to(t.device)
+
+
 def max_over_ranks(value, device="cpu"):
     """Max of a float over ranks (the bench's job time)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:

@@ -431,8 +431,8 @@ class PTAChains:
         if hyper is not None:
             if red_col is not None:
                 raise ValueError("give either red_col (conditional red draws) or hyper (Metropolis), not both")
-            if self.PG != P or gather is not None or allreduce is not None:
-                raise NotImplementedError("redsample='mh' runs chain-sharded only (each rank holds every pulsar)")
+            if hyper.P != self.PG:
+                raise ValueError(f"the hyper tables cover {hyper.P} pulsars, the array {self.PG}")
             if hyper.kind == 0:
                 red_col = hyper.red_col_host           # the free-spectrum red columns (irn, phiinv)
         # the exchange runs when pulsars are split over ranks, or whenever one is given (a
@@ -464,11 +464,21 @@ class PTAChains:
             rg = np.asarray(red_col, np.int32).reshape(self.PG, self.n_f)
             self.red_col_g = _t(rg.ravel(), torch.int32, dev)
             self.red_col = _t(rg[self.psr_lo:self.psr_lo + P].ravel(), torch.int32, dev)
-            self.red_col_l64 = torch.as_tensor(rg[self.psr_lo:self.psr_lo + P].ravel(), dtype=torch.long,
-                                               device=dev)
-            self.red_col_g64 = torch.as_tensor(rg.ravel(), dtype=torch.long, device=dev)
         else:
             self.red_col = self.red_col_g = None
+        # the x columns of each pulsar's red parameters [PG x W] -- what a pulsar-sharded run exchanges
+        # besides tau (a rank draws only its own pulsars' red parameters): the red free spectrum
+        # (W = n_f) or the power law's (log10_A, gamma) (W = 2)
+        xred = None
+        if self.hyper_pl:
+            xred = np.asarray(hyper.pl_col_host, np.int64).reshape(self.PG, -1)
+        elif red_col is not None:
+            xred = np.asarray(red_col, np.int64).reshape(self.PG, self.n_f)
+        self.xred_w = 0 if xred is None else xred.shape[1]
+        self.xred_rows = -(-self.xred_w // self.n_f)          # slab rows the red x values take
+        if xred is not None:
+            self.xred_l64 = torch.as_tensor(xred[self.psr_lo:self.psr_lo + P].ravel(), dtype=torch.long, device=dev)
+            self.xred_g64 = torch.as_tensor(xred.ravel(), dtype=torch.long, device=dev)
         self.grid_gw = grid3(*gw_bounds, n=ngrid, device=dev)
         self.grid_red = grid3(*red_bounds, n=ngrid, device=dev) if self.red_cond else None
         self.x = _t(np.broadcast_to(np.asarray(x0, float), (C, self.n_param)), torch.float64, dev)
@@ -492,13 +502,13 @@ class PTAChains:
         self.xlast = torch.empty(C, dtype=torch.float64, device=dev)
         self.info = torch.zeros(P * C, dtype=torch.int32, device=dev)
         self.fail_count = torch.zeros(P * C, dtype=torch.int32, device=dev)   # failed draws (b kept)
-        self.slab_shape = ((2 if self.red else 1), self.n_f, C)
+        self.slab_shape = (1 + self.xred_rows, self.n_f, C)
         self.it = 0
         self.redraw_b = False      # draw b | x first at the next sweep, as at sweep 0 (resume)
         self.hyper = None
         if hyper is not None:
             from .pta_hyper import HYPER_WARMUP, HyperMH
-            self.hyper = HyperMH(hyper, model, C, self.n_param, self.gw_col)
+            self.hyper = HyperMH(hyper, model, C, self.n_param, self.gw_col, psr_lo=self.psr_lo)
             self.hyper_acl = None if hyper_acl is None else int(hyper_acl)
             self.hyper_warmup = HYPER_WARMUP if hyper_warmup is None else int(hyper_warmup)
             self.hyper_short_chain = None      # chain 0's sweep-0 warm-up proposals (q[hind] rows)
@@ -588,13 +598,19 @@ class PTAChains:
         if self.hyper is not None:                             # pta_gibbs.py:689-697 (redsample='mh')
             if ii == 0:
                 n = self.hyper_warmup
-                q_rec = torch.empty(n, self.C, 3, dtype=torch.float64, device=self.ctx.device) \
+                # zeroed: a pulsar-sharded rank records only the steps of its own pulsars, and the
+                # ranks' records are summed below (every step is owned by exactly one rank)
+                q_rec = torch.zeros(n, self.C, 3, dtype=torch.float64, device=self.ctx.device) \
                     if self.hyper_acl is None else None
                 x_start = self.x[0].cpu().numpy() if q_rec is not None else None
                 self.hyper_block(n, inj=mh_inj, q_rec=q_rec, seed=not self.hyper.fresh)
                 if q_rec is not None:                          # aclength_hyper from the warm-up (:311-315)
                     from .pta_hyper import hyper_aclength
-                    self.hyper_short_chain = self.hyper_spec.short_chain(x_start, q_rec[:, 0].cpu().numpy())
+                    q0 = q_rec[:, 0].contiguous()
+                    if self.sharded:
+                        from .distributed import allreduce_sum
+                        q0 = allreduce_sum(q0, group=getattr(self.gather, "group", None))
+                    self.hyper_short_chain = self.hyper_spec.short_chain(x_start, q0.cpu().numpy())
                     self.hyper_acl = hyper_aclength(self.hyper_short_chain)
             else:
                 self.hyper_block(self.hyper_acl, inj=mh_inj, seed=not self.hyper.fresh)
@@ -613,11 +629,12 @@ class PTAChains:
                                  self.n_param, ptr(self.red_col), None), "gs_rho_red")
         if not self.sharded:
             return None
-        parts = [self.tau.unsqueeze(1)]
-        if self.red:
-            xr = self.x.index_select(1, self.red_col_l64).T.reshape(self.P, 1, self.n_f, self.C)
-            parts.append(xr)
-        return torch.cat(parts, dim=1)
+        slab = torch.zeros((self.P,) + self.slab_shape, dtype=torch.float64, device=self.ctx.device)
+        slab[:, 0] = self.tau
+        if self.xred_w:
+            xr = self.x.index_select(1, self.xred_l64).T.reshape(self.P, self.xred_w, self.C)
+            slab[:, 1:].view(self.P, self.xred_rows * self.n_f, self.C)[:, :self.xred_w] = xr
+        return slab
 
     def sweep_end(self, slab_g=None, z=None, u_curn=None):
         """Common draw on the global inputs, gate, gated b|rho."""
@@ -637,9 +654,9 @@ class PTAChains:
             return
         if self.sharded:
             self.tau_g.copy_(slab_g[:, 0])
-            if self.red:
-                xr = slab_g[:, 1].reshape(self.PG * self.n_f, self.C).T
-                self.x.index_copy_(1, self.red_col_g64, xr.contiguous())
+            if self.xred_w:
+                xr = slab_g[:, 1:].reshape(self.PG, self.xred_rows * self.n_f, self.C)[:, :self.xred_w]
+                self.x.index_copy_(1, self.xred_g64, xr.reshape(self.PG * self.xred_w, self.C).T.contiguous())
         self._update_irn()
         check(lib.gs_rho_curn(h, self.PG, self.C, self.n_f, ptr(self.tau_g), ptr(self.irn), self.ngrid,
                               ptr(self.grid_gw), ptr(u_curn), ii, self.chain_base, ptr(self.x),
@@ -647,6 +664,18 @@ class PTAChains:
         self._gate_phiinv(with_gate=True)                      # pta_gibbs.py:703
         self._bdraw(z, _lib.EV_B, self.gate)                   # pta_gibbs.py:704
         self.it += 1
+
+    def hyper_acceptance(self):
+        """Accepted fraction of the red MH steps per chain since the engine was built; a
+        pulsar-sharded run sums the ranks' counts (each rank takes the steps of its own pulsars).
+        Syncs."""
+        if self.hyper is None:
+            return None
+        acc = self.hyper.acc_total.double()
+        if self.sharded:
+            from .distributed import allreduce_sum
+            acc = allreduce_sum(acc.clone(), group=getattr(self.gather, "group", None))
+        return (acc / max(1, self.hyper.steps_total)).cpu().numpy()
 
     def check_fx(self):
         """curn_mode='sum': raise if gs_tau_sum_fx_b saw a tau it cannot sum exactly (negative,
@@ -688,6 +717,9 @@ class PTAChains:
         self.ctx.set_stream(cap)
         check(lib.gs_ctx_set_sweep_counter(h, ptr(self._gcount)), "gs_ctx_set_sweep_counter")
         self.graph = torch.cuda.CUDAGraph()
+        # the hyper block's step count is host-side: nothing runs during capture, and each replay
+        # adds the captured sweeps' steps (its accepted-step counter is a device add the graph replays)
+        hsteps0 = self.hyper.steps_total if self.hyper is not None else 0
         try:
             with torch.cuda.graph(self.graph, stream=cap):
                 for i in range(n):
@@ -697,6 +729,9 @@ class PTAChains:
             check(lib.gs_ctx_set_sweep_counter(h, None), "gs_ctx_set_sweep_counter")
             self.ctx.set_stream(old)
             self.it = self._gbase          # nothing ran during capture
+            if self.hyper is not None:
+                self._g_hsteps = self.hyper.steps_total - hsteps0
+                self.hyper.steps_total = hsteps0
         return self.graph_rec
 
     def replay(self):
@@ -704,6 +739,8 @@ class PTAChains:
         self._gcount.fill_(self.it - self._gbase)   # stays right if eager sweeps ran between
         self.graph.replay()
         self.it += self._gn
+        if self.hyper is not None:
+            self.hyper.steps_total += self._g_hsteps
         return self.graph_rec
 
     def sweep(self, x_rec=None, z0=None, z=None, u_red=None, u_curn=None, mh_inj=None):

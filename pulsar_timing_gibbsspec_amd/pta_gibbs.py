@@ -200,6 +200,9 @@ class PTABlockGibbs(object):
         for p, bb in enumerate(self._b):
             b[p, :bb.size] = bb
         eng.b.copy_(torch.as_tensor(np.repeat(b, eng.C, axis=0), device=self.ctx.device))
+        # the per-pulsar red phi (irn) at xs: the gate's phiinv and the common draw read it
+        # (power-law red noise or a red free spectrum; without red noise irn is None)
+        eng._update_irn()
         return eng
 
     def update_b(self, xs):
@@ -217,9 +220,6 @@ class PTABlockGibbs(object):
         lib, h, m = self.ctx.lib, self.ctx.handle, eng.model
         _lib.check(lib.gs_tau(h, eng.P, eng.C, m.NF, m.ldb, _lib.ptr(m.fidx), _lib.ptr(eng.b), 0,
                               _lib.ptr(eng.tau)), "gs_tau")
-        if eng.red:
-            _lib.check(lib.gs_phi_from_x(h, eng.C, eng.P * eng.n_f, _lib.ptr(eng.x), eng.n_param,
-                                         _lib.ptr(eng.red_col), _lib.ptr(eng.irn)), "gs_phi_from_x")
         _lib.check(lib.gs_rho_curn(h, eng.P, eng.C, eng.n_f, _lib.ptr(eng.tau), _lib.ptr(eng.irn),
                                    eng.ngrid, _lib.ptr(eng.grid_gw), None, eng.it, eng.chain_base, _lib.ptr(eng.x),
                                    eng.n_param, _lib.ptr(eng.gw_col), None), "gs_rho_curn")
@@ -231,8 +231,6 @@ class PTABlockGibbs(object):
         GPU: -1/2 (log det N + r^T N^-1 r) + 1/2 (d^T Sigma^-1 d - log det Sigma - log det phi) per
         pulsar; -inf if a Sigma is not positive definite."""
         eng = self._engine_at(xs)
-        if eng.hyper_pl:
-            eng._update_irn()
         ph = torch.empty(eng.P * eng.C, eng.model.NF, dtype=torch.float64, device=self.ctx.device)
         gate = torch.empty(eng.C, dtype=torch.int32, device=self.ctx.device)
         if eng.phi_shared:
@@ -256,8 +254,11 @@ class PTABlockGibbs(object):
             eng = self._engine_at(xs)
             if eng.hyper is None:
                 return np.asarray(xs, float).copy()
+            if iters is not None and int(iters) <= 0:
+                raise ValueError(f"iters must be positive (got {iters})")
             n = int(iters) if iters is not None else int(self.aclength_hyper)
-            q_rec = torch.empty(n, eng.C, 3, dtype=torch.float64, device=self.ctx.device) if iters else None
+            q_rec = torch.empty(n, eng.C, 3, dtype=torch.float64, device=self.ctx.device) \
+                if iters is not None else None
             eng.hyper_block(n, q_rec=q_rec)
             eng.it += 1
             if iters is not None:

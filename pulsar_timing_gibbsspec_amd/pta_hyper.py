@@ -128,11 +128,27 @@ class HyperMH:
     """The device side of one PTA engine's hyper block: per-(pulsar, chain) lnL_p and the
     launches (seed lnL_p from the phiinv of the current x, then gs_hyper_mh)."""
 
-    def __init__(self, spec: HyperSpec, model, n_chain, n_param, gw_col):
+    def __init__(self, spec: HyperSpec, model, n_chain, n_param, gw_col, psr_lo=0):
+        """psr_lo: the model holds pulsars [psr_lo, psr_lo + model.P) of the spec's array (a
+        pulsar-sharded rank).  The step tables are then this rank's: a parameter of another rank's
+        pulsar gets hpsr = -1 and its steps are skipped (every rank draws the same step table from
+        the chain-level Philox counters, and each applies the steps of its own pulsars -- each
+        pulsar's subsequence in the reference's order; pta_gibbs.py:294-305), and the per-pulsar
+        tables (red columns, power-law table) are the model's slices.  The red phi of every pulsar
+        (``irn``, for the common draw) uses the spec's whole-array tables."""
         self.spec, self.model, self.ctx = spec, model, model.ctx
         self.C, self.n_param = int(n_chain), int(n_param)
         dev = self.ctx.device
         self.gw_col = gw_col
+        lo, P = int(psr_lo), model.P
+        if lo < 0 or lo + P > spec.P:
+            raise ValueError(f"pulsars [{lo}, {lo + P}) outside the spec's {spec.P}")
+        hp = spec.hpsr_host - lo
+        hp[(hp < 0) | (hp >= P)] = -1
+        self.hpsr = _t(hp.astype(np.int32), torch.int32, dev)
+        self.red_col = _t(spec.red_col_host[lo:lo + P].ravel(), torch.int32, dev)
+        self.pl_col = _t(spec.pl_col_host[lo:lo + P].ravel(), torch.int32, dev)
+        self.lnphi = _t(spec.lnphi_host[lo:lo + P].ravel(), torch.float64, dev)
         self.lnl_p = torch.empty(model.P * self.C, dtype=torch.float64, device=dev)
         self.n_acc = torch.zeros(self.C, dtype=torch.int32, device=dev)
         self.acc_total = torch.zeros(self.C, dtype=torch.int64, device=dev)
@@ -149,18 +165,26 @@ class HyperMH:
         m, sp = self.model, self.spec
         if nsteps <= 0:
             return
+        if inj is not None:
+            if tuple(inj.shape) != (int(nsteps), self.C, 4):
+                raise ValueError(f"inj must be (nsteps, n_chain, 4) = {(int(nsteps), self.C, 4)}, got "
+                                 f"{tuple(inj.shape)}")
+            j = inj[..., 1]
+            if bool(((j < 0) | (j > sp.n_h - 1) | (j != torch.floor(j))).any()):
+                raise ValueError(f"inj[..., 1] (the parameter index) must be an integer in [0, {sp.n_h - 1}]")
         check(self.ctx.lib.gs_hyper_mh(self.ctx.handle, m.P, self.C, m.NF, m.NMX, ptr(m.model), ptr(m.nm_dev),
-                                       ptr(x), self.n_param, ptr(self.gw_col), sp.n_h, ptr(sp.hcol), ptr(sp.hpsr),
-                                       ptr(sp.hlo), ptr(sp.hhi), sp.kind, ptr(sp.red_col), ptr(sp.pl_col),
-                                       ptr(sp.lnphi), ptr(self.lnl_p), int(nsteps), int(sweep), int(chain_base),
+                                       ptr(x), self.n_param, ptr(self.gw_col), sp.n_h, ptr(sp.hcol), ptr(self.hpsr),
+                                       ptr(sp.hlo), ptr(sp.hhi), sp.kind, ptr(self.red_col), ptr(self.pl_col),
+                                       ptr(self.lnphi), ptr(self.lnl_p), int(nsteps), int(sweep), int(chain_base),
                                        ptr(inj), ptr(q_rec), ptr(self.n_acc)), "gs_hyper_mh")
         self.acc_total += self.n_acc
         self.steps_total += int(nsteps)
 
     def irn(self, x, out):
-        """Per-pulsar red phi [P x n_f x C] at x (power law; the free spectrum uses gs_phi_from_x)."""
+        """Per-pulsar red phi [P x n_f x C] of the whole array at x (power law; the free spectrum uses
+        gs_phi_from_x)."""
         sp = self.spec
-        check(self.ctx.lib.gs_phi_powerlaw(self.ctx.handle, self.model.P, self.C, sp.n_f, ptr(x), self.n_param,
+        check(self.ctx.lib.gs_phi_powerlaw(self.ctx.handle, sp.P, self.C, sp.n_f, ptr(x), self.n_param,
                                            ptr(sp.pl_col), ptr(sp.lnphi), ptr(out)), "gs_phi_powerlaw")
 
     def acceptance(self):

@@ -373,6 +373,42 @@ def pta_hyper_mh(ref, out, kind="curn_plred", niter=8, warm=100, acl=20, n_psr=N
           int(sum(np.sum(a != b) for a, b in zip(hyper_in, hyper_out))))
 
 
+def pta_long_plred(ref, out, niter=40000, seed=31, n_psr=6, warm=100, acl=20, thin=10):
+    """Long chain of the reference's DEFAULT PTA model (redsample='mh', power-law red noise per
+    pulsar + CURN free spectrum) for the KS comparison of the device's curn_plred posteriors.
+    sample() itself cannot pass sweep 0 on this path (its iters=100 warm-up ends in an SVD of the
+    empty short_chain[100:] covariance, see pta_hyper_mh), so the reference's own methods are
+    driven in sample()'s order (pta_gibbs.py:664-704) with sweep 0's 100 warm-up steps run through
+    the steady-state branch (aclength_hyper = warm) and aclength_hyper = acl afterwards -- the
+    patch pta_hyper_mh pins draw for draw.  Seeded, single-threaded BLAS; keeps the gw log10 rho
+    and the red (log10_A, gamma) columns as float32, every ``thin``-th sweep."""
+    pta = synthetic.array_pta(kind="curn_plred", n_psr=n_psr, seed=0)
+    np.random.seed(seed)
+    g = _quiet(ref.PTABlockGibbs, pta, hypersample="conditional", redsample="mh")
+    x0 = np.concatenate([p.sample().flatten() for p in g.params])
+    names = list(g.param_names)
+    chain = np.empty((niter, len(x0)))
+    xnew = x0.copy()
+    np.random.seed(seed + 1)
+    for ii in range(niter):
+        chain[ii] = xnew
+        if ii == 0:
+            g._b = g.update_b(x0)
+        g.TNT, g.d = [], []
+        g.aclength_hyper = warm if ii == 0 else acl
+        xnew = g.update_hyper_params(xnew, iters=None)
+        xnew = g.update_rho_params(xnew)
+        if np.all(xnew != chain[ii][-1]):
+            g._b = g.update_b(xnew)
+        if ii % 1000 == 0:
+            print("pta long plred", seed, ii, flush=True)
+    keep = [i for i, n in enumerate(names) if ("gw" in n and "rho" in n) or "red_noise" in n]
+    np.savez_compressed(out, chain=chain[::thin, keep].astype(np.float32), cols=np.array(keep),
+                        names=np.array([names[i] for i in keep]), niter=niter, thin=thin, x0=x0,
+                        kind="curn_plred", n_psr=n_psr, seed=seed, warm=warm, aclength=acl)
+    print("pta long plred:", out, chain.shape)
+
+
 def likelihoods(ref, out):
     """White-noise and fully-marginalised likelihoods (pulsar_gibbs.py:523-546, 569-610)."""
     pta = synthetic.single_pulsar_pta("J1713+0747", seed=0, efac_vary=True, n_backends=3)
@@ -625,6 +661,13 @@ def main(root):
         if f"--only-pta-long-{kind}" in sys.argv:
             pta_long(PT, os.path.join(HERE, f"pta_long_{kind}.npz"), kind)
             return
+    if "--only-pta-long-plred" in sys.argv:
+        # one seed per process: --seed=S --niter=N -> pta_long_curn_plred_s{S}.npz
+        opt = dict(a[2:].split("=", 1) for a in sys.argv if a.startswith("--") and "=" in a)
+        s = int(opt.get("seed", 31))
+        pta_long_plred(PT, os.path.join(HERE, f"pta_long_curn_plred_s{s}.npz"), niter=int(opt.get("niter", 40000)),
+                       seed=s)
+        return
     if "--only-pta-mh" in sys.argv:
         pta_hyper_mh(PT, os.path.join(HERE, "pta_plred_mh.npz"), "curn_plred")
         pta_hyper_mh(PT, os.path.join(HERE, "pta_red_mh.npz"), "curn_red", n_psr=6, niter=6, acl=30)

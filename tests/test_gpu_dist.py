@@ -32,6 +32,24 @@ def _setup(kind):
     return T, N, R, names, rind, red_col, gwid, fixed
 
 
+def _x0_hyper(kind, C, dev):
+    """x0 over the priors and, for curn_plred (the reference's default redsample='mh'), the red
+    hyper tables (pta_hyper.HyperSpec) of the 8-pulsar array."""
+    from pulsar_timing_gibbsspec_amd import synthetic
+    from pulsar_timing_gibbsspec_amd.pta_hyper import HyperSpec
+    pta = synthetic.array_pta(kind=kind, n_psr=8, seed=3)
+    names = pta.param_names
+    rng = np.random.default_rng(0)
+    x0 = rng.uniform(-9, -4, (C, len(names)))
+    if kind != "curn_plred":
+        return x0, None
+    hidx = np.array([i for i, n in enumerate(names) if "red" in n and ("log10_A" in n or "gamma" in n)])
+    sigs = [s for s in (pta.signals[k] for k in pta.signals) if "red" in s.name]
+    hyper = HyperSpec(pta, pta.params, sigs, hidx, np.zeros(len(names)), 30, dev)
+    x0[:, hyper.hind] = rng.uniform(hyper.hlo_host, hyper.hhi_host, (C, hyper.n_h))
+    return x0, hyper
+
+
 def _worker(rank, world, port, kind, mode, S, out_dir):
     import torch
     import torch.distributed as dist
@@ -43,27 +61,41 @@ def _worker(rank, world, port, kind, mode, S, out_dir):
         from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
         T, N, R, names, rind, red_col, gwid, fixed = _setup(kind)
         C = 8
-        x0 = np.random.default_rng(0).uniform(-9, -4, (C, len(names)))
+        x0, hyper = _x0_hyper(kind, C, "cuda")
         lo, hi = shard_range(len(T), rank, world)
         ctx = _lib.Context(0, seed=31)
         mdl = DeviceModel(ctx, T[lo:hi], N[lo:hi], R[lo:hi], gwid[lo:hi], fixed[lo:hi])
         assign = [np.arange(*shard_range(len(T), r, world)) for r in range(world)]
-        ex = dict(allreduce=TauSumAllReduce()) if mode == "sum" else \
-            dict(gather=PulsarAllGather(assign, ((2 if red_col is not None else 1), 30, C), device="cuda"))
+        eng = None
+        if mode == "sum":
+            ex = dict(allreduce=TauSumAllReduce())
+        else:
+            # the slab: tau and each pulsar's red x values (free spectrum: n_f of them; power law: 2)
+            rows = 1 if (red_col is None and hyper is None) else 2
+            ex = dict(gather=PulsarAllGather(assign, (rows, 30, C), device="cuda"))
         eng = PTAChains(mdl, len(names), rind, red_col, (1e-18, 1e-8), (1e-20, 1e-8), C, x0,
-                        P_global=len(T), psr_lo=lo, curn_mode=mode, **ex)
+                        P_global=len(T), psr_lo=lo, curn_mode=mode, hyper=hyper, hyper_warmup=40, **ex)
+        assert eng.slab_shape == ex["gather"].slab_shape if mode != "sum" else True
         xr = torch.zeros(S, C, len(names), dtype=torch.float64, device="cuda")
         for i in range(S):
             eng.sweep(x_rec=xr[i])
         np.save(os.path.join(out_dir, f"x{rank}.npy"), xr.cpu().numpy())
+        if hyper is not None:
+            np.save(os.path.join(out_dir, f"h{rank}.npy"),
+                    np.concatenate([[eng.hyper_acl], eng.hyper_acceptance()]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,mode,world", [("curn", "sum", 2), ("curn", "sum", 4), ("curn_red", "exact", 2)])
+@pytest.mark.parametrize("kind,mode,world", [("curn", "sum", 2), ("curn", "sum", 4), ("curn_red", "exact", 2),
+                                             ("curn_plred", "exact", 2), ("curn_plred", "exact", 4)])
 def test_pulsar_sharded_processes(tmp_path, kind, mode, world):
     """world processes on the one GPU, pulsars sharded, against the unsharded engine bit for bit
-    (CURN: the fixed-point tau-sum digits all-reduced, order-free for any shard count)."""
+    (CURN: the fixed-point tau-sum digits all-reduced, order-free for any shard count).
+    curn_plred: the red MH block (redsample='mh', the reference's default) pulsar-sharded with no
+    new collective -- every rank draws the same step table and applies its own pulsars' steps, the
+    (log10_A, gamma) values travel in the [tau | x_red] all-gather; the sweep-0 warm-up's
+    aclength_hyper and the acceptance (summed over ranks) equal the unsharded engine's."""
     if not gpu_available():
         pytest.skip("no GPU")
     import torch
@@ -81,15 +113,20 @@ def test_pulsar_sharded_processes(tmp_path, kind, mode, world):
         assert p.exitcode == 0
     T, N, R, names, rind, red_col, gwid, fixed = _setup(kind)
     C = 8
-    x0 = np.random.default_rng(0).uniform(-9, -4, (C, len(names)))
+    x0, hyper = _x0_hyper(kind, C, "cuda")
     ref = PTAChains(DeviceModel(_lib.Context(0, seed=31), T, N, R, gwid, fixed), len(names), rind, red_col,
-                    (1e-18, 1e-8), (1e-20, 1e-8), C, x0, curn_mode=mode)
+                    (1e-18, 1e-8), (1e-20, 1e-8), C, x0, curn_mode=mode, hyper=hyper, hyper_warmup=40)
     xr = torch.zeros(S, C, len(names), dtype=torch.float64, device="cuda")
     for i in range(S):
         ref.sweep(x_rec=xr[i])
     want = xr.cpu().numpy()
     for r in range(world):
         assert np.array_equal(np.load(tmp_path / f"x{r}.npy"), want), r
+    if hyper is not None:
+        hw = np.concatenate([[ref.hyper_acl], ref.hyper_acceptance()])
+        assert 0 < hw[1:].mean() < 1
+        for r in range(world):
+            assert np.array_equal(np.load(tmp_path / f"h{r}.npy"), hw), r
 
 
 def _capture_worker(port, kind, mode, out_dir):

@@ -223,14 +223,17 @@ def test_pta_resume(tmp_path):
     assert not np.all(gw == gw.max())                                  # not pinned to rho_max
 
 
-@pytest.mark.parametrize("kind", ["curn", "curn_red"])
-def test_pulsar_sharded_engine_bit_identical(kind):
-    """Two pulsar shards (own context, own DeviceModel) exchanging [tau | x_red] slabs
+@pytest.mark.parametrize("kind,nsh", [("curn", 2), ("curn_red", 2), ("curn_plred", 2), ("curn_plred", 3)])
+def test_pulsar_sharded_engine_bit_identical(kind, nsh):
+    """nsh pulsar shards (own context, own DeviceModel) exchanging [tau | x_red] slabs
     reproduce the unsharded engine's chains bit for bit under device Philox
-    (global chain and pulsar ids in the counters)."""
+    (global chain and pulsar ids in the counters).  curn_plred: the red MH block of the
+    reference's default redsample='mh' runs pulsar-sharded -- each shard applies the steps of its
+    own pulsars from the common step table, the power-law (log10_A, gamma) travel in the slab."""
     from pulsar_timing_gibbsspec_amd import _lib, synthetic
     from pulsar_timing_gibbsspec_amd.distributed import shard_range
     from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
+    from pulsar_timing_gibbsspec_amd.pta_hyper import HyperSpec
     pta = synthetic.array_pta(kind=kind, n_psr=9, seed=2)
     T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
     names = pta.param_names
@@ -240,32 +243,45 @@ def test_pulsar_sharded_engine_bit_identical(kind):
     gwid = [np.arange(t.shape[1] - 60, t.shape[1]) for t in T]
     fixed = [np.full(t.shape[1] - 60, 1e-40) for t in T]
     C, S = 16, 6
-    x0 = np.random.default_rng(0).uniform(-9, -4, (C, len(names)))
+    rng = np.random.default_rng(0)
+    x0 = rng.uniform(-9, -4, (C, len(names)))
     bounds = ((1e-18, 1e-8), (1e-20, 1e-8))
+    hy = {}
+    if kind == "curn_plred":
+        hidx = np.array([i for i, n in enumerate(names) if "red" in n and ("log10_A" in n or "gamma" in n)])
+        sigs = [s for s in (pta.signals[k] for k in pta.signals) if "red" in s.name]
+        spec = HyperSpec(pta, pta.params, sigs, hidx, np.zeros(len(names)), 30, "cuda")
+        x0[:, spec.hind] = rng.uniform(spec.hlo_host, spec.hhi_host, (C, spec.n_h))
+        hy = dict(hyper=spec, hyper_acl=9, hyper_warmup=30)
 
     ref_ctx = _lib.Context(0, seed=77)
-    ref = PTAChains(DeviceModel(ref_ctx, T, N, R, gwid, fixed), len(names), rind, red_col, *bounds, C, x0)
+    ref = PTAChains(DeviceModel(ref_ctx, T, N, R, gwid, fixed), len(names), rind, red_col, *bounds, C, x0, **hy)
     xr_ref = torch.zeros(S, C, len(names), dtype=torch.float64, device="cuda")
     for i in range(S):
         ref.sweep(x_rec=xr_ref[i])
 
     shards = []
-    for r in range(2):
-        lo, hi = shard_range(len(T), r, 2)
+    for r in range(nsh):
+        lo, hi = shard_range(len(T), r, nsh)
         ctx = _lib.Context(0, seed=77)
         mdl = DeviceModel(ctx, T[lo:hi], N[lo:hi], R[lo:hi], gwid[lo:hi], fixed[lo:hi])
         shards.append(PTAChains(mdl, len(names), rind, red_col, *bounds, C, x0, P_global=len(T), psr_lo=lo,
-                                gather=lambda s: s))
-    xr = [torch.zeros(S, C, len(names), dtype=torch.float64, device="cuda") for _ in range(2)]
+                                gather=lambda s: s, **hy))
+    xr = [torch.zeros(S, C, len(names), dtype=torch.float64, device="cuda") for _ in range(nsh)]
     for i in range(S):
         slabs = [sh.sweep_begin(x_rec=xr[j][i]) for j, sh in enumerate(shards)]
         glob = torch.cat(slabs, dim=0)            # the all-gather, in global pulsar order
         for sh in shards:
             sh.sweep_end(glob)
-    assert torch.equal(xr[0], xr_ref) and torch.equal(xr[1], xr_ref)
+    for j in range(nsh):
+        assert torch.equal(xr[j], xr_ref), j
+    if kind == "curn_plred":
+        assert not torch.equal(xr_ref[-1][:, spec.hind], xr_ref[0][:, spec.hind])     # the block moved
+        acc = sum(sh.hyper.acc_total for sh in shards)
+        assert torch.equal(acc, ref.hyper.acc_total)
     bref = ref.b.view(len(T), C, -1)
     for r, sh in enumerate(shards):
-        lo, hi = shard_range(len(T), r, 2)
+        lo, hi = shard_range(len(T), r, nsh)
         bs = sh.b.view(hi - lo, C, -1)
         w = bs.shape[2]
         assert torch.equal(bs, bref[lo:hi, :, :w]) and not bref[lo:hi, :, w:].any()
