@@ -817,9 +817,9 @@ def main():
         from oracle.cpu_baseline import ess_start
         ess_procs = {"single": ess_start("single", 500, 10000)}
         for kind in [k for k in args.pta.split(",") if k in ("curn", "curn_red", "curn_plred")]:
-            # (the MH line's CPU sweep is ~5 it/s: a shorter run, 100 + 400 sweeps)
-            ess_procs[kind] = ess_start(kind, 500 if kind != "curn_plred" else 100, 2000 if kind != "curn_plred"
-                                        else 400)
+            # >= 2000 recorded sweeps everywhere: a 400-sweep run is ~5 IATs of the MH line and its
+            # Sokal-window IAT comes out short, i.e. the ESS per sweep long
+            ess_procs[kind] = ess_start(kind, 500 if kind != "curn_plred" else 200, 2000)
 
     from pulsar_timing_gibbsspec_amd import _lib, synthetic
     from pulsar_timing_gibbsspec_amd.engine import DeviceModel, FreeSpectrumChains, HistoryStreamer

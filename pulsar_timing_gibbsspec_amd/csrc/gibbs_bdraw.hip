@@ -957,7 +957,12 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
           U = act ? A.u_inj[rec * NFR + kf] : 0.5;
         } else {
           double u2;
+#ifdef GS_PROBE_NO_RHO_PHILOX  // cost attribution only (wrong draws): the rho uniform without Philox
+          U = 0.25 + 0.5 * __builtin_amdgcn_fract(tau * 1e3);
+          (void)u2;
+#else
           gs_uniform2(gs_counter(kf, ii, gchain, p + A.psr_base, GS_EV_RHO), A.key, U, u2);
+#endif
         }
 #if GS_FAST_MATH
         // the reference's expressions with its divisions by the prior bounds as products with
@@ -979,7 +984,11 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
 #endif
         const double eta = 0.0 + hi * U;
 #if GS_FAST_MATH
+#ifdef GS_PROBE_NO_RHO_LOG  // cost attribution only (wrong draws)
+        const double den = t1 + eta;
+#else
         const double den = t1 - gs_log_pos(1 - eta);
+#endif
         const double rho = tau * rcp_nr2(den);
         const double xnew = act ? gs_log_pos(rho) * 0x1.bcb7b1526e50ep-3 : 0.0;  // 0.5 log10 rho
         // phiinv = 1/rho = den / tau
@@ -1009,7 +1018,12 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
         zF = act ? zinj[zrow * A.ldb + fi] : 0.0;
         zM = actm ? zinj[zrow * A.ldb + mi] : 0.0;
       } else {
+#ifdef GS_PROBE_NO_NORMALS  // cost attribution only (wrong draws): no Philox + Box-Muller pass
+        zF = __builtin_amdgcn_fract(x * 7.0) - 0.5;
+        zM = __builtin_amdgcn_fract(x * 3.0) - 0.5;
+#else
         gs_normal2(gs_counter(lane, ii, gchain, p + A.psr_base, ev), A.key, zF, zM);
+#endif
       }
       if (pass == 0) phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;  // first draw from xs
       GS_PH(7)

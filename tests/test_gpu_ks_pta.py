@@ -6,9 +6,17 @@ Reference: a 20k-sweep PTABlockGibbs.sample chain of the reference itself on the
 array (pta_gibbs.py:631-713; tests/golden/make_golden.py --only-pta-long-<kind>, seeded,
 single-threaded BLAS), thinned per bin by its own integrated autocorrelation time so its draws
 are ~independent.  Device: chains in the bench's modes -- CURN from the tau sums
-(curn_mode='sum', the fixed-point sufficient statistic and k_rho_curn_sum_wave), CURN + red
-with the default fast grid kernels (k_rho_red_wave, k_rho_curn_fast) -- one draw per
+(curn_mode='sum', the fixed-point sufficient statistic and k_rho_curn_sum_cert16), CURN + red
+with the default certified grid kernels (k_rho_red_cert16, k_rho_curn_fast) -- one draw per
 independent chain after burn-in.  Bonferroni over the tested bins.
+
+curn_plred: the reference's DEFAULT model (redsample='mh': per-pulsar power-law red noise by the
+Metropolis block, pta_gibbs.py:278-340) on 6 pulsars, against six independent 40k-sweep runs of
+the reference's own methods in sample()'s order (make_golden.py --only-pta-long-plred; sample()
+itself cannot pass sweep 0 on this path, so the 100 warm-up steps run through the steady-state
+branch, aclength_hyper = 20 after), every common log10 rho bin and every pulsar's (log10_A,
+gamma).  Device: k_hyper_mh with device Philox (no injected draws), the lnL seed from the gated
+k_bdraw_tiled draw, k_rho_curn_fast with the power-law irn.
 """
 import numpy as np
 import pytest
@@ -22,20 +30,37 @@ torch = pytest.importorskip("torch")
 ALPHA = 1e-3
 
 
-def _ref_draws(kind, burn=1000):
+PLRED_PSR = 6       # the curn_plred reference runs' array (make_golden.pta_long_plred)
+
+
+def _thin(c, burn):
     from pulsar_timing_gibbsspec_amd.diagnostics import iat
+    c = c[burn:]
+    return [c[::max(1, int(np.ceil(iat(c[:, k])))), k] for k in range(c.shape[1])]
+
+
+def _ref_draws(kind, burn=1000):
+    if kind == "curn_plred":
+        import glob
+        import os
+
+        from tests.conftest import GOLDEN
+        files = sorted(glob.glob(os.path.join(GOLDEN, "pta_long_curn_plred_s*.npz")))
+        if not files:
+            raise FileNotFoundError("pta_long_curn_plred_s*.npz")
+        parts, g = [], None
+        for f in files:                         # each independent run thinned by its own IATs
+            g = np.load(f, allow_pickle=False)
+            parts.append(_thin(g["chain"].astype(np.float64), burn // int(g["thin"])))
+        out = [np.concatenate([p[k] for p in parts]) for k in range(len(parts[0]))]
+        return out, list(g["names"]), np.asarray(g["cols"])
     g = golden(f"pta_long_{kind}.npz")
-    c = g["chain"].astype(np.float64)[burn:]
-    out = []
-    for k in range(c.shape[1]):
-        t = max(1, int(np.ceil(iat(c[:, k]))))
-        out.append(c[::t, k])
-    return out, list(g["names"]), np.asarray(g["cols"])
+    return _thin(g["chain"].astype(np.float64), burn), list(g["names"]), np.asarray(g["cols"])
 
 
 def _device_draws(kind, C=2048, sweeps=1500, seed=77):
     from pulsar_timing_gibbsspec_amd import PTABlockGibbs, synthetic
-    pta = synthetic.array_pta(kind=kind, seed=0)
+    pta = synthetic.array_pta(kind=kind, seed=0, n_psr=PLRED_PSR if kind == "curn_plred" else None)
     gb = PTABlockGibbs(pta, hypersample="conditional", redsample="conditional" if kind == "curn_red" else "mh",
                        nchains=C, seed=seed)
     rng = np.random.default_rng(seed)
@@ -44,6 +69,10 @@ def _device_draws(kind, C=2048, sweeps=1500, seed=77):
     assert eng.curn_mode == ("sum" if kind == "curn" else "exact")
     # independent starting points over the prior, one per chain
     x = rng.uniform(lo, hi, (C, len(gb.param_names)))
+    if eng.hyper is not None:
+        hs = eng.hyper_spec
+        x[:, hs.hind] = rng.uniform(hs.hlo_host, hs.hhi_host, (C, hs.n_h))
+        eng.hyper_acl = 20                      # the reference runs' aclength_hyper
     eng.x.copy_(torch.as_tensor(x, device=eng.ctx.device))
     for _ in range(sweeps):
         eng.sweep()
@@ -51,7 +80,7 @@ def _device_draws(kind, C=2048, sweeps=1500, seed=77):
     return eng.x.cpu().numpy(), list(gb.param_names)
 
 
-@pytest.mark.parametrize("kind", ["curn", "curn_red"])
+@pytest.mark.parametrize("kind", ["curn", "curn_red", "curn_plred"])
 def test_pta_posterior_ks_against_reference(kind):
     try:
         ref, names_ref, cols = _ref_draws(kind)
