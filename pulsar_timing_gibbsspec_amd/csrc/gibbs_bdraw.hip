@@ -374,6 +374,10 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
 #ifndef GS_BDRAW_TILED
 #define GS_BDRAW_TILED 0
 #endif
+// k_bdraw_tiled's persistent ranges in XCD-major order (1) or in workgroup order (0)
+#ifndef GS_BDRAW_XCD
+#define GS_BDRAW_XCD 1
+#endif
 // lnl[sys] of k_lnlike_marg from the two factorisation terms (gs_ctx_set_bdraw_lnl)
 __device__ __forceinline__ void bdraw_lnl_store(const BdrawArgs& A, int p, int64_t sys, int NF, int lane, double phinv,
                                                 int fail, double yy, double lp) {
@@ -509,7 +513,12 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
     // (pulsar, chain group) items [w n / G, (w + 1) n / G) in pulsar-major order: every workgroup
     // draws the same number of groups, restaging the model only where its range crosses a pulsar
     const int64_t n_items = (int64_t)A.n_psr * nb;
-    const int64_t lo = (int64_t)blockIdx.x * n_items / A.persist, hi = (int64_t)(blockIdx.x + 1) * n_items / A.persist;
+    // XCD-major ranges: workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
+    // one, MI355X_MICROARCH.md), so the workgroups of one XCD take one contiguous run of items --
+    // each pulsar's block is fetched into one or two XCDs' L2 instead of all eight
+    int64_t w = blockIdx.x;
+    if (GS_BDRAW_XCD && (A.persist & 7) == 0) w = (w & 7) * (A.persist >> 3) + (w >> 3);
+    const int64_t lo = w * n_items / A.persist, hi = (w + 1) * n_items / A.persist;
     int cur = -1, nM = 0, fi = 0, mi = 0, NMXe = A.NMX;
     ModelTiled M;
 #pragma unroll 1

@@ -541,6 +541,31 @@ def pulsar_ptas(pta):
     return [PTA([m]) for m in pta.models]
 
 
+def config5_pulsar_pta(seed=1, n_toa=10_000, n_f=100, n_tm=16, n_bk=4, span_yr=15.0, rho_prior=(-9.0, -4.0),
+                       efac_prior=(0.5, 2.0), equad_prior=(-8.5, -5.0), log10_A=np.log10(2e-15), gamma=13.0 / 3.0):
+    """One pulsar of BASELINE configs[4] as an enterprise-shaped single-pulsar PTA (the shapes of
+    ``config5_array``: 10^4 TOAs, n_bk backends with EFAC / log10 EQUAD, an n_f-bin free spectrum,
+    an n_tm-column timing model; signals white, gw, tm -> T = [F | M]), for drivers that take a
+    PTA -- e.g. the reference's own PulsarBlockGibbs in tools/calibrate_cpu_baseline.py."""
+    rng = np.random.default_rng(seed)
+    Tspan = span_yr * 365.25 * DAY
+    psr = "C5P0000"
+    toas = np.sort(rng.uniform(0.0, Tspan, n_toa))
+    sigma = 10 ** rng.uniform(np.log10(0.05e-6), np.log10(5e-6), n_toa)
+    bk = np.minimum((np.arange(n_toa) * n_bk) // n_toa, n_bk - 1)
+    efp = [Uniform(f"{psr}_b{k}_efac", *efac_prior) for k in range(n_bk)]
+    eqp = [Uniform(f"{psr}_b{k}_log10_tnequad", *equad_prior) for k in range(n_bk)]
+    white = MeasurementNoise(psr, sigma, bk, efp, eqp)
+    rho = Uniform("gw_log10_rho", rho_prior[0], rho_prior[1], size=n_f)
+    gw = FourierGP(psr, "gw", toas, Tspan, n_f, "spectrum", [rho])
+    tm = TimingModelGP(psr, synthetic_design_matrix(toas, n_tm), use_svd=True)
+    ef = rng.uniform(*efac_prior, n_bk)[bk]
+    eq = 10 ** rng.uniform(*equad_prior, n_bk)[bk]
+    r = _simulate_residuals(rng, gw.get_basis(), gw.freqs, Tspan, tm.get_basis(), np.sqrt(ef ** 2 * sigma ** 2 + eq ** 2),
+                            log10_A, gamma)
+    return PTA([PulsarModel(psr, toas, r, [white, gw, tm])])
+
+
 def config5_array(n_psr=200, n_toa=10_000, n_f=100, n_tm=16, n_bk=4, span_yr=15.0, seed=0,
                   rho_prior=(-9.0, -4.0), efac_prior=(0.5, 2.0), equad_prior=(-8.5, -5.0),
                   log10_A=np.log10(2e-15), gamma=13.0 / 3.0):

@@ -94,3 +94,54 @@ def test_pta_posterior_ks_against_reference(kind):
         pv.append(ks_2samp(x[:, c], ref[j]).pvalue)
     pv = np.array(pv)
     assert pv.min() > ALPHA / len(pv), (kind, pv.min(), int(np.argmin(pv)), [len(r) for r in ref][:5])
+
+
+def _lag1(rows):
+    """Pooled lag-1 autocorrelation per column of (chains, n, k) rows, each chain demeaned."""
+    x = rows - rows.mean(axis=1, keepdims=True)
+    return np.sum(x[:, 1:] * x[:, :-1], axis=(0, 1)) / np.sum(x * x, axis=(0, 1))
+
+
+def test_plred_mixing_matches_reference():
+    """The device's Markov kernel mixes like the reference's on the reference-default model
+    (curn_plred, redsample='mh', aclength_hyper 20): the lag-10-sweep autocorrelation of every
+    common log10 rho bin and every (log10_A, gamma) agrees with the six 40k-sweep reference runs
+    (their rows are every 10th sweep) within 5 standard errors (the reference's from the spread over
+    its six runs, floored at 0.01).  ESS per sweep follows from these autocorrelations; this is the
+    like-for-like check behind the bench's GPU vs CPU ESS figures."""
+    import glob
+    import os
+
+    from pulsar_timing_gibbsspec_amd import PTABlockGibbs, synthetic
+    from tests.conftest import GOLDEN
+    files = sorted(glob.glob(os.path.join(GOLDEN, "pta_long_curn_plred_s*.npz")))
+    if len(files) < 3:
+        pytest.skip("reference plred runs not generated")
+    refs = [np.load(f, allow_pickle=False) for f in files]
+    thin, names_ref, cols = int(refs[0]["thin"]), list(refs[0]["names"]), np.asarray(refs[0]["cols"])
+    burn = 2000 // thin
+    r_ref = np.stack([_lag1(g["chain"].astype(np.float64)[burn:][None]) for g in refs])   # (runs, k)
+    se = np.maximum(r_ref.std(axis=0, ddof=1) / np.sqrt(len(refs)), 0.01)
+    C, rows = 512, 1500
+    pta = synthetic.array_pta(kind="curn_plred", seed=0, n_psr=PLRED_PSR)
+    gb = PTABlockGibbs(pta, nchains=C, seed=19)
+    eng = gb._new_engine(np.zeros(len(gb.param_names)))
+    assert [gb.param_names[c] for c in cols] == names_ref
+    rng = np.random.default_rng(19)
+    lo, hi = np.log10(gb.rhomin_gw) / 2, np.log10(gb.rhomax_gw) / 2
+    x = rng.uniform(lo, hi, (C, len(gb.param_names)))
+    hs = eng.hyper_spec
+    x[:, hs.hind] = rng.uniform(hs.hlo_host, hs.hhi_host, (C, hs.n_h))
+    eng.hyper_acl = 20
+    eng.x.copy_(torch.as_tensor(x, device=eng.ctx.device))
+    for _ in range(2000):                                    # burn-in, as the reference rows above
+        eng.sweep()
+    rec = torch.empty(rows, C, len(cols), dtype=torch.float64, device=eng.ctx.device)
+    ci = torch.as_tensor(cols, dtype=torch.long, device=eng.ctx.device)
+    for i in range(rows):
+        for _ in range(thin):
+            eng.sweep()
+        rec[i] = eng.x.index_select(1, ci)
+    r_dev = _lag1(rec.cpu().numpy().transpose(1, 0, 2))
+    z = np.abs(r_dev - r_ref.mean(axis=0)) / se
+    assert z.max() < 5.0, (names_ref[int(np.argmax(z))], float(z.max()), np.round(r_dev, 3), np.round(r_ref.mean(0), 3))
