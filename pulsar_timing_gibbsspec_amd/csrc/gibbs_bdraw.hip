@@ -374,9 +374,13 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
 #ifndef GS_BDRAW_TILED
 #define GS_BDRAW_TILED 0
 #endif
-// k_bdraw_tiled's persistent ranges in XCD-major order (1) or in workgroup order (0)
+// k_bdraw_tiled's persistent ranges in XCD-major order (1) or in workgroup order (0).  Measured on
+// MI355X (r05b, interleaved A/B, 2048 chains x 45 pulsars): XCD-major was SLOWER -- CURN 4.01e6 vs
+// 4.11-4.12e6 chain-it/s, curn_plred 1.75e6 vs 1.78e6 -- although it fetches each pulsar's block
+// into one or two XCDs' L2 instead of eight: the draw is issue bound, and a contiguous run of
+// pulsars per XCD loads the XCDs unevenly (the per-pulsar cost varies with the timing model).  Off.
 #ifndef GS_BDRAW_XCD
-#define GS_BDRAW_XCD 1
+#define GS_BDRAW_XCD 0
 #endif
 // lnl[sys] of k_lnlike_marg from the two factorisation terms (gs_ctx_set_bdraw_lnl)
 __device__ __forceinline__ void bdraw_lnl_store(const BdrawArgs& A, int p, int64_t sys, int NF, int lane, double phinv,
@@ -513,9 +517,9 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
     // (pulsar, chain group) items [w n / G, (w + 1) n / G) in pulsar-major order: every workgroup
     // draws the same number of groups, restaging the model only where its range crosses a pulsar
     const int64_t n_items = (int64_t)A.n_psr * nb;
-    // XCD-major ranges: workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
-    // one, MI355X_MICROARCH.md), so the workgroups of one XCD take one contiguous run of items --
-    // each pulsar's block is fetched into one or two XCDs' L2 instead of all eight
+    // GS_BDRAW_XCD (off): XCD-major ranges -- workgroups are dealt round-robin over the 8 XCDs
+    // (blocks b and b + 8 share one, MI355X_MICROARCH.md), so the workgroups of one XCD would take
+    // one contiguous run of items
     int64_t w = blockIdx.x;
     if (GS_BDRAW_XCD && (A.persist & 7) == 0) w = (w & 7) * (A.persist >> 3) + (w >> 3);
     const int64_t lo = w * n_items / A.persist, hi = (w + 1) * n_items / A.persist;
@@ -797,6 +801,14 @@ __global__ __launch_bounds__(64 * GS_HY_W, GS_HY_W == 1 ? 2 : 3) void k_hyper_mh
 }
 
 // ------------------------------------------------------------ fused sweep
+// GS_RNG_MERGE (off): one Philox block per lane per sweep for the rho uniforms and the normals.
+// Measured on MI355X (r05d/r05e, interleaved A/B, 4096 chains, 300 launches): 2.078-2.086 ms per
+// launch merged vs 2.042-2.049 with the two blocks -- the crossbar redistribution and the pair kept
+// for Box-Muller raise the 12-wave kernel's spills 6 -> 19-26 VGPRs, which costs more than the 2.0 %
+// the rho uniforms' Philox pass takes (profiles/r05b).
+#ifndef GS_RNG_MERGE
+#define GS_RNG_MERGE 0
+#endif
 #ifndef GS_RHO_EXP
 #define GS_RHO_EXP 0
 #endif
@@ -934,6 +946,15 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
     const int64_t brow0 = A.brec_nc == 0 ? sys : (int64_t)p * A.brec_nc + c;
     double* bFp = (brec && act) ? A.b_rec + sw_a * br_step + brow0 * A.ldb + fi : nullptr;
     double* bMp = (brec && actm) ? A.b_rec + sw_a * br_step + brow0 * A.ldb + mi : nullptr;
+  // Merged RNG (production draws: nothing injected): ONE Philox block per lane per sweep feeds both
+  // the rho|b uniforms and the b|rho normals.  Lane l < npair turns its two 53-bit uniforms into the
+  // Box-Muller pair (normals 2l, 2l+1 of [z_F | z_M]); lane npair + j lends its two uniforms to
+  // frequencies 2j, 2j+1 of the rho draw; the values reach their consumer lanes through the LDS
+  // crossbar (ds_bpermute, no VALU).  One Philox pass per sweep instead of two (the separate rho
+  // uniforms cost 2.0 % of the headline launch, profiles/r05b); falls back to the two-block scheme
+  // when the lanes do not suffice (NF + nM + NF / 2 > 128).
+  const int npair = (NF + nM + 1) >> 1;
+  const bool mrg = GS_RNG_MERGE && !A.u_inj && !A.z_inj && npair + ((NFR + 1) >> 1) <= 64;
 #pragma unroll 1
   for (int sw = sw_a; sw < sw_b; ++sw) {
     const long long ii = A.it0 + sw;
@@ -964,6 +985,16 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
         double U;
         if (A.u_inj) {
           U = act ? A.u_inj[rec * NFR + kf] : 0.5;
+        } else if (mrg) {
+          double mu1, mu2;
+          gs_uniform2(gs_counter(lane, ii, gchain, p + A.psr_base, GS_EV_B), A.key, mu1, mu2);
+          const int src = npair + (kf >> 1);
+          const double ua = gtile::bcast_lane_bp(mu1, src), ub = gtile::bcast_lane_bp(mu2, src);
+          U = (kf & 1) ? ub : ua;
+          // the pair waits for Box-Muller in the wave's save slot (free until the draw), not in
+          // 4 VGPRs across the rho step (26 spilled VGPRs that way)
+          bsave[lane] = mu1;
+          bsave[64 + lane] = mu2;
         } else {
           double u2;
 #ifdef GS_PROBE_NO_RHO_PHILOX  // cost attribution only (wrong draws): the rho uniform without Philox
@@ -1031,7 +1062,20 @@ __device__ __forceinline__ void sweep_freespec_body(const SweepArgs& A) {
         zF = __builtin_amdgcn_fract(x * 7.0) - 0.5;
         zM = __builtin_amdgcn_fract(x * 3.0) - 0.5;
 #else
-        gs_normal2(gs_counter(lane, ii, gchain, p + A.psr_base, ev), A.key, zF, zM);
+        if (mrg && pass == 1) {
+          // normal j of [z_F | z_M] is component j & 1 of lane j >> 1's pair
+          double n1, n2;
+          gtile::lds_fence();
+          gs_box_muller(bsave[lane], bsave[64 + lane], n1, n2);
+          gtile::lds_fence();
+          const int sf = lane >> 1, sm = (NF + lane) >> 1;
+          const double f1 = gtile::bcast_lane_bp(n1, sf), f2 = gtile::bcast_lane_bp(n2, sf);
+          const double m1 = gtile::bcast_lane_bp(n1, sm), m2 = gtile::bcast_lane_bp(n2, sm);
+          zF = (lane & 1) ? f2 : f1;
+          zM = ((NF + lane) & 1) ? m2 : m1;
+        } else {
+          gs_normal2(gs_counter(lane, ii, gchain, p + A.psr_base, ev), A.key, zF, zM);
+        }
 #endif
       }
       if (pass == 0) phinv = act ? 1.0 / pow(10.0, 2.0 * x) : 0.0;  // first draw from xs

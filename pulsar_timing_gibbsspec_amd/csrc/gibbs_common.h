@@ -236,15 +236,34 @@ __device__ __forceinline__ void gs_sincos2pi(double u, double& sn, double& cs) {
 #endif
 }
 
-// Two independent standard normals (Box-Muller) for one counter.
-__device__ __forceinline__ void gs_normal2(gs_u4 c, gs_key k, double& n1, double& n2) {
-  double u1, u2;
-  gs_uniform2(c, k, u1, u2);
-  const double r = sqrt(-2.0 * gs_log_pos(1.0 - u1));
+// sqrt(x) for finite x >= 0: x v_rsq_f64(x) with two Newton steps on the reciprocal root (~1 ulp;
+// 0 at x = 0) instead of the IEEE sequence's scaling, fixups and class checks (~15 VALU -> 9)
+__device__ __forceinline__ double gs_sqrt_nn(double x) {
+#if GS_FAST_MATH
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  y = y * fma(-hx * y, y, 1.5);
+  y = y * fma(-hx * y, y, 1.5);
+  return x > 0.0 ? x * y : 0.0;
+#else
+  return sqrt(x);
+#endif
+}
+
+// Two independent standard normals from two uniforms in [0, 1) (Box-Muller).
+__device__ __forceinline__ void gs_box_muller(double u1, double u2, double& n1, double& n2) {
+  const double r = gs_sqrt_nn(-2.0 * gs_log_pos(1.0 - u1));
   double s, co;
   gs_sincos2pi(u2, s, co);
   n1 = r * co;
   n2 = r * s;
+}
+
+// Two independent standard normals (Box-Muller) for one counter.
+__device__ __forceinline__ void gs_normal2(gs_u4 c, gs_key k, double& n1, double& n2) {
+  double u1, u2;
+  gs_uniform2(c, k, u1, u2);
+  gs_box_muller(u1, u2, n1, n2);
 }
 
 // ---------------------------------------------------------------- separately rounded ops

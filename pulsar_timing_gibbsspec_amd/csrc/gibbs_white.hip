@@ -331,11 +331,19 @@ __host__ __device__ constexpr int sy_ld(int nb) { return 16 * nb + ((nb & 1) ? 0
 // B operand per block column per 4-TOA step shared by both rows (NB+2 LDS reads and 2
 // multiplies per NB+1 MFMAs).  The wave index is made uniform (readfirstlane) so the
 // ownership tests are scalar branches and the MFMAs issue back to back.
+// BAL (NB = 2 SY_WAVES - 2, e.g. m + 1 = 217 -> NB = 14): the paired rows leave the last wave idle
+// (NH = SY_WAVES - 1 waves with NB + 1 tiles each); instead the last wave takes the NB diagonal tiles
+// and every pair wave keeps its NB - 1 off-diagonal ones -- at most 2 NB - 1 MFMAs per 4-TOA step on
+// a SIMD (its two waves) instead of 2 NB + 2, and no idle SIMD slot.
+#ifndef GS_SY_BAL
+#define GS_SY_BAL 1
+#endif
 template <int NB>
 __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
   extern __shared__ double lds[];
   __shared__ double sb[3][GS_WHITE_MAX_BK + 1];
-  constexpr int NH = (NB + 1) / 2;  // waves with tiles
+  constexpr bool BAL = GS_SY_BAL && NB == 2 * SY_WAVES - 2;
+  constexpr int NH = (NB + 1) / 2;  // waves with paired rows
   constexpr int LDC = sy_ld(NB), WC = 16 * NB;
   const int64_t n_sys = (int64_t)A.n_psr * A.n_chain;
   // XCD-major: consecutive workgroup ids go round-robin over the 8 XCDs
@@ -399,34 +407,60 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
   load(0);
   store(buf0);
   __syncthreads();
-  for (int64_t ch = 0; ch < nch; ++ch) {
-    const double* cur = (ch & 1) ? buf1 : buf0;
-    double* nxt = (ch & 1) ? buf0 : buf1;
-    if (ch + 1 < nch) load((ch + 1) * SY_TC);
-    // keep the next chunk's global loads here, ahead of the MFMAs: their latency is
-    // hidden behind this chunk's math (the scheduler would otherwise sink them)
-    __builtin_amdgcn_sched_barrier(0);
-    if (act) {
+  // the chunk loop, instantiated once per role so each role's registers are allocated on their own
+  // (role 1: the diagonal-tile wave of BAL; role 0: the paired-row waves).  Measured (r05e/r05f):
+  // the diagonal wave in slots 0..NB-1 of the shared accumulator array 389-392 config5 sweeps/s,
+  // with its own accumulator array 373 (= the unbalanced kernel's 372-374).
+  auto stream = [&](auto role) {
+    for (int64_t ch = 0; ch < nch; ++ch) {
+      const double* cur = (ch & 1) ? buf1 : buf0;
+      double* nxt = (ch & 1) ? buf0 : buf1;
+      if (ch + 1 < nch) load((ch + 1) * SY_TC);
+      // keep the next chunk's global loads here, ahead of the MFMAs: their latency is
+      // hidden behind this chunk's math (the scheduler would otherwise sink them)
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (decltype(role)::value == 1) {
+        // the diagonal tiles (j, j), j < NB: A = row j / N, B = row j; one 4-TOA step at a time
+        // (an unrolled step loop hoists every step's products and spills)
+#pragma unroll 1
+        for (int kk = 0; kk < SY_TC / 4; ++kk) {
+          const double* row = cur + (4 * kk + k) * LDC + i;
+          const double iv = cur[SY_TC * LDC + 4 * kk + k];
 #pragma unroll
-      for (int kk = 0; kk < SY_TC / 4; ++kk) {
-        const double* row = cur + (4 * kk + k) * LDC + i;
-        const double iv = cur[SY_TC * LDC + 4 * kk + k];
-        const double a1 = row[16 * r1] * iv;
-        const double a2 = row[16 * r2] * iv;
-        double bv[NB];  // every B operand of the step in flight at once
+          for (int j = 0; j < NB; ++j) {
+            const double bj = row[16 * j];
+            acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(bj * iv, bj, acc[j], 0, 0, 0);
+          }
+        }
+      } else if (act) {
 #pragma unroll
-        for (int j = 0; j < NB; ++j) bv[j] = row[16 * j];
+        for (int kk = 0; kk < SY_TC / 4; ++kk) {
+          const double* row = cur + (4 * kk + k) * LDC + i;
+          const double iv = cur[SY_TC * LDC + 4 * kk + k];
+          const double a1 = row[16 * r1] * iv;
+          const double a2 = row[16 * r2] * iv;
+          double bv[NB];  // every B operand of the step in flight at once
 #pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          if (j <= r2) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, bv[j], acc[j], 0, 0, 0);
-          if (two && j <= r1) acc[NB - j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bv[j], acc[NB - j], 0, 0, 0);
+          for (int j = 0; j < NB; ++j) bv[j] = row[16 * j];
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            // BAL: the diagonal tiles belong to the last wave
+            if (BAL ? j < r2 : j <= r2) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, bv[j], acc[j], 0, 0, 0);
+            if (two && (BAL ? j < r1 : j <= r1))
+              acc[NB - j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bv[j], acc[NB - j], 0, 0, 0);
+          }
         }
       }
+      if (ch + 1 < nch) store(nxt);
+      __syncthreads();
     }
-    if (ch + 1 < nch) store(nxt);
-    __syncthreads();
-  }
-  if (!act) return;
+  };
+  const bool diagw = BAL && w == SY_WAVES - 1;
+  if (diagw)
+    stream(std::integral_constant<int, 1>{});
+  else
+    stream(std::integral_constant<int, 0>{});
+  if (!act && !diagw) return;
 
   double* out = A.TNT + D.tnt_off + (int64_t)c * A.tnt_cstride;
   double* dout = A.d + D.d_off + (int64_t)c * A.d_cstride;
@@ -443,10 +477,17 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
       }
     }
   };
+  if constexpr (BAL) {
+    if (diagw) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) emit(j, j, acc[j]);
+      return;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    if (j <= r2) emit(r2, j, acc[j]);
-    if (two && j <= r1) emit(r1, j, acc[NB - j]);
+    if (BAL ? j < r2 : j <= r2) emit(r2, j, acc[j]);
+    if (two && (BAL ? j < r1 : j <= r1)) emit(r1, j, acc[NB - j]);
   }
 }
 
