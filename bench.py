@@ -51,7 +51,7 @@ def executed_flops_per_chain_sweep(nf, nm):
 
 def pmc_traffic(S, C):
     """HBM bytes per launch of k_sweep_freespec from the committed PMC profile
-    (tools/gpu_profile.sh -> tools/pmc_traffic.py), valid for the same launch shape."""
+    (tools/archive/gpu_profile.sh -> tools/pmc_traffic.py), valid for the same launch shape."""
     f = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(f))
@@ -318,6 +318,7 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
         own = float(np.mean((hm.hpsr >= 0).cpu().numpy()))
         kernels["k_hyper_mh"] = dict(
             kernel_avg_ms=ms_mh, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
+            traffic=_ecorr_traffic(C, "pmc_traffic_hyper.json") if own == 1.0 else None,
             achieved=own * HYPER_ACL * C * fl / (ms_mh * 1e-3) / 1e12, alg_per_launch=own * HYPER_ACL * C * fl,
             own_step_share=own,
             note=f"{HYPER_ACL} single-parameter MH steps per chain (pta_gibbs.py:319-340), each one pulsar's "
@@ -355,7 +356,7 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
             alg_bytes_per_launch=eng.P * n_f * C * 24,
             note="grid-point evaluations ratio*exp(-ratio/2)*ln10 (pta_gibbs.py:265-266): P x n_f x C x 1000 "
                  "per launch (certified f32 pass, f64 redo of unproven rows: f64_redo_rows_frac); traffic: PMC "
-                 "FETCH_SIZE x2 + WRITE_SIZE per launch (tools/gpu_pmc_red.sh; algorithmic 24 B per row: tau, "
+                 "FETCH_SIZE x2 + WRITE_SIZE per launch (tools/archive/gpu_pmc_red.sh; algorithmic 24 B per row: tau, "
                  "irn and the x write) -- ~60 GB/s, far from the HBM roof; peak = "
                  "hardware VALU issue rate / the minimal op count per point in packed f32 (5 plain ops = 2.5 "
                  "v_pk_* slots at 4 cycles + rcp and exp at 8 per wave64: 26 cycles)")
@@ -532,13 +533,14 @@ def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, a
                           "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": tflops / FP64_PEAK_TFLOPS, "kernel_avg_ms": refresh_ms,
                           "alg_flops_per_launch": flops,
+                          "traffic": _ecorr_traffic(C, "pmc_traffic_syrk.json") if n_psr == 200 else None,
                           "note": "per-chain TNT/d of all 200 pulsars (n m (m+1) + 2 n m flop per system) "
                                   "over the HIP-event time of one refresh (SYRK + prefix)"})
 
 
 def _ecorr_traffic(C, fname="pmc_traffic_ecorr.json"):
     """HBM bytes per launch of k_ecorr_prefix<likelihood> from the committed PMC passes
-    (tools/gpu_pmc_ecorr.sh -> profiles/pmc_traffic_ecorr.json for the shared-operand kernel,
+    (tools/archive/gpu_pmc_ecorr.sh -> profiles/pmc_traffic_ecorr.json for the shared-operand kernel,
     profiles/pmc_traffic_ecorr_white.json for the per-chain-operand one), same chain count only."""
     try:
         d = json.load(open(os.path.join(ROOT, "profiles", fname)))

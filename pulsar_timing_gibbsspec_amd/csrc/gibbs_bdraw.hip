@@ -385,7 +385,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
 // lnl[sys] of k_lnlike_marg from the two factorisation terms (gs_ctx_set_bdraw_lnl)
 __device__ __forceinline__ void bdraw_lnl_store(const BdrawArgs& A, int p, int64_t sys, int NF, int lane, double phinv,
                                                 int fail, double yy, double lp) {
-  double lph = lane < NF ? log(phinv) : 0.0;
+  double lph = lane < NF ? gs_log_lnl(phinv) : 0.0;  // phinv > 0 (lnl_terms)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) lph += __shfl_xor(lph, o);
   if (lane == 0) {
@@ -580,7 +580,7 @@ __device__ __forceinline__ void lnlike_item(const LnlArgs& A, const double* mb, 
     fail = bdraw_tile_n<NTC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr, NF);
   else
     fail = bdraw_tile<NFC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr);
-  double lph = lane < NF ? log(phinv) : 0.0;
+  double lph = lane < NF ? gs_log_lnl(phinv) : 0.0;  // phinv > 0 (lnl_terms)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) lph += __shfl_xor(lph, o);
   const int64_t ao = model_aux_offset(NF, A.NMX);
@@ -763,7 +763,7 @@ __global__ __launch_bounds__(64 * GS_HY_W, GS_HY_W == 1 ? 2 : 3) void k_hyper_mh
           fail = bdraw_tile_n<NTC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr, NF);
         else
           fail = bdraw_tile<NFC, true>(M, A.NMX, A.nm[p], lane, phinv, 0.0, 0.0, yy, ldS, scr);
-        double lph = act ? log(phinv) : 0.0;
+        double lph = act ? gs_log_lnl(phinv) : 0.0;  // as gs_lnlike_marg (bit-identical seeds)
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) lph += __shfl_xor(lph, o);
         const int64_t ao = model_aux_offset(NF, A.NMX);

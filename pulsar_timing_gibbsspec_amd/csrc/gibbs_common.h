@@ -147,6 +147,19 @@ __device__ __forceinline__ double gs_log_pos(double x) {
 #endif
 }
 
+// log of the marginalised likelihood's terms (lnl_terms' pivots, the sum of log phiinv): gs_log_pos,
+// or libm's log with GS_LNL_LIBM=1 (A/B builds)
+#ifndef GS_LNL_LIBM
+#define GS_LNL_LIBM 0
+#endif
+__device__ __forceinline__ double gs_log_lnl(double x) {
+#if GS_LNL_LIBM
+  return log(x);
+#else
+  return gs_log_pos(x);
+#endif
+}
+
 // exp(x) for x <= 0 (the grid pdfs' exponents; -inf and NaN-free inputs below -800 give 0):
 // n = rint(x log2 e), r = x - n ln2 (two-term Cody-Waite), the degree-11 minimax polynomial
 // of the device library's exp on |r| <= ln2/2, ldexp.  No overflow / special-case branches

@@ -45,7 +45,7 @@ __device__ __forceinline__ double ec_wave_sum_u(double v) {
 __device__ __forceinline__ void ec_phi(double x, double& inv, double& lg) {
   const double ph = pow(10.0, 2.0 * x);
   inv = 1.0 / ph;
-  lg = log(ph);
+  lg = gs_log_lnl(ph);
 }
 
 // Batched ECORR Schur complement, one wavefront per chain, EC_WAVES chains per
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
         const int kb = A.ebk[e];
         const double a = A.Dg[e] + sinv[w][kb];
         wreg = 1.0 / a;
-        sla += log(a);
+        sla += gs_log_lnl(a);
         slp += slog[w][kb];
       }
     }
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
         const int kb = A.ebk[e];
         const double a = A.Dg[e] + sinv[w][kb];
         wreg = 1.0 / a;
-        sla += log(a);
+        sla += gs_log_lnl(a);
         slp += slog[w][kb];
       }
     }
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
         const int kb = A.ebk[e];
         const double a = Dc[e] + sinv[w][kb];
         wv = 1.0 / a;
-        sla += log(a);
+        sla += gs_log_lnl(a);
         slp += slog[w][kb];
       }
       wave_lds_sync();  // previous chunk's LDS reads are done before the overwrite

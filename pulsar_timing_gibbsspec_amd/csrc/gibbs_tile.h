@@ -568,10 +568,12 @@ struct model_is_tiled<ModelTiled> {
 // (U^T y = dF) at tb[128 + l] and the pivot^-1/2 of column l at tb[l] (bdraw_tile_core, LNL != 0);
 // |y|^2 = sum y_l^2 and log det S = sum -2 log(pivot^-1/2), one term per lane, wave-summed in one
 // fixed order.  The draw (after its solves) and the likelihood mode run the same code: bit-identical.
+// The logs are gs_log_pos (0.77 ulp, ~35 VALU) rather than libm's (~90): with the phiinv term below
+// they were about a fifth of a likelihood-mode factorisation's VALU (k_hyper_mh, r05).
 __device__ __forceinline__ void lnl_terms(const double* tb, int lane, int NF, double& yy, double& lp) {
   const double y = lane < NF ? tb[128 + lane] : 0.0;
   yy = y * y;
-  lp = lane < NF ? -2.0 * log(tb[lane]) : 0.0;
+  lp = lane < NF ? -2.0 * gs_log_lnl(tb[lane]) : 0.0;  // (a failed pivot's lane: the caller returns -inf)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     yy += __shfl_xor(yy, o);
