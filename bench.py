@@ -745,7 +745,31 @@ def launch_ranks(args_list, n):
     return subprocess.call(cmd, env=env)
 
 
+_PHASE = ["start"]
+
+
+def phase(name):
+    """Progress marker on stderr (stdout carries only the result line)."""
+    _PHASE[0] = name
+    print(f"[bench] {name}", file=sys.stderr, flush=True)
+
+
+def _heartbeat(period=30.0):
+    """A line on stderr every ``period`` seconds while the bench runs, so a supervisor that takes a
+    silent command for a hung one (no output for minutes) sees the CPU-baseline and ESS phases --
+    several minutes of host work with nothing else to print -- as alive."""
+    import threading
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(period)
+            print(f"[bench] ... {_PHASE[0]} ({time.time() - t0:.0f} s)", file=sys.stderr, flush=True)
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main():
+    _heartbeat()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20, help="headline steps = fused 100-sweep launches")
@@ -823,6 +847,7 @@ def main():
             # Sokal-window IAT comes out short, i.e. the ESS per sweep long
             ess_procs[kind] = ess_start(kind, 500 if kind != "curn_plred" else 200, 2000)
 
+    phase("headline configs[1]")
     from pulsar_timing_gibbsspec_amd import _lib, synthetic
     from pulsar_timing_gibbsspec_amd.engine import DeviceModel, FreeSpectrumChains, HistoryStreamer
 
@@ -950,11 +975,13 @@ def main():
             sec[name] = d
 
     if args.indep:
+        phase("configs[2] indep")
         d = bench_indep(args.indep_chains, args.indep_steps, 2, 100, rank, world, dev)
         d["config"] = ("configs[2]: 45 simulated pulsars, each its own 30-bin free spectrum (m 68..77), "
                        f"{args.indep_chains} chains per pulsar, one fused launch per 100 sweeps")
         add("indep", d, "indep")
     for kind in [k for k in args.pta.split(",") if k and k != "none"]:
+        phase(f"configs[3] {kind}")
         d = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, shard="chain",
                       ess_sweeps=args.pta_ess_sweeps)
         d["config"] = (f"configs[3]: 45-pulsar CURN{' + per-pulsar red' if kind == 'curn_red' else ''} free "
@@ -968,6 +995,7 @@ def main():
             d["config"] = f"configs[3] {kind}, pulsars sharded over the ranks with the per-sweep RCCL exchange"
             add(kind + "_pulsar_sharded", d)
     if args.ecorr:
+        phase("ecorr")
         d = bench_ecorr(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev)
         d["sharding"] = "chains, weak"
         add("ecorr", d, "ecorr")
@@ -975,11 +1003,13 @@ def main():
         d["sharding"] = "chains, weak"
         add("ecorr_white", d, "ecorr_white")
     if args.config5:
+        phase("configs[4] config5")
         d = bench_config5(args.c5_chains, args.c5_steps, 1, rank, world, dev)
         d["config"] = ("configs[4]: 200 synthetic pulsars x 10^4 TOAs x 100 frequencies (m=216), "
                        "white-noise MH (20 steps) + per-chain TNT recompute every sweep, chain-sharded")
         add("config5", d, "config5")
     if rank == 0 and cpu:
+        phase("cpu baseline (ESS runs, then one single-thread process per core per line)")
         from oracle.cpu_baseline import ess_collect
         ess_cpu = {k: ess_collect(p) for k, p in ess_procs.items()}
         calib = cpu_calibration()
