@@ -338,6 +338,10 @@ __host__ __device__ constexpr int sy_ld(int nb) { return 16 * nb + ((nb & 1) ? 0
 #ifndef GS_SY_BAL
 #define GS_SY_BAL 1
 #endif
+#ifndef GS_SY_GLDS
+#define GS_SY_GLDS 1
+#endif
+typedef __attribute__((address_space(3))) void* gs_white_lds_vptr;
 template <int NB>
 __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
   extern __shared__ double lds[];
@@ -377,11 +381,11 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
   // chunk loader: thread tid owns column tid & 255 of rows (tid >> 8) + 2 e, e < 8
   const int lcol = tid & 255, lrow = tid >> 8;
   const bool colok = lcol < WC;
-  double reg[SY_TC / 2];
+  double reg[GS_SY_GLDS ? 1 : SY_TC / 2];
   double rinv = 0.0;
   auto load = [&](int64_t t0) {
 #pragma unroll
-    for (int e = 0; e < SY_TC / 2; ++e) {
+    for (int e = 0; e < (GS_SY_GLDS ? 0 : SY_TC / 2); ++e) {
       const int64_t t = t0 + lrow + 2 * e;
       double v = 0.0;
       if (colok && t < n) v = (lcol < m) ? Tp[t * m + lcol] : ((lcol == m) ? rp[t] : 0.0);
@@ -399,23 +403,85 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
   auto store = [&](double* b) {
     if (colok)
 #pragma unroll
-      for (int e = 0; e < SY_TC / 2; ++e) b[(lrow + 2 * e) * LDC + lcol] = reg[e];
+      for (int e = 0; e < (GS_SY_GLDS ? 0 : SY_TC / 2); ++e) b[(lrow + 2 * e) * LDC + lcol] = reg[e];
     if (tid < SY_TC) b[SY_TC * LDC + tid] = rinv;
   };
 
   const int64_t nch = (n + SY_TC - 1) / SY_TC;
-  load(0);
-  store(buf0);
-  __syncthreads();
+  // LDS-DMA staging (GS_SY_GLDS; rows of an even number of columns at a 16-byte aligned start): the T
+  // rows of the next chunk go straight into LDS by global_load_lds_dwordx4 (one wave-instruction per
+  // 128 columns of a row, lane-linear), so no 32-VGPR register copy of the chunk is live across the
+  // MFMAs; the r column and 1/N come from 32 threads through registers.  Rows past n are never
+  // loaded: the buffers start zeroed and those rows get 1/N = 0 and r = 0, so their stale (finite)
+  // columns contribute nothing.
+  // 16-byte units where every row starts 16-byte aligned (m and the pulsar's offset even), else 4-byte
+  // ones (any m); compiled without the register path (GS_SY_GLDS: 193 VGPRs, none spilled, against 256
+  // with 26 spilled when both are in the kernel)
+  constexpr bool gl = GS_SY_GLDS;
+  const bool w16 = (m % 2 == 0) && (D.T_off % 2 == 0);  // uniform
+  double rr = 0.0;
+  auto load_gl = [&](int64_t t0, double* b) {
+    if (tid < SY_TC) {  // ordinary loads first, used at once: no DMA is in flight yet
+      const int64_t t = t0 + tid;
+      rinv = 0.0;
+      rr = 0.0;
+      if (t < n) {
+        const int kb = bk[t];
+        rinv = 1.0 / (sb[0][kb] * (s2[t] + sb[1][kb]) + sb[2][kb]);
+        rr = rp[t];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < SY_TC / SY_WAVES; ++e) {
+      const int row = w + SY_WAVES * e;
+      const int64_t t = t0 + row;
+      if (t >= n) continue;
+      if (w16) {
+        const int nu = m >> 1;  // 16-byte units per row, 64 per wave-instruction
+        for (int base = 0; base < nu; base += 64)
+          if (base + l < nu)
+            __builtin_amdgcn_global_load_lds((const void*)(Tp + t * m + 2 * (base + l)),
+                                             (gs_white_lds_vptr)(b + row * LDC + 2 * base), 16, 0, 0);
+      } else {
+        const int nu = 2 * m;   // 4-byte units
+        const float* src = reinterpret_cast<const float*>(Tp + t * m);
+        for (int base = 0; base < nu; base += 64)
+          if (base + l < nu)
+            __builtin_amdgcn_global_load_lds((const void*)(src + base + l),
+                                             (gs_white_lds_vptr)(reinterpret_cast<float*>(b + row * LDC) + base), 4, 0,
+                                             0);
+      }
+    }
+  };
+  auto store_gl = [&](double* b) {
+    if (tid < SY_TC) {
+      b[tid * LDC + m] = rr;
+      b[SY_TC * LDC + tid] = rinv;
+    }
+  };
+  if (gl) {
+    for (int i = tid; i < 2 * (SY_TC * LDC + SY_TC); i += 64 * SY_WAVES) lds[i] = 0.0;
+    __syncthreads();
+    load_gl(0, buf0);
+    store_gl(buf0);
+  } else {
+    load(0);
+    store(buf0);
+  }
+  __syncthreads();  // (waits for the DMA too: vmcnt(0) before the barrier)
   // the chunk loop, instantiated once per role so each role's registers are allocated on their own
   // (role 1: the diagonal-tile wave of BAL; role 0: the paired-row waves).  Measured (r05e/r05f):
   // the diagonal wave in slots 0..NB-1 of the shared accumulator array 389-392 config5 sweeps/s,
   // with its own accumulator array 373 (= the unbalanced kernel's 372-374).
-  auto stream = [&](auto role) {
+  auto stream = [&](auto role, auto dma) {
     for (int64_t ch = 0; ch < nch; ++ch) {
       const double* cur = (ch & 1) ? buf1 : buf0;
       double* nxt = (ch & 1) ? buf0 : buf1;
-      if (ch + 1 < nch) load((ch + 1) * SY_TC);
+      if constexpr (decltype(dma)::value == 1) {
+        if (ch + 1 < nch) load_gl((ch + 1) * SY_TC, nxt);  // nxt was last read before the previous barrier
+      } else {
+        if (ch + 1 < nch) load((ch + 1) * SY_TC);
+      }
       // keep the next chunk's global loads here, ahead of the MFMAs: their latency is
       // hidden behind this chunk's math (the scheduler would otherwise sink them)
       __builtin_amdgcn_sched_barrier(0);
@@ -451,15 +517,22 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
           }
         }
       }
-      if (ch + 1 < nch) store(nxt);
-      __syncthreads();
+      if constexpr (decltype(dma)::value == 1) {
+        if (ch + 1 < nch) store_gl(nxt);
+      } else {
+        if (ch + 1 < nch) store(nxt);
+      }
+      __syncthreads();  // with the DMA in flight: vmcnt(0) first (nxt complete for the next chunk)
     }
   };
   const bool diagw = BAL && w == SY_WAVES - 1;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using IG = std::integral_constant<int, GS_SY_GLDS ? 1 : 0>;
   if (diagw)
-    stream(std::integral_constant<int, 1>{});
+    stream(I1{}, IG{});
   else
-    stream(std::integral_constant<int, 0>{});
+    stream(I0{}, IG{});
   if (!act && !diagw) return;
 
   double* out = A.TNT + D.tnt_off + (int64_t)c * A.tnt_cstride;

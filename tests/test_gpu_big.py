@@ -82,13 +82,17 @@ def test_big_bdraw_flags_non_positive_definite(ctx):
     assert info[0] == 0 and info[1] > 0
 
 
-def test_syrk_tnt_per_system(ctx):
+@pytest.mark.parametrize("n_tm,n_toa", [(16, 700), (15, 700), (15, 701)])
+def test_syrk_tnt_per_system(ctx, n_tm, n_toa):
     """gs_white_tnt (batched SYRK, augmented r column) == numpy TNT/d for every
-    (pulsar, chain) system at m = 216, x one row per system (GS_OPT_X_PER_SYS)."""
+    (pulsar, chain) system at m = 216, x one row per system (GS_OPT_X_PER_SYS).  T reaches LDS by
+    LDS-DMA in 16-byte units when every row starts 16-byte aligned (m = 216), else in 4-byte units
+    (m = 215; with 701 TOAs the second pulsar's rows start at odd offsets too), and the last chunk is
+    partial (700 = 21 x 32 + 28)."""
     import torch
     from pulsar_timing_gibbsspec_amd import _lib, synthetic
     from pulsar_timing_gibbsspec_amd.white import WhiteNoiseModel
-    d = synthetic.config5_array(n_psr=2, n_toa=700, n_f=100, seed=6)
+    d = synthetic.config5_array(n_psr=2, n_toa=n_toa, n_f=100, n_tm=n_tm, seed=6)
     C = 3
     c2 = _lib.Context(0, seed=1)
     c2.set_option(_lib.OPT_X_PER_SYS, 1)
