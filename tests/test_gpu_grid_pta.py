@@ -427,10 +427,12 @@ def test_curn_sum_sharded_engine_matches_unsharded():
     assert np.isfinite(gw).all() and (gw >= -9).all() and (gw <= -4).all()
 
 
-@pytest.mark.parametrize("kind,mode", [("curn", "sum"), ("curn_red", "exact")])
+@pytest.mark.parametrize("kind,mode", [("curn", "sum"), ("curn_red", "exact"), ("curn_plred", "exact")])
 def test_graph_replay_equals_eager_sweeps(kind, mode):
     """hipGraph-captured sweeps (device sweep counter advanced inside the graph) replay
-    to the same chains as eager sweeps, replay after replay."""
+    to the same chains as eager sweeps, replay after replay.  curn_plred (redsample='mh'): the red
+    MH block inside the graph too, and its acceptance counts (a device add replayed with the graph,
+    the step count kept on the host per replay) equal the eager engine's."""
     from pulsar_timing_gibbsspec_amd import _lib, synthetic
     from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
     pta = synthetic.array_pta(kind=kind, n_psr=7, seed=4)
@@ -442,13 +444,22 @@ def test_graph_replay_equals_eager_sweeps(kind, mode):
     gwid = [np.arange(t.shape[1] - 60, t.shape[1]) for t in T]
     fixed = [np.full(t.shape[1] - 60, 1e-40) for t in T]
     C, K = 8, 4
-    x0 = np.random.default_rng(1).uniform(-9, -4, (C, len(names)))
+    rng = np.random.default_rng(1)
+    x0 = rng.uniform(-9, -4, (C, len(names)))
     bounds = ((1e-18, 1e-8), (1e-20, 1e-8))
+    hy = {}
+    if kind == "curn_plred":
+        from pulsar_timing_gibbsspec_amd.pta_hyper import HyperSpec
+        hidx = np.array([i for i, n in enumerate(names) if "red" in n and ("log10_A" in n or "gamma" in n)])
+        sigs = [s for s in (pta.signals[k] for k in pta.signals) if "red" in s.name]
+        spec = HyperSpec(pta, pta.params, sigs, hidx, np.zeros(len(names)), 30, "cuda")
+        x0[:, spec.hind] = rng.uniform(spec.hlo_host, spec.hhi_host, (C, spec.n_h))
+        hy = dict(hyper=spec, hyper_acl=7, hyper_warmup=25)
 
     def engine():
         ctx = _lib.Context(0, seed=5)
         return PTAChains(DeviceModel(ctx, T, N, R, gwid, fixed), len(names), rind, red_col, *bounds, C, x0,
-                         curn_mode=mode)
+                         curn_mode=mode, **hy)
     ref = engine()
     xr = torch.zeros(1 + 3 * K, C, len(names), dtype=torch.float64, device="cuda")
     for i in range(1 + 3 * K):
@@ -462,6 +473,10 @@ def test_graph_replay_equals_eager_sweeps(kind, mode):
         xg[1 + r * K:1 + (r + 1) * K].copy_(g.graph_rec)
     torch.cuda.synchronize()
     assert torch.equal(xg, xr)
+    if kind == "curn_plred":
+        assert g.hyper.steps_total == ref.hyper.steps_total == 25 + 3 * K * 7
+        assert torch.equal(g.hyper.acc_total, ref.hyper.acc_total)
+        assert np.array_equal(g.hyper_acceptance(), ref.hyper_acceptance())
 
 
 def test_tau_sum_fixed_point_kernels():
