@@ -19,11 +19,64 @@ namespace {
 
 typedef double gs_d4_t __attribute__((ext_vector_type(4)));
 
+// 4-chain workgroups (one wavefront per chain), at least 2 waves per SIMD (<= 256 VGPRs), 3 for
+// k_ecorr_prefix with the shared chunks (<= 168 VGPRs: NB = 5 fits with 3 spilled): independent
+// workgroups per CU whose epoch loops and epilogues overlap.  Measured (r05o, 4096 chains, NB = 5,
+// likelihood mode): shared 0.1269 ms (8-wave workgroups, register-staged chunks) -> 0.1249 (8 waves,
+// LDS-DMA chunks) -> 0.1238 (4 waves) -> 0.1200 (4 waves, 3 per SIMD); per-chain operands 0.169 ->
+// 0.154 (8 waves, LDS-DMA double buffer) -> 0.146 (4 waves)
 #ifndef GS_EC_WAVES
-#define GS_EC_WAVES 8
+#define GS_EC_WAVES 4
 #endif
 constexpr int EC_WAVES = GS_EC_WAVES;  // chains per workgroup (one wavefront each)
+#ifndef GS_EC_MINW
+#define GS_EC_MINW 2
+#endif
+#ifndef GS_EC_MINW_SH
+#define GS_EC_MINW_SH 3  // k_ecorr_prefix with the shared chunks
+#endif
 constexpr int EC_CH = 32;    // epochs per LDS chunk
+// per-chain operands (k_ecorr_prefix<.., PC = true>) staged by LDS-DMA, double-buffered 8-epoch
+// chunks (1) or through registers, one 16-epoch chunk at a time (0)
+#ifndef GS_EC_PCDMA
+#define GS_EC_PCDMA 1
+#endif
+constexpr int EC_PCH = GS_EC_PCDMA ? 8 : 16;  // epochs per per-chain chunk
+// shared [B | d_E] chunks (one copy per workgroup) staged by LDS-DMA (1) or through registers (0)
+#ifndef GS_EC_GLDS
+#define GS_EC_GLDS 1
+#endif
+typedef __attribute__((address_space(3))) void* gs_ec_lds_vptr;
+// s_waitcnt immediate waiting for vmcnt <= n only (gfx9 layout: vmcnt[3:0] + [15:14], expcnt[6:4],
+// lgkmcnt[11:8] left at their maxima)
+constexpr int ec_vmcnt(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
+// LDS-DMA of ROWS rows of LDB doubles (row-major, stride LDB) starting at row e0 of src into the
+// contiguous LDS block dst: wave-instructions k = wv, wv + nw, ... of the copy (lane-linear, 16-byte
+// units when src is 16-byte aligned, else 4-byte units); rows at or past ne re-read row ne - 1, so
+// every lane loads and the per-wave instruction count is fixed (finite data; callers weight those
+// rows by 0).  Returns nothing to registers: the data is in LDS once vmcnt has drained.
+template <int LDB, int ROWS>
+__device__ __forceinline__ void ec_dma_rows(const double* src, int e0, int ne, double* dst, int wv, int nw, int l,
+                                            bool w16) {
+  if (w16) {
+    constexpr int NI = ROWS * LDB / 128;
+    for (int k = wv; k < NI; k += nw) {
+      const int lin = 2 * (64 * k + l);
+      const int e = min(e0 + lin / LDB, ne - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)e * LDB + lin % LDB), (gs_ec_lds_vptr)(dst + 128 * k),
+                                       16, 0, 0);
+    }
+  } else {
+    constexpr int NI = ROWS * LDB / 32;
+    for (int k = wv; k < NI; k += nw) {
+      const int lin = 64 * k + l;  // 4-byte unit of the block
+      const int e = min(e0 + lin / (2 * LDB), ne - 1);
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(reinterpret_cast<const float*>(src + (int64_t)e * LDB) + lin % (2 * LDB)),
+          (gs_ec_lds_vptr)(reinterpret_cast<float*>(dst) + 64 * k), 4, 0, 0);
+    }
+  }
+}
 
 __device__ __forceinline__ double ec_wave_sum(double v) {
 #pragma unroll
@@ -59,7 +112,7 @@ __device__ __forceinline__ void ec_phi(double x, double& inv, double& lg) {
 // NB = 8 would need 288 VGPRs and spilled ~1.8k) are split over NP launches, launch PART
 // keeping tiles t with t % NP == PART; each launch streams Bx again.
 template <int NB, int NP = 1, int PART = 0>
-__global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A) {
+__global__ __launch_bounds__(64 * EC_WAVES, GS_EC_MINW) void k_ecorr_schur(EcorrSchurArgs A) {
   extern __shared__ double lds[];
   __shared__ double wb[2][EC_WAVES][EC_CH];
   __shared__ double sinv[EC_WAVES][GS_WHITE_MAX_BK + 1], slog[EC_WAVES][GS_WHITE_MAX_BK + 1];
@@ -85,41 +138,54 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
   double sla = 0.0, slp = 0.0;
 
   constexpr int LPT = EC_CH * LDB / (64 * EC_WAVES);  // chunk elements per thread
-  double reg[LPT];
-  double wreg = 0.0;
-  auto load = [&](int e0) {
+  double reg[GS_EC_GLDS ? 1 : LPT];
+  int kreg = -1;
+  double dreg = 0.0;
+  const bool bx16 = (reinterpret_cast<uintptr_t>(A.Bx) & 15) == 0;  // uniform
+  auto load = [&](int e0, int buf) {
+    if constexpr (GS_EC_GLDS) {
+      // straight into LDS buffer buf (its last reads ended at the previous barrier); waited by
+      // the vmcnt(0) the weights' loads below take in store() and the barrier after it
+      if (ne > 0) ec_dma_rows<LDB, EC_CH>(A.Bx, e0, ne, lds + buf * (EC_CH * LDB), w, EC_WAVES, l, bx16);
+    } else {
 #pragma unroll
-    for (int q = 0; q < LPT; ++q) {
-      const int idx = tid + 64 * EC_WAVES * q;
-      const int e = e0 + idx / LDB;
-      reg[q] = (e < ne) ? A.Bx[(int64_t)e0 * LDB + idx] : 0.0;
-    }
-    wreg = 0.0;
-    if (l < EC_CH && live) {
-      const int e = e0 + l;
-      if (e < ne) {
-        const int kb = A.ebk[e];
-        const double a = A.Dg[e] + sinv[w][kb];
-        wreg = 1.0 / a;
-        sla += gs_log_lnl(a);
-        slp += slog[w][kb];
+      for (int q = 0; q < LPT; ++q) {
+        const int idx = tid + 64 * EC_WAVES * q;
+        const int e = e0 + idx / LDB;
+        reg[q] = (e < ne) ? A.Bx[(int64_t)e0 * LDB + idx] : 0.0;
       }
     }
+    kreg = -1;
+    if (l < EC_CH && live && e0 + l < ne) {
+      kreg = A.ebk[e0 + l];
+      dreg = A.Dg[e0 + l];
+    }
   };
+  // the weights are formed here, after the chunk's MFMAs: using the loaded ebk / Dg inside load()
+  // made the whole chunk prefetch wait (vmcnt(0)) before the MFMAs
   auto store = [&](int buf) {
-    double* dst = lds + buf * (EC_CH * LDB);
+    if constexpr (!GS_EC_GLDS) {
+      double* dst = lds + buf * (EC_CH * LDB);
 #pragma unroll
-    for (int q = 0; q < LPT; ++q) dst[tid + 64 * EC_WAVES * q] = reg[q];
-    if (l < EC_CH) wb[buf][w][l] = wreg;
+      for (int q = 0; q < LPT; ++q) dst[tid + 64 * EC_WAVES * q] = reg[q];
+    }
+    double wv = 0.0;
+    if (kreg >= 0) {
+      const double a = dreg + sinv[w][kreg];
+      wv = 1.0 / a;
+      sla += gs_log_lnl(a);
+      slp += slog[w][kreg];
+    }
+    if (l < EC_CH) wb[buf][w][l] = wv;
   };
 
   const int nch = (ne + EC_CH - 1) / EC_CH;
-  load(0);
+  load(0, 0);
   store(0);
   __syncthreads();
   for (int ch = 0; ch < nch; ++ch) {
     const int cb = ch & 1;
-    if (ch + 1 < nch) load((ch + 1) * EC_CH);
+    if (ch + 1 < nch) load((ch + 1) * EC_CH, cb ^ 1);
     __builtin_amdgcn_sched_barrier(0);
     const double* cur = lds + cb * (EC_CH * LDB);
     const int nk = min(EC_CH / 4, (ne - ch * EC_CH + 3) / 4);  // k-steps holding epochs (uniform)
@@ -197,7 +263,7 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_schur(EcorrSchurArgs A)
 //                system (Ap_dd = 0), so no solve is needed and nothing per chain but lnl
 //                goes to HBM.
 template <int NB, bool LNL, bool PC>
-__global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs A) {
+__global__ __launch_bounds__(64 * EC_WAVES, PC ? GS_EC_MINW : GS_EC_MINW_SH) void k_ecorr_prefix(EcorrPrefixArgs A) {
   extern __shared__ double lds[];
   __shared__ double wb[2][EC_WAVES][EC_CH];
   __shared__ double sinv[EC_WAVES][GS_WHITE_MAX_BK + 1], slog[EC_WAVES][GS_WHITE_MAX_BK + 1];
@@ -241,93 +307,161 @@ __global__ __launch_bounds__(64 * EC_WAVES) void k_ecorr_prefix(EcorrPrefixArgs 
       for (int s = 0; s < 4; ++s) acc[ts(jj, r)][s] = live ? Aq(16 * jj, 16 * r, s) : 0.0;
   double sla = 0.0, slp = 0.0;
   constexpr int LPT = EC_CH * LDB / (64 * EC_WAVES);  // chunk elements per thread
-  double reg[LPT];
-  double wreg = 0.0;
-  auto load = [&](int e0) {
+  double reg[GS_EC_GLDS ? 1 : LPT];
+  int kreg = -1;
+  double dreg = 0.0;
+  const bool bx16 = (reinterpret_cast<uintptr_t>(A.Bx) & 15) == 0;  // uniform
+  auto load = [&](int e0, int buf) {
+    if constexpr (GS_EC_GLDS) {
+      // straight into LDS buffer buf (its last reads ended at the previous barrier); waited by
+      // the vmcnt(0) the weights' loads below take in store() and the barrier after it
+      if (ne > 0) ec_dma_rows<LDB, EC_CH>(A.Bx, e0, ne, lds + buf * (EC_CH * LDB), w, EC_WAVES, l, bx16);
+    } else {
 #pragma unroll
-    for (int u = 0; u < LPT; ++u) {
-      const int idx = tid + 64 * EC_WAVES * u;
-      const int e = e0 + idx / LDB;
-      reg[u] = (e < ne) ? A.Bx[(int64_t)e0 * LDB + idx] : 0.0;
-    }
-    wreg = 0.0;
-    if (l < EC_CH && live) {
-      const int e = e0 + l;
-      if (e < ne) {
-        const int kb = A.ebk[e];
-        const double a = A.Dg[e] + sinv[w][kb];
-        wreg = 1.0 / a;
-        sla += gs_log_lnl(a);
-        slp += slog[w][kb];
+      for (int u = 0; u < LPT; ++u) {
+        const int idx = tid + 64 * EC_WAVES * u;
+        const int e = e0 + idx / LDB;
+        reg[u] = (e < ne) ? A.Bx[(int64_t)e0 * LDB + idx] : 0.0;
       }
     }
+    kreg = -1;
+    if (l < EC_CH && live && e0 + l < ne) {
+      kreg = A.ebk[e0 + l];
+      dreg = A.Dg[e0 + l];
+    }
   };
+  // the weights are formed here, after the chunk's MFMAs: using the loaded ebk / Dg inside load()
+  // made the whole chunk prefetch wait (vmcnt(0)) before the MFMAs
   auto store = [&](int buf) {
-    double* dst = lds + buf * (EC_CH * LDB);
+    if constexpr (!GS_EC_GLDS) {
+      double* dst = lds + buf * (EC_CH * LDB);
 #pragma unroll
-    for (int u = 0; u < LPT; ++u) dst[tid + 64 * EC_WAVES * u] = reg[u];
-    if (l < EC_CH) wb[buf][w][l] = wreg;
+      for (int u = 0; u < LPT; ++u) dst[tid + 64 * EC_WAVES * u] = reg[u];
+    }
+    double wv = 0.0;
+    if (kreg >= 0) {
+      const double a = dreg + sinv[w][kreg];
+      wv = 1.0 / a;
+      sla += gs_log_lnl(a);
+      slp += slog[w][kreg];
+    }
+    if (l < EC_CH) wb[buf][w][l] = wv;
   };
   if constexpr (PC) {
     // per-chain [B | d_E] (white noise sampled: TNT differs per chain): no sharing across
-    // waves; each wavefront stages 16-epoch chunks of its own rows in its slice of the
-    // dynamic LDS (all of a chunk's loads in flight at once), 1/a by lanes 0..15
+    // waves; each wavefront stages chunks of its own rows in its slice of the dynamic LDS
     if (!live) return;  // no workgroup barriers below
     const double* Bc = A.Bx + (int64_t)ch_id * A.bx_cs;
     const double* Dc = A.Dg + (int64_t)ch_id * A.dg_cs;
-    constexpr int PCH = 16;
-    constexpr int PL = PCH * LDB / 64;  // doubles per lane per chunk
-    double* buf = lds + (int64_t)w * (PCH * LDB + PCH);
-    double* wsl = buf + PCH * LDB;
-    for (int e0 = 0; e0 < ne; e0 += PCH) {
-      double rg[PL];
+    constexpr int PCH = EC_PCH;
+    auto kstep = [&](const double* buf, const double* wrow, int kk) {
+      const double* row = buf + (4 * kk + q) * LDB + c;
+      const double wk = -wrow[4 * kk + q];
+      double v[NB];
 #pragma unroll
-      for (int u = 0; u < PL; ++u) {
-        const int idx = l + 64 * u;
-        rg[u] = (e0 + idx / LDB < ne) ? Bc[(int64_t)e0 * LDB + idx] : 0.0;
+      for (int r = 0; r < NB; ++r) v[r] = row[16 * r];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const double av = v[j] * wk;
+#pragma unroll
+        for (int r = j; r < NB; ++r) {
+          const int t = (j == 0) ? r : ts(j, r);
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, v[r], acc[t], 0, 0, 0);
+        }
       }
-      double wv = 0.0;
-      if (l < PCH && e0 + l < ne) {
-        const int e = e0 + l;
-        const int kb = A.ebk[e];
-        const double a = Dc[e] + sinv[w][kb];
-        wv = 1.0 / a;
-        sla += gs_log_lnl(a);
-        slp += slog[w][kb];
-      }
-      wave_lds_sync();  // previous chunk's LDS reads are done before the overwrite
-#pragma unroll
-      for (int u = 0; u < PL; ++u) buf[l + 64 * u] = rg[u];
-      if (l < PCH) wsl[l] = wv;
-      wave_lds_sync();
-      const int nk = min(PCH / 4, (ne - e0 + 3) / 4);
-#pragma unroll
-      for (int kk = 0; kk < PCH / 4; ++kk) {
-        if (kk >= nk) break;
-        const double* row = buf + (4 * kk + q) * LDB + c;
-        const double wk = -wsl[4 * kk + q];
-        double v[NB];
-#pragma unroll
-        for (int r = 0; r < NB; ++r) v[r] = row[16 * r];
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          const double av = v[j] * wk;
-#pragma unroll
-          for (int r = j; r < NB; ++r) {
-            const int t = (j == 0) ? r : ts(j, r);
-            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, v[r], acc[t], 0, 0, 0);
+    };
+    if constexpr (GS_EC_PCDMA) {
+      // LDS-DMA: the rows of chunk i + 1 go global -> LDS (lane-linear, NB wave-instructions of
+      // 16-byte units, or 4 NB of 4-byte units when the chain's rows are not 16-byte aligned)
+      // while chunk i is multiplied; the chunk's rows past ne re-read row ne - 1, so every chunk
+      // issues the same instruction count (the vmcnt wait below counts them) and those rows have
+      // weight 0.  1/a of a 64-epoch segment is computed by its lanes at the segment's first
+      // chunk (the only ordinary loads of the loop; their wait also covers chunk i's DMA).
+      constexpr int CHD = PCH * LDB;
+      double* bufs = lds + (int64_t)w * (2 * CHD + 64);
+      double* wsl = bufs + 2 * CHD;
+      const bool w16 = (reinterpret_cast<uintptr_t>(Bc) & 15) == 0;  // uniform
+      auto dma = [&](int e0, double* dst) { ec_dma_rows<LDB, PCH>(Bc, e0, ne, dst, 0, 1, l, w16); };
+      constexpr int WAIT16 = ec_vmcnt(NB), WAIT4 = ec_vmcnt(4 * NB), WAIT0 = ec_vmcnt(0);
+      const int nch = (ne + PCH - 1) / PCH;
+      // the accumulators' Ap loads land here: otherwise the loop's first MFMA waits vmcnt(0) (the
+      // waitcnt pass merges the loop entry into every iteration) and no DMA overlaps the math
+      __builtin_amdgcn_s_waitcnt(WAIT0);
+      dma(0, bufs);
+      for (int i = 0; i < nch; ++i) {
+        const int e0 = i * PCH;
+        if ((e0 & 63) == 0) {
+          double wv = 0.0;
+          if (e0 + l < ne) {
+            const int e = e0 + l;
+            const int kb = A.ebk[e];
+            const double a = Dc[e] + sinv[w][kb];
+            wv = 1.0 / a;
+            sla += gs_log_lnl(a);
+            slp += slog[w][kb];
           }
+          wsl[l] = wv;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (i + 1 < nch) {
+          dma(e0 + PCH, bufs + ((i + 1) & 1) * CHD);  // that buffer's reads ended with chunk i - 1
+          if (w16) __builtin_amdgcn_s_waitcnt(WAIT16);
+          else __builtin_amdgcn_s_waitcnt(WAIT4);
+        } else {
+          __builtin_amdgcn_s_waitcnt(WAIT0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        wave_lds_sync();
+        const double* cur = bufs + (i & 1) * CHD;
+        const int nk = min(PCH / 4, (ne - e0 + 3) / 4);
+#pragma unroll
+        for (int kk = 0; kk < PCH / 4; ++kk) {
+          if (kk >= nk) break;
+          kstep(cur, wsl + (e0 & 63), kk);
+        }
+      }
+    } else {
+      // register-staged: all of a chunk's loads in flight at once, 1/a by lanes 0..PCH-1
+      constexpr int PL = PCH * LDB / 64;  // doubles per lane per chunk
+      double* buf = lds + (int64_t)w * (PCH * LDB + PCH);
+      double* wsl = buf + PCH * LDB;
+      for (int e0 = 0; e0 < ne; e0 += PCH) {
+        double rg[PL];
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+          const int idx = l + 64 * u;
+          rg[u] = (e0 + idx / LDB < ne) ? Bc[(int64_t)e0 * LDB + idx] : 0.0;
+        }
+        double wv = 0.0;
+        if (l < PCH && e0 + l < ne) {
+          const int e = e0 + l;
+          const int kb = A.ebk[e];
+          const double a = Dc[e] + sinv[w][kb];
+          wv = 1.0 / a;
+          sla += gs_log_lnl(a);
+          slp += slog[w][kb];
+        }
+        wave_lds_sync();  // previous chunk's LDS reads are done before the overwrite
+#pragma unroll
+        for (int u = 0; u < PL; ++u) buf[l + 64 * u] = rg[u];
+        if (l < PCH) wsl[l] = wv;
+        wave_lds_sync();
+        const int nk = min(PCH / 4, (ne - e0 + 3) / 4);
+#pragma unroll
+        for (int kk = 0; kk < PCH / 4; ++kk) {
+          if (kk >= nk) break;
+          kstep(buf, wsl, kk);
         }
       }
     }
   } else {
   const int nch = (ne + EC_CH - 1) / EC_CH;
-  load(0);
+  load(0, 0);
   store(0);
   __syncthreads();
   for (int chk = 0; chk < nch; ++chk) {
     const int cb = chk & 1;
-    if (chk + 1 < nch) load((chk + 1) * EC_CH);
+    if (chk + 1 < nch) load((chk + 1) * EC_CH, cb ^ 1);
     __builtin_amdgcn_sched_barrier(0);
     const double* cur = lds + cb * (EC_CH * LDB);
     const int nk = min(EC_CH / 4, (ne - chk * EC_CH + 3) / 4);  // k-steps holding epochs (uniform)
@@ -688,7 +822,8 @@ void launch_schur_nb(hipStream_t s, const EcorrSchurArgs& a) {
 template <int NB, bool LNL, bool PC>
 void launch_prefix_nbp(hipStream_t s, const EcorrPrefixArgs& a) {
   static bool attr = false;
-  const size_t lds = PC ? (size_t)EC_WAVES * (16 * 16 * NB + 16) * sizeof(double)
+  const size_t lds = PC ? (size_t)EC_WAVES *
+                               (GS_EC_PCDMA ? 2 * EC_PCH * 16 * NB + 64 : EC_PCH * 16 * NB + EC_PCH) * sizeof(double)
                         : (size_t)2 * EC_CH * 16 * NB * sizeof(double);
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k_ecorr_prefix<NB, LNL, PC>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -413,16 +413,18 @@ def test_ecorr_bdraw_chain_mask_mixed(ctx):
             assert np.all(B[c] == sentinel), c
 
 
-@pytest.mark.parametrize("mR", [60, 100, 120])
-def test_ecorr_schur_direct(ctx, mR):
+@pytest.mark.parametrize("mR,ne,offset", [(60, 137, 0), (100, 137, 0), (120, 137, 0), (60, 1, 1), (76, 33, 1),
+                                           (100, 64, 1)])
+def test_ecorr_schur_direct(ctx, mR, ne, offset):
     """gs_ecorr_schur through the C-ABI on random operands: TNT = A - B^T diag(1/a) B,
     d = dR - B^T (d_E / a), aux = (sum log a, sum d_E^2 / a, sum log phi_E, 0), against
     numpy.  mR = 100 / 120 use 7 / 8 tile columns, whose accumulators are split over two
-    launches (one would need ~290 VGPRs)."""
+    launches (one would need ~290 VGPRs).  offset = 1: Bx at an 8-byte offset address (the LDS-DMA
+    staging in 4-byte units); ne = 1 / 33 / 64: partial and exact 32-epoch chunks."""
     import torch
     from pulsar_timing_gibbsspec_amd._lib import check, ptr
-    rng = np.random.default_rng(mR)
-    C, ne, n_bk = 5, 137, 3
+    rng = np.random.default_rng(mR + ne)
+    C, n_bk = 5, 3
     ldbx = 16 * ((mR + 16) // 16)
     Bx = np.zeros((ne, ldbx))
     Bx[:, :mR + 1] = rng.standard_normal((ne, mR + 1))
@@ -437,6 +439,11 @@ def test_ecorr_schur_direct(ctx, mR):
     dev = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=ctx.device)  # noqa: E731
     g = {k: dev(v) for k, v in dict(Bx=Bx, Dg=Dg, x=x, A=A, dR=dR).items()}
     g["ebk"], g["xcol"] = dev(ebk, torch.int32), dev(xcol, torch.int32)
+    if offset:
+        buf = torch.zeros(Bx.size + 1, dtype=torch.float64, device=ctx.device)
+        buf[1:] = g["Bx"].reshape(-1)
+        g["Bx"] = buf[1:]
+        assert ptr(g["Bx"]) % 16 == 8
     TNT = torch.empty(C, mR, mR, dtype=torch.float64, device=ctx.device)
     d = torch.empty(C, mR, dtype=torch.float64, device=ctx.device)
     aux = torch.empty(C, 4, dtype=torch.float64, device=ctx.device)
@@ -479,3 +486,75 @@ def test_ecorr_lnlike_wide_timing_model(ctx, n_tm):
         got = gb.get_lnlikelihood(x)
         assert gb._em1.mR == 60 + n_tm and not gb._em1.fused
         assert abs(got - ref) < 1e-7 * max(1.0, abs(ref)), (n_tm, got, ref)
+
+
+def _prefix_lnl_numpy(Bp, Dg, ebk, Ap, xrow, ecol, phiinv_F, NF):
+    """Likelihood-mode gs_ecorr_prefix outputs from its operands (the [M (16) | F | d | pad]
+    layout): T = Ap - Bp^T diag(1/a) Bp, Sigma = T_RR + diag(0_M, phiinv_F), dd = T_Rd;
+    lnl = (P_dd + dd^T Sigma^-1 dd - logdet Sigma + sum log phiinv_F) / 2, aux = (sum log a, 0,
+    sum log phi_E, P_dd)."""
+    ph = 10.0 ** (2.0 * xrow[ecol])
+    a = Dg + 1.0 / ph[ebk]
+    P = Bp.T @ (Bp / a[:, None])
+    T = Ap - P
+    R, dc = 16 + NF, 16 + NF
+    S = T[:R, :R] + np.diag(np.concatenate([np.zeros(16), phiinv_F]))
+    dd = T[:R, dc]
+    quad = P[dc, dc] + dd @ np.linalg.solve(S, dd)
+    lnl = 0.5 * (quad - np.linalg.slogdet(S)[1] + np.sum(np.log(phiinv_F)))
+    return lnl, np.array([np.sum(np.log(a)), 0.0, np.sum(np.log(ph[ebk])), P[dc, dc]])
+
+
+@pytest.mark.parametrize("ne", [1, 7, 64, 65, 136])
+def test_ecorr_prefix_staging_edges(ctx, ne):
+    """gs_ecorr_prefix (likelihood mode) on the first ne epochs of the J1713 operands, four ways:
+    shared [B | d_E] at a 16-byte aligned and at an 8-byte offset address (LDS-DMA in 16- / 4-byte
+    units), and per-chain copies with a chain stride of ne*KB (aligned) and ne*KB + 1 doubles
+    (every other chain 8-byte offset) -- the lnl bit-identical across the four, and against numpy
+    from the same operands to 1e-9 (ne = 1, 7: partial chunks; 64 / 65: the per-chain path's
+    64-epoch weight segments)."""
+    import torch
+    from pulsar_timing_gibbsspec_amd._lib import check, ptr
+    g = golden("ecorr_mh_j1713.npz")
+    X = g["x_like"][:6]
+    C = X.shape[0]
+    em = _model(ctx, g, C)
+    assert em.fused and not em.per_chain
+    NF, KB = em.NF, em.ldbp
+    Bp = em.Bp[:ne].contiguous()
+    Dg, ebk = em.Dg[:ne].contiguous(), em.ebk[:ne].contiguous()
+    Ap = em.Ap
+    x = _dev(X)
+    phf = _dev(_phiinv_F(g, X))
+    Bn, Dn, En, An = Bp.cpu().numpy(), Dg.cpu().numpy(), ebk.cpu().numpy(), Ap.cpu().numpy()
+    ecol = em.ecol.cpu().numpy()
+
+    def run(Bx, Dgx, Apx, strides):
+        lnl = torch.empty(C, dtype=torch.float64, device="cuda")
+        aux = torch.empty(C, 4, dtype=torch.float64, device="cuda")
+        info = torch.zeros(C, dtype=torch.int32, device="cuda")
+        check(ctx.lib.gs_ecorr_prefix(ctx.handle, C, NF, em.NMX, em.nm, ne, KB, ptr(Bx), ptr(Dgx), ptr(ebk), em.n_bk,
+                                      ptr(em.ecol), ptr(x), x.shape[1], ptr(Apx), ptr(phf), None, ptr(aux), ptr(lnl),
+                                      ptr(info), *strides), "gs_ecorr_prefix")
+        assert int(info.abs().max()) == 0
+        return lnl.cpu().numpy(), aux.cpu().numpy()
+
+    off = torch.zeros(ne * KB + 1, dtype=torch.float64, device="cuda")
+    off[1:] = Bp.reshape(-1)
+    assert ptr(off[1:]) % 16 == 8
+    outs = [run(Bp, Dg, Ap, (0, 0, 0)), run(off[1:], Dg, Ap, (0, 0, 0))]
+    for extra in (0, 1):
+        cs = ne * KB + extra
+        Bc = torch.zeros(C * cs, dtype=torch.float64, device="cuda")
+        for c in range(C):
+            Bc[c * cs:c * cs + ne * KB] = Bp.reshape(-1)
+        Dc = Dg.repeat(C).contiguous()
+        Ac = Ap.reshape(1, -1).repeat(C, 1).contiguous()
+        outs.append(run(Bc, Dc, Ac, (cs, ne, KB * KB)))
+    for lnl, aux in outs[1:]:
+        assert np.array_equal(lnl, outs[0][0])
+        np.testing.assert_allclose(aux, outs[0][1], rtol=1e-13, atol=0)
+    for c in range(C):
+        want, waux = _prefix_lnl_numpy(Bn, Dn, En, An, X[c], ecol, _phiinv_F(g, X)[c], NF)
+        assert abs(outs[0][0][c] - want) < 1e-9 * max(1.0, abs(want)), (ne, c, outs[0][0][c], want)
+        np.testing.assert_allclose(outs[0][1][c], waux, rtol=1e-11, atol=1e-11)
