@@ -387,7 +387,7 @@ __global__ __launch_bounds__(64 * EC_WAVES, PC ? GS_EC_MINW : GS_EC_MINW_SH) voi
       // the accumulators' Ap loads land here: otherwise the loop's first MFMA waits vmcnt(0) (the
       // waitcnt pass merges the loop entry into every iteration) and no DMA overlaps the math
       __builtin_amdgcn_s_waitcnt(WAIT0);
-      dma(0, bufs);
+      if (nch > 0) dma(0, bufs);  // (ne = 0: no rows to read)
       for (int i = 0; i < nch; ++i) {
         const int e0 = i * PCH;
         if ((e0 & 63) == 0) {
