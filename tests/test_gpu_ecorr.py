@@ -443,7 +443,7 @@ def test_ecorr_schur_direct(ctx, mR, ne, offset):
         buf = torch.zeros(Bx.size + 1, dtype=torch.float64, device=ctx.device)
         buf[1:] = g["Bx"].reshape(-1)
         g["Bx"] = buf[1:]
-        assert ptr(g["Bx"]) % 16 == 8
+        assert g["Bx"].data_ptr() % 16 == 8
     TNT = torch.empty(C, mR, mR, dtype=torch.float64, device=ctx.device)
     d = torch.empty(C, mR, dtype=torch.float64, device=ctx.device)
     aux = torch.empty(C, 4, dtype=torch.float64, device=ctx.device)
@@ -541,7 +541,7 @@ def test_ecorr_prefix_staging_edges(ctx, ne):
 
     off = torch.zeros(ne * KB + 1, dtype=torch.float64, device="cuda")
     off[1:] = Bp.reshape(-1)
-    assert ptr(off[1:]) % 16 == 8
+    assert off[1:].data_ptr() % 16 == 8
     outs = [run(Bp, Dg, Ap, (0, 0, 0)), run(off[1:], Dg, Ap, (0, 0, 0))]
     for extra in (0, 1):
         cs = ne * KB + extra
