@@ -646,7 +646,9 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
                           "hbm_frac": alg_bytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                           "note": "as the ecorr line; each chain's own [B | d_E] rows and Ap tiles stream from "
                                   "HBM (alg_bytes_per_launch); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE, the x2 "
-                                  "wide-read correction makes it an upper estimate"},
+                                  "wide-read correction makes it an upper estimate (measured on the round-3 "
+                                  "kernel, profiles/pmc_traffic_ecorr_white.json: PMC passes over the ECORR "
+                                  "lines crash in rocprofv3 on this image, profiles/r05t/SUMMARY.md)"},
                 config="SURVEY 8f-4 with EFAC/EQUAD sampled: J1713-like pulsar, 2 backends, 136 ECORR epochs, "
                        "white MH + per-chain TNT + ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
 
@@ -723,7 +725,8 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
                           "traffic": _ecorr_traffic(C),
                           "note": "ne (mR+1)(mR+2) + nM (NF+1)(NF+2) + (NF+1)^3/3 flop per chain (epoch-weighted "
                                   "SYRK with the d_E row + fixed-prior Schur update + F-block Cholesky) over the "
-                                  "HIP-event time of one all-chain likelihood launch"},
+                                  "HIP-event time of one all-chain likelihood launch; traffic: PMC of the round-3 kernel "
+                                  "(profiles/pmc_traffic_ecorr.json; same operands, L2-resident)"},
                 config="SURVEY 8f-4: J1713-like pulsar, basis ECORR (2 backends, 136 epochs) + 30-bin free "
                        "spectrum + 16-col TM, ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
 
