@@ -105,6 +105,27 @@ def timed_region(world, dev, fn):
     return el
 
 
+# untimed warm-up of every secondary line: the line's own sweeps for at least this long (and at least
+# the line's W), since the shader clock ramps back up over ~10-20 ms of sustained load after the idle
+# host-side setup between lines (profiles/r05z2/launch_stats.log: the first launches of each kernel
+# 10-15 % slower).  The headline keeps exactly the driver's --warmup steps.
+WARM_MS = 60.0
+
+
+def warm(fn, min_calls=1, min_ms=WARM_MS):
+    """Call fn() (one untimed sweep / launch of the line) at least min_calls times and until min_ms of
+    wall time has passed, synchronising every few calls so the wall time follows the GPU."""
+    t0 = time.perf_counter()
+    n = 0
+    while n < min_calls or (time.perf_counter() - t0) * 1e3 < min_ms:
+        fn()
+        n += 1
+        if n % 4 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    return n
+
+
 def event_ms(stream, fn, reps, warm=10):
     """Average HIP-event time of fn() on ``stream`` (the context stream the C-ABI launches on),
     after `warm` untimed calls: the clock ramps back up over ~10 ms of sustained load after the
@@ -261,8 +282,7 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
                              hyper_acl=HYPER_ACL if hyper is not None else None)
         eng = make(C)
     rec = torch.empty(K, C, len(names), dtype=torch.float64, device=dev)
-    for _ in range(max(1, W)):
-        eng.sweep(x_rec=rec[0])
+    n_warm = warm(lambda: eng.sweep(x_rec=rec[0]), max(1, W))
 
     def run():
         for i in range(K):
@@ -274,7 +294,7 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
         eng.check_fx()
     total_chains = C if sharded else C * world
     value = total_chains * K / el
-    out = dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+    out = dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K, warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
                chains_per_gpu=C, n_psr=len(T), n_param=len(names), n_gpus=world,
                scaling="strong" if sharded else "weak",
                sharding=("pulsars over %d GPUs (RCCL %s per sweep)" %
@@ -436,8 +456,7 @@ def bench_indep(C, K, W, S, rank, world, dev):
     x_rec = torch.empty(S, P * C, 30, dtype=torch.float64, device=dev)
     b_rec = torch.empty(S, P * C, model.ldb, dtype=torch.float64, device=dev)
     xs = []
-    if W:
-        run.run(min(W, S), x_rec=x_rec[:min(W, S)], b_rec=b_rec[:min(W, S)])
+    n_warm = warm(lambda: run.run(S, x_rec=x_rec[:S], b_rec=b_rec[:S]), 1) if W else 0  # full launches
     # the timed loop's strided ESS-sample copy once untimed: its first use loads torch's copy
     # kernel (tens of ms on a fresh box, which showed up as 1.5e6 instead of 3.0e6 array-it/s)
     x_rec[:1].view(1, P, C, 30)[:, :, :min(C, 4)].clone()
@@ -468,7 +487,7 @@ def bench_indep(C, K, W, S, rank, world, dev):
     ess = None
     if K >= 50:                                      # min over (pulsar, bin) of the whole-job ESS/s
         ess = min(ess_min_bin(xh[:, p], el, C) for p in range(P))
-    return dict(value=C * K / el, unit="array-iters/s", ms_per_step=el / K * 1e3, steps=K,
+    return dict(value=C * K / el, unit="array-iters/s", ms_per_step=el / K * 1e3, steps=K, warmup={"n": n_warm, "unit": "launches", "min_ms": WARM_MS},
                 chains_per_pulsar=C, n_psr=len(ptas), n_psr_local=P, m_range=[int(model.m.min()), int(model.m.max())],
                 n_gpus=world, scaling="strong" if world > 1 else "weak",
                 sharding=(f"pulsars over {world} GPUs (no collective)" if world > 1 else "one GPU"),
@@ -497,9 +516,7 @@ def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, a
     del d["T"]
     eng = WhiteArrayChains(wm, d["n_param"], d["gw_cols"], d["rhomin"], d["rhomax"],
                            np.repeat(d["x0"], C, axis=0), aclength=aclength, chain_base=rank * C)
-    for _ in range(W):
-        eng.sweep()
-    torch.cuda.synchronize()
+    n_warm = warm(eng.sweep, W)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -527,7 +544,7 @@ def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, a
     n_sys = n_psr * C
     flops = n_sys * (n_toa * m * (m + 1) + 2 * n_toa * m)      # SYRK + TNr per system
     tflops = flops / (refresh_ms * 1e-3) / 1e12
-    return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+    return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K, warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
                 chains_per_gpu=C, n_psr=n_psr, n_toa=n_toa, m=m, aclength=aclength,
                 roofline={"bound": "mfma", "kernel": "k_white_syrk + k_prefix (gs_white_tnt + gs_prefix_sys)",
                           "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -593,9 +610,7 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
     x0[:, eind] = -6.3
     x0[:, gw] = rng.uniform(-9, -4, (C, len(gw)))
     eng = EcorrWhiteChains(wm, em, gw, gwid, 1e-18, 1e-8, x0, aclength, aclength, chain_base=rank * C, wmR=wmR)
-    for _ in range(W):
-        eng.sweep()
-    torch.cuda.synchronize()
+    n_warm = warm(eng.sweep, W)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -633,7 +648,7 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
     alg_bytes = C * 8 * (ne * em.ldbx + 256 * nb * (nb + 1) // 2 + ne + NF + 5)
     traffic = _ecorr_traffic(C, "pmc_traffic_ecorr_white.json")
     value = C * world * K / el
-    return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+    return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K, warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
                 ess_per_s=value * ess_frac,
                 ess={"per_chain_sweep_min_bin": ess_frac, "burn_in": 300, "sweeps": 1000, "chains": ess_c,
                      "note": "the bench's chains continued untimed: 300 more sweeps dropped, 1000 recorded"},
@@ -675,9 +690,7 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
     rng = np.random.default_rng(rank)
     x0 = np.concatenate([np.full((C, len(eind)), -6.3), rng.uniform(-9, -4, (C, len(gw)))], axis=1)
     eng = EcorrFreeSpectrumChains(em, gw, gwid, 1e-18, 1e-8, x0, aclength=aclength, chain_base=rank * C)
-    for _ in range(W):
-        eng.sweep()
-    torch.cuda.synchronize()
+    n_warm = warm(eng.sweep, W)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -712,7 +725,7 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
     flops = C * (ne * (mR + 1) * (mR + 2) + nM * (NF + 1) * (NF + 2) + (NF + 1) ** 3 // 3)
     tflops = flops / (k_ms * 1e-3) / 1e12
     value = C * world * K / el
-    return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+    return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K, warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
                 ess_per_s=value * ess_frac,
                 ess={"per_chain_sweep_min_bin": ess_frac, "burn_in": 300, "sweeps": 1000, "chains": ess_c,
                      "note": "the bench's chains continued untimed: 300 more sweeps dropped, 1000 recorded"},
