@@ -509,7 +509,7 @@ __global__ __launch_bounds__(64 * EC_WAVES, PC ? GS_EC_MINW : GS_EC_MINW_SH) voi
     const unsigned long long m = __ballot(bad);
     if (m) fail = __builtin_ctzll(m) + 1;
   }
-  double ldl = (q == 0 && c < nM) ? -log(rsd) : 0.0;  // sum log diag L_M
+  double ldl = (q == 0 && c < nM) ? -gs_log_lnl(rsd) : 0.0;  // sum log diag L_M
   ldl = ec_wave_sum_u(ldl);
 
   // W_r = L_M^-1 T_0r = V^T T_0r;  S_jr = T_jr - W_j^T W_r
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(64 * EC_WAVES, PC ? GS_EC_MINW : GS_EC_MINW_SH) voi
       const bool badk = (q == 0) && (c < lim) && !(rk > 0.0 && rk < INFINITY);
       const unsigned long long mk = __ballot(badk);
       if (mk && fail == 0) fail = 16 * K + __builtin_ctzll(mk) + 1;
-      ldS += (q == 0 && c < lim) ? -2.0 * log(rk) : 0.0;
+      ldS += (q == 0 && c < lim) ? -2.0 * gs_log_lnl(rk) : 0.0;
 #pragma unroll
       for (int s = 0; s < 4; ++s) Vk[s] *= rk;
       // U_KJ = V_K^T T_KJ (J > K), then T_IJ -= U_KI^T U_KJ (K < I <= J)
@@ -571,7 +571,7 @@ __global__ __launch_bounds__(64 * EC_WAVES, PC ? GS_EC_MINW : GS_EC_MINW_SH) voi
     }
     ldS = ec_wave_sum_u(ldS);
     quad = ec_wave_sum_u(quad);
-    double lph = (l < NF) ? log(ph[l]) : 0.0;
+    double lph = (l < NF) ? gs_log_lnl(ph[l]) : 0.0;
     lph = ec_wave_sum_u(lph);
     if (l == 0) {
       // in gs_ecorr_accept's convention: lnl + (aux1 - aux0 - aux2) / 2, with aux1 = 0 here
