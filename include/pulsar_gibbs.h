@@ -582,6 +582,26 @@ int gs_ecorr_prefix(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, i
                     int ldx, const double* Ap, const double* phiinv_F, double* model, double* aux,
                     double* lnl, int32_t* info, int64_t bx_cstride, int64_t dg_cstride, int64_t ap_cstride);
 /*
+ * gs_ecorr_lnl_state: gs_ecorr_prefix's likelihood mode with a stored per-chain state, for the
+ * Metropolis steps of update_ecorr_params (pulsar_gibbs.py:456-484; the reference re-factors the full
+ * system per step).  tbuf [2][n_chain][NT x 256] doubles (NT = the 16 x 16 tiles of the [M | F | d]
+ * upper triangle, (ldbx / 16) (ldbx / 16 + 1) / 2), tidx [n_chain] the chain's current slot.
+ *   x_old == NULL: full evaluation at x (as gs_ecorr_prefix), T = Ap - P(x) stored in slot tidx[c].
+ *   x_old != NULL: one step from the state at x_old to the proposal x, which moves one backend's
+ *     ECORR parameter (column prop[c * 4], gs_ecorr_propose's record): only that backend's epochs
+ *     are re-weighted, T(x) = T(x_old) - sum_{e of the backend} (1/a_e(x) - 1/a_e(x_old)) Bx_e^T Bx_e,
+ *     read from slot tidx[c] and written to slot tidx[c] ^ 1.  Epochs must be grouped by backend:
+ *     eoff [n_bk + 1] the first epoch of each backend (eoff[n_bk] = ne); Ap is not read.
+ * lnl / aux / info as gs_ecorr_prefix's likelihood mode.  gs_ecorr_accept_propose2 with tidx adopts
+ * the proposal's slot on acceptance.  Equal to the full evaluation to rounding (tests); the host
+ * re-evaluates from Ap at every Metropolis block's start.
+ */
+int gs_ecorr_lnl_state(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, int ldbx, const double* Bx,
+                       const double* Dg, const int32_t* ebk, int n_bk, const int32_t* xcol, const int32_t* eoff,
+                       const double* x, const double* x_old, const double* prop, int ldx, const double* Ap,
+                       const double* phiinv_F, double* tbuf, int32_t* tidx, double* aux, double* lnl, int32_t* info,
+                       int64_t bx_cstride, int64_t dg_cstride, int64_t ap_cstride);
+/*
  * White noise sampled with ECORR (per-chain N): Bx / Dg / Ap differ per chain.  gs_ecorr_gather
  * builds them from per-chain TNT [c][m x m] (tnt_cstride) and d [c][m] (d_cstride), e.g.
  * gs_white_tnt's output: Bx [c][ne x kb], Dg [c][ne], Ap [c][kb x kb] with colmap [kb] = the
@@ -618,6 +638,13 @@ int gs_ecorr_accept_propose(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ec
                             double* xq, double* x, int ldx, double* lnl0, double* q_rec, int32_t* n_acc,
                             const double* emin, const double* emax, int n_param, int next_step, int64_t sweep,
                             int64_t chain_base, const double* inj);
+/* gs_ecorr_accept_propose that also flips tidx [c] (gs_ecorr_lnl_state's slot) on acceptance
+ * (tidx == NULL: identical to gs_ecorr_accept_propose). */
+int gs_ecorr_accept_propose2(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, int init, const double* lnl,
+                             const int32_t* info, const int32_t* pinfo, const double* aux, double* prop,
+                             double* xq, double* x, int ldx, double* lnl0, double* q_rec, int32_t* n_acc,
+                             const double* emin, const double* emax, int n_param, int next_step, int64_t sweep,
+                             int64_t chain_base, const double* inj, int32_t* tidx);
 int gs_ecorr_bdraw_e(gs_ctx* ctx, int n_chain, int mR, int ne, int ldbx, const double* Bx, const double* Dg,
                      const int32_t* ebk, const int32_t* xcol, const double* x, int ldx, const double* bR,
                      int ldbR, const int32_t* ecid, const int32_t* rcol, int m, const double* z,

@@ -966,7 +966,7 @@ int gs_ecorr_prefix(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, i
   if (!Ap || !aux) return fail_arg(15, "NULL Ap / aux");
   if (lnl ? !phiinv_F : !model) return fail_arg(16, "likelihood mode needs phiinv_F, block mode needs model");
   if (n_chain == 0) return 0;
-  EcorrPrefixArgs a;
+  EcorrPrefixArgs a = {};
   a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.nM = nM; a.ne = ne; a.ldbx = ldbx; a.ldx = ldx; a.n_bk = n_bk;
   a.mstride = model_stride_doubles(NF, NMX);
   a.Bx = Bx; a.Dg = Dg; a.Ap = Ap; a.x = x; a.ebk = ebk; a.xcol = xcol; a.model = model; a.aux = aux; a.info = info;
@@ -975,6 +975,39 @@ int gs_ecorr_prefix(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, i
   if ((bx_cstride == 0) != (ap_cstride == 0) || (bx_cstride == 0) != (dg_cstride == 0))
     return fail_arg(20, "per-chain strides must be all zero or all nonzero");
   a.bx_cs = bx_cstride; a.dg_cs = dg_cstride; a.ap_cs = ap_cstride;
+  if (launch_ecorr_prefix(ctx->stream, a)) return fail_arg(7, "unsupported ldbx");
+  return after_launch("k_ecorr_prefix");
+}
+
+int gs_ecorr_lnl_state(gs_ctx* ctx, int n_chain, int NF, int NMX, int nM, int ne, int ldbx, const double* Bx,
+                       const double* Dg, const int32_t* ebk, int n_bk, const int32_t* xcol, const int32_t* eoff,
+                       const double* x, const double* x_old, const double* prop, int ldx, const double* Ap,
+                       const double* phiinv_F, double* tbuf, int32_t* tidx, double* aux, double* lnl, int32_t* info,
+                       int64_t bx_cstride, int64_t dg_cstride, int64_t ap_cstride) {
+  if (!ctx) return fail_arg(1, "ctx is NULL");
+  if (n_chain < 0) return fail_arg(2, "n_chain < 0");
+  if (NF != 20 && NF != 40 && NF != 60) return fail_arg(3, "NF must be 20, 40 or 60");
+  if (nM <= 0 || nM > 16 || NMX < nM || NMX > 64) return fail_arg(5, "need 1 <= nM <= 16, nM <= NMX <= 64");
+  if (ne < 0) return fail_arg(6, "ne < 0");
+  if (ldbx != 16 * (1 + (NF + 1 + 15) / 16)) return fail_arg(7, "ldbx must be 16 (1 + ceil((NF + 1) / 16))");
+  if (!Bx || !Dg || !ebk) return fail_arg(8, "NULL Bx / Dg / ebk");
+  if (n_bk <= 0 || n_bk > GS_WHITE_MAX_BK) return fail_arg(11, "n_bk must be in 1..15");
+  if (!xcol || !x || ldx <= 0) return fail_arg(12, "xcol / x / ldx");
+  if (x_old && (!prop || !eoff)) return fail_arg(14, "an incremental step needs prop and eoff");
+  if (!x_old && !Ap) return fail_arg(17, "a full evaluation needs Ap");
+  if (!phiinv_F || !aux || !lnl) return fail_arg(19, "NULL phiinv_F / aux / lnl");
+  if (!tbuf || !tidx) return fail_arg(20, "NULL tbuf / tidx");
+  if (bx_cstride < 0 || dg_cstride < 0 || ap_cstride < 0) return fail_arg(25, "negative per-chain stride");
+  if ((bx_cstride == 0) != (dg_cstride == 0) || (!x_old && (bx_cstride == 0) != (ap_cstride == 0)))
+    return fail_arg(25, "per-chain strides must be all zero or all nonzero");
+  if (n_chain == 0) return 0;
+  EcorrPrefixArgs a = {};
+  a.n_chain = n_chain; a.NF = NF; a.NMX = NMX; a.nM = nM; a.ne = ne; a.ldbx = ldbx; a.ldx = ldx; a.n_bk = n_bk;
+  a.mstride = model_stride_doubles(NF, NMX);
+  a.Bx = Bx; a.Dg = Dg; a.Ap = Ap; a.x = x; a.ebk = ebk; a.xcol = xcol; a.model = nullptr; a.aux = aux;
+  a.info = info; a.phiinv_F = phiinv_F; a.lnl = lnl;
+  a.bx_cs = bx_cstride; a.dg_cs = dg_cstride; a.ap_cs = ap_cstride;
+  a.xold = x_old; a.prop = prop; a.eoff = eoff; a.tbuf = tbuf; a.tidx = tidx;
   if (launch_ecorr_prefix(ctx->stream, a)) return fail_arg(7, "unsupported ldbx");
   return after_launch("k_ecorr_prefix");
 }
@@ -1067,6 +1100,15 @@ int gs_ecorr_accept_propose(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ec
                             double* xq, double* x, int ldx, double* lnl0, double* q_rec, int32_t* n_acc,
                             const double* emin, const double* emax, int n_param, int next_step, int64_t sweep,
                             int64_t chain_base, const double* inj) {
+  return gs_ecorr_accept_propose2(ctx, n_chain, n_e, ecol, init, lnl, info, pinfo, aux, prop, xq, x, ldx, lnl0,
+                                  q_rec, n_acc, emin, emax, n_param, next_step, sweep, chain_base, inj, nullptr);
+}
+
+int gs_ecorr_accept_propose2(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ecol, int init, const double* lnl,
+                             const int32_t* info, const int32_t* pinfo, const double* aux, double* prop,
+                             double* xq, double* x, int ldx, double* lnl0, double* q_rec, int32_t* n_acc,
+                             const double* emin, const double* emax, int n_param, int next_step, int64_t sweep,
+                             int64_t chain_base, const double* inj, int32_t* tidx) {
   if (!ctx) return fail_arg(1, "ctx is NULL");
   if (n_chain < 0) return fail_arg(2, "n_chain < 0");
   if (n_e <= 0 || !ecol) return fail_arg(3, "n_e / ecol");
@@ -1082,6 +1124,7 @@ int gs_ecorr_accept_propose(gs_ctx* ctx, int n_chain, int n_e, const int32_t* ec
   a.prop = prop; a.xq = xq; a.x = x; a.lnl0 = lnl0; a.q_rec = q_rec; a.n_acc = n_acc;
   a.n_param = n_param; a.emin = emin; a.emax = emax; a.inj = inj;
   a.sweep = sweep; a.chain_base = chain_base; a.sweep_dev = ctx->sweep_dev; a.key = key_of(ctx);
+  a.tidx = tidx;
   launch_ecorr_accept(ctx->stream, a);
   return after_launch("k_ecorr_accept");
 }

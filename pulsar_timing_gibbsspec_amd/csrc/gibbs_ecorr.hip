@@ -35,6 +35,9 @@ constexpr int EC_WAVES = GS_EC_WAVES;  // chains per workgroup (one wavefront ea
 #ifndef GS_EC_MINW_SH
 #define GS_EC_MINW_SH 3  // k_ecorr_prefix with the shared chunks
 #endif
+#ifndef GS_EC_MINW_INC
+#define GS_EC_MINW_INC 2  // the incremental Metropolis step
+#endif
 constexpr int EC_CH = 32;    // epochs per LDS chunk
 // per-chain operands (k_ecorr_prefix<.., PC = true>) staged by LDS-DMA, double-buffered 8-epoch
 // chunks (1) or through registers, one 16-epoch chunk at a time (0)
@@ -42,6 +45,13 @@ constexpr int EC_CH = 32;    // epochs per LDS chunk
 #define GS_EC_PCDMA 1
 #endif
 constexpr int EC_PCH = GS_EC_PCDMA ? 8 : 16;  // epochs per per-chain chunk
+// LDS buffers per wave of the per-wave DMA path: chunk i + NBUF - 1 is issued while chunk i is
+// multiplied (an 8-epoch chunk is only 2 k-steps = 30 MFMAs, ~1.9k cycles, against the L2 / HBM latency)
+#ifndef GS_EC_NBUF
+#define GS_EC_NBUF 2  // 3 measured no faster (r05z: the chunk latency is hidden at 2)
+#endif
+constexpr int EC_NBUF = GS_EC_NBUF;
+static_assert(EC_NBUF >= 2 && EC_NBUF <= 4, "GS_EC_NBUF in 2..4");
 // shared [B | d_E] chunks (one copy per workgroup) staged by LDS-DMA (1) or through registers (0)
 #ifndef GS_EC_GLDS
 #define GS_EC_GLDS 1
@@ -262,8 +272,17 @@ __global__ __launch_bounds__(64 * EC_WAVES, GS_EC_MINW) void k_ecorr_schur(Ecorr
 //                F pivot the eliminated (d, d) entry is -(d^T Sigma^-1 d) of the whole
 //                system (Ap_dd = 0), so no solve is needed and nothing per chain but lnl
 //                goes to HBM.
-template <int NB, bool LNL, bool PC>
-__global__ __launch_bounds__(64 * EC_WAVES, PC ? GS_EC_MINW : GS_EC_MINW_SH) void k_ecorr_prefix(EcorrPrefixArgs A) {
+// INC (likelihood mode, GS_EC_PCDMA): one Metropolis step from the chain's stored state instead of
+// the full epoch SYRK.  A step moves ONE backend's ECORR parameter, so only that backend's epochs
+// change weight: T(x') = T(x) - sum_{e in b} (1/a'_e - 1/a_e) [B | d_E]_e^T [B | d_E]_e, with T(x) =
+// Ap - P(x) read from tbuf[tidx[c]] (lane layout of the accumulator tiles) and T(x') written to the
+// other slot for k_ecorr_accept to adopt (tidx ^= 1) when the step is accepted.  Epochs are grouped by
+// backend (eoff[k] .. eoff[k + 1]), so the loop covers one backend's rows: half the MFMAs with two
+// backends.  Per-wave staging as the per-chain path (each chain's backend differs).
+template <int NB, bool LNL, bool PC, bool INC = false>
+__global__ __launch_bounds__(64 * EC_WAVES, INC ? GS_EC_MINW_INC : (PC ? GS_EC_MINW : GS_EC_MINW_SH)) void k_ecorr_prefix(
+    EcorrPrefixArgs A) {
+  static_assert(!INC || (LNL && GS_EC_PCDMA), "the incremental step is a likelihood-mode, LDS-DMA kernel");
   extern __shared__ double lds[];
   __shared__ double wb[2][EC_WAVES][EC_CH];
   __shared__ double sinv[EC_WAVES][GS_WHITE_MAX_BK + 1], slog[EC_WAVES][GS_WHITE_MAX_BK + 1];
@@ -293,18 +312,27 @@ __global__ __launch_bounds__(64 * EC_WAVES, PC ? GS_EC_MINW : GS_EC_MINW_SH) voi
   const double* Apc = A.Ap + (int64_t)(live ? ch_id : 0) * A.ap_cs;
   auto Aq = [&](int r0, int c0, int s) { return Apc[(int64_t)(r0 + 4 * s + q) * LDB + c0 + c]; };
   gs_d4_t acc[NT];
+  if constexpr (INC) {
+    const int tc = live ? A.tidx[ch_id] : 0;
+    const double* tb = A.tbuf + ((int64_t)tc * A.n_chain + (live ? ch_id : 0)) * (NT * 256);
 #pragma unroll
-  for (int s = 0; s < 4; ++s) acc[0][s] = live ? Aq(0, 0, s) : 0.0;
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
-  for (int r = 1; r < NB; ++r)
+      for (int s = 0; s < 4; ++s) acc[t][s] = live ? tb[(4 * t + s) * 64 + l] : 0.0;
+  } else {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) acc[r][s] = live ? Aq(0, 16 * r, s) : 0.0;
+    for (int s = 0; s < 4; ++s) acc[0][s] = live ? Aq(0, 0, s) : 0.0;
 #pragma unroll
-  for (int jj = 1; jj < NB; ++jj)
+    for (int r = 1; r < NB; ++r)
 #pragma unroll
-    for (int r = jj; r < NB; ++r)
+      for (int s = 0; s < 4; ++s) acc[r][s] = live ? Aq(0, 16 * r, s) : 0.0;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc[ts(jj, r)][s] = live ? Aq(16 * jj, 16 * r, s) : 0.0;
+    for (int jj = 1; jj < NB; ++jj)
+#pragma unroll
+      for (int r = jj; r < NB; ++r)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[ts(jj, r)][s] = live ? Aq(16 * jj, 16 * r, s) : 0.0;
+  }
   double sla = 0.0, slp = 0.0;
   constexpr int LPT = EC_CH * LDB / (64 * EC_WAVES);  // chunk elements per thread
   double reg[GS_EC_GLDS ? 1 : LPT];
@@ -347,7 +375,7 @@ __global__ __launch_bounds__(64 * EC_WAVES, PC ? GS_EC_MINW : GS_EC_MINW_SH) voi
     }
     if (l < EC_CH) wb[buf][w][l] = wv;
   };
-  if constexpr (PC) {
+  if constexpr (PC || INC) {
     // per-chain [B | d_E] (white noise sampled: TNT differs per chain): no sharing across
     // waves; each wavefront stages chunks of its own rows in its slice of the dynamic LDS
     if (!live) return;  // no workgroup barriers below
@@ -378,46 +406,85 @@ __global__ __launch_bounds__(64 * EC_WAVES, PC ? GS_EC_MINW : GS_EC_MINW_SH) voi
       // weight 0.  1/a of a 64-epoch segment is computed by its lanes at the segment's first
       // chunk (the only ordinary loads of the loop; their wait also covers chunk i's DMA).
       constexpr int CHD = PCH * LDB;
-      double* bufs = lds + (int64_t)w * (2 * CHD + 64);
-      double* wsl = bufs + 2 * CHD;
+      double* bufs = lds + (int64_t)w * (EC_NBUF * CHD + 64);
+      double* wsl = bufs + EC_NBUF * CHD;
       const bool w16 = (reinterpret_cast<uintptr_t>(Bc) & 15) == 0;  // uniform
-      auto dma = [&](int e0, double* dst) { ec_dma_rows<LDB, PCH>(Bc, e0, ne, dst, 0, 1, l, w16); };
-      constexpr int WAIT16 = ec_vmcnt(NB), WAIT4 = ec_vmcnt(4 * NB), WAIT0 = ec_vmcnt(0);
-      const int nch = (ne + PCH - 1) / PCH;
+      // epoch range [e_lo, e_hi): all epochs, or (INC) the moved backend's
+      int e_lo = 0, e_hi = ne;
+      double s_new = 0.0, s_old = 0.0;  // INC: 1/phi of the moved backend at the proposal / the state
+      if constexpr (INC) {
+        const int col = (int)A.prop[(int64_t)ch_id * 4];
+        const unsigned long long mk = __ballot(l < A.n_bk && A.xcol[l < A.n_bk ? l : 0] == col);
+        const int k = mk ? (int)__builtin_ctzll(mk) : -1;
+        if (k >= 0) {
+          e_lo = __builtin_amdgcn_readfirstlane(A.eoff[k]);
+          e_hi = __builtin_amdgcn_readfirstlane(A.eoff[k + 1]);
+          s_new = sinv[w][k];
+          double lg;
+          ec_phi(A.xold[(int64_t)ch_id * A.ldx + col], s_old, lg);
+        } else {
+          e_hi = 0;  // nothing moved: T(x') = T(x)
+        }
+        // sum log a and sum log phi_E over every epoch at the proposal
+        for (int e = l; e < ne; e += 64) {
+          const int kb = A.ebk[e];
+          sla += gs_log_lnl(Dc[e] + sinv[w][kb]);
+          slp += slog[w][kb];
+        }
+      }
+      auto dma = [&](int e0, double* dst) { ec_dma_rows<LDB, PCH>(Bc, e0, e_hi, dst, 0, 1, l, w16); };
+      constexpr int WAIT0 = ec_vmcnt(0);
+      const int nch = (e_hi - e_lo + PCH - 1) / PCH;
       // the accumulators' Ap loads land here: otherwise the loop's first MFMA waits vmcnt(0) (the
       // waitcnt pass merges the loop entry into every iteration) and no DMA overlaps the math
       __builtin_amdgcn_s_waitcnt(WAIT0);
-      if (nch > 0) dma(0, bufs);  // (ne = 0: no rows to read)
+      // chunks 0 .. NBUF - 2 in flight before the loop (no rows: nothing to read)
+#pragma unroll
+      for (int j = 0; j < EC_NBUF - 1; ++j)
+        if (j < nch) dma(e_lo + j * PCH, bufs + j * CHD);
+      // s_waitcnt immediates: chunk i has landed once at most n chunks issued after it are pending
+      auto wait_chunks = [&](int n) {  // n uniform, 0 .. NBUF - 2
+        if (w16) {
+          if (n >= 2) __builtin_amdgcn_s_waitcnt(ec_vmcnt(2 * NB));
+          else if (n == 1) __builtin_amdgcn_s_waitcnt(ec_vmcnt(NB));
+          else __builtin_amdgcn_s_waitcnt(WAIT0);
+        } else {
+          if (n >= 2) __builtin_amdgcn_s_waitcnt(ec_vmcnt(8 * NB));
+          else if (n == 1) __builtin_amdgcn_s_waitcnt(ec_vmcnt(4 * NB));
+          else __builtin_amdgcn_s_waitcnt(WAIT0);
+        }
+      };
       for (int i = 0; i < nch; ++i) {
-        const int e0 = i * PCH;
-        if ((e0 & 63) == 0) {
+        const int e0 = e_lo + i * PCH, er = i * PCH;
+        if ((er & 63) == 0) {
           double wv = 0.0;
-          if (e0 + l < ne) {
+          if (e0 + l < e_hi) {
             const int e = e0 + l;
-            const int kb = A.ebk[e];
-            const double a = Dc[e] + sinv[w][kb];
-            wv = 1.0 / a;
-            sla += gs_log_lnl(a);
-            slp += slog[w][kb];
+            if constexpr (INC) {
+              const double dg = Dc[e];
+              wv = 1.0 / (dg + s_new) - 1.0 / (dg + s_old);
+            } else {
+              const int kb = A.ebk[e];
+              const double a = Dc[e] + sinv[w][kb];
+              wv = 1.0 / a;
+              sla += gs_log_lnl(a);
+              slp += slog[w][kb];
+            }
           }
           wsl[l] = wv;
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (i + 1 < nch) {
-          dma(e0 + PCH, bufs + ((i + 1) & 1) * CHD);  // that buffer's reads ended with chunk i - 1
-          if (w16) __builtin_amdgcn_s_waitcnt(WAIT16);
-          else __builtin_amdgcn_s_waitcnt(WAIT4);
-        } else {
-          __builtin_amdgcn_s_waitcnt(WAIT0);
-        }
+        const int ia = i + EC_NBUF - 1;  // the chunk issued now (its buffer's reads ended with chunk i - 1)
+        if (ia < nch) dma(e0 + (EC_NBUF - 1) * PCH, bufs + (ia % EC_NBUF) * CHD);
+        wait_chunks(min(EC_NBUF - 1, nch - 1 - i));
         __builtin_amdgcn_sched_barrier(0);
         wave_lds_sync();
-        const double* cur = bufs + (i & 1) * CHD;
-        const int nk = min(PCH / 4, (ne - e0 + 3) / 4);
+        const double* cur = bufs + (i % EC_NBUF) * CHD;
+        const int nk = min(PCH / 4, (e_hi - e0 + 3) / 4);
 #pragma unroll
         for (int kk = 0; kk < PCH / 4; ++kk) {
           if (kk >= nk) break;
-          kstep(cur, wsl + (e0 & 63), kk);
+          kstep(cur, wsl + (er & 63), kk);
         }
       }
     } else {
@@ -486,6 +553,15 @@ __global__ __launch_bounds__(64 * EC_WAVES, PC ? GS_EC_MINW : GS_EC_MINW_SH) voi
     if (chk + 1 < nch) store(cb ^ 1);
     __syncthreads();
   }
+  }
+  if (A.tbuf && live) {
+    // T = Ap - P of this evaluation into the chain's state slot (INC: the proposal's slot)
+    const int tc = A.tidx[ch_id] ^ (INC ? 1 : 0);
+    double* tb = A.tbuf + ((int64_t)tc * A.n_chain + ch_id) * (NT * 256);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) tb[(4 * t + s) * 64 + l] = acc[t][s];
   }
   sla = ec_wave_sum_u(sla);
   slp = ec_wave_sum_u(slp);
@@ -712,6 +788,7 @@ __global__ __launch_bounds__(256) void k_ecorr_accept(EcorrMhArgs A) {
       A.x[(int64_t)c * A.ldx + (int)pr[0]] = pr[3];
       A.lnl0[c] = l1;
       if (A.n_acc) A.n_acc[c] += 1;
+      if (A.tidx) A.tidx[c] ^= 1;  // the proposal's stored T becomes the chain's state
     }
   }
   // gs_ecorr_accept_propose: the next step's proposal from the updated state, same thread
@@ -819,23 +896,30 @@ void launch_schur_nb(hipStream_t s, const EcorrSchurArgs& a) {
   }
 }
 
-template <int NB, bool LNL, bool PC>
+template <int NB, bool LNL, bool PC, bool INC = false>
 void launch_prefix_nbp(hipStream_t s, const EcorrPrefixArgs& a) {
   static bool attr = false;
-  const size_t lds = PC ? (size_t)EC_WAVES *
-                               (GS_EC_PCDMA ? 2 * EC_PCH * 16 * NB + 64 : EC_PCH * 16 * NB + EC_PCH) * sizeof(double)
+  const size_t lds = (PC || INC) ? (size_t)EC_WAVES *
+                               (GS_EC_PCDMA ? EC_NBUF * EC_PCH * 16 * NB + 64 : EC_PCH * 16 * NB + EC_PCH) *
+                               sizeof(double)
                         : (size_t)2 * EC_CH * 16 * NB * sizeof(double);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_ecorr_prefix<NB, LNL, PC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_ecorr_prefix<NB, LNL, PC, INC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((k_ecorr_prefix<NB, LNL, PC>), dim3((unsigned)((a.n_chain + EC_WAVES - 1) / EC_WAVES)),
+  hipLaunchKernelGGL((k_ecorr_prefix<NB, LNL, PC, INC>), dim3((unsigned)((a.n_chain + EC_WAVES - 1) / EC_WAVES)),
                      dim3(64 * EC_WAVES), lds, s, a);
 }
 
 template <int NB, bool LNL>
 void launch_prefix_nb(hipStream_t s, const EcorrPrefixArgs& a) {
+  if constexpr (LNL) {
+    if (a.xold) {  // incremental Metropolis step (shared or per-chain operands alike)
+      launch_prefix_nbp<NB, true, false, true>(s, a);
+      return;
+    }
+  }
   if (a.bx_cs) launch_prefix_nbp<NB, LNL, true>(s, a);
   else launch_prefix_nbp<NB, LNL, false>(s, a);
 }

@@ -296,6 +296,7 @@ struct EcorrMhArgs {
   const int32_t *info, *pinfo;
   double *x, *xq, *prop, *lnl0, *q_rec;
   int32_t* n_acc;
+  int32_t* tidx;  // incremental ECORR state: flipped on acceptance (NULL: none)
 };
 struct EcorrBArgs {
   int n_chain, mR, ne, ldbx, ldx, ldbR, m, ldb, event, dcol;
@@ -315,6 +316,13 @@ struct EcorrPrefixArgs {
   const int32_t *ebk, *xcol;
   double *model, *aux, *lnl;
   int32_t* info;
+  // stored state T = Ap - P (gs_ecorr_lnl_state): tbuf [2][n_chain][NT x 256], tidx [n_chain] the
+  // current slot; xold != NULL: incremental step from the state at xold to x (prop: the proposal
+  // records, eoff: per-backend epoch offsets)
+  const double *xold, *prop;
+  const int32_t* eoff;
+  double* tbuf;
+  int32_t* tidx;
 };
 int launch_ecorr_prefix(hipStream_t s, const EcorrPrefixArgs& a);
 struct EcorrGatherArgs {

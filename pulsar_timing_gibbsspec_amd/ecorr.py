@@ -19,6 +19,7 @@ configuration of SURVEY 8f-4's J1713 run: efac/equad from a noise dictionary).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -47,6 +48,10 @@ class EcorrModel:
         T = np.ascontiguousarray(T, float)
         n_toa, m = T.shape
         ecid = np.asarray(ecid, np.int64)
+        # epochs grouped by backend (stable order): each backend's epochs are one contiguous row range
+        # of [B | d_E], which the incremental Metropolis step (gs_ecorr_lnl_state) re-weights alone
+        order = np.argsort(np.asarray(epoch_backend, np.int64), kind="stable")
+        ecid, epoch_backend = ecid[order], np.asarray(epoch_backend, np.int64)[order]
         gwid = np.asarray(gwid, np.int64)
         NF = gwid.size
         if NF not in TUNED_NF:
@@ -86,6 +91,8 @@ class EcorrModel:
         self.dR = d[r_t].contiguous()
         self.TNT_full, self.d_full = TNT, d
         self.ebk = _t(np.asarray(epoch_backend, np.int32), torch.int32, dev)
+        self.eoff_host = np.searchsorted(epoch_backend, np.arange(len(ecol) + 1)).astype(np.int32)
+        self.eoff = _t(self.eoff_host, torch.int32, dev)
         self.ecol = _t(np.asarray(ecol, np.int32), torch.int32, dev)
         self.ecol_host = np.asarray(ecol, np.int64)
         self.n_bk = len(ecol)
@@ -104,6 +111,9 @@ class EcorrModel:
         # fused path (gs_ecorr_prefix): columns [M (<= 16) | F | d], phiinv_M on the M diagonal
         self.fused = self.nm <= 16
         self.fused_lnl = True   # likelihood-mode launches for the Metropolis steps
+        # Metropolis steps from the stored state (gs_ecorr_lnl_state): only the moved backend's epochs
+        # re-weighted per step; a full evaluation starts every block and every REFRESH steps
+        self.incremental = os.environ.get("GS_ECORR_INC", "1") != "0"   # (GS_ECORR_INC=0: A/B builds)
         if self.fused:
             KB = 16 * (1 + (NF + 1 + 15) // 16)
             self.ldbp = KB
@@ -237,6 +247,25 @@ class EcorrModel:
         val = self.lnl + 0.5 * (a[:, 1] - a[:, 0] - a[:, 2]) + const
         return torch.where(ok, val, torch.full_like(val, -np.inf))
 
+    REFRESH = 64   # incremental steps between full evaluations of the state (rounding does not pile up)
+
+    def _state_buffers(self):
+        if not hasattr(self, "tbuf"):
+            nb = self.ldbp // 16
+            nt = nb * (nb + 1) // 2
+            self.tbuf = torch.empty(2, self.C, nt * 256, dtype=torch.float64, device=self.ctx.device)
+            self.tidx = torch.zeros(self.C, dtype=torch.int32, device=self.ctx.device)
+
+    def _eval_state(self, x, phiinv_F, x_old=None):
+        """gs_ecorr_lnl_state: lnl / aux / pinfo at x, fully (x_old None: the state slot tidx gets
+        T(x)) or as one Metropolis step from the stored state at x_old (the other slot gets T(x))."""
+        bs, ds, aps = self.strides
+        check(self.ctx.lib.gs_ecorr_lnl_state(
+            self.ctx.handle, self.C, self.NF, self.NMX, self.nm, self.ne, self.ldbp, ptr(self.Bp), ptr(self.Dg),
+            ptr(self.ebk), self.n_bk, ptr(self.ecol), ptr(self.eoff), ptr(x), ptr(x_old),
+            ptr(self.prop) if x_old is not None else None, x.shape[1], ptr(self.Ap), ptr(phiinv_F), ptr(self.tbuf),
+            ptr(self.tidx), ptr(self.aux), ptr(self.lnl), ptr(self.pinfo), bs, ds, aps), "gs_ecorr_lnl_state")
+
     def mh(self, x, phiinv_F, n_steps, sweep=0, chain_base=0, inj=None, q_rec=None, n_acc=None):
         """n_steps Metropolis steps of update_ecorr_params (pulsar_gibbs.py:456-484) for every
         chain, x (C, n_param) updated in place.  inj (n_steps, C, 4) or None (Philox);
@@ -244,20 +273,35 @@ class EcorrModel:
         lib, h = self.ctx.lib, self.ctx.handle
         ne_p = self.n_bk
         n_steps = int(n_steps)
-        self._eval(x, phiinv_F)
+        inc = self.incremental and self.fused and self.fused_lnl
+        if inc:
+            self._state_buffers()
+            if self._linfo_dirty:   # the likelihood-mode kernels report through pinfo only
+                self.linfo.zero_()
+                self._linfo_dirty = False
+            self.tidx.zero_()
+            self._eval_state(x, phiinv_F)
+        else:
+            self._eval(x, phiinv_F)
+        tidx = self.tidx if inc else None
 
         # each accept launch also draws the next step's proposal (gs_ecorr_accept_propose):
         # init + propose(0), then per step likelihood -> accept(s) + propose(s + 1)
         def accept_propose(init, qr, nxt):
-            check(lib.gs_ecorr_accept_propose(
+            check(lib.gs_ecorr_accept_propose2(
                 h, self.C, ne_p, ptr(self.ecol), init, ptr(self.lnl), ptr(self.linfo), ptr(self.pinfo),
                 ptr(self.aux), ptr(self.prop), ptr(self.xq), ptr(x), x.shape[1], ptr(self.lnl0), ptr(qr),
                 None if init else ptr(n_acc), ptr(self.emin), ptr(self.emax), self.n_param, nxt, sweep,
-                chain_base, ptr(inj)), "gs_ecorr_accept_propose")
+                chain_base, ptr(inj), ptr(tidx)), "gs_ecorr_accept_propose2")
 
         accept_propose(1, None, 0 if n_steps > 0 else -1)
         for s in range(n_steps):
-            self._eval(self.xq, phiinv_F)
+            if inc:
+                if s and s % self.REFRESH == 0:
+                    self._eval_state(x, phiinv_F)          # re-base the state at x (lnl0 kept)
+                self._eval_state(self.xq, phiinv_F, x_old=x)
+            else:
+                self._eval(self.xq, phiinv_F)
             accept_propose(0, q_rec[s] if q_rec is not None else None, s + 1 if s + 1 < n_steps else -1)
 
     def bdraw(self, x, phiinv_F, b, z=None, sweep=0, first=False, chain_base=0, chain_mask=None):

@@ -558,3 +558,58 @@ def test_ecorr_prefix_staging_edges(ctx, ne):
         want, waux = _prefix_lnl_numpy(Bn, Dn, En, An, X[c], ecol, _phiinv_F(g, X)[c], NF)
         assert abs(outs[0][0][c] - want) < 1e-9 * max(1.0, abs(want)), (ne, c, outs[0][0][c], want)
         np.testing.assert_allclose(outs[0][1][c], waux, rtol=1e-11, atol=1e-11)
+
+
+def _mh_both_ways(em, x0, phf, n_steps, sweep=3):
+    """em.mh from x0 with the incremental state steps and with a full evaluation per step (same
+    Philox draws): (x, lnl0, n_acc) of each, and the stored state's deviation from a fresh T(x)."""
+    import torch
+    out = []
+    for inc in (True, False):
+        em.incremental = inc
+        x = x0.clone()
+        n_acc = torch.zeros(x.shape[0], dtype=torch.int32, device="cuda")
+        em.mh(x, phf, n_steps, sweep=sweep, n_acc=n_acc)
+        out.append((x.cpu().numpy(), em.lnl0.cpu().numpy().copy(), n_acc.cpu().numpy()))
+        if inc:
+            C = x.shape[0]
+            cur = em.tbuf[em.tidx.long(), torch.arange(C, device="cuda")].clone()
+            em.tidx.zero_()
+            em._eval_state(x, phf)               # fresh full T(x) into slot 0
+            fresh = em.tbuf[0].clone()
+            dev = float(((cur - fresh).abs().amax(dim=1) / fresh.abs().amax(dim=1)).max())
+    em.incremental = True
+    return out, dev
+
+
+def test_ecorr_incremental_steps_match_full(ctx):
+    """The incremental Metropolis step (gs_ecorr_lnl_state: only the moved backend's epochs
+    re-weighted from the stored T) against a full evaluation per step, 256 chains x 200 Philox steps
+    (past one REFRESH): identical accept/reject decisions (x and acceptance counts bit-identical),
+    lnL0 within 1e-9 relative, and the stored state within 1e-11 of a fresh T(x)."""
+    g = golden("ecorr_mh_j1713.npz")
+    C = 256
+    X = np.repeat(g["x_like"][:1], C, axis=0)
+    em = _model(ctx, g, C)
+    assert em.eoff_host[0] == 0 and em.eoff_host[-1] == em.ne and np.all(np.diff(em.eoff_host) > 0)
+    (a, b), dev = _mh_both_ways(em, _dev(X), _dev(_phiinv_F(g, X)), 200)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[2], b[2])
+    assert a[2].min() > 0
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-9, atol=0)
+    assert dev < 1e-11, dev
+
+
+def test_ecorr_white_incremental_steps_match_full(ctx):
+    """The same with per-chain operands (white noise sampled: gs_white_tnt -> gs_ecorr_gather), the
+    chains at different white-noise states."""
+    g = golden("ecorr_white_j1713.npz")
+    X = g["x_like"]
+    C = X.shape[0]
+    wm, em, _, _ = _white_setup(ctx, g, C)
+    x = _dev(X)
+    wm.tnt(x, x.shape[1])
+    em.gather(wm.TNT, wm.d, wm.tnt_cstride, wm.d_cstride)
+    (a, b), dev = _mh_both_ways(em, x, _dev(_phiinv_F(g, X)), 80)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[2], b[2])
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-9, atol=0)
+    assert dev < 1e-11, dev

@@ -49,9 +49,10 @@ HOT = [
     ("k_rho_curn_sum_waveILi16EE", 2, 0),
     ("k_white_syrkILi14EE", 2, 0),                 # configs[4] per-chain TNT (m = 216)
     ("k_tntEPK", 4, 0),                            # TNT / d, compensated block sums
-    ("k_ecorr_prefixILi5ELb1ELb0E", 3, 4),         # ECORR likelihood, shared chunks (round 5:
+    ("k_ecorr_prefixILi5ELb1ELb0ELb0E", 3, 4),     # ECORR likelihood, shared chunks (round 5:
                                                    # 3 waves/SIMD with 3 spills, 5 % faster than 2)
-    ("k_ecorr_prefixILi5ELb1ELb1E", 2, 0),         # ... per-chain operands (white noise sampled)
+    ("k_ecorr_prefixILi5ELb1ELb1ELb0E", 2, 0),     # ... per-chain operands (white noise sampled)
+    ("k_ecorr_prefixILi5ELb1ELb0ELb1E", 2, 0),     # ... incremental Metropolis step
 ]
 
 
