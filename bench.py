@@ -581,6 +581,44 @@ def chain_ess(eng, cols, burn=300, sweeps=1000, max_chains=256):
     return ess_fraction(xe.cpu().numpy(), burn_frac=0.0), ce
 
 
+def ecorr_step_roofline(ctx, em, x, phiinv_F, reps=10):
+    """The ECORR Metropolis step's kernel (gs_ecorr_lnl_state, incremental: the moved backend's epochs
+    only), HIP-event timed alone on the context stream: a full evaluation stores the state at x, one
+    proposal (gs_ecorr_propose, step 0) is drawn, then `reps` steps from that state (the state slot is
+    not adopted, so every step reads the same T).  Algorithmic flops per chain: the moved backend's
+    epochs (n_E / n_backends on average) x (mR+1)(mR+2) + nM (NF+1)(NF+2) + (NF+1)^3/3."""
+    from pulsar_timing_gibbsspec_amd._lib import check as lcheck, ptr
+    if not (em.incremental and em.fused and em.fused_lnl):
+        return None
+    em._state_buffers()
+    em.tidx.zero_()
+    em._eval_state(x, phiinv_F)
+    lcheck(ctx.lib.gs_ecorr_propose(ctx.handle, em.C, em.n_bk, ptr(em.ecol), ptr(em.emin), ptr(em.emax), ptr(x),
+                                    x.shape[1], em.n_param, ptr(em.xq), 0, 0, 0, None, ptr(em.prop)),
+           "gs_ecorr_propose")
+    for _ in range(3):
+        em._eval_state(em.xq, phiinv_F, x_old=x)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(ctx.stream)
+    for _ in range(reps):
+        em._eval_state(em.xq, phiinv_F, x_old=x)
+    e1.record(ctx.stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    mR, NF, nM, C = em.mR, em.NF, em.nm, em.C
+    flops = C * (em.ne / em.n_bk * (mR + 1) * (mR + 2) + nM * (NF + 1) * (NF + 2) + (NF + 1) ** 3 // 3)
+    nb = em.ldbp // 16
+    tfl = flops / (ms * 1e-3) / 1e12
+    return {"kernel": "k_ecorr_prefix<likelihood mode, incremental step> (gs_ecorr_lnl_state)", "bound": "mfma",
+            "achieved": tfl, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tfl / FP64_PEAK_TFLOPS,
+            "kernel_avg_ms": ms, "alg_flops_per_launch": flops, "traffic": None,
+            "state_bytes_per_launch": C * 2 * 8 * 256 * nb * (nb + 1) // 2,
+            "note": "the per-step kernel of the ECORR Metropolis block (aclength launches per sweep; the full "
+                    "evaluation runs once per block): the moved backend's epochs re-weighted from the stored "
+                    "T = Ap - P (read and the proposal's written: state_bytes_per_launch); traffic null (PMC "
+                    "passes over the ECORR lines crash in rocprofv3 on this image)"}
+
+
 def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
     """SURVEY 8f-4 with white noise sampled too (the notebook's J1713 configuration): per sweep
     white MH (aclength steps) -> per-chain TNT (gs_white_tnt) -> per-chain ECORR operands ->
@@ -638,6 +676,7 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
     e1.record(stream)
     torch.cuda.synchronize()
     k_ms = e0.elapsed_time(e1) / reps
+    step = ecorr_step_roofline(ctx, em, eng.x, eng.phiinv_F)
     mR, NF, nM = em.mR, em.NF, em.nm
     flops = C * (ne * (mR + 1) * (mR + 2) + nM * (NF + 1) * (NF + 2) + (NF + 1) ** 3 // 3)
     tflops = flops / (k_ms * 1e-3) / 1e12
@@ -663,7 +702,9 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
                                   "HBM (alg_bytes_per_launch); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE, the x2 "
                                   "wide-read correction makes it an upper estimate (measured on the round-3 "
                                   "kernel, profiles/pmc_traffic_ecorr_white.json: PMC passes over the ECORR "
-                                  "lines crash in rocprofv3 on this image, profiles/r05t/SUMMARY.md)"},
+                                  "lines crash in rocprofv3 on this image, profiles/r05t/SUMMARY.md); the full "
+                                  "evaluation (once per Metropolis block); the per-step kernel: step_roofline"},
+                step_roofline=step,
                 config="SURVEY 8f-4 with EFAC/EQUAD sampled: J1713-like pulsar, 2 backends, 136 ECORR epochs, "
                        "white MH + per-chain TNT + ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
 
@@ -719,6 +760,7 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
     e1.record(stream)
     torch.cuda.synchronize()
     k_ms = e0.elapsed_time(e1) / reps
+    step = ecorr_step_roofline(ctx, em, eng.x, eng.phiinv_F)
     mR, NF, nM = em.mR, em.NF, em.nm
     # epoch-weighted SYRK (lower triangle of [B | d_E]^T W [B | d_E]) + the fixed-prior Schur
     # update + the (NF+1)-augmented Cholesky of the free-spectrum block
@@ -739,7 +781,9 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
                           "note": "ne (mR+1)(mR+2) + nM (NF+1)(NF+2) + (NF+1)^3/3 flop per chain (epoch-weighted "
                                   "SYRK with the d_E row + fixed-prior Schur update + F-block Cholesky) over the "
                                   "HIP-event time of one all-chain likelihood launch; traffic: PMC of the round-3 kernel "
-                                  "(profiles/pmc_traffic_ecorr.json; same operands, L2-resident)"},
+                                  "(profiles/pmc_traffic_ecorr.json; same operands, L2-resident); the full evaluation "
+                                  "(once per Metropolis block); the per-step kernel: step_roofline"},
+                step_roofline=step,
                 config="SURVEY 8f-4: J1713-like pulsar, basis ECORR (2 backends, 136 epochs) + 30-bin free "
                        "spectrum + 16-col TM, ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
 
