@@ -312,7 +312,12 @@ __global__ __launch_bounds__(64 * EC_WAVES, INC ? GS_EC_MINW_INC : (PC ? GS_EC_M
   const double* Apc = A.Ap + (int64_t)(live ? ch_id : 0) * A.ap_cs;
   auto Aq = [&](int r0, int c0, int s) { return Apc[(int64_t)(r0 + 4 * s + q) * LDB + c0 + c]; };
   gs_d4_t acc[NT];
+  // (GS_EC_PROBE_INC_NOLOAD / _NOSTORE: cost-attribution builds only, wrong results)
+#ifdef GS_EC_PROBE_INC_NOLOAD
+  if constexpr (false) {
+#else
   if constexpr (INC) {
+#endif
     const int tc = live ? A.tidx[ch_id] : 0;
     const double* tb = A.tbuf + ((int64_t)tc * A.n_chain + (live ? ch_id : 0)) * (NT * 256);
 #pragma unroll
@@ -554,7 +559,11 @@ __global__ __launch_bounds__(64 * EC_WAVES, INC ? GS_EC_MINW_INC : (PC ? GS_EC_M
     __syncthreads();
   }
   }
+#ifdef GS_EC_PROBE_INC_NOSTORE
+  if (A.tbuf && live && !INC) {
+#else
   if (A.tbuf && live) {
+#endif
     // T = Ap - P of this evaluation into the chain's state slot (INC: the proposal's slot)
     const int tc = A.tidx[ch_id] ^ (INC ? 1 : 0);
     double* tb = A.tbuf + ((int64_t)tc * A.n_chain + ch_id) * (NT * 256);
