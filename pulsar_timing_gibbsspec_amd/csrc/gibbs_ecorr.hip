@@ -404,12 +404,12 @@ __global__ __launch_bounds__(64 * EC_WAVES, INC ? GS_EC_MINW_INC : (PC ? GS_EC_M
       }
     };
     if constexpr (GS_EC_PCDMA) {
-      // LDS-DMA: the rows of chunk i + 1 go global -> LDS (lane-linear, NB wave-instructions of
-      // 16-byte units, or 4 NB of 4-byte units when the chain's rows are not 16-byte aligned)
-      // while chunk i is multiplied; the chunk's rows past ne re-read row ne - 1, so every chunk
-      // issues the same instruction count (the vmcnt wait below counts them) and those rows have
-      // weight 0.  1/a of a 64-epoch segment is computed by its lanes at the segment's first
-      // chunk (the only ordinary loads of the loop; their wait also covers chunk i's DMA).
+      // LDS-DMA: the rows of chunk i + NBUF - 1 go global -> LDS (lane-linear, NB wave-instructions
+      // of 16-byte units, or 4 NB of 4-byte units when the chain's rows are not 16-byte aligned)
+      // while chunk i is multiplied; a chunk's rows past the range end e_hi re-read row e_hi - 1, so
+      // every chunk issues the same instruction count (the vmcnt waits below count them) and those
+      // rows have weight 0.  The weights of a 64-epoch segment are computed by its lanes at the
+      // segment's first chunk (the only ordinary loads of the loop; their wait also covers the DMA).
       constexpr int CHD = PCH * LDB;
       double* bufs = lds + (int64_t)w * (EC_NBUF * CHD + 64);
       double* wsl = bufs + EC_NBUF * CHD;
