@@ -613,3 +613,45 @@ def test_ecorr_white_incremental_steps_match_full(ctx):
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[2], b[2])
     np.testing.assert_allclose(a[1], b[1], rtol=1e-9, atol=0)
     assert dev < 1e-11, dev
+
+
+def test_ecorr_four_backends_incremental_and_oracle(ctx):
+    """Four backends, the epoch columns handed over in a shuffled order (EcorrModel groups them by
+    backend for the incremental step): incremental vs full-evaluation Metropolis steps (identical
+    decisions), and the likelihood at the chains' final states against the oracle's
+    get_lnlikelihood_fullmarg restatement (pulsar_gibbs.py:569-610) on the full basis, to 1e-7."""
+    import torch
+    from pulsar_timing_gibbsspec_amd import synthetic
+    from pulsar_timing_gibbsspec_amd.ecorr import EcorrModel
+    from pulsar_timing_gibbsspec_amd.pulsar_gibbs import PulsarBlockGibbs
+    pta = synthetic.ecorr_pulsar_pta("J1713+0747", seed=5, n_backends=4, n_epoch=120)
+    names = pta.param_names
+    ebk = pta.signals["J1713+0747_basis_ecorr"].epoch_backend
+    ne = ebk.size
+    perm = np.random.default_rng(3).permutation(ne)
+    assert not np.all(np.diff(ebk[perm]) >= 0)
+    eind = [i for i, n in enumerate(names) if "ecorr" in n]
+    gw = [i for i, n in enumerate(names) if "rho" in n]
+    T, r = pta.get_basis()[0], pta.get_residuals()[0]
+    gwid = ne + np.arange(2 * len(gw))
+    C = 128
+    em = EcorrModel(ctx, T, pta.get_ndiag()[0], r, perm, ebk[perm], gwid, eind, [-8.5] * 4, [-5.0] * 4,
+                    len(names), C)
+    assert np.all(np.diff(em.ebk.cpu().numpy()) >= 0) and em.eoff_host.size == 5
+    rng = np.random.default_rng(7)
+    X = np.concatenate([rng.uniform(-7.5, -5.5, (C, len(eind))), rng.uniform(-8, -5, (C, len(gw)))], axis=1)
+    phf = _dev(1.0 / np.repeat(10.0 ** (2.0 * X[:, gw]), 2, axis=1))
+    (a, b), dev = _mh_both_ways(em, _dev(X), phf, 120)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[2], b[2]) and a[2].min() > 0
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-9, atol=0)
+    assert dev < 1e-11, dev
+    Xf = a[0]
+    got = em.lnlike(_dev(Xf), _dev(1.0 / np.repeat(10.0 ** (2.0 * Xf[:, gw]), 2, axis=1))).cpu().numpy()
+    gb = PulsarBlockGibbs(pta, nchains=1, seed=0)
+    for c in range(0, C, 37):
+        params = gb.map_params(Xf[c])
+        N = pta.get_ndiag(params)[0]
+        phiinv, logdet = pta.get_phiinv(params, logdet=True)[0]
+        TNT, d = O.tnt(T, N, r)
+        ref = O.lnlike_fullmarg(r, N, TNT, d, phiinv, logdet)
+        assert abs(got[c] - ref) < 1e-7 * max(1.0, abs(ref)), (c, got[c], ref)
