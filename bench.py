@@ -1057,10 +1057,10 @@ def main():
     if args.ecorr:
         phase("ecorr")
         d = bench_ecorr(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev)
-        d["sharding"] = "chains, weak"
+        d.update(sharding="chains (no collective)", scaling="weak", n_gpus=world)
         add("ecorr", d, "ecorr")
         d = bench_ecorr_white(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev)
-        d["sharding"] = "chains, weak"
+        d.update(sharding="chains (no collective)", scaling="weak", n_gpus=world)
         add("ecorr_white", d, "ecorr_white")
     if args.config5:
         phase("configs[4] config5")
