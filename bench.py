@@ -294,7 +294,8 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
         eng.check_fx()
     total_chains = C if sharded else C * world
     value = total_chains * K / el
-    out = dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K, warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
+    out = dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+               warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
                chains_per_gpu=C, n_psr=len(T), n_param=len(names), n_gpus=world,
                scaling="strong" if sharded else "weak",
                sharding=("pulsars over %d GPUs (RCCL %s per sweep)" %
@@ -487,7 +488,8 @@ def bench_indep(C, K, W, S, rank, world, dev):
     ess = None
     if K >= 50:                                      # min over (pulsar, bin) of the whole-job ESS/s
         ess = min(ess_min_bin(xh[:, p], el, C) for p in range(P))
-    return dict(value=C * K / el, unit="array-iters/s", ms_per_step=el / K * 1e3, steps=K, warmup={"n": n_warm, "unit": "launches", "min_ms": WARM_MS},
+    return dict(value=C * K / el, unit="array-iters/s", ms_per_step=el / K * 1e3, steps=K,
+                warmup={"n": n_warm, "unit": "launches", "min_ms": WARM_MS},
                 chains_per_pulsar=C, n_psr=len(ptas), n_psr_local=P, m_range=[int(model.m.min()), int(model.m.max())],
                 n_gpus=world, scaling="strong" if world > 1 else "weak",
                 sharding=(f"pulsars over {world} GPUs (no collective)" if world > 1 else "one GPU"),
@@ -544,7 +546,8 @@ def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, a
     n_sys = n_psr * C
     flops = n_sys * (n_toa * m * (m + 1) + 2 * n_toa * m)      # SYRK + TNr per system
     tflops = flops / (refresh_ms * 1e-3) / 1e12
-    return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K, warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
+    return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+                warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
                 chains_per_gpu=C, n_psr=n_psr, n_toa=n_toa, m=m, aclength=aclength,
                 roofline={"bound": "mfma", "kernel": "k_white_syrk + k_prefix (gs_white_tnt + gs_prefix_sys)",
                           "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -687,7 +690,8 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
     alg_bytes = C * 8 * (ne * em.ldbx + 256 * nb * (nb + 1) // 2 + ne + NF + 5)
     traffic = _ecorr_traffic(C, "pmc_traffic_ecorr_white.json")
     value = C * world * K / el
-    return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K, warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
+    return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+                warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
                 ess_per_s=value * ess_frac,
                 ess={"per_chain_sweep_min_bin": ess_frac, "burn_in": 300, "sweeps": 1000, "chains": ess_c,
                      "note": "the bench's chains continued untimed: 300 more sweeps dropped, 1000 recorded"},
@@ -767,7 +771,8 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
     flops = C * (ne * (mR + 1) * (mR + 2) + nM * (NF + 1) * (NF + 2) + (NF + 1) ** 3 // 3)
     tflops = flops / (k_ms * 1e-3) / 1e12
     value = C * world * K / el
-    return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K, warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
+    return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
+                warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
                 ess_per_s=value * ess_frac,
                 ess={"per_chain_sweep_min_bin": ess_frac, "burn_in": 300, "sweeps": 1000, "chains": ess_c,
                      "note": "the bench's chains continued untimed: 300 more sweeps dropped, 1000 recorded"},
@@ -780,8 +785,9 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
                           "traffic": _ecorr_traffic(C),
                           "note": "ne (mR+1)(mR+2) + nM (NF+1)(NF+2) + (NF+1)^3/3 flop per chain (epoch-weighted "
                                   "SYRK with the d_E row + fixed-prior Schur update + F-block Cholesky) over the "
-                                  "HIP-event time of one all-chain likelihood launch; traffic: PMC of the round-3 kernel "
-                                  "(profiles/pmc_traffic_ecorr.json; same operands, L2-resident); the full evaluation "
+                                  "HIP-event time of one all-chain likelihood launch; traffic: PMC of the round-3 "
+                                  "kernel (profiles/pmc_traffic_ecorr.json; same operands, L2-resident); the full "
+                                  "evaluation "
                                   "(once per Metropolis block); the per-step kernel: step_roofline"},
                 step_roofline=step,
                 config="SURVEY 8f-4: J1713-like pulsar, basis ECORR (2 backends, 136 epochs) + 30-bin free "
