@@ -29,6 +29,23 @@ from ._lib import check, ptr
 from .engine import TUNED_NF, _t
 
 
+def group_epochs(ecid, epoch_backend, n_backend):
+    """The ECORR epochs grouped by backend, stable within a backend: (ecid, epoch_backend, eoff) with
+    eoff [n_backend + 1] the first epoch of each backend (eoff[-1] = number of epochs).  Each backend's
+    epochs are then one contiguous row range of [B | d_E], which the incremental Metropolis step
+    (gs_ecorr_lnl_state) re-weights alone; the epoch order is otherwise arbitrary (every result is a
+    sum over epochs or is written back by epoch column)."""
+    ecid = np.asarray(ecid, np.int64)
+    ebk = np.asarray(epoch_backend, np.int64)
+    if ecid.shape != ebk.shape:
+        raise ValueError("ecid and epoch_backend differ in length")
+    if ebk.size and (ebk.min() < 0 or ebk.max() >= n_backend):
+        raise ValueError(f"epoch_backend must be in 0..{n_backend - 1}")
+    order = np.argsort(ebk, kind="stable")
+    ebk = ebk[order]
+    return ecid[order], ebk, np.searchsorted(ebk, np.arange(n_backend + 1)).astype(np.int32)
+
+
 class EcorrModel:
     """One pulsar with a basis-ECORR signal, n_chain chains, fixed white noise.
 
@@ -48,10 +65,7 @@ class EcorrModel:
         T = np.ascontiguousarray(T, float)
         n_toa, m = T.shape
         ecid = np.asarray(ecid, np.int64)
-        # epochs grouped by backend (stable order): each backend's epochs are one contiguous row range
-        # of [B | d_E], which the incremental Metropolis step (gs_ecorr_lnl_state) re-weights alone
-        order = np.argsort(np.asarray(epoch_backend, np.int64), kind="stable")
-        ecid, epoch_backend = ecid[order], np.asarray(epoch_backend, np.int64)[order]
+        ecid, epoch_backend, eoff = group_epochs(ecid, epoch_backend, len(ecol))
         gwid = np.asarray(gwid, np.int64)
         NF = gwid.size
         if NF not in TUNED_NF:
@@ -91,7 +105,7 @@ class EcorrModel:
         self.dR = d[r_t].contiguous()
         self.TNT_full, self.d_full = TNT, d
         self.ebk = _t(np.asarray(epoch_backend, np.int32), torch.int32, dev)
-        self.eoff_host = np.searchsorted(epoch_backend, np.arange(len(ecol) + 1)).astype(np.int32)
+        self.eoff_host = eoff
         self.eoff = _t(self.eoff_host, torch.int32, dev)
         self.ecol = _t(np.asarray(ecol, np.int32), torch.int32, dev)
         self.ecol_host = np.asarray(ecol, np.int64)
