@@ -318,8 +318,9 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
     kernels = {"k_bdraw": dict(kernel_avg_ms=ms_b, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
                                achieved=bflop / (ms_b * 1e-3) / 1e12, alg_per_launch=bflop,
                                traffic=_ecorr_traffic(m.P * C, {"curn": "pmc_traffic_curn.json",
-                                                                "curn_red": "pmc_traffic_red_bdraw.json"}[kind])
-                               if kind in ("curn", "curn_red") else None,
+                                                                "curn_red": "pmc_traffic_red_bdraw.json",
+                                                                "curn_plred": "pmc_traffic_plred_bdraw.json"}[kind])
+                               if kind in ("curn", "curn_red", "curn_plred") else None,
                                name="k_bdraw_tiled" if m.model_tiled is not None else "k_bdraw",
                                note="b|rho of every (pulsar, chain) system: sum_p m^3/3 + m^2/2 + m/6 + 3 m^2 "
                                     "flop per chain (SURVEY 8d)")}
