@@ -500,9 +500,12 @@ def bench_indep(C, K, W, S, rank, world, dev):
                           "bound": "mfma", "unit": "TFLOP/s", "achieved": ach,
                           "peak": FP64_PEAK_TFLOPS, "frac": ach / FP64_PEAK_TFLOPS,
                           "kernel_avg_ms": per_sweep * S * 1e3, "sweeps_per_launch": S,
-                          "alg_flops_per_launch": flops_sweep * S, "traffic": None,
+                          "alg_flops_per_launch": flops_sweep * S,
+                          "traffic": _ecorr_traffic(P * C, "pmc_traffic_indep.json") if S == 100 else None,
+                          "alg_bytes_per_launch": P * C * S * 8 * (30 + model.ldb),
                           "note": "sum over the rank's pulsars of m^3/3 + m^2/2 + m/6 + 3 m^2 flop per chain-sweep "
-                                  "(SURVEY 8d) x C x S over the HIP-event launch time"})
+                                  "(SURVEY 8d) x C x S over the HIP-event launch time; traffic: PMC of the largest "
+                                  "launch (profiles/pmc_traffic_indep.json), alg_bytes: the x and b rows recorded"})
 
 
 def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, aclength=20, reps=5):
