@@ -62,29 +62,37 @@ def pmc_traffic(S, C):
     return d["bytes_per_launch"]
 
 
-def ess_fraction(x_rec, max_chains=256, burn_frac=0.2):
-    """Min over the bins of the ESS per chain-sweep of log10 rho (mean over up to ``max_chains``
-    chains of 1 / IAT on the post-burn-in rows, the first ``burn_frac`` dropped)."""
-    from pulsar_timing_gibbsspec_amd.diagnostics import iat
-    xr = x_rec[:, :max_chains]                      # (K, C, n_f)
-    K, C, nf = xr.shape
-    burn = int(K * burn_frac)
-    return float(min(np.mean([1.0 / max(iat(xr[burn:, c, k]), 1.0) for c in range(C)]) for k in range(nf)))
+def gpu_ess(block, kind):
+    """The GPU leg of the ESS comparison.  ``block(n_max, rec)`` advances the engine by n <= n_max
+    sweeps and returns (n, rows): rows = the (n, chains, k) device tensor of the recorded log10 rho
+    columns when ``rec``, else None.  The run lengths (burn-in, recorded sweeps) are the CPU leg's
+    (diagnostics.ESS_RUN) and so is the estimator (diagnostics.ess_summary: pooled ACF over the
+    chains, Sokal window, standard error from Sokal's variance): the two legs' ESS per sweep compare
+    like for like."""
+    from pulsar_timing_gibbsspec_amd.diagnostics import ESS_RUN, ess_summary
+    burn, sweeps = ESS_RUN[kind]
+    done = 0
+    while done < burn:
+        done += block(burn - done, False)[0]
+    parts, done = [], 0
+    while done < sweeps:
+        n, rows = block(sweeps - done, True)
+        parts.append(rows.to("cpu", copy=True))
+        done += n
+    X = torch.cat(parts).permute(1, 0, 2).contiguous().numpy()      # (chains, sweeps, k)
+    return ess_summary(X, burn)
 
 
-def ess_min_bin(x_rec, elapsed, n_chains_total, max_chains=256):
-    """Min over the bins of the whole-job ESS/s of log10 rho.
+def sweep_block(eng, cols, chains=None):
+    """gpu_ess's block for an engine with .sweep() and .x (chains, n_param): one sweep per call,
+    the x columns ``cols`` of the first ``chains`` chains recorded."""
+    idx = torch.as_tensor(np.asarray(cols), dtype=torch.long, device=eng.x.device)
+    ce = chains or eng.x.shape[0]
 
-    IAT per chain on the post-burn-in rows (first 20 % dropped) of up to
-    ``max_chains`` chains; ESS/s = mean ESS per chain x all chains / the time
-    the post-burn-in sweeps took."""
-    from pulsar_timing_gibbsspec_amd.diagnostics import iat
-    xr = x_rec[:, :max_chains]                      # (K, C, n_f)
-    K, C, nf = xr.shape
-    burn = K // 5
-    n = K - burn
-    ess = np.array([np.mean([n / max(iat(xr[burn:, c, k]), 1.0) for c in range(C)]) for k in range(nf)])
-    return float(ess.min() * n_chains_total / (elapsed * n / K))
+    def block(n_max, rec):
+        eng.sweep()
+        return 1, (eng.x[:ce].index_select(1, idx).unsqueeze(0) if rec else None)
+    return block
 
 
 def timed_region(world, dev, fn):
@@ -198,20 +206,6 @@ def cpu_line(kind, seconds):
         return {"value": None, "unit": "iters/s", "kind": "port", "error": str(exc)[-500:]}
 
 
-def pta_ess(eng_factory, rind, ce, burn, sweeps, dev):
-    """ESS per chain-sweep (worst bin of the common log10 rho) of a PTA engine: an untimed run of
-    ``ce`` chains from the bench's start, ``burn`` sweeps dropped, then ``sweeps`` recorded."""
-    eng = eng_factory(ce)
-    ri = torch.as_tensor(np.asarray(rind), dtype=torch.long, device=dev)
-    xe = torch.empty(sweeps, ce, len(rind), dtype=torch.float64, device=dev)
-    for _ in range(burn):
-        eng.sweep()
-    for i in range(sweeps):
-        eng.sweep()
-        xe[i] = eng.x.index_select(1, ri)
-    return ess_fraction(xe.cpu().numpy(), burn_frac=0.0)
-
-
 HYPER_ACL = 20     # aclength_hyper of the curn_plred line (as configs[4] fixes aclength_white = 20)
 
 
@@ -224,7 +218,7 @@ def cpu_calibration():
         return None
 
 
-def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500, ess_sweeps=2000):
+def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess=True):
     """configs[3]: PTAChains over the 45 simulated pulsars.  shard='chain': C chains per
     GPU, no collective (weak).  shard='pulsar' (N > 1): every rank runs the same C chains
     over its pulsar block (balanced by m^3) and exchanges per sweep over RCCL -- the
@@ -301,14 +295,11 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess_burn=500,
                sharding=("pulsars over %d GPUs (RCCL %s per sweep)" %
                          (world, "all-reduce of the tau sums" if curn_mode == "sum" else "all-gather of [tau | x_red]"))
                if sharded else "chains (no collective)")
-    if not sharded and ess_sweeps > 0:
-        # ESS from a separate untimed run as for the headline: burn-in, then >= 2000 recorded sweeps
-        ce = min(C, 256)
-        frac = pta_ess(make, rind, ce, ess_burn, ess_sweeps, dev)
-        out["ess_per_s"] = value * frac
-        out["ess"] = {"per_chain_sweep_min_bin": frac, "burn_in": ess_burn, "sweeps": ess_sweeps, "chains": ce,
-                      "note": "ess_per_s = value x the worst common-rho bin's mean ESS per chain-sweep (1/IAT) of a "
-                              "separate untimed run from the same start, burn-in dropped"}
+    if not sharded and ess:
+        # ESS per sweep of the common log10 rho from a separate untimed run of 256 chains from the
+        # bench's start (gpu_ess: the CPU leg's run lengths and estimator)
+        out["ess"] = gpu_ess(sweep_block(make(min(C, 256)), rind), kind)
+        out["ess_per_s"] = value * out["ess"]["per_chain_sweep_min_bin"]
     # roofline of the dominant kernels, each HIP-event timed alone on the context stream
     lib, h, m = ctx.lib, ctx.handle, eng.model
     st = ctx.stream
@@ -457,11 +448,7 @@ def bench_indep(C, K, W, S, rank, world, dev):
     run = FreeSpectrumChains(model, 1e-18, 1e-8, C, x0)
     x_rec = torch.empty(S, P * C, 30, dtype=torch.float64, device=dev)
     b_rec = torch.empty(S, P * C, model.ldb, dtype=torch.float64, device=dev)
-    xs = []
     n_warm = warm(lambda: run.run(S, x_rec=x_rec[:S], b_rec=b_rec[:S]), 1) if W else 0  # full launches
-    # the timed loop's strided ESS-sample copy once untimed: its first use loads torch's copy
-    # kernel (tens of ms on a fresh box, which showed up as 1.5e6 instead of 3.0e6 array-it/s)
-    x_rec[:1].view(1, P, C, 30)[:, :, :min(C, 4)].clone()
     torch.cuda.synchronize()
     launches = []
 
@@ -474,7 +461,6 @@ def bench_indep(C, K, W, S, rank, world, dev):
             run.run(n, x_rec=x_rec[:n], b_rec=b_rec[:n])
             e1.record(ctx.stream)
             launches.append((e0, e1, n))
-            xs.append(x_rec[:n].view(n, P, C, 30)[:, :, :min(C, 4)].clone())
             done += n
     el = timed_region(world, dev, go)
     if run.info.cpu().numpy().any():
@@ -485,17 +471,24 @@ def bench_indep(C, K, W, S, rank, world, dev):
     mm = model.m.astype(float)
     flops_sweep = C * float(np.sum(mm ** 3 / 3 + mm ** 2 / 2 + mm / 6 + 3 * mm ** 2))
     ach = flops_sweep / per_sweep / 1e12
-    xh = torch.cat(xs).cpu().numpy()                 # (K, P, <= 4 chains per pulsar, 30)
-    ess = None
-    if K >= 50:                                      # min over (pulsar, bin) of the whole-job ESS/s
-        ess = min(ess_min_bin(xh[:, p], el, C) for p in range(P))
+    # ESS per sweep, min over (pulsar, bin): a separate untimed run of CE chains per pulsar (gpu_ess)
+    CE = min(C, 64)
+    ess_run = FreeSpectrumChains(model, 1e-18, 1e-8, CE, np.random.default_rng(1).uniform(-9, -4, (P * CE, 30)))
+    xe = torch.empty(S, P * CE, 30, dtype=torch.float64, device=dev)
+
+    def block(n_max, rec):
+        n = min(S, n_max)
+        ess_run.run(n, record_b=False, x_rec=xe[:n])
+        return n, (xe[:n].view(n, P, CE, 30).permute(0, 2, 1, 3).reshape(n, CE, P * 30) if rec else None)
+    ess = gpu_ess(block, "indep")
+    del ess_run, xe
     return dict(value=C * K / el, unit="array-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 warmup={"n": n_warm, "unit": "launches", "min_ms": WARM_MS},
                 chains_per_pulsar=C, n_psr=len(ptas), n_psr_local=P, m_range=[int(model.m.min()), int(model.m.max())],
                 n_gpus=world, scaling="strong" if world > 1 else "weak",
                 sharding=(f"pulsars over {world} GPUs (no collective)" if world > 1 else "one GPU"),
                 pulsar_iters_per_s=C * K * len(ptas) / el,
-                ess_per_s=ess,
+                ess_per_s=C * K / el * ess["per_chain_sweep_min_bin"], ess=ess,
                 roofline={"kernel": "k_sweep_freespec" + ("" if model.NMX <= 16 else "_rm"),
                           "bound": "mfma", "unit": "TFLOP/s", "achieved": ach,
                           "peak": FP64_PEAK_TFLOPS, "frac": ach / FP64_PEAK_TFLOPS,
@@ -547,11 +540,21 @@ def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, a
     e1.record(stream)
     torch.cuda.synchronize()
     refresh_ms = e0.elapsed_time(e1) / reps
+    # ESS per sweep of log10 rho: an untimed run of 64 chains on the CPU leg's pulsar
+    # (config5_array(n_psr=1, seed=1), oracle/cpu_baseline.py config5), same start x0
+    d1 = synthetic.config5_array(n_psr=1, n_toa=n_toa, n_f=n_f, seed=1)
+    wm1 = WhiteNoiseModel(ctx, d1["T"], d1["r"], d1["sigma"], d1["backend"], [d1["fidx"]], [d1["phiinv_fixed"]],
+                          [d1["white"]], 64)
+    e1n = WhiteArrayChains(wm1, d1["n_param"], d1["gw_cols"], d1["rhomin"], d1["rhomax"],
+                           np.repeat(d1["x0"], 64, axis=0), aclength=aclength, chain_base=rank * 64)
+    ess = gpu_ess(sweep_block(e1n, d1["gw_cols"]), "config5")
+    del e1n, wm1, d1
     n_sys = n_psr * C
     flops = n_sys * (n_toa * m * (m + 1) + 2 * n_toa * m)      # SYRK + TNr per system
     tflops = flops / (refresh_ms * 1e-3) / 1e12
     return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
+                ess_per_s=C * world * K / el * ess["per_chain_sweep_min_bin"], ess=ess,
                 chains_per_gpu=C, n_psr=n_psr, n_toa=n_toa, m=m, aclength=aclength,
                 roofline={"bound": "mfma", "kernel": "k_white_syrk + k_prefix (gs_white_tnt + gs_prefix_sys)",
                           "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -571,21 +574,6 @@ def _ecorr_traffic(C, fname="pmc_traffic_ecorr.json"):
     except (OSError, ValueError):
         return None
     return d.get("bytes_per_launch") if d.get("chains") == C else None
-
-
-def chain_ess(eng, cols, burn=300, sweeps=1000, max_chains=256):
-    """ESS per chain-sweep of the worst log10_rho bin from the engine's own chains continued past
-    the timed region (untimed): ``burn`` more sweeps dropped, then ``sweeps`` recorded (x columns
-    ``cols`` of the first max_chains chains)."""
-    for _ in range(burn):
-        eng.sweep()
-    idx = torch.as_tensor(cols, dtype=torch.long, device=eng.x.device)
-    ce = min(max_chains, eng.x.shape[0])
-    xe = torch.empty(sweeps, ce, len(cols), dtype=torch.float64, device=eng.x.device)
-    for i in range(sweeps):
-        eng.sweep()
-        xe[i] = eng.x[:ce].index_select(1, idx)
-    return ess_fraction(xe.cpu().numpy(), burn_frac=0.0), ce
 
 
 def ecorr_step_roofline(ctx, em, x, phiinv_F, reps=10):
@@ -671,7 +659,7 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
         el = float(t.item())
     if int(em.binfo.abs().sum()) or int(em.pinfo.abs().sum()):
         raise RuntimeError("non-PD system in the white + ECORR bench")
-    ess_frac, ess_c = chain_ess(eng, gw)
+    ess = gpu_ess(sweep_block(eng, gw, 256), "ecorr_white")     # the bench's chains continued, untimed
     # dominant kernel: gs_ecorr_prefix in likelihood mode on per-chain operands, timed alone
     stream = ctx.stream
     eng._phiinv(False)
@@ -696,9 +684,7 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
     value = C * world * K / el
     return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
-                ess_per_s=value * ess_frac,
-                ess={"per_chain_sweep_min_bin": ess_frac, "burn_in": 300, "sweeps": 1000, "chains": ess_c,
-                     "note": "the bench's chains continued untimed: 300 more sweeps dropped, 1000 recorded"},
+                ess_per_s=value * ess["per_chain_sweep_min_bin"], ess=ess,
                 chains_per_gpu=C, m=m, n_epoch=ne, aclength_white=aclength, aclength_ecorr=aclength,
                 roofline={"bound": "mfma", "kernel": "k_ecorr_prefix<likelihood mode, per-chain operands>",
                           "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -755,7 +741,7 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
         el = float(t.item())
     if int(em.binfo.abs().sum()) or int(em.pinfo.abs().sum()):
         raise RuntimeError("non-PD system in the ECORR bench")
-    ess_frac, ess_c = chain_ess(eng, gw)
+    ess = gpu_ess(sweep_block(eng, gw, 256), "ecorr")           # the bench's chains continued, untimed
     # dominant kernel: gs_ecorr_prefix in likelihood mode (one launch per Metropolis step:
     # epoch Schur complement + fixed-prior prefix + F-block factorisation), timed alone
     stream = ctx.stream
@@ -777,9 +763,7 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
     value = C * world * K / el
     return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
-                ess_per_s=value * ess_frac,
-                ess={"per_chain_sweep_min_bin": ess_frac, "burn_in": 300, "sweeps": 1000, "chains": ess_c,
-                     "note": "the bench's chains continued untimed: 300 more sweeps dropped, 1000 recorded"},
+                ess_per_s=value * ess["per_chain_sweep_min_bin"], ess=ess,
                 chains_per_gpu=C, m=m, n_epoch=ne, m_R=mR, aclength=aclength,
                 roofline={"bound": "mfma", "kernel": ("k_ecorr_prefix<likelihood mode>" if em.fused and em.fused_lnl
                                                       else "k_ecorr_schur + k_prefix + k_lnlike_marg"),
@@ -796,6 +780,94 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
                 step_roofline=step,
                 config="SURVEY 8f-4: J1713-like pulsar, basis ECORR (2 backends, 136 epochs) + 30-bin free "
                        "spectrum + 16-col TM, ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
+
+
+LINE_MAX = 8192            # the driver parses stdout's last line; round 5's 22.9 KB line did not parse
+
+
+def _sig(v, n=5):
+    """A float rounded to n significant digits (ints, None and strings unchanged)."""
+    if isinstance(v, float) and v == v and v not in (float("inf"), float("-inf")) and v != 0.0:
+        return float(f"{v:.{n}g}")
+    return v
+
+
+def _pick(d, keys, n=5):
+    return {k: _sig(d[k], n) for k in keys if isinstance(d, dict) and d.get(k) is not None}
+
+
+def _cpu_brief(c, full=False):
+    if not c:
+        return None
+    b = _pick(c, ("value", "unit", "cores", "kind", "per_process", "ess_per_s", "error"))
+    if full and c.get("sample"):
+        b["sample"] = c["sample"]
+    if (c.get("reference_equivalent") or {}).get("value"):
+        b["reference_equivalent"] = _sig(c["reference_equivalent"]["value"])
+    e = c.get("ess") or {}
+    if e.get("ess_per_sweep") is not None:
+        b["ess_per_sweep"] = _pick(e, ("ess_per_sweep", "se", "chains", "sweeps", "burn_in"))
+    return b
+
+
+def _ess_brief(e):
+    return _pick(e or {}, ("per_chain_sweep_min_bin", "se", "bin", "chains", "sweeps", "burn_in", "z_vs_cpu"))
+
+
+def result_line(out):
+    """The ONE stdout JSON line: the contract's keys, the headline's roofline / cpu_baseline / ESS,
+    and per secondary line only {value, ms_per_step, ess, roofline frac + kernel time, traffic
+    ratio, cpu value}.  Notes, per-kernel tables and calibration text go to the detail file
+    (bench_detail.json).  Kept under LINE_MAX bytes (tests/test_bench_line.py)."""
+    keys = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "ess_per_s")
+    line = {k: out.get(k) for k in keys}
+    line["ess"] = _ess_brief(out.get("ess"))
+    rf = out.get("roofline") or {}
+    line["roofline"] = _pick(rf, ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_avg_ms",
+                                  "alg_flops_per_launch", "executed_frac"), 6)
+    si = rf.get("simd_issue") or {}
+    if si:
+        line["roofline"]["simd_issue"] = _pick(si, ("frac", "valu_per_draw", "mfma_per_draw", "source"))
+    line["cpu_baseline"] = _cpu_brief(out.get("cpu_baseline"), full=True)
+    hs = out.get("with_host_stream")
+    if hs:
+        line["with_host_stream"] = dict(_pick(hs, ("value", "ms_per_step")),
+                                        all_b=_pick(hs.get("all_b") or {}, ("value", "ms_per_step")))
+    sec = {}
+    for name, d in (out.get("secondary") or {}).items():
+        s = _pick(d, ("value", "unit", "ms_per_step", "ess_per_s", "n_gpus", "scaling"))
+        if d.get("ess"):
+            s["ess"] = _ess_brief(d["ess"])
+        r = d.get("roofline") or {}
+        s["roofline"] = _pick(r, ("kernel", "frac", "kernel_avg_ms", "traffic_over_alg"))
+        if r.get("traffic") and r.get("alg_bytes_per_launch") and "traffic_over_alg" not in s["roofline"]:
+            s["roofline"]["traffic_over_alg"] = _sig(r["traffic"] / r["alg_bytes_per_launch"])
+        if d.get("step_roofline"):
+            s["step_roofline"] = _pick(d["step_roofline"], ("frac", "kernel_avg_ms", "traffic_over_state"))
+        if d.get("cpu_baseline"):
+            s["cpu_baseline"] = _cpu_brief(d["cpu_baseline"])
+        sec[name] = s
+    line["secondary"] = sec
+    if out.get("detail"):
+        line["detail"] = out["detail"]
+    txt = json.dumps(line, separators=(",", ":"))
+    if len(txt) > LINE_MAX:                     # last resort: the headline alone still parses
+        line["secondary"] = {k: _pick(v, ("value", "ms_per_step", "ess_per_s")) for k, v in sec.items()}
+        txt = json.dumps(line, separators=(",", ":"))
+    return txt
+
+
+def write_detail(out, path=None):
+    """The full record (every note, kernel table, calibration and ESS per bin) beside the line."""
+    path = path or os.environ.get("GS_BENCH_DETAIL") or os.path.join(ROOT, "gpurun_out", "bench_detail.json")
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1, default=str)
+        return os.path.relpath(path, ROOT)
+    except OSError:
+        return None
 
 
 def launch_ranks(args_list, n):
@@ -844,13 +916,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20, help="headline steps = fused 100-sweep launches")
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--ess-sweeps", type=int, default=2000, help="untimed sweeps of the ESS estimate")
+    ap.add_argument("--ess", type=int, default=1, help="measure ESS per sweep on the GPU (untimed runs, "
+                    "diagnostics.ESS_RUN lengths) and, with the CPU baseline, on the CPU port too (1/0)")
     ap.add_argument("--chains", type=int, default=4096, help="chains per GPU")
     ap.add_argument("--sweeps-per-launch", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="seconds per CPU-baseline process")
-    ap.add_argument("--cpu-ess", type=int, default=1, help="measure the CPU port's ESS per sweep (single-process "
-                    "runs of 500 + 10000 (J1713) / 2000 (PTA) sweeps beside the GPU work)")
+    ap.add_argument("--cpu-ess-procs", type=int, default=12, help="CPU ESS chains run at once beside the GPU "
+                    "work (4 independent single-thread chains per line, oracle.cpu_baseline.EssPool)")
     ap.add_argument("--bcast", type=int, default=None, help="GS_OPT_BCAST (0 readlane, 1 LDS, 2 batched, 3 tile)")
     ap.add_argument("--host-stream", type=int, default=1,
                     help="also time the headline with every recorded row streamed to pinned host memory (1/0)")
@@ -864,8 +937,6 @@ def main():
                     help="chains per GPU for the PTA lines (measured: 256 -> 1024 -> 2048 -> 4096 chains give "
                          "CURN + red 3.0e5 -> 3.8e5 -> 3.9e5 -> 4.0e5 chain-it/s: saturated at 2048)")
     ap.add_argument("--pta-steps", type=int, default=200)
-    ap.add_argument("--pta-ess-sweeps", type=int, default=2000,
-                    help="untimed sweeps of each PTA line's ESS run after a 500-sweep burn-in (0: no ESS)")
     ap.add_argument("--config5", type=int, default=1, help="measure BASELINE configs[4] too (1/0)")
     ap.add_argument("--ecorr", type=int, default=1, help="measure the basis-ECORR path (SURVEY 8f-4) too (1/0)")
     ap.add_argument("--ecorr-chains", type=int, default=4096)
@@ -908,14 +979,16 @@ def main():
     # the CPU port's ESS per sweep: one single-process run per chain-mixing config, started now so
     # it runs beside the GPU work (numpy only, one thread each); the throughput processes of
     # cpu_baseline run at the very end, after these have finished, so nothing competes with them
-    ess_procs = {}
-    if cpu and args.cpu_ess:
-        from oracle.cpu_baseline import ess_start
-        ess_procs = {"single": ess_start("single", 500, 10000)}
-        for kind in [k for k in args.pta.split(",") if k in ("curn", "curn_red", "curn_plred")]:
-            # >= 2000 recorded sweeps everywhere: a 400-sweep run is ~5 IATs of the MH line and its
-            # Sokal-window IAT comes out short, i.e. the ESS per sweep long
-            ess_procs[kind] = ess_start(kind, 500 if kind != "curn_plred" else 200, 2000)
+    pool = None
+    if cpu and args.ess:
+        from oracle.cpu_baseline import EssPool
+        pool = EssPool(args.cpu_ess_procs, os.path.join(ROOT, "gpurun_out", "ess_rows"))
+        # slowest first, so the longest chains start while the GPU lines run
+        lines = [k for k in ("curn_red", "curn_plred", "curn") if k in args.pta.split(",")]
+        lines += (["config5"] if args.config5 else []) + (["indep"] if args.indep else [])
+        lines += (["ecorr_white", "ecorr"] if args.ecorr else []) + ["single"]
+        for kind in lines:
+            pool.submit(kind)
 
     phase("headline configs[1]")
     from pulsar_timing_gibbsspec_amd import _lib, synthetic
@@ -962,15 +1035,18 @@ def main():
     alg_flops_launch = flops_per_chain_sweep(m) * C * S
     achieved = alg_flops_launch / launch_s / 1e12
     exe = executed_flops_per_chain_sweep(model.NF, int(model.nm[0])) * C * S / launch_s / 1e12
-    # ESS per chain-sweep from a separate untimed run of 256 chains (same kernel, same law)
+    # ESS per chain-sweep from a separate untimed run of 256 chains (same kernel, same law; gpu_ess:
+    # the CPU leg's run lengths and estimator)
     ce = min(C, 256)
     ess_run = FreeSpectrumChains(model, 1e-18, 1e-8, ce, x0[:ce], chain_base=rank * C)
-    xe = torch.empty(args.ess_sweeps, ce, 30, dtype=torch.float64, device=dev)
-    for i in range(0, args.ess_sweeps, S):
-        n = min(S, args.ess_sweeps - i)
-        ess_run.run(n, record_b=False, x_rec=xe[i:i + n])
-    ess_frac = ess_fraction(xe.cpu().numpy())
-    ess = value * ess_frac
+    xe = torch.empty(S, ce, 30, dtype=torch.float64, device=dev)
+
+    def ess_block(n_max, rec):
+        n = min(S, n_max)
+        ess_run.run(n, record_b=False, x_rec=xe[:n])
+        return n, (xe[:n] if rec else None)
+    ess_rec = gpu_ess(ess_block, "single") if args.ess else None
+    ess = value * ess_rec["per_chain_sweep_min_bin"] if ess_rec else None
     del xe, ess_run
     K_sweeps = K * S
 
@@ -1021,9 +1097,7 @@ def main():
                        "bcast": ctx.get_option(_lib.OPT_BCAST),
                        "parallelism": f"chains sharded over {world} GPU(s), no collective"},
             "ess_per_s": ess,
-            "ess": {"per_chain_sweep_min_bin": ess_frac, "sweeps": args.ess_sweeps, "chains": ce,
-                    "note": "ess_per_s = value x the worst bin's mean ESS per chain-sweep (1/IAT, first 20 % "
-                            "dropped) from a separate untimed run"},
+            "ess": ess_rec,
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
                          "traffic": pmc_traffic(S, C),
@@ -1053,7 +1127,7 @@ def main():
     for kind in [k for k in args.pta.split(",") if k and k != "none"]:
         phase(f"configs[3] {kind}")
         d = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, shard="chain",
-                      ess_sweeps=args.pta_ess_sweeps)
+                      ess=bool(args.ess))
         d["config"] = (f"configs[3]: 45-pulsar CURN{' + per-pulsar red' if kind == 'curn_red' else ''} free "
                        f"spectrum, common draw {'from the tau sums' if kind == 'curn' else 'exact product'}")
         if kind == "curn_plred":
@@ -1061,7 +1135,7 @@ def main():
                            f"per-pulsar power-law red noise by {HYPER_ACL} Metropolis steps per sweep")
         add(kind, d, kind)
         if world > 1:
-            d = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, shard="pulsar")
+            d = bench_pta(kind, args.pta_chains, args.pta_steps, 2, rank, world, dev, ctx, shard="pulsar", ess=False)
             d["config"] = f"configs[3] {kind}, pulsars sharded over the ranks with the per-sweep RCCL exchange"
             add(kind + "_pulsar_sharded", d)
     if args.ecorr:
@@ -1080,17 +1154,25 @@ def main():
         add("config5", d, "config5")
     if rank == 0 and cpu:
         phase("cpu baseline (ESS runs, then one single-thread process per core per line)")
-        from oracle.cpu_baseline import ess_collect
-        ess_cpu = {k: ess_collect(p) for k, p in ess_procs.items()}
+        from pulsar_timing_gibbsspec_amd.diagnostics import ess_compare
+        ess_cpu = {}
+        if pool is not None:
+            for kind in ["single"] + list(cpu_kinds.values()):
+                ess_cpu[kind] = pool.collect(kind)
         calib = cpu_calibration()
 
-        def baseline(kind):
+        def baseline(kind, gpu_ess_rec):
             b = cpu_line(kind, args.cpu_seconds)
             e = ess_cpu.get(kind)
             if e is not None:
                 b["ess"] = e
                 if b.get("value") and "ess_per_sweep" in e:
                     b["ess_per_s"] = b["value"] * e["ess_per_sweep"]
+                if gpu_ess_rec and "per_bin" in e:
+                    cmp_ = ess_compare(gpu_ess_rec, e)
+                    if cmp_:
+                        gpu_ess_rec["vs_cpu"] = cmp_
+                        gpu_ess_rec["z_vs_cpu"] = cmp_["z"]
             c = (calib or {}).get("ratios", {}).get(kind)
             if c and b.get("value"):
                 b["reference_equivalent"] = {
@@ -1098,12 +1180,13 @@ def main():
                     "note": "the port's host rate scaled by the reference/port speed ratio measured single-threaded "
                             "in the build container (profiles/cpu_calibration.json, tools/calibrate_cpu_baseline.py)"}
             return b
-        out["cpu_baseline"] = baseline("single")
+        out["cpu_baseline"] = baseline("single", out.get("ess"))
         for name, kind in cpu_kinds.items():
-            sec[name]["cpu_baseline"] = baseline(kind)
+            sec[name]["cpu_baseline"] = baseline(kind, sec[name].get("ess"))
     if rank == 0:
         out["secondary"] = sec
-        print(json.dumps(out), flush=True)
+        out["detail"] = write_detail(out)
+        print(result_line(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -245,6 +245,7 @@ __device__ __forceinline__ void stage_model(double* lds, const double* g, int64_
       __builtin_amdgcn_global_load_lds((const void*)(g + 2 * (base + lane)), (gs_lds_vptr)(lds + 2 * base), 16, 0,
                                        0);
   }
+  gs_wait_dma();
 #else
   const double2* __restrict__ g2 = reinterpret_cast<const double2*>(g);
   double2* l2 = reinterpret_cast<double2*>(lds);

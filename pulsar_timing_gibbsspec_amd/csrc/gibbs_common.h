@@ -29,6 +29,11 @@ __host__ __device__ constexpr int gs_tile_scr(int NF) {
 // (chain, system, pointers) would sit in VGPRs: the 12-wave fused sweep spilled 37 VGPRs that way,
 // 6 with this (r04).
 __device__ __forceinline__ int gs_wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+// vmcnt(0) (gfx9 s_waitcnt layout: vmcnt[3:0] + [15:14] = 0, expcnt[6:4] and lgkmcnt[11:8] at their
+// maxima): issued by every wave before a barrier that publishes LDS-DMA (global_load_lds) data, so
+// the other waves' reads after the barrier see it whatever waits the compiler places around the
+// barrier (a workgroup-scope release need not drain vmcnt on gfx9)
+__device__ __forceinline__ void gs_wait_dma() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -192,6 +192,7 @@ __global__ __launch_bounds__(64 * EC_WAVES, GS_EC_MINW) void k_ecorr_schur(Ecorr
   const int nch = (ne + EC_CH - 1) / EC_CH;
   load(0, 0);
   store(0);
+  if constexpr (GS_EC_GLDS) gs_wait_dma();
   __syncthreads();
   for (int ch = 0; ch < nch; ++ch) {
     const int cb = ch & 1;
@@ -218,6 +219,7 @@ __global__ __launch_bounds__(64 * EC_WAVES, GS_EC_MINW) void k_ecorr_schur(Ecorr
       }
     }
     if (ch + 1 < nch) store(cb ^ 1);
+    if constexpr (GS_EC_GLDS) gs_wait_dma();  // the next chunk's DMA complete before the barrier
     __syncthreads();
   }
   sla = ec_wave_sum(sla);
@@ -530,6 +532,7 @@ __global__ __launch_bounds__(64 * EC_WAVES, INC ? GS_EC_MINW_INC : (PC ? GS_EC_M
   const int nch = (ne + EC_CH - 1) / EC_CH;
   load(0, 0);
   store(0);
+  if constexpr (GS_EC_GLDS) gs_wait_dma();
   __syncthreads();
   for (int chk = 0; chk < nch; ++chk) {
     const int cb = chk & 1;
@@ -556,6 +559,7 @@ __global__ __launch_bounds__(64 * EC_WAVES, INC ? GS_EC_MINW_INC : (PC ? GS_EC_M
       }
     }
     if (chk + 1 < nch) store(cb ^ 1);
+    if constexpr (GS_EC_GLDS) gs_wait_dma();  // the next chunk's DMA complete before the barrier
     __syncthreads();
   }
   }

@@ -468,7 +468,8 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
     load(0);
     store(buf0);
   }
-  __syncthreads();  // (waits for the DMA too: vmcnt(0) before the barrier)
+  if (gl) gs_wait_dma();
+  __syncthreads();
   // the chunk loop, instantiated once per role so each role's registers are allocated on their own
   // (role 1: the diagonal-tile wave of BAL; role 0: the paired-row waves).  Measured (r05e/r05f):
   // the diagonal wave in slots 0..NB-1 of the shared accumulator array 389-392 config5 sweeps/s,
@@ -522,7 +523,8 @@ __global__ __launch_bounds__(64 * SY_WAVES) void k_white_syrk(WhiteTntArgs A) {
       } else {
         if (ch + 1 < nch) store(nxt);
       }
-      __syncthreads();  // with the DMA in flight: vmcnt(0) first (nxt complete for the next chunk)
+      if constexpr (decltype(dma)::value == 1) gs_wait_dma();  // nxt's DMA complete before the barrier
+      __syncthreads();
     }
   };
   const bool diagw = BAL && w == SY_WAVES - 1;

@@ -25,6 +25,70 @@ def iat(x, c=5.0):
     return float(tau[-1])
 
 
+# bench.py's ESS runs: (burn-in, recorded sweeps) per chain for each line, the same on the GPU leg and
+# the CPU port's (oracle/cpu_baseline.py); recorded >= 50 x the slowest bin's IAT
+ESS_RUN = {"single": (1000, 6000), "indep": (500, 3000), "curn": (500, 5000), "curn_red": (500, 5000),
+           "curn_plred": (1000, 5000), "ecorr": (500, 3000), "ecorr_white": (500, 3000), "config5": (500, 3000)}
+
+
+def pooled_iat(x, c=5.0):
+    """(tau, M) of independent chains of one quantity, x: (chains, n).  Each chain's mean is
+    removed, the chains' autocovariances (biased, / n) are averaged lag by lag, and tau is read
+    off the pooled autocorrelation with Sokal's adaptive window (smallest M with M >= c tau(M)).
+    One estimator for every leg of the bench (GPU chains and the CPU port's processes alike)."""
+    x = np.atleast_2d(np.asarray(x, float))
+    x = x - x.mean(axis=1, keepdims=True)
+    C, n = x.shape
+    if n < 4:
+        return 1.0, 0
+    f = np.fft.rfft(x, 2 * n, axis=1)
+    acov = np.fft.irfft(f.real ** 2 + f.imag ** 2, axis=1)[:, :n].mean(axis=0)
+    if acov[0] <= 0:
+        return 1.0, 0
+    tau = 2.0 * np.cumsum(acov / acov[0]) - 1.0
+    ok = np.arange(n) >= c * tau
+    M = int(np.argmax(ok)) if ok.any() else n - 1
+    return float(max(tau[M], 1.0)), M
+
+
+def ess_table(X, c=5.0):
+    """Per column of X (chains, n, k): the ESS per chain-sweep 1/tau of the pooled chains and its
+    standard error, from Sokal's asymptotic variance var(tau) = 2 (2M + 1) tau^2 / N with N =
+    chains x n pooled samples (so se(1/tau) = (1/tau) sqrt(2 (2M + 1) / N))."""
+    X = np.asarray(X)
+    C, n, k = X.shape
+    out = np.empty(k)
+    se = np.empty(k)
+    for j in range(k):
+        tau, M = pooled_iat(X[:, :, j], c)
+        out[j] = 1.0 / tau
+        se[j] = out[j] * np.sqrt(2.0 * (2 * M + 1) / (C * n))
+    return out, se
+
+
+def ess_summary(X, burn_in, c=5.0):
+    """The bench's ESS record of X (chains, n, k) recorded after ``burn_in`` dropped sweeps: the
+    worst column's ESS per chain-sweep with its standard error, and every column's."""
+    e, se = ess_table(X, c)
+    j = int(np.argmin(e))
+    return {"per_chain_sweep_min_bin": float(e[j]), "se": float(se[j]), "bin": j, "chains": int(X.shape[0]),
+            "sweeps": int(X.shape[1]), "burn_in": int(burn_in), "per_bin": [float(v) for v in e],
+            "se_bin": [float(v) for v in se], "estimator": "pooled ACF over chains, Sokal window c=5"}
+
+
+def ess_compare(gpu, cpu):
+    """z-score of the GPU and CPU ESS per sweep at the GPU's worst column (both from ess_summary),
+    and the share of columns that agree within 2 standard errors."""
+    g, gs = np.array(gpu["per_bin"]), np.array(gpu["se_bin"])
+    h, hs = np.array(cpu["per_bin"]), np.array(cpu["se_bin"])
+    if g.shape != h.shape:
+        return None
+    z = (g - h) / np.sqrt(gs ** 2 + hs ** 2)
+    j = int(gpu["bin"])
+    return {"bin": j, "gpu": float(g[j]), "gpu_se": float(gs[j]), "cpu": float(h[j]), "cpu_se": float(hs[j]),
+            "z": float(z[j]), "frac_bins_within_2se": float(np.mean(np.abs(z) < 2.0))}
+
+
 def ess(chain, c=5.0):
     """Effective sample size of each column of a (n, k) chain."""
     chain = np.atleast_2d(np.asarray(chain, float))

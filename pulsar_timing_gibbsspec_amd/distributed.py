@@ -111,9 +111,11 @@ class TauSumAllReduce:
 def allreduce_sum(t, group=None):
     """Sum of a small tensor over the ranks of ``group`` (host-side bookkeeping, not the data path:
     the red MH warm-up records, acceptance counts).  gloo reduces on the host, so a device tensor is
-    staged through host memory there; RCCL reduces it in place."""
-    if not (dist.is_available() and dist.is_initialized()):
-        raise RuntimeError("a pulsar-sharded engine needs torch.distributed initialised for this reduction")
+    staged through host memory there; RCCL reduces it in place.  Without an initialised process group,
+    or in a 1-rank one, the local tensor is the sum (a 1-rank exchange such as ``gather=lambda s: s``
+    holds every pulsar) and is returned as it is."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return t
     if dist.get_backend(group) == "nccl" or t.device.type == "cpu":
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
         return t

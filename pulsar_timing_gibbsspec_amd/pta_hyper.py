@@ -170,7 +170,10 @@ class HyperMH:
                 raise ValueError(f"inj must be (nsteps, n_chain, 4) = {(int(nsteps), self.C, 4)}, got "
                                  f"{tuple(inj.shape)}")
             j = inj[..., 1]
-            if bool(((j < 0) | (j > sp.n_h - 1) | (j != torch.floor(j))).any()):
+            # a host check of a device tensor syncs (and raises inside graph capture): validated on
+            # CPU tensors and outside capture only -- the kernel clamps j either way
+            chk = inj.device.type == "cpu" or not torch.cuda.is_current_stream_capturing()
+            if chk and bool(((j < 0) | (j > sp.n_h - 1) | (j != torch.floor(j))).any()):
                 raise ValueError(f"inj[..., 1] (the parameter index) must be an integer in [0, {sp.n_h - 1}]")
         check(self.ctx.lib.gs_hyper_mh(self.ctx.handle, m.P, self.C, m.NF, m.NMX, ptr(m.model), ptr(m.nm_dev),
                                        ptr(x), self.n_param, ptr(self.gw_col), sp.n_h, ptr(sp.hcol), ptr(self.hpsr),

@@ -19,6 +19,7 @@ import importlib.util
 import os
 import sys
 import tempfile
+import time
 import types
 
 os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
@@ -400,8 +401,8 @@ def pta_long_plred(ref, out, niter=40000, seed=31, n_psr=6, warm=100, acl=20, th
         xnew = g.update_rho_params(xnew)
         if np.all(xnew != chain[ii][-1]):
             g._b = g.update_b(xnew)
-        if ii % 1000 == 0:
-            print("pta long plred", seed, ii, flush=True)
+        if ii % 1000 == 0 or (n_psr > 6 and ii % 100 == 0):
+            print("pta long plred", seed, ii, time.strftime("%H:%M:%S"), flush=True)
     keep = [i for i, n in enumerate(names) if ("gw" in n and "rho" in n) or "red_noise" in n]
     np.savez_compressed(out, chain=chain[::thin, keep].astype(np.float32), cols=np.array(keep),
                         names=np.array([names[i] for i in keep]), niter=niter, thin=thin, x0=x0,
@@ -665,8 +666,10 @@ def main(root):
         # one seed per process: --seed=S --niter=N -> pta_long_curn_plred_s{S}.npz
         opt = dict(a[2:].split("=", 1) for a in sys.argv if a.startswith("--") and "=" in a)
         s = int(opt.get("seed", 31))
-        pta_long_plred(PT, os.path.join(HERE, f"pta_long_curn_plred_s{s}.npz"), niter=int(opt.get("niter", 40000)),
-                       seed=s)
+        n_psr = int(opt.get("npsr", 6))
+        tag = f"pta_long_curn_plred_s{s}.npz" if n_psr == 6 else f"pta_long_curn_plred_p{n_psr}_s{s}.npz"
+        pta_long_plred(PT, os.path.join(HERE, tag), niter=int(opt.get("niter", 40000)), seed=s, n_psr=n_psr,
+                       thin=int(opt.get("thin", 10)))
         return
     if "--only-pta-mh" in sys.argv:
         pta_hyper_mh(PT, os.path.join(HERE, "pta_plred_mh.npz"), "curn_plred")

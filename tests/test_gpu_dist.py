@@ -140,14 +140,21 @@ def _capture_worker(port, kind, mode, out_dir):
         from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
         T, N, R, names, rind, red_col, gwid, fixed = _setup(kind)
         C = 8
-        x0 = np.random.default_rng(0).uniform(-9, -4, (C, len(names)))
+        x0, hyper = _x0_hyper(kind, C, "cuda")
+        _, hyper_ref = _x0_hyper(kind, C, "cuda")
+        rows = 2 if (red_col is not None or hyper is not None) else 1
         ex = dict(allreduce=TauSumAllReduce()) if mode == "sum" else \
-            dict(gather=PulsarAllGather([np.arange(len(T))], ((2 if red_col is not None else 1), 30, C), device="cuda"))
+            dict(gather=PulsarAllGather([np.arange(len(T))], (rows, 30, C), device="cuda"))
+        # curn_plred: the red MH block (redsample='mh') with the sweep-0 warm-up fixing aclength_hyper
+        # eagerly (its allreduce_sum runs before the capture), then the captured sweeps' only
+        # collective is the [tau | x_red] all-gather
+        hy = dict(hyper=hyper, hyper_warmup=40) if hyper is not None else {}
+        hy_ref = dict(hyper=hyper_ref, hyper_warmup=40) if hyper is not None else {}
         # the exchange engine (RCCL collective in every sweep) and the plain one, same seeds
         eng = PTAChains(DeviceModel(_lib.Context(0, seed=31), T, N, R, gwid, fixed), len(names), rind, red_col,
-                        (1e-18, 1e-8), (1e-20, 1e-8), C, x0, curn_mode=mode, **ex)
+                        (1e-18, 1e-8), (1e-20, 1e-8), C, x0, curn_mode=mode, **hy, **ex)
         ref = PTAChains(DeviceModel(_lib.Context(0, seed=31), T, N, R, gwid, fixed), len(names), rind, red_col,
-                        (1e-18, 1e-8), (1e-20, 1e-8), C, x0, curn_mode=mode)
+                        (1e-18, 1e-8), (1e-20, 1e-8), C, x0, curn_mode=mode, **hy_ref)
         assert eng.sharded and not ref.sharded
         eng.sweep()
         rec = eng.capture(4)                      # sweeps 1..4, the all-reduce / all-gather inside
@@ -160,15 +167,21 @@ def _capture_worker(port, kind, mode, out_dir):
         np.save(os.path.join(out_dir, "got.npy"), torch.cat(got).cpu().numpy())
         np.save(os.path.join(out_dir, "want.npy"), want[1:].cpu().numpy())
         assert rec.shape == (4, C, len(names))
+        if hyper is not None:
+            assert eng.hyper_acl == ref.hyper_acl and eng.hyper.steps_total == ref.hyper.steps_total
+            assert torch.equal(eng.hyper.acc_total, ref.hyper.acc_total)
+            assert not torch.equal(want[-1][:, hyper.hind], want[0][:, hyper.hind])    # the block moved
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,mode", [("curn", "sum"), ("curn_red", "exact")])
+@pytest.mark.parametrize("kind,mode", [("curn", "sum"), ("curn_red", "exact"), ("curn_plred", "exact")])
 def test_graph_capture_with_rccl_exchange(tmp_path, kind, mode):
     """PTAChains.capture of sweeps whose exchange is an RCCL collective (1-rank 'nccl' group on the
     one GPU): the collective is a node of the hipGraph, and two replays (8 sweeps) equal 8 eager
-    sweeps of the engine without an exchange bit for bit."""
+    sweeps of the engine without an exchange bit for bit.  curn_plred (the reference's default
+    redsample='mh', pta_gibbs.py:689-704): the sweep-0 warm-up (and its aclength all-reduce) runs
+    eagerly, the captured sweeps hold the red MH steps and the [tau | x_red] all-gather."""
     if not gpu_available():
         pytest.skip("no GPU")
     import torch.multiprocessing as mp

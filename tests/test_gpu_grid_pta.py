@@ -287,6 +287,49 @@ def test_pulsar_sharded_engine_bit_identical(kind, nsh):
         assert torch.equal(bs, bref[lo:hi, :, :w]) and not bref[lo:hi, :, w:].any()
 
 
+def test_one_rank_gather_warmup_without_process_group():
+    """A pulsar-sharded engine whose exchange is a 1-rank gather (gather=lambda s: s: one shard holding
+    every pulsar, no torch.distributed process group) runs the red block's sweep-0 warm-up with
+    aclength_hyper left to it (hyper_acl=None): distributed.allreduce_sum passes the local records
+    through, and the chains, aclength_hyper and acceptance equal the unsharded engine's."""
+    import torch.distributed as dist
+    from pulsar_timing_gibbsspec_amd import _lib, synthetic
+    from pulsar_timing_gibbsspec_amd.engine import DeviceModel, PTAChains
+    from pulsar_timing_gibbsspec_amd.pta_hyper import HyperSpec
+    assert not dist.is_initialized()
+    pta = synthetic.array_pta(kind="curn_plred", n_psr=5, seed=2)
+    T, N, R = pta.get_basis(), pta.get_ndiag({}), pta.get_residuals()
+    names = pta.param_names
+    rind = [i for i, n in enumerate(names) if "rho" in n and "gw" in n]
+    gwid = [np.arange(t.shape[1] - 60, t.shape[1]) for t in T]
+    fixed = [np.full(t.shape[1] - 60, 1e-40) for t in T]
+    hidx = np.array([i for i, n in enumerate(names) if "red" in n and ("log10_A" in n or "gamma" in n)])
+    sigs = [s for s in (pta.signals[k] for k in pta.signals) if "red" in s.name]
+    C, S = 16, 4
+    rng = np.random.default_rng(0)
+    x0 = rng.uniform(-9, -4, (C, len(names)))
+    engs, recs = [], []
+    for sharded in (False, True):
+        spec = HyperSpec(pta, pta.params, sigs, hidx, np.zeros(len(names)), 30, "cuda")
+        if not sharded:
+            x0[:, spec.hind] = rng.uniform(spec.hlo_host, spec.hhi_host, (C, spec.n_h))
+        ex = dict(P_global=len(T), psr_lo=0, gather=lambda s: s) if sharded else {}
+        eng = PTAChains(DeviceModel(_lib.Context(0, seed=91), T, N, R, gwid, fixed), len(names), rind, None,
+                        (1e-18, 1e-8), (1e-20, 1e-8), C, x0, hyper=spec, hyper_warmup=30, **ex)
+        assert eng.sharded == sharded
+        xr = torch.zeros(S, C, len(names), dtype=torch.float64, device="cuda")
+        for i in range(S):
+            if sharded:
+                eng.sweep_end(eng.sweep_begin(x_rec=xr[i]))
+            else:
+                eng.sweep(x_rec=xr[i])
+        engs.append(eng)
+        recs.append(xr)
+    assert torch.equal(recs[0], recs[1])
+    assert engs[0].hyper_acl == engs[1].hyper_acl and engs[0].hyper_acl >= 1
+    assert np.array_equal(engs[0].hyper_acceptance(), engs[1].hyper_acceptance())
+
+
 def test_curn_sum_kernel_matches_reference(ctx):
     """gs_tau_sum + gs_rho_curn_sum (the sufficient-statistic CURN draw a sharded run
     all-reduces for) pick the reference's grid index on every sweep of the fixture."""
