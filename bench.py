@@ -923,7 +923,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="seconds per CPU-baseline process")
     ap.add_argument("--cpu-ess-procs", type=int, default=12, help="CPU ESS chains run at once beside the GPU "
-                    "work (4 independent single-thread chains per line, oracle.cpu_baseline.EssPool)")
+                    "work (oracle.cpu_baseline.ESS_CHAINS independent single-thread chains per line, EssPool)")
     ap.add_argument("--bcast", type=int, default=None, help="GS_OPT_BCAST (0 readlane, 1 LDS, 2 batched, 3 tile)")
     ap.add_argument("--host-stream", type=int, default=1,
                     help="also time the headline with every recorded row streamed to pinned host memory (1/0)")

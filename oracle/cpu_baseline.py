@@ -412,7 +412,7 @@ def ess_rows(kind, burn, sweeps, path):
     return dict(burn_in=burn, sweeps=sweeps, seconds=el, what=what, path=path)
 
 
-ESS_CHAINS = 4              # independent CPU chains (processes) per line
+ESS_CHAINS = 6              # independent CPU chains (processes) per line
 
 
 class EssPool:

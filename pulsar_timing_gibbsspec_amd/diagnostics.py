@@ -27,8 +27,10 @@ def iat(x, c=5.0):
 
 # bench.py's ESS runs: (burn-in, recorded sweeps) per chain for each line, the same on the GPU leg and
 # the CPU port's (oracle/cpu_baseline.py); recorded >= 50 x the slowest bin's IAT
-ESS_RUN = {"single": (1000, 6000), "indep": (500, 3000), "curn": (500, 5000), "curn_red": (500, 5000),
-           "curn_plred": (1000, 5000), "ecorr": (500, 3000), "ecorr_white": (500, 3000), "config5": (500, 3000)}
+# (round-6 measurement, profiles/r06a: slowest-bin IAT 29 / 65 / 72 / 261 / 159 / 41 / 42 / 57 sweeps in the
+# order below)
+ESS_RUN = {"single": (1000, 6000), "indep": (500, 3500), "curn": (500, 5000), "curn_red": (500, 13000),
+           "curn_plred": (1000, 8000), "ecorr": (500, 3000), "ecorr_white": (500, 3000), "config5": (500, 3000)}
 
 
 def pooled_iat(x, c=5.0):

@@ -63,6 +63,18 @@ def resolve_seed(seed):
     return int(seed), int(np.random.SeedSequence(int(seed)).generate_state(1, np.uint64)[0])
 
 
+def save_rows(s, outdir, n, chains=False, bchains=False):
+    """Write rows [:n] of s.chain / s.bchain to chain.npy / bchain.npy (the reference's periodic
+    save, pulsar_gibbs.py:701-710) and, for multi-chain runs, the leading-chain-axis chains.npy /
+    bchains.npy beside them."""
+    np.save(f"{outdir}/chain.npy", s.chain[:n, :])
+    np.save(f"{outdir}/bchain.npy", s.bchain[:n, :])
+    if chains:
+        np.save(f"{outdir}/chains.npy", s.chains[:, :n])
+    if bchains:
+        np.save(f"{outdir}/bchains.npy", s.bchains[:, :n])
+
+
 def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_every, psr_base=0,
                          record_bchains=None):
     """The free-spectrum sample loop (PulsarBlockGibbs.sample, pulsar_gibbs.py:620-710) for
@@ -185,12 +197,7 @@ def sample_free_spectrum(samplers, model, xs_list, outdirs, niter, resume, save_
                 s.bchains[:, ii:nxt] = np.moveaxis(bp, 1, 0)
             s.iter = last
             if save:
-                np.save(f"{o}/chain.npy", s.chain[:last + 1, :])
-                np.save(f"{o}/bchain.npy", s.bchain[:last + 1, :])
-                if nc > 1:
-                    np.save(f"{o}/chains.npy", s.chains[:, :last + 1])
-                if allb:
-                    np.save(f"{o}/bchains.npy", s.bchains[:, :last + 1])
+                save_rows(s, o, last + 1, nc > 1, allb)
 
     ii, slot, pending = start, 0, None
     while ii < niter:
@@ -765,13 +772,8 @@ class PulsarBlockGibbs(object):
     def _flush(self, outdir):
         """flush_final=True: also write the rows after the last multiple of
         save_every, which the reference never saves (pulsar_gibbs.py:701-710, Appendix A.8)."""
-        n = self.iter + 1
-        np.save(f"{outdir}/chain.npy", self.chain[:n, :])
-        np.save(f"{outdir}/bchain.npy", self.bchain[:n, :])
-        if self.chains is not None:
-            np.save(f"{outdir}/chains.npy", self.chains[:, :n])
-        if getattr(self, "bchains", None) is not None:
-            np.save(f"{outdir}/bchains.npy", self.bchains[:, :n])
+        save_rows(self, outdir, self.iter + 1, self.chains is not None,
+                  getattr(self, "bchains", None) is not None)
 
     def _sample_white(self, xs, outdir, niter, resume, save_every):
         """sample() with the white-noise MH block (pulsar_gibbs.py:656-698): one device
@@ -823,11 +825,7 @@ class PulsarBlockGibbs(object):
             self.iter = ii - 1
             last = ii - 1
             if last % save_every == 0 and last > 0:
-                np.save(f"{outdir}/chain.npy", self.chain[:last + 1, :])
-                np.save(f"{outdir}/bchain.npy", self.bchain[:last + 1, :])
-                if nc > 1:
-                    np.save(f"{outdir}/chains.npy", self.chains[:, :last + 1])
-                    np.save(f"{outdir}/bchains.npy", self.bchains[:, :last + 1])
+                save_rows(self, outdir, last + 1, nc > 1, nc > 1)
         if runner.short_chain is not None:
             sc = runner.short_chain
             self.cov_white = np.cov(sc[100:, :], rowvar=False)
@@ -908,11 +906,7 @@ class PulsarBlockGibbs(object):
             self.iter = ii - 1
             last = ii - 1
             if last % save_every == 0 and last > 0:
-                np.save(f"{outdir}/chain.npy", self.chain[:last + 1, :])
-                np.save(f"{outdir}/bchain.npy", self.bchain[:last + 1, :])
-                if nc > 1:
-                    np.save(f"{outdir}/chains.npy", self.chains[:, :last + 1])
-                    np.save(f"{outdir}/bchains.npy", self.bchains[:, :last + 1])
+                save_rows(self, outdir, last + 1, nc > 1, nc > 1)
         if runner.short_chain is not None:
             sc = runner.short_chain
             self.cov_ecorr = np.cov(sc[100:, :], rowvar=False)
@@ -978,11 +972,7 @@ class PulsarBlockGibbs(object):
             self.iter = ii - 1
             last = ii - 1
             if last % save_every == 0 and last > 0:
-                np.save(f"{outdir}/chain.npy", self.chain[:last + 1, :])
-                np.save(f"{outdir}/bchain.npy", self.bchain[:last + 1, :])
-                if nc > 1:
-                    np.save(f"{outdir}/chains.npy", self.chains[:, :last + 1])
-                    np.save(f"{outdir}/bchains.npy", self.bchains[:, :last + 1])
+                save_rows(self, outdir, last + 1, nc > 1, nc > 1)
         info = runner.info.cpu().numpy()
         if info.any():
             print(f"WARNING: {int((info != 0).sum())} chains hit a non-positive-definite Sigma")
