@@ -165,16 +165,31 @@ def grid_peak():
 SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 
-def simd_issue(launch_s, draws, valu=1459, mfma=64, valu_cycles=4.5):
+def sq_counts():
+    """Per-draw SQ instruction counts of the shipped headline kernel (one --pmc pass of SQ counters,
+    tools/gpu_r06_pmc.sh -> profiles/sq_headline.json), or None."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "sq_headline.json")))
+        return d["per_draw"]["SQ_INSTS_VALU"], d["per_draw"]["SQ_INSTS_MFMA"], d
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def simd_issue(launch_s, draws, valu_cycles=4.5):
     """The headline kernel against the SIMD's issue capacity: on MI355X an f64 MFMA (64 cycles) does
     not overlap the SIMD's VALU (tools/probe/mfma_probe.hip, profiles/r04o/mfma_probe.txt), so a draw
-    costs at least its VALU issue cycles + 64 per f64 MFMA.  Per-draw instruction counts from the SQ
-    counters of profiles/r03t (SQ_INSTS_VALU / SQ_INSTS_MFMA per draw); ~4.5 SIMD cycles per VALU
-    instruction (f64 FMA ~5, 32-bit ~2.5, profiles/valu_rate.json)."""
-    cyc = launch_s * 2.4e9 * 1024 / draws
+    costs at least its VALU issue cycles + 64 per f64 MFMA.  Per-draw instruction counts from the
+    committed SQ counters of the shipped kernel (profiles/sq_headline.json: SQ_INSTS_VALU / SQ_INSTS_MFMA
+    per draw); ~4.5 SIMD cycles per VALU instruction (f64 FMA ~5, 32-bit ~2.5, profiles/valu_rate.json)."""
+    sq = sq_counts()
+    if sq is None:
+        return None
+    valu, mfma, d = sq
+    cyc = launch_s * CLOCK_HZ * SIMDS / draws
     need = valu * valu_cycles + mfma * 64
     return {"simd_cycles_per_draw": cyc, "valu_per_draw": valu, "mfma_per_draw": mfma,
-            "issue_cycles_per_draw": need, "frac": need / cyc,
+            "issue_cycles_per_draw": need, "frac": need / cyc, "source": "profiles/sq_headline.json",
+            "sq_library_sources": d.get("library_sources"),
             "note": "fraction of the SIMD time a draw's instructions need to issue (MFMA and VALU serialise "
                     "on MI355X); the rest is dependency wait nobody fills"}
 
@@ -426,7 +441,7 @@ def check(lib, rc):
         raise RuntimeError(lib.gs_last_error().decode(errors="replace"))
 
 
-def bench_indep(C, K, W, S, rank, world, dev):
+def bench_indep(C, K, W, S, rank, world, dev, ess_on=True):
     """BASELINE configs[2]: the 45 simulated pulsars, each with its own 30-bin free
     spectrum (PulsarBlockGibbs per pulsar, pulsar_gibbs.py:620-710), C chains per pulsar,
     all (pulsar, chain) systems in one fused persistent launch per S sweeps.  N > 1:
@@ -480,7 +495,7 @@ def bench_indep(C, K, W, S, rank, world, dev):
         n = min(S, n_max)
         ess_run.run(n, record_b=False, x_rec=xe[:n])
         return n, (xe[:n].view(n, P, CE, 30).permute(0, 2, 1, 3).reshape(n, CE, P * 30) if rec else None)
-    ess = gpu_ess(block, "indep")
+    ess = gpu_ess(block, "indep") if ess_on else None
     del ess_run, xe
     return dict(value=C * K / el, unit="array-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 warmup={"n": n_warm, "unit": "launches", "min_ms": WARM_MS},
@@ -488,7 +503,7 @@ def bench_indep(C, K, W, S, rank, world, dev):
                 n_gpus=world, scaling="strong" if world > 1 else "weak",
                 sharding=(f"pulsars over {world} GPUs (no collective)" if world > 1 else "one GPU"),
                 pulsar_iters_per_s=C * K * len(ptas) / el,
-                ess_per_s=C * K / el * ess["per_chain_sweep_min_bin"], ess=ess,
+                ess_per_s=C * K / el * ess["per_chain_sweep_min_bin"] if ess else None, ess=ess,
                 roofline={"kernel": "k_sweep_freespec" + ("" if model.NMX <= 16 else "_rm"),
                           "bound": "mfma", "unit": "TFLOP/s", "achieved": ach,
                           "peak": FP64_PEAK_TFLOPS, "frac": ach / FP64_PEAK_TFLOPS,
@@ -501,7 +516,7 @@ def bench_indep(C, K, W, S, rank, world, dev):
                                   "launch (profiles/pmc_traffic_indep.json), alg_bytes: the x and b rows recorded"})
 
 
-def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, aclength=20, reps=5):
+def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, aclength=20, reps=5, ess_on=True):
     """BASELINE configs[4]: n_psr independent pulsars x C chains per GPU, white-noise MH
     (aclength steps) forcing the per-chain TNT (batched SYRK) every sweep."""
     from pulsar_timing_gibbsspec_amd import _lib, synthetic
@@ -542,19 +557,21 @@ def bench_config5(C, K, W, rank, world, dev, n_psr=200, n_toa=10_000, n_f=100, a
     refresh_ms = e0.elapsed_time(e1) / reps
     # ESS per sweep of log10 rho: an untimed run of 64 chains on the CPU leg's pulsar
     # (config5_array(n_psr=1, seed=1), oracle/cpu_baseline.py config5), same start x0
-    d1 = synthetic.config5_array(n_psr=1, n_toa=n_toa, n_f=n_f, seed=1)
-    wm1 = WhiteNoiseModel(ctx, d1["T"], d1["r"], d1["sigma"], d1["backend"], [d1["fidx"]], [d1["phiinv_fixed"]],
-                          [d1["white"]], 64)
-    e1n = WhiteArrayChains(wm1, d1["n_param"], d1["gw_cols"], d1["rhomin"], d1["rhomax"],
-                           np.repeat(d1["x0"], 64, axis=0), aclength=aclength, chain_base=rank * 64)
-    ess = gpu_ess(sweep_block(e1n, d1["gw_cols"]), "config5")
-    del e1n, wm1, d1
+    ess = None
+    if ess_on:
+        d1 = synthetic.config5_array(n_psr=1, n_toa=n_toa, n_f=n_f, seed=1)
+        wm1 = WhiteNoiseModel(ctx, d1["T"], d1["r"], d1["sigma"], d1["backend"], [d1["fidx"]], [d1["phiinv_fixed"]],
+                              [d1["white"]], 64)
+        e1n = WhiteArrayChains(wm1, d1["n_param"], d1["gw_cols"], d1["rhomin"], d1["rhomax"],
+                               np.repeat(d1["x0"], 64, axis=0), aclength=aclength, chain_base=rank * 64)
+        ess = gpu_ess(sweep_block(e1n, d1["gw_cols"]), "config5")
+        del e1n, wm1, d1
     n_sys = n_psr * C
     flops = n_sys * (n_toa * m * (m + 1) + 2 * n_toa * m)      # SYRK + TNr per system
     tflops = flops / (refresh_ms * 1e-3) / 1e12
     return dict(value=C * world * K / el, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
-                ess_per_s=C * world * K / el * ess["per_chain_sweep_min_bin"], ess=ess,
+                ess_per_s=C * world * K / el * ess["per_chain_sweep_min_bin"] if ess else None, ess=ess,
                 chains_per_gpu=C, n_psr=n_psr, n_toa=n_toa, m=m, aclength=aclength,
                 roofline={"bound": "mfma", "kernel": "k_white_syrk + k_prefix (gs_white_tnt + gs_prefix_sys)",
                           "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -614,7 +631,7 @@ def ecorr_step_roofline(ctx, em, x, phiinv_F, reps=10):
                     "passes over the ECORR lines crash in rocprofv3 on this image)"}
 
 
-def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
+def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10, ess_on=True):
     """SURVEY 8f-4 with white noise sampled too (the notebook's J1713 configuration): per sweep
     white MH (aclength steps) -> per-chain TNT (gs_white_tnt) -> per-chain ECORR operands ->
     ECORR MH (aclength steps) -> rho|b -> gated b, C chains per GPU."""
@@ -659,7 +676,7 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
         el = float(t.item())
     if int(em.binfo.abs().sum()) or int(em.pinfo.abs().sum()):
         raise RuntimeError("non-PD system in the white + ECORR bench")
-    ess = gpu_ess(sweep_block(eng, gw, 256), "ecorr_white")     # the bench's chains continued, untimed
+    ess = gpu_ess(sweep_block(eng, gw, 256), "ecorr_white") if ess_on else None   # the chains continued, untimed
     # dominant kernel: gs_ecorr_prefix in likelihood mode on per-chain operands, timed alone
     stream = ctx.stream
     eng._phiinv(False)
@@ -684,7 +701,7 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
     value = C * world * K / el
     return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
-                ess_per_s=value * ess["per_chain_sweep_min_bin"], ess=ess,
+                ess_per_s=value * ess["per_chain_sweep_min_bin"] if ess else None, ess=ess,
                 chains_per_gpu=C, m=m, n_epoch=ne, aclength_white=aclength, aclength_ecorr=aclength,
                 roofline={"bound": "mfma", "kernel": "k_ecorr_prefix<likelihood mode, per-chain operands>",
                           "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -703,7 +720,7 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10):
                        "white MH + per-chain TNT + ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
 
 
-def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
+def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10, ess_on=True):
     """single pulsar with basis ECORR (J1713-like, 2 backends, 136 epochs,
     m = 212), C chains per GPU, aclength ECORR MH steps per sweep (each a batched
     likelihood evaluation: k_ecorr_schur + prefix + lnlike), analytic rho|b, gated b."""
@@ -741,7 +758,7 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
         el = float(t.item())
     if int(em.binfo.abs().sum()) or int(em.pinfo.abs().sum()):
         raise RuntimeError("non-PD system in the ECORR bench")
-    ess = gpu_ess(sweep_block(eng, gw, 256), "ecorr")           # the bench's chains continued, untimed
+    ess = gpu_ess(sweep_block(eng, gw, 256), "ecorr") if ess_on else None   # the chains continued, untimed
     # dominant kernel: gs_ecorr_prefix in likelihood mode (one launch per Metropolis step:
     # epoch Schur complement + fixed-prior prefix + F-block factorisation), timed alone
     stream = ctx.stream
@@ -763,7 +780,7 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10):
     value = C * world * K / el
     return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
-                ess_per_s=value * ess["per_chain_sweep_min_bin"], ess=ess,
+                ess_per_s=value * ess["per_chain_sweep_min_bin"] if ess else None, ess=ess,
                 chains_per_gpu=C, m=m, n_epoch=ne, m_R=mR, aclength=aclength,
                 roofline={"bound": "mfma", "kernel": ("k_ecorr_prefix<likelihood mode>" if em.fused and em.fused_lnl
                                                       else "k_ecorr_schur + k_prefix + k_lnlike_marg"),
@@ -1120,7 +1137,7 @@ def main():
 
     if args.indep:
         phase("configs[2] indep")
-        d = bench_indep(args.indep_chains, args.indep_steps, 2, 100, rank, world, dev)
+        d = bench_indep(args.indep_chains, args.indep_steps, 2, 100, rank, world, dev, ess_on=bool(args.ess))
         d["config"] = ("configs[2]: 45 simulated pulsars, each its own 30-bin free spectrum (m 68..77), "
                        f"{args.indep_chains} chains per pulsar, one fused launch per 100 sweeps")
         add("indep", d, "indep")
@@ -1140,15 +1157,15 @@ def main():
             add(kind + "_pulsar_sharded", d)
     if args.ecorr:
         phase("ecorr")
-        d = bench_ecorr(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev)
+        d = bench_ecorr(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev, ess_on=bool(args.ess))
         d.update(sharding="chains (no collective)", scaling="weak", n_gpus=world)
         add("ecorr", d, "ecorr")
-        d = bench_ecorr_white(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev)
+        d = bench_ecorr_white(args.ecorr_chains, args.ecorr_steps, 2, rank, world, dev, ess_on=bool(args.ess))
         d.update(sharding="chains (no collective)", scaling="weak", n_gpus=world)
         add("ecorr_white", d, "ecorr_white")
     if args.config5:
         phase("configs[4] config5")
-        d = bench_config5(args.c5_chains, args.c5_steps, 1, rank, world, dev)
+        d = bench_config5(args.c5_chains, args.c5_steps, 1, rank, world, dev, ess_on=bool(args.ess))
         d["config"] = ("configs[4]: 200 synthetic pulsars x 10^4 TOAs x 100 frequencies (m=216), "
                        "white-noise MH (20 steps) + per-chain TNT recompute every sweep, chain-sharded")
         add("config5", d, "config5")
