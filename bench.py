@@ -593,7 +593,7 @@ def _ecorr_traffic(C, fname="pmc_traffic_ecorr.json"):
     return d.get("bytes_per_launch") if d.get("chains") == C else None
 
 
-def ecorr_step_roofline(ctx, em, x, phiinv_F, reps=10):
+def ecorr_step_roofline(ctx, em, x, phiinv_F, reps=10, traffic_file="pmc_traffic_ecorr_step.json"):
     """The ECORR Metropolis step's kernel (gs_ecorr_lnl_state, incremental: the moved backend's epochs
     only), HIP-event timed alone on the context stream: a full evaluation stores the state at x, one
     proposal (gs_ecorr_propose, step 0) is drawn, then `reps` steps from that state (the state slot is
@@ -621,14 +621,18 @@ def ecorr_step_roofline(ctx, em, x, phiinv_F, reps=10):
     flops = C * (em.ne / em.n_bk * (mR + 1) * (mR + 2) + nM * (NF + 1) * (NF + 2) + (NF + 1) ** 3 // 3)
     nb = em.ldbp // 16
     tfl = flops / (ms * 1e-3) / 1e12
+    state = C * 2 * 8 * 256 * nb * (nb + 1) // 2
+    traffic = _ecorr_traffic(C, traffic_file)
     return {"kernel": "k_ecorr_prefix<likelihood mode, incremental step> (gs_ecorr_lnl_state)", "bound": "mfma",
             "achieved": tfl, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tfl / FP64_PEAK_TFLOPS,
-            "kernel_avg_ms": ms, "alg_flops_per_launch": flops, "traffic": None,
-            "state_bytes_per_launch": C * 2 * 8 * 256 * nb * (nb + 1) // 2,
+            "kernel_avg_ms": ms, "alg_flops_per_launch": flops, "traffic": traffic,
+            "state_bytes_per_launch": state, "traffic_over_state": (traffic / state) if traffic else None,
+            "hbm_gbs": (traffic / (ms * 1e-3) / 1e9) if traffic else None,
             "note": "the per-step kernel of the ECORR Metropolis block (aclength launches per sweep; the full "
                     "evaluation runs once per block): the moved backend's epochs re-weighted from the stored "
-                    "T = Ap - P (read and the proposal's written: state_bytes_per_launch); traffic null (PMC "
-                    "passes over the ECORR lines crash in rocprofv3 on this image)"}
+                    "T = Ap - P (read and the proposal's written: state_bytes_per_launch); traffic = PMC "
+                    "FETCH_SIZE x2 + WRITE_SIZE of the bench's own step launches (profiles/r06d, r06e, "
+                    "tools/pmc_ecorr_r06.py)"}
 
 
 def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10, ess_on=True):
@@ -688,7 +692,7 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10, ess_on=True):
     e1.record(stream)
     torch.cuda.synchronize()
     k_ms = e0.elapsed_time(e1) / reps
-    step = ecorr_step_roofline(ctx, em, eng.x, eng.phiinv_F)
+    step = ecorr_step_roofline(ctx, em, eng.x, eng.phiinv_F, traffic_file="pmc_traffic_ecorr_white_step.json")
     mR, NF, nM = em.mR, em.NF, em.nm
     flops = C * (ne * (mR + 1) * (mR + 2) + nM * (NF + 1) * (NF + 2) + (NF + 1) ** 3 // 3)
     tflops = flops / (k_ms * 1e-3) / 1e12
@@ -710,10 +714,8 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10, ess_on=True):
                           "traffic_over_alg": (traffic / alg_bytes) if traffic else None,
                           "hbm_frac": alg_bytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                           "note": "as the ecorr line; each chain's own [B | d_E] rows and Ap tiles stream from "
-                                  "HBM (alg_bytes_per_launch); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE, the x2 "
-                                  "wide-read correction makes it an upper estimate (measured on the round-3 "
-                                  "kernel, profiles/pmc_traffic_ecorr_white.json: PMC passes over the ECORR "
-                                  "lines crash in rocprofv3 on this image, profiles/r05t/SUMMARY.md); the full "
+                                  "HBM (alg_bytes_per_launch); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE of the "
+                                  "bench's own launches (profiles/r06d, r06e; tools/pmc_ecorr_r06.py); the full "
                                   "evaluation (once per Metropolis block); the per-step kernel: step_roofline"},
                 step_roofline=step,
                 config="SURVEY 8f-4 with EFAC/EQUAD sampled: J1713-like pulsar, 2 backends, 136 ECORR epochs, "
@@ -790,10 +792,10 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10, ess_on=True):
                           "traffic": _ecorr_traffic(C),
                           "note": "ne (mR+1)(mR+2) + nM (NF+1)(NF+2) + (NF+1)^3/3 flop per chain (epoch-weighted "
                                   "SYRK with the d_E row + fixed-prior Schur update + F-block Cholesky) over the "
-                                  "HIP-event time of one all-chain likelihood launch; traffic: PMC of the round-3 "
-                                  "kernel (profiles/pmc_traffic_ecorr.json; same operands, L2-resident); the full "
-                                  "evaluation "
-                                  "(once per Metropolis block); the per-step kernel: step_roofline"},
+                                  "HIP-event time of one all-chain likelihood launch; traffic: PMC FETCH_SIZE x2 + "
+                                  "WRITE_SIZE of the bench's own launches (profiles/r06d, r06e; operands "
+                                  "L2-resident); the full evaluation (once per Metropolis block); the per-step "
+                                  "kernel: step_roofline"},
                 step_roofline=step,
                 config="SURVEY 8f-4: J1713-like pulsar, basis ECORR (2 backends, 136 epochs) + 30-bin free "
                        "spectrum + 16-col TM, ECORR MH + analytic rho|b + gated b per sweep, chain-sharded")
@@ -1166,6 +1168,7 @@ def main():
     if args.config5:
         phase("configs[4] config5")
         d = bench_config5(args.c5_chains, args.c5_steps, 1, rank, world, dev, ess_on=bool(args.ess))
+        d.update(n_gpus=world, scaling="weak", sharding="chains (no collective)")
         d["config"] = ("configs[4]: 200 synthetic pulsars x 10^4 TOAs x 100 frequencies (m=216), "
                        "white-noise MH (20 steps) + per-chain TNT recompute every sweep, chain-sharded")
         add("config5", d, "config5")
