@@ -134,13 +134,12 @@ def warm(fn, min_calls=1, min_ms=WARM_MS):
     return n
 
 
-def event_ms(stream, fn, reps, warm=10):
+def event_ms(stream, fn, reps, warm_calls=10):
     """Average HIP-event time of fn() on ``stream`` (the context stream the C-ABI launches on),
-    after `warm` untimed calls: the clock ramps back up over ~10 ms of sustained load after the
-    small ESS launches (rocprof r04f: the red grid kernel at 0.84 ms right after them, 0.745 in the
-    sweeps)."""
-    for _ in range(warm):
-        fn()
+    after at least `warm_calls` untimed calls and WARM_MS of wall time of them: the clock ramps back
+    up over ~10-20 ms of sustained load after host-bound phases (rocprof r04f: the red grid kernel at
+    0.84 ms right after the small ESS launches, 0.745 in the sweeps)."""
+    warm(fn, warm_calls)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(reps):
@@ -310,11 +309,6 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess=True):
                sharding=("pulsars over %d GPUs (RCCL %s per sweep)" %
                          (world, "all-reduce of the tau sums" if curn_mode == "sum" else "all-gather of [tau | x_red]"))
                if sharded else "chains (no collective)")
-    if not sharded and ess:
-        # ESS per sweep of the common log10 rho from a separate untimed run of 256 chains from the
-        # bench's start (gpu_ess: the CPU leg's run lengths and estimator)
-        out["ess"] = gpu_ess(sweep_block(make(min(C, 256)), rind), kind)
-        out["ess_per_s"] = value * out["ess"]["per_chain_sweep_min_bin"]
     # roofline of the dominant kernels, each HIP-event timed alone on the context stream
     lib, h, m = ctx.lib, ctx.handle, eng.model
     st = ctx.stream
@@ -433,6 +427,12 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess=True):
     dom = max(kernels, key=lambda k: kernels[k]["kernel_avg_ms"])
     out["roofline"] = dict(kernel=dom, **kernels[dom])
     out["kernels"] = kernels
+    if not sharded and ess:
+        # ESS per sweep of the common log10 rho from a separate untimed run of 256 chains from the
+        # bench's start (gpu_ess: the CPU leg's run lengths and estimator), after the kernel timings
+        # (its host-bound sweeps let the clock drop)
+        out["ess"] = gpu_ess(sweep_block(make(min(C, 256)), rind), kind)
+        out["ess_per_s"] = value * out["ess"]["per_chain_sweep_min_bin"]
     return out
 
 
@@ -680,7 +680,6 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10, ess_on=True):
         el = float(t.item())
     if int(em.binfo.abs().sum()) or int(em.pinfo.abs().sum()):
         raise RuntimeError("non-PD system in the white + ECORR bench")
-    ess = gpu_ess(sweep_block(eng, gw, 256), "ecorr_white") if ess_on else None   # the chains continued, untimed
     # dominant kernel: gs_ecorr_prefix in likelihood mode on per-chain operands, timed alone
     stream = ctx.stream
     eng._phiinv(False)
@@ -703,6 +702,7 @@ def bench_ecorr_white(C, K, W, rank, world, dev, aclength=10, ess_on=True):
     alg_bytes = C * 8 * (ne * em.ldbx + 256 * nb * (nb + 1) // 2 + ne + NF + 5)
     traffic = _ecorr_traffic(C, "pmc_traffic_ecorr_white.json")
     value = C * world * K / el
+    ess = gpu_ess(sweep_block(eng, gw, 256), "ecorr_white") if ess_on else None   # the chains continued, untimed
     return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
                 ess_per_s=value * ess["per_chain_sweep_min_bin"] if ess else None, ess=ess,
@@ -760,7 +760,6 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10, ess_on=True):
         el = float(t.item())
     if int(em.binfo.abs().sum()) or int(em.pinfo.abs().sum()):
         raise RuntimeError("non-PD system in the ECORR bench")
-    ess = gpu_ess(sweep_block(eng, gw, 256), "ecorr") if ess_on else None   # the chains continued, untimed
     # dominant kernel: gs_ecorr_prefix in likelihood mode (one launch per Metropolis step:
     # epoch Schur complement + fixed-prior prefix + F-block factorisation), timed alone
     stream = ctx.stream
@@ -780,6 +779,7 @@ def bench_ecorr(C, K, W, rank, world, dev, aclength=10, reps=10, ess_on=True):
     flops = C * (ne * (mR + 1) * (mR + 2) + nM * (NF + 1) * (NF + 2) + (NF + 1) ** 3 // 3)
     tflops = flops / (k_ms * 1e-3) / 1e12
     value = C * world * K / el
+    ess = gpu_ess(sweep_block(eng, gw, 256), "ecorr") if ess_on else None   # the chains continued, untimed
     return dict(value=value, unit="chain-iters/s", ms_per_step=el / K * 1e3, steps=K,
                 warmup={"n": n_warm, "unit": "sweeps", "min_ms": WARM_MS},
                 ess_per_s=value * ess["per_chain_sweep_min_bin"] if ess else None, ess=ess,

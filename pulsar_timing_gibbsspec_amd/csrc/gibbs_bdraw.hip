@@ -383,29 +383,6 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_wide(BdrawArgs A) {
 #ifndef GS_BDRAW_XCD
 #define GS_BDRAW_XCD 0
 #endif
-// k_bdraw_tiled's persistent loop loads the NEXT item's phiinv_F row and gate flag while the current
-// item's draw runs (1), instead of at the head of each draw, where the wave waited for them (0)
-#ifndef GS_BDRAW_PREFETCH
-#define GS_BDRAW_PREFETCH 1
-#endif
-// the per-item inputs a draw starts from (loaded ahead by the persistent loop)
-struct BdrawPre {
-  double phinv;
-  int mask;  // the gate flag as loaded (0: shut), compared where it is used
-};
-__device__ __forceinline__ BdrawPre bdraw_pre(const BdrawArgs& A, int p, int c, int NF, int lane) {
-  const int64_t sys = (int64_t)p * A.n_chain + c;
-  BdrawPre r;
-#ifdef GS_BDRAW_PROBE_NOLOAD  // cost attribution only (wrong draws): no phiinv / gate loads
-  r.mask = 1;
-  r.phinv = 1e10;
-#else
-  r.mask = A.chain_mask ? A.chain_mask[A.mask_per_sys ? sys : (int64_t)c] : 1;
-  r.phinv = lane < NF ? A.phiinv_F[(A.phi_per_chain ? (int64_t)c : sys) * NF + lane] : 0.0;
-#endif
-  return r;
-}
-
 // lnl[sys] of k_lnlike_marg from the two factorisation terms (gs_ctx_set_bdraw_lnl)
 __device__ __forceinline__ void bdraw_lnl_store(const BdrawArgs& A, int p, int64_t sys, int NF, int lane, double phinv,
                                                 int fail, double yy, double lp) {
@@ -424,16 +401,14 @@ __device__ __forceinline__ void bdraw_lnl_store(const BdrawArgs& A, int p, int64
 // systems the gate skips as well (likelihood mode on the already staged block: no second launch).
 template <int NFC, int NTC, int BC, bool LNLD = false, typename ModelT>
 __device__ __forceinline__ void bdraw_item(const BdrawArgs& A, const ModelT& M, int p, int c, int NF, int nM, int fi,
-                                           int mi, double* scr, int lane, int NMXe = -1,
-                                           const BdrawPre* pre = nullptr) {
+                                           int mi, double* scr, int lane, int NMXe = -1) {
   if (NMXe < 0) NMXe = A.NMX;  // the NMX the block is indexed with (model_tiled_view_psr)
   const int64_t sys = (int64_t)p * A.n_chain + c;
-  const BdrawPre in = pre ? *pre : bdraw_pre(A, p, c, NF, lane);
-  const bool shut = in.mask == 0;  // gate closed: keep b
+  const bool shut = A.chain_mask && A.chain_mask[A.mask_per_sys ? sys : (int64_t)c] == 0;  // gate closed: keep b
   if constexpr (!LNLD) {
     if (shut) return;
   }
-  const double phinv = in.phinv;
+  const double phinv = lane < NF ? A.phiinv_F[(A.phi_per_chain ? (int64_t)c : sys) * NF + lane] : 0.0;
   if constexpr (LNLD) {
     if (shut) {  // no draw, but the lnL at this phiinv all the same (likelihood mode: no solves)
       double yy = 0.0, lp = 0.0;
@@ -551,12 +526,6 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
     const int64_t lo = w * n_items / A.persist, hi = (w + 1) * n_items / A.persist;
     int cur = -1, nM = 0, fi = 0, mi = 0, NMXe = A.NMX;
     ModelTiled M;
-    // GS_BDRAW_PREFETCH: item it + 1's phiinv row and gate flag are in flight during item it's draw
-    BdrawPre nxt{0.0, 1};
-    if (GS_BDRAW_PREFETCH && lo < hi) {
-      const int c0 = (int)(lo % nb) * WPB + wave;
-      if (c0 < A.n_chain) nxt = bdraw_pre(A, (int)(lo / nb), c0, NF, lane);
-    }
 #pragma unroll 1
     for (int64_t it = lo; it < hi; ++it) {
       const int p = (int)(it / nb), grp = (int)(it % nb);
@@ -570,16 +539,7 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
         M = model_tiled_view_psr<FX>(lds, NF, A.NMX, nM, NMXe);
       }
       const int c = grp * WPB + wave;
-      if constexpr (GS_BDRAW_PREFETCH) {
-        const BdrawPre now = nxt;
-        if (it + 1 < hi) {
-          const int c1 = (int)((it + 1) % nb) * WPB + wave;
-          if (c1 < A.n_chain) nxt = bdraw_pre(A, (int)((it + 1) / nb), c1, NF, lane);
-        }
-        if (c < A.n_chain) bdraw_item<NFC, NTC, GS_BCAST_TILE, LNLD>(A, M, p, c, NF, nM, fi, mi, scr, lane, NMXe, &now);
-      } else {
-        if (c < A.n_chain) bdraw_item<NFC, NTC, GS_BCAST_TILE, LNLD>(A, M, p, c, NF, nM, fi, mi, scr, lane, NMXe);
-      }
+      if (c < A.n_chain) bdraw_item<NFC, NTC, GS_BCAST_TILE, LNLD>(A, M, p, c, NF, nM, fi, mi, scr, lane, NMXe);
     }
     return;
   }
