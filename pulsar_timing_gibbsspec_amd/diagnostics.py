@@ -53,18 +53,26 @@ def pooled_iat(x, c=5.0):
     return float(max(tau[M], 1.0)), M
 
 
-def ess_table(X, c=5.0):
+def ess_table(X, c=5.0, groups=16):
     """Per column of X (chains, n, k): the ESS per chain-sweep 1/tau of the pooled chains and its
-    standard error, from Sokal's asymptotic variance var(tau) = 2 (2M + 1) tau^2 / N with N =
-    chains x n pooled samples (so se(1/tau) = (1/tau) sqrt(2 (2M + 1) / N))."""
+    standard error -- the larger of (a) Sokal's asymptotic one, var(tau) = 2 (2M + 1) tau^2 / N with
+    N = chains x n pooled samples (se(1/tau) = (1/tau) sqrt(2 (2M + 1) / N)), and (b) the spread over
+    G = min(chains, groups) disjoint groups of chains, each group's pooled 1/tau (se = std / sqrt(G)),
+    which also covers chains that visit a slowly mixing tail only now and then (for which (a), an
+    asymptotic formula, reads low with few chains)."""
     X = np.asarray(X)
     C, n, k = X.shape
     out = np.empty(k)
     se = np.empty(k)
+    G = min(C, groups)
+    parts = np.array_split(np.arange(C), G) if G >= 3 else None
     for j in range(k):
         tau, M = pooled_iat(X[:, :, j], c)
         out[j] = 1.0 / tau
         se[j] = out[j] * np.sqrt(2.0 * (2 * M + 1) / (C * n))
+        if parts is not None:
+            f = np.array([1.0 / pooled_iat(X[g, :, j], c)[0] for g in parts])
+            se[j] = max(se[j], float(np.std(f, ddof=1)) / np.sqrt(G))
     return out, se
 
 

@@ -26,9 +26,10 @@ def test_pooled_iat_recovers_ar1():
         assert M >= 5 * tau * 0.99
 
 
-def test_sokal_standard_error_matches_the_spread():
-    """Over independent replicas the ESS estimates scatter by about the standard error the
-    estimator reports (within a factor 1.6 either way), and sit within 3 SE of 1/tau."""
+def test_standard_error_covers_the_spread():
+    """Over independent replicas the ESS estimates scatter by no more than about the standard error
+    the estimator reports (the larger of Sokal's and the spread over chain groups: within a factor
+    1.6 below, 2.5 above), and sit within 3 SE of 1/tau."""
     rng = np.random.default_rng(1)
     a = 0.9
     f_true = (1 - a) / (1 + a)
@@ -39,7 +40,7 @@ def test_sokal_standard_error_matches_the_spread():
         est.append(e[0])
         ses.append(se[0])
     est, ses = np.array(est), np.array(ses)
-    assert 1 / 1.6 < np.std(est) / np.mean(ses) < 1.6
+    assert 1 / 2.5 < np.std(est) / np.mean(ses) < 1.6
     assert abs(np.mean(est) - f_true) < 3 * np.mean(ses) / np.sqrt(len(est)) + 0.02 * f_true
 
 
