@@ -751,5 +751,9 @@ class PTAChains:
         with fail_counts(self.ctx, self.fail_count):
             slab = self.sweep_begin(x_rec=x_rec, z0=z0, u_red=u_red, mh_inj=mh_inj)
             if self.sharded:
-                slab = self.allreduce(slab) if self.curn_mode == "sum" else self.gather(slab)
+                # the collective is ordered after the slab's kernels: torch issues it against the
+                # CURRENT stream, which is made the context's (the kernels' stream; a no-op when the
+                # context runs on torch's current stream, as by default and inside graph capture)
+                with torch.cuda.stream(self.ctx.stream):
+                    slab = self.allreduce(slab) if self.curn_mode == "sum" else self.gather(slab)
             self.sweep_end(slab, z=z, u_curn=u_curn)
