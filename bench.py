@@ -944,6 +944,9 @@ def main():
     ap.add_argument("--cpu-ess-procs", type=int, default=12, help="CPU ESS chains run at once beside the GPU "
                     "work (oracle.cpu_baseline.ESS_CHAINS independent single-thread chains per line, EssPool)")
     ap.add_argument("--bcast", type=int, default=None, help="GS_OPT_BCAST (0 readlane, 1 LDS, 2 batched, 3 tile)")
+    ap.add_argument("--sched", type=int, default=None,
+                    help="GS_OPT_SWEEP_SCHED for the headline (0 cost model, 1 hand-off, 2 one chain per wave, "
+                         "3 two chains per wave)")
     ap.add_argument("--host-stream", type=int, default=1,
                     help="also time the headline with every recorded row streamed to pinned host memory (1/0)")
     ap.add_argument("--indep", type=int, default=1, help="measure BASELINE configs[2] (45 independent pulsars)")
@@ -1019,6 +1022,8 @@ def main():
     ctx = _lib.Context(local, seed=20251015)
     if args.bcast is not None:
         ctx.set_option(_lib.OPT_BCAST, args.bcast)
+    if args.sched is not None:
+        ctx.set_option(_lib.OPT_SWEEP_SCHED, args.sched)
     model = DeviceModel(ctx, [T], [N], [r], [gwid], [np.full(T.shape[1] - 60, 1e-40)])
     C = args.chains
     x0 = np.random.default_rng(rank).uniform(-9, -4, (C, 30))

@@ -89,7 +89,9 @@ enum {
                          of 16 chains, each trio of waves running a 13th..16th chain in thirds of
                          the sweeps (every wave draws 4/3 chains: n_psr x n_chain = 4096 fills the
                          3072 wave slots of 3 waves/SIMD in one round); 2 = 4-wave workgroups,
-                         one chain per wave.  The 12-wave shape is used only when its LDS (model
+                         one chain per wave; 3 = two chains per wave (NF = 60 tile variant with
+                         device Philox, even chain counts; else as 0), both chains' draws sharing
+                         the diagonal-tile eliminations at 2 waves/SIMD.  The 12-wave shape is used only when its LDS (model
                          block + 12 waves' scratch, save, park and hand-off slots) fits the
                          device's per-workgroup limit; otherwise the 4-wave shape runs.  A
                          hand-off that does not arrive within the bounded wait (or arrives from a

@@ -279,7 +279,7 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
       ctx->phi_per_chain = value;
       return 0;
     case GS_OPT_SWEEP_SCHED:
-      if (value < 0 || value > 2) return fail_arg(3, "GS_OPT_SWEEP_SCHED must be 0, 1 or 2");
+      if (value < 0 || value > 3) return fail_arg(3, "GS_OPT_SWEEP_SCHED must be 0, 1, 2 or 3");
       ctx->sweep_sched = value;
       return 0;
     case GS_OPT_DEBUG_HANDOFF:

@@ -23,6 +23,7 @@
 #include "gibbs_common.h"
 #include "gibbs_internal.h"
 #include "gibbs_tile.h"
+#include "gibbs_tile2.h"
 
 #ifndef GS_SWEEP_MINW
 #define GS_SWEEP_MINW 2
@@ -1129,6 +1130,229 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_sweep_frees
   sweep_freespec_body<NFC, NTC, WPB, BC, false>(A);
 }
 
+// ------------------------------------------------------------ fused sweep, two chains per wave
+// GS_OPT_SWEEP_SCHED = 3 (and the cost model's choice where it applies, launch_sweep_freespec): the
+// same sweep as sweep_freespec_body for NF = 60 on the tiled model block (nm <= 16) with device Philox,
+// each wavefront running chains c, c + 1 side by side and drawing their b together
+// (gibbs_tile2.h bdraw_tile_pair60).  Every draw, uniform and record is the one-chain kernel's bit for
+// bit: the Philox counters are per chain, a chain whose gate is shut has its (computed) draw discarded
+// exactly where the one-chain kernel skips it, and a failed factorisation keeps that chain's b.
+// 2 waves per SIMD (both chains' tiles: ~200 VGPRs): 4096 chains are 2048 waves, one round.
+constexpr int GS_PAIR_SCR = 2 * gs_tile_scr(60) + 256 + 128 + 128;
+// GS_PAIR_RHO_MERGE: both chains' rho steps in one pass over the wave (30 frequencies each)
+#ifndef GS_PAIR_RHO_MERGE
+#define GS_PAIR_RHO_MERGE 1
+#endif  // per wave: 2 scratches, b save, z_M, x park
+
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB, 2) void k_sweep_pair(SweepArgs A) {
+  extern __shared__ double lds[];
+  constexpr int NF = 60, NFR = 30;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
+  constexpr int CPB = 2 * WPB;
+  const int nb = (A.n_chain + CPB - 1) / CPB;
+  const int p = blockIdx.x / nb;
+  const int cA = (blockIdx.x % nb) * CPB + 2 * wave;  // chains cA, cA + 1 (n_chain is even)
+  const int nM = __builtin_amdgcn_readfirstlane(A.nm[p]);
+  stage_model_tiled(lds, A.model + (int64_t)p * A.mstride, NF, A.NMX, nM);
+  const int64_t mlds = model_tiled_doubles(NF, A.NMX);
+  if (cA >= A.n_chain) return;
+  int NMXe = A.NMX;
+  const ModelTiled M = model_tiled_view_psr<true>(lds, NF, A.NMX, nM, NMXe);
+  const int64_t n_sys = (int64_t)A.n_psr * A.n_chain;
+  const bool act = lane < NF, actm = lane < nM;
+  const int kf = act ? (lane >> 1) : 0;
+  const int fi = act ? A.fidx[p * NF + lane] : 0;
+  const int mi = actm ? A.midx[p * A.NMX + lane] : 0;
+  double* wl = lds + mlds + (int64_t)wave * GS_PAIR_SCR;
+  double* const scr[2] = {wl, wl + gs_tile_scr(60)};
+  double* bsave = wl + 2 * gs_tile_scr(60);  // [2][128]: the chains' previous b (failed or shut draws)
+  double* zmslot = bsave + 256;              // [2][64]: the chains' z_M during the draw
+  double* xpark = zmslot + 128;              // [2][64]: the chains' x during the draw (not in VGPRs)
+
+  const double irhomin = 1.0 / A.rhomin, irhomax = 1.0 / A.rhomax;
+  const int64_t xr_step = n_sys * NFR;
+  const int64_t br_step = (A.brec_nc == 0 ? n_sys : (int64_t)A.n_psr * A.brec_nc) * A.ldb;
+  const int S = A.n_sweeps;
+  int64_t sys[2];
+  long long gchain[2];
+  double x[2], bF[2], bM[2];
+  int fail[2] = {0, 0};
+  // record targets: per-lane 32/64-bit offsets from the uniform record bases (-1: this lane records
+  // nothing), advanced by one sweep's rows per iteration
+  int xro[2], bFo[2], bMo[2];
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch) {
+    const int c = cA + ch;
+    sys[ch] = (int64_t)p * A.n_chain + c;
+    gchain[ch] = A.chain_base + c;
+    x[ch] = act ? A.x_state[sys[ch] * NFR + kf] : 0.0;
+    bF[ch] = act ? A.b_state[sys[ch] * A.ldb + fi] : 0.0;
+    bM[ch] = actm ? A.b_state[sys[ch] * A.ldb + mi] : 0.0;
+    xro[ch] = (A.x_rec && act && !(lane & 1)) ? (int)(sys[ch] * NFR + kf) : -1;
+    const bool brec = A.b_rec && (A.brec_nc == 0 || c < A.brec_nc);
+    const int64_t brow0 = A.brec_nc == 0 ? sys[ch] : (int64_t)p * A.brec_nc + c;
+    bFo[ch] = (brec && act) ? (int)(brow0 * A.ldb + fi) : -1;
+    bMo[ch] = (brec && actm) ? (int)(brow0 * A.ldb + mi) : -1;
+  }
+#pragma unroll 1
+  for (int sw = 0; sw < S; ++sw) {
+    const long long ii = A.it0 + sw;
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {  // record-before-update (pulsar_gibbs.py:658-659)
+      if (xro[ch] >= 0) A.x_rec[sw * xr_step + xro[ch]] = x[ch];
+      if (bFo[ch] >= 0) A.b_rec[sw * br_step + bFo[ch]] = bF[ch];
+      if (bMo[ch] >= 0) A.b_rec[sw * br_step + bMo[ch]] = bM[ch];
+    }
+#pragma unroll 1
+    for (int pass = (ii == 0) ? 0 : 1; pass < 2; ++pass) {
+      int ev = GS_EV_B0;
+      double phinv[2] = {0.0, 0.0};
+      bool draw[2] = {true, true};
+      if (pass == 1) {
+        if constexpr (GS_RHO_PRIO > 0) __builtin_amdgcn_s_setprio(GS_RHO_PRIO);
+#if GS_PAIR_RHO_MERGE
+        {
+          // rho|b analytic (pulsar_gibbs.py:208-216, 236), as sweep_freespec_body, for both chains in
+          // one pass: lane 32 h + k computes frequency k of chain h (the one-chain layout has each
+          // frequency on two lanes), same operations and Philox counter per (chain, k)
+          const int h = lane >> 5, k = lane & 31;
+          const bool am = k < NFR;
+          double tau2[2];
+#pragma unroll
+          for (int ch = 0; ch < 2; ++ch) {
+            const double partner = __shfl_xor(bF[ch], 1);
+            const double be = (lane & 1) ? partner : bF[ch], bo = (lane & 1) ? bF[ch] : partner;
+            tau2[ch] = gs_add_rn(gs_mul_rn(be, be), gs_mul_rn(bo, bo)) / 2;
+          }
+          const int src = am ? 2 * k : 0;
+          const double ta = gtile::bcast_lane_bp(tau2[0], src), tb = gtile::bcast_lane_bp(tau2[1], src);
+          const double tau = h ? tb : ta;
+          double U, u2;
+          gs_uniform2(gs_counter(k, ii, h ? gchain[1] : gchain[0], p + A.psr_base, GS_EV_RHO), A.key, U, u2);
+#if GS_FAST_MATH
+          const double t1 = tau * irhomax;
+          const double arg = t1 - tau * irhomin;
+#else
+          const double t1 = tau / A.rhomax;
+          const double arg = t1 - (tau / A.rhomin);
+#endif
+          // (1 - exp(arg) is exactly 1 where the skip applies, so one ballot over both chains draws
+          // the same values as a ballot per chain)
+          double hi = 1.0;
+#if GS_FAST_MATH && GS_RHO_EXP
+          if (__ballot(am && !(arg < -40.0))) hi = 1 - gs_exp_neg(arg);
+#else
+          if (__ballot(am && !(arg < -40.0))) hi = 1 - exp(arg);
+#endif
+          const double eta = 0.0 + hi * U;
+#if GS_FAST_MATH
+          const double den = t1 - gs_log_pos(1 - eta);
+          const double rho = tau * rcp_nr2(den);
+          const double xnew = am ? gs_log_pos(rho) * 0x1.bcb7b1526e50ep-3 : 0.0;
+          const double phm = am ? den * rcp_nr2(tau) : 0.0;
+#else
+          const double den = t1 - log(1 - eta);
+          const double rho = tau / den;
+          const double xnew = am ? 0.5 * log10(rho) : 0.0;
+          const double phm = am ? rcp_nr2(rho) : 0.0;
+#endif
+          // gate: all(xnew != x_old[-1])  (pulsar_gibbs.py:697), per chain
+          const double xl0 = rdlane(x[0], NF - 1), xl1 = rdlane(x[1], NF - 1);
+          const unsigned long long same = __ballot(am && (xnew == (h ? xl1 : xl0)));
+          draw[0] = (same & 0xffffffffull) == 0ull;
+          draw[1] = (same >> 32) == 0ull;
+          // back to the one-chain layout: lane l of chain ch holds frequency l >> 1
+#pragma unroll
+          for (int ch = 0; ch < 2; ++ch) {
+            const int from = 32 * ch + (act ? (lane >> 1) : 0);
+            const double xv = gtile::bcast_lane_bp(xnew, from), pv = gtile::bcast_lane_bp(phm, from);
+            x[ch] = act ? xv : 0.0;
+            phinv[ch] = act ? pv : 0.0;
+          }
+        }
+#else
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch) {
+          // rho|b analytic (pulsar_gibbs.py:208-216, 236), as sweep_freespec_body
+          const double partner = __shfl_xor(bF[ch], 1);
+          const double be = (lane & 1) ? partner : bF[ch], bo = (lane & 1) ? bF[ch] : partner;
+          const double tau = gs_add_rn(gs_mul_rn(be, be), gs_mul_rn(bo, bo)) / 2;
+          double U, u2;
+          gs_uniform2(gs_counter(kf, ii, gchain[ch], p + A.psr_base, GS_EV_RHO), A.key, U, u2);
+#if GS_FAST_MATH
+          const double t1 = tau * irhomax;
+          const double arg = t1 - tau * irhomin;
+#else
+          const double t1 = tau / A.rhomax;
+          const double arg = t1 - (tau / A.rhomin);
+#endif
+          double hi = 1.0;
+#if GS_FAST_MATH && GS_RHO_EXP
+          if (__ballot(act && !(arg < -40.0))) hi = 1 - gs_exp_neg(arg);
+#else
+          if (__ballot(act && !(arg < -40.0))) hi = 1 - exp(arg);
+#endif
+          const double eta = 0.0 + hi * U;
+#if GS_FAST_MATH
+          const double den = t1 - gs_log_pos(1 - eta);
+          const double rho = tau * rcp_nr2(den);
+          const double xnew = act ? gs_log_pos(rho) * 0x1.bcb7b1526e50ep-3 : 0.0;
+          phinv[ch] = act ? den * rcp_nr2(tau) : 0.0;
+#else
+          const double den = t1 - log(1 - eta);
+          const double rho = tau / den;
+          const double xnew = act ? 0.5 * log10(rho) : 0.0;
+          phinv[ch] = act ? rcp_nr2(rho) : 0.0;
+#endif
+          // gate: all(xnew != x_old[-1])  (pulsar_gibbs.py:697)
+          const double xlast = rdlane(x[ch], NF - 1);
+          draw[ch] = __ballot(act && (xnew == xlast)) == 0ull;
+          x[ch] = xnew;
+        }
+#endif
+        if constexpr (GS_RHO_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+        if (!draw[0] && !draw[1]) break;
+        ev = GS_EV_B;
+      }
+      double zF[2], zM[2];
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch) {
+        gs_normal2(gs_counter(lane, ii, gchain[ch], p + A.psr_base, ev), A.key, zF[ch], zM[ch]);
+        if (pass == 0) phinv[ch] = act ? 1.0 / pow(10.0, 2.0 * x[ch]) : 0.0;  // first draw from xs
+        // the previous b waits in the wave's save slot (a failed or shut draw keeps it)
+        bsave[128 * ch + lane] = bF[ch];
+        bsave[128 * ch + 64 + lane] = bM[ch];
+        xpark[64 * ch + lane] = x[ch];
+      }
+      int f[2];
+      bdraw_tile_pair60<true>(M, NMXe, nM, lane, phinv, zF, zM, bF, bM, scr, zmslot, f);
+      gtile::lds_fence();
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch) {
+        x[ch] = xpark[64 * ch + lane];
+        const bool keep = !draw[ch] || f[ch];
+        if (keep) {
+          gtile::lds_fence();
+          bF[ch] = bsave[128 * ch + lane];
+          bM[ch] = bsave[128 * ch + 64 + lane];
+        }
+        if (draw[ch] && f[ch]) {
+          if (!fail[ch]) fail[ch] = f[ch];
+          if (A.fail_count && lane == 0) A.fail_count[sys[ch]] += 1;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch) {
+    if (act && !(lane & 1)) A.x_state[sys[ch] * NFR + kf] = x[ch];
+    if (act) A.b_state[sys[ch] * A.ldb + fi] = bF[ch];
+    if (actm) A.b_state[sys[ch] * A.ldb + mi] = bM[ch];
+    if (A.info && lane == 0) A.info[sys[ch]] = fail[ch];
+  }
+}
+
 // ------------------------------------------------------------ rho|b analytic
 __global__ void k_rho_analytic(RhoArgs A) {
   const int64_t n_sys = (int64_t)A.n_psr * A.n_chain;
@@ -1312,10 +1536,29 @@ static bool sweep_handoff_wins(const SweepArgs& a) {
   const double c12 = std::ceil(wg / ncu) * (4.0 / 3.0);
   return c12 < 0.97 * (k + g);
 }
+// GS_SWEEP_PAIR_AUTO: the cost model (GS_OPT_SWEEP_SCHED 0) picks the two-chains-per-wave kernel
+// wherever it applies
+#ifndef GS_SWEEP_PAIR_AUTO
+#define GS_SWEEP_PAIR_AUTO 0
+#endif
 int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
   const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
   const bool tiled = GS_SWEEP_TILED && (!fixed || a.bcast == GS_BCAST_TILE);
   const size_t mlds = tiled ? (size_t)model_tiled_doubles(a.NF, a.NMX) : (size_t)a.mstride;
+  // two chains per wave (k_sweep_pair): NF = 60 on the tiled block with a tiled fixed part, device
+  // Philox (no injected draws), an even chain count
+  const bool pair_ok = a.NF == 60 && tiled && model_tiled_fix(a.NMX) && !a.z0_inj && !a.z_inj && !a.u_inj &&
+                       (a.n_chain % 2) == 0 && !a.dbg_handoff;
+  if (pair_ok && (a.sched == 3 || (a.sched == 0 && GS_SWEEP_PAIR_AUTO))) {
+    constexpr int WPB = 4;
+    const size_t lds = (mlds + (size_t)WPB * GS_PAIR_SCR) * sizeof(double);
+    if (lds <= device_lds_optin()) {
+      const int nb = (a.n_chain + 2 * WPB - 1) / (2 * WPB);
+      if (lds > 65536 && set_lds(k_sweep_pair<WPB>, lds)) return 2;
+      hipLaunchKernelGGL((k_sweep_pair<WPB>), dim3((unsigned)(a.n_psr * nb)), dim3(64 * WPB), lds, s, a);
+      return 0;
+    }
+  }
   // the 12-wave hand-off shape holds 12 waves' scratch, save and park slots beside the model
   // block: at large NF x NMX (e.g. NF = 60, NMX = 64: 168 KB) it does not fit, and the 4-wave
   // shape (~102 KB there) runs instead, whatever the cost model or GS_OPT_SWEEP_SCHED say

@@ -1,0 +1,281 @@
+// b|rho draws of TWO chains per wavefront (the fused sweep's GS_OPT_SWEEP_SCHED = 3 shape).
+//
+// The draw is gibbs_tile.h's bdraw_tile_core (register tiles in the v_mfma_f64_16x16x4f64 C layout,
+// augmented Schur block, stored transposes, tiled fixed block) for two systems at once, with the same
+// arithmetic per system, so both chains' draws are bit-identical to the one-chain kernel's.  What the
+// pairing changes is the diagonal tiles' column elimination (63 % of a draw's VALU): both chains' tiles
+// sit in ONE register set -- lanes 0..31 chain a, 32..63 chain b, register 2s + j holding row
+// 4s + 2j + h at lane 32X + 16h + c -- so each elimination step's pivot broadcast, v_rcp_f64, Newton
+// step and lane mask serve both chains (tile_elim_pair).  The layout is entered and left by
+// v_permlane32_swap (16 32-bit swaps each way per tile pair); the TRSM and trailing update run per
+// chain in the MFMA layout, their two instruction streams independent (ILP), and the solves and fixed
+// block one chain after the other (interleaved they spill).  Both chains' 2 x 10 tiles fit 2 waves per
+// SIMD (k_sweep_pair: 254 VGPRs, 44 B of scratch outside the draw); measured in
+// tools/probe/pair_fact_probe.hip (r06j): the factorisation at 2 waves/SIMD 8,187 SIMD cycles per chain
+// against the one-chain kernel's 9,430 at its 3 waves/SIMD.
+#pragma once
+#include "gibbs_tile.h"
+
+namespace gpair {
+
+// exchange lanes 32..63 of a with lanes 0..31 of b (a double = two 32-bit swaps)
+__device__ __forceinline__ void swap32(double& a, double& b) {
+  const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
+  const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
+  auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+  auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+  a = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+  b = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+}
+
+// register of row k in the paired layout
+__host__ __device__ constexpr int ptk(int k) { return 2 * (k >> 2) + ((k >> 1) & 1); }
+
+}  // namespace gpair
+
+// tile_elim1's column elimination on two chains at once (paired layout): on return B * rsd is U^-1 of
+// each chain's tile and A its column-eliminated tile, both paired; rsd the lane's chain's pivot^-1/2
+// of column c.  Same operations per element as tile_elim1<KMAX, PR>.
+template <int KMAX, bool PR>
+__device__ __forceinline__ void tile_elim_pair(double (&A)[8], double (&B)[8], double& rsd, int lane) {
+  using namespace gtile;
+  using gpair::ptk;
+  if constexpr (PR && GS_DIAG_PRIO > 0) __builtin_amdgcn_s_setprio(GS_DIAG_PRIO);
+  const int h = (lane >> 4) & 1, c = lane & 15, base = lane & 32;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) B[t] = (4 * (t >> 1) + 2 * (t & 1) + h == c) ? 1.0 : 0.0;
+  double akc = bcast_lane_bp(A[ptk(0)], base + c);  // row 0 of the lane's chain
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    const int k1 = k >> 2;
+    double rn = 0.0;
+    if (k + 1 < KMAX) rn = bcast_lane_bp(A[ptk(k + 1)], base + 16 * ((k + 1) & 1) + c);
+    __builtin_amdgcn_sched_barrier(0);
+    const double akk = newbcast(akc, k);
+    if (k + 1 < KMAX) {
+#if GS_EXEC_MASK
+      const double akm = zero_cols_le(akc, k);
+#else
+      const double akm = (c > opq(k)) ? akc : 0.0;
+#endif
+      const double i0 = __builtin_amdgcn_rcp(akk);
+#if GS_PIV_NR2
+      const double n1 = i0 * fma(akk, i0, -2.0);
+      const double ng = (akm * n1) * fma(akk, n1, 2.0);
+#else
+      const double ng = (akm * i0) * fma(akk, i0, -2.0);
+#endif
+      akc = fmac_nb(rn, rn, ng, k);
+#pragma unroll
+      for (int t = 2 * k1; t < 8; ++t) A[t] = fmac_nb(A[t], A[t], ng, k);
+#pragma unroll
+      for (int t = 0; t <= 2 * k1 + 1; ++t) B[t] = fmac_nb(B[t], B[t], ng, k);
+    }
+  }
+  // A[ptk(c)] as a select tree on the bits of ptk(c) (a select chain on a lane-varying index is turned
+  // into a private-array load, i.e. scratch)
+  int pk = ptk(c);
+  asm volatile("" : "+v"(pk));
+  const bool b0 = pk & 1, b1 = pk & 2, b2 = pk & 4;
+  const double d01 = b0 ? A[1] : A[0], d23 = b0 ? A[3] : A[2], d45 = b0 ? A[5] : A[4], d67 = b0 ? A[7] : A[6];
+  const double d03 = b1 ? d23 : d01, d47 = b1 ? d67 : d45;
+  const double dg = b2 ? d47 : d03;
+  double piv = bcast_lane_bp(dg, base + 16 * (c & 1) + c);
+  if (KMAX < 16) piv = (c >= KMAX) ? 1.0 : piv;
+  rsd = rsq_nr(piv);
+  if constexpr (PR && GS_DIAG_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+}
+
+// Two systems' draws (chains a = 0, b = 1) on the tiled model block M: bdraw_tile_core<NT = 4,
+// CPC = 12 (NF = 60), LNL = 0, !WIDE, PR> for each, sharing the block's loads and the diagonal
+// eliminations.  scr[ch]: each chain's gs_tile_scr(60) doubles of the wave's LDS scratch; zmslot: 128
+// more (the chains' z_M, staged before the factorisation so they are not held in registers).  Returns each
+// chain's first failed pivot (0: the draw is valid) in fail[ch].
+template <bool PR>
+__device__ __forceinline__ void bdraw_tile_pair60(const ModelTiled& M, int NMX, int nM, int lane, const double (&phinv)[2],
+                                                  const double (&zF)[2], const double (&zM)[2], double (&bF)[2],
+                                                  double (&bM)[2], double* const (&scr)[2], double* zmslot,
+                                                  int (&fail)[2]) {
+  using namespace gtile;
+  constexpr int NT = 4, NF = 60, CP = 12, NTILE = NT * (NT + 1) / 2;
+  const int q = lane >> 4, c = lane & 15;
+  double* tb[2] = {scr[0], scr[1]};
+  double* vb[2] = {scr[0] + 272, scr[1] + 272};
+  double* ob[2] = {scr[0] + 336, scr[1] + 336};
+  double* zm[2] = {zmslot, zmslot + 64};  // z_M of each chain, read by the fixed block
+
+  lds_fence();
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch) {
+    vb[ch][lane] = phinv[ch];
+    ob[ch][lane] = (lane < NF) ? zF[ch] : 0.0;
+    zm[ch][lane] = (lane < nM) ? zM[ch] : 0.0;
+  }
+  lds_fence();
+  double phc[2][NT];
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+    for (int K = 0; K < NT; ++K) {
+      const int i = 16 * K + c;
+      phc[ch][K] = (i < NF) ? vb[ch][i] : 0.0;  // the tiled S' holds the padding's 1
+    }
+  lds_fence();
+
+  // ---- S tiles of both chains: one load of the shared block, phiinv_F on each chain's diagonal
+  int z0 = 0;
+  asm volatile("" : "+s"(z0));
+  gs_d4 t[2][NTILE];
+  {
+    const double* Sl = M.S + lane + z0;
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = I; J < NT; ++J) {
+        const int ti = tix(I, J, NT);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const double v = Sl[(4 * ti + s) * 64];
+#pragma unroll
+          for (int ch = 0; ch < 2; ++ch) {
+#if GS_EXEC_MASK
+            t[ch][ti][s] = (I == J) ? add_on_diag(v, phc[ch][I], s) : v;
+#else
+            t[ch][ti][s] = v + ((I == J && 4 * s + q == c) ? phc[ch][I] : 0.0);
+#endif
+          }
+        }
+      }
+  }
+
+  // ---- factorisation
+  double ylast[2] = {0.0, 0.0};
+  fail[0] = fail[1] = 0;
+#pragma unroll
+  for (int K = 0; K < NT; ++K) {
+    const int kk = tix(K, K, NT);
+    double PA[8], PB[8];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      PA[2 * s] = t[0][kk][s];
+      PA[2 * s + 1] = t[1][kk][s];
+      gpair::swap32(PA[2 * s], PA[2 * s + 1]);
+    }
+    double rsd;
+    if (K == NT - 1)
+      tile_elim_pair<CP, PR>(PA, PB, rsd, lane);
+    else
+      tile_elim_pair<16, PR>(PA, PB, rsd, lane);
+    if (K == NT - 1) {
+      // y_last[k] = (row CP of the eliminated tile)[k] * pivot_k^-1/2, k < CP, of the lane's chain,
+      // then to each chain's column layout (every row group)
+      const double yl = bcast_lane_bp(PA[gpair::ptk(CP)], (lane & 32) + 16 * (CP & 1) + c);
+      const double yp = (c < CP) ? yl * rsd : 0.0;
+      ylast[0] = bcast_lane_bp(yp, c);
+      ylast[1] = bcast_lane_bp(yp, 32 + c);
+    }
+    // first bad pivot of this tile, per chain (row h = 0 of each chain's lanes)
+    const unsigned long long badm = __ballot(!(rsd > 0.0 && rsd < __builtin_inf()));
+    const unsigned long long bada = badm & 0xffffull, badb = (badm >> 32) & 0xffffull;
+    if (!fail[0] && bada) fail[0] = 16 * K + __ffsll((long long)bada);
+    if (!fail[1] && badb) fail[1] = 16 * K + __ffsll((long long)badb);
+    // U_KK^-1 of both chains back to the MFMA layout
+    gs_d4 V[2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      double x = PB[2 * s] * rsd, y = PB[2 * s + 1] * rsd;
+      gpair::swap32(x, y);
+      V[0][s] = x;
+      V[1][s] = y;
+    }
+    if constexpr (PR && GS_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(GS_UPD_PRIO);
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      t[ch][kk] = V[ch];
+#pragma unroll
+      for (int J = K + 1; J < NT; ++J) {
+        const gs_d4 z = {0.0, 0.0, 0.0, 0.0};
+        t[ch][tix(K, J, NT)] = mfma_tn(z, V[ch], t[ch][tix(K, J, NT)]);
+      }
+    }
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) t[ch][kk] = transpose(V[ch], tb[ch], q, c);
+#pragma unroll
+    for (int I = K + 1; I < NT; ++I)
+#pragma unroll
+      for (int J = I; J < NT; ++J)
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch)
+          t[ch][tix(I, J, NT)] = mfma_tn_sub(t[ch][tix(I, J, NT)], t[ch][tix(K, I, NT)], t[ch][tix(K, J, NT)]);
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int J = K + 1; J < NT; ++J) t[ch][tix(K, J, NT)] = transpose(t[ch][tix(K, J, NT)], tb[ch], q, c);
+    if constexpr (PR && GS_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+  }
+
+  // ---- the solves and the fixed block, one chain after the other: chain a's tiles and solution rows
+  // are dead before chain b's solve needs its own (interleaving the two held ~250 VGPRs and spilled)
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch) {
+    // forward (augmented): y_K = column CP of U_K,last = row CP of the stored U_K,last^T
+    double ycol[NT];
+#pragma unroll
+    for (int K = 0; K + 1 < NT; ++K) ycol[K] = bcast_group_bp(t[ch][tix(K, NT - 1, NT)][CP >> 2], CP & 3, c);
+    ycol[NT - 1] = ylast[ch];
+
+    if constexpr (PR && GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_SOLVE_PRIO);
+    // backward: U x = y + zF
+    double xcol[NT];
+    gs_d4 xrow[NT];
+#pragma unroll
+    for (int K = NT - 1; K >= 0; --K) {
+      double p = 0.0;
+#pragma unroll
+      for (int J = K + 1; J < NT; ++J) {
+        const gs_d4 ut = t[ch][tix(K, J, NT)];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) p = fma(ut[s], xrow[J][s], p);
+      }
+      if (K + 1 < NT) p = qsum(p);
+      const gs_d4 sr = to_row(ycol[K] + ob[ch][16 * K + c] - p, vb[ch], q, c);
+      const gs_d4 W = t[ch][tix(K, K, NT)];
+      double p2 = 0.0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) p2 = fma(W[s], sr[s], p2);
+      xcol[K] = qsum(p2);
+      xrow[K] = to_row(xcol[K], vb[ch], q, c);
+    }
+    lds_fence();
+#pragma unroll
+    for (int K = 0; K < NT; ++K) ob[ch][16 * K + c] = xcol[K];
+    lds_fence();
+    bF[ch] = (lane < NF) ? ob[ch][lane] : 0.0;
+    lds_fence();
+    if constexpr (PR && GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+
+    if constexpr (PR && GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_FIX_PRIO);
+    // fixed-prior block x_M = h + R z_M - G x_F (tiled G' = -G and R', nM <= 16: one chunk); z_M was
+    // staged in the chain's zm slot before the factorisation
+    {
+      const int row = c;
+      const bool rok = row < nM;
+      double p = 0.0;
+      const double* Gl = M.G + lane + z0;
+#pragma unroll
+      for (int J = 0; J < NT; ++J)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) p = fma(Gl[(4 * J + s) * 64], xrow[J][s], p);
+      const double* Rl = M.R + lane + z0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) p = fma(Rl[s * 64], zm[ch][4 * s + q], p);
+      p = qsum(p);
+      const double xm = rok ? M.h[row + z0] + p : 0.0;
+      ob[ch][row] = xm;
+    }
+    lds_fence();
+    bM[ch] = (lane < nM) ? ob[ch][lane] : 0.0;
+    lds_fence();
+    if constexpr (PR && GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+  }
+}

@@ -434,6 +434,31 @@ def test_sweep_handoff_workgroups_equal_one_chain_per_wave(ctx, model, replay, C
     assert not out[0][-1].any()
 
 
+@pytest.mark.parametrize("C,S", [(2, 1), (38, 7), (64, 12)])
+def test_sweep_two_chains_per_wave_equal_one_chain_per_wave(ctx, model, replay, C, S):
+    """GS_OPT_SWEEP_SCHED = 3 (k_sweep_pair: two chains per wavefront, the diagonal-tile eliminations
+    of both in one paired register set, gibbs_tile2.h) gives bit for bit the chains of
+    GS_OPT_SWEEP_SCHED = 2: every recorded row, a continued second launch and the final state; a
+    partial last workgroup (38 chains = 4 full workgroups of 8 + 3 pairs)."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import FreeSpectrumChains
+    x0 = np.random.default_rng(6).uniform(-9, -5, (C, 30))
+    out = []
+    prev = ctx.get_option(_lib.OPT_SWEEP_SCHED)
+    try:
+        for sched in (2, 3):
+            ctx.set_option(_lib.OPT_SWEEP_SCHED, sched)
+            run = FreeSpectrumChains(model, replay["rhomin"], replay["rhomax"], C, x0)
+            xr, br = run.run(S)
+            xr2, br2 = run.run(S + 3)
+            out.append([t.cpu().numpy() for t in (xr, br, xr2, br2, run.x, run.b, run.info)])
+    finally:
+        ctx.set_option(_lib.OPT_SWEEP_SCHED, prev)
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    assert not out[1][-1].any()
+
+
 def test_sweep_handoff_timeout_fails_loudly(ctx, model, replay):
     """A hand-off that never arrives (GS_OPT_DEBUG_HANDOFF: workgroup 0's first trio does not
     publish its first third) must not be read: the extra chain (chain 12 of workgroup 0) ends with
