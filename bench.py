@@ -50,8 +50,9 @@ def executed_flops_per_chain_sweep(nf, nm):
 
 
 def pmc_traffic(S, C):
-    """HBM bytes per launch of k_sweep_freespec from the committed PMC profile
-    (tools/archive/gpu_profile.sh -> tools/pmc_traffic.py), valid for the same launch shape."""
+    """HBM bytes per launch of the headline's fused-sweep kernel from the committed PMC profile
+    (profiles/pmc_traffic.json: FETCH_SIZE / WRITE_SIZE passes, tools/gpu_r06m.sh), valid for the same
+    launch shape."""
     f = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(f))
@@ -162,6 +163,18 @@ def grid_peak():
 # 78.6 TF = 1024 SIMDs x 2.4 GHz x 16 FMA lanes per clock): a wave64 add/mul/fma/min/cmp (f64 or
 # f32) issues in 4 SIMD cycles, a transcendental (v_rcp / v_exp / v_log) in 8.
 SIMDS, CLOCK_HZ = 1024, 2.4e9
+
+
+SWEEP_SHAPES = {1: "k_sweep_freespec (12-wave hand-off workgroups)", 2: "k_sweep_freespec (one chain per wave)",
+                3: "k_sweep_pair (two chains per wave)"}
+
+
+def sweep_kernel(ctx, rm=False):
+    """Name of the fused-sweep kernel the context's last gs_sweep_freespec launch ran
+    (GS_OPT_LAST_SWEEP_SHAPE, chosen by the library's cost model unless --sched asks)."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    name = SWEEP_SHAPES.get(ctx.get_option(_lib.OPT_LAST_SWEEP_SHAPE), "k_sweep_freespec")
+    return name.replace("k_sweep_freespec", "k_sweep_freespec_rm") if rm else name
 
 
 def sq_counts():
@@ -478,6 +491,7 @@ def bench_indep(C, K, W, S, rank, world, dev, ess_on=True):
             launches.append((e0, e1, n))
             done += n
     el = timed_region(world, dev, go)
+    kname = sweep_kernel(ctx, rm=model.NMX > 16)     # the timed launches' shape (before the ESS run's)
     if run.info.cpu().numpy().any():
         raise RuntimeError("non-PD Sigma in the configs[2] bench")
     ms = np.array([a.elapsed_time(b) for a, b, _ in launches])
@@ -504,7 +518,7 @@ def bench_indep(C, K, W, S, rank, world, dev, ess_on=True):
                 sharding=(f"pulsars over {world} GPUs (no collective)" if world > 1 else "one GPU"),
                 pulsar_iters_per_s=C * K * len(ptas) / el,
                 ess_per_s=C * K / el * ess["per_chain_sweep_min_bin"] if ess else None, ess=ess,
-                roofline={"kernel": "k_sweep_freespec" + ("" if model.NMX <= 16 else "_rm"),
+                roofline={"kernel": kname,
                           "bound": "mfma", "unit": "TFLOP/s", "achieved": ach,
                           "peak": FP64_PEAK_TFLOPS, "frac": ach / FP64_PEAK_TFLOPS,
                           "kernel_avg_ms": per_sweep * S * 1e3, "sweeps_per_launch": S,
@@ -1047,6 +1061,7 @@ def main():
             e1.record(stream)
             evs.append((e0, e1))
     el = timed_region(world, dev, headline)
+    kname = sweep_kernel(ctx)                        # the timed launches' shape (before the ESS run's)
     info = run.info.cpu().numpy()
     if info.any():
         raise RuntimeError(f"{int((info != 0).sum())} chains hit a non-PD Sigma")
@@ -1125,7 +1140,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
                          "traffic": pmc_traffic(S, C),
-                         "kernel": "k_sweep_freespec", "kernel_avg_ms": launch_s * 1e3,
+                         "kernel": kname, "kernel_avg_ms": launch_s * 1e3,
                          "alg_flops_per_launch": alg_flops_launch,
                          "note": "achieved = SURVEY 8d's algorithmic flops (dense m=76 potrf + 3 solves); the kernel "
                                  "executes fewer (executed_*: NF=60 Schur block after the fixed-prior prefix)",

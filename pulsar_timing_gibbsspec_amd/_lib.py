@@ -26,6 +26,7 @@ OPT_BREC_CHAINS = 5
 OPT_PHI_PER_CHAIN = 6
 OPT_SWEEP_SCHED = 7
 OPT_DEBUG_HANDOFF = 8
+OPT_LAST_SWEEP_SHAPE = 9
 EV_B0, EV_RHO, EV_B, EV_RED, EV_CURN, EV_GUMBEL, EV_WHITE, EV_REDMH, EV_USER = 1, 2, 3, 4, 5, 6, 7, 8, 16
 EV_ECORR, EV_ECORR_B, EV_ECORR_B0, EV_HYPER = 9, 10, 11, 12
 

@@ -18,6 +18,7 @@ struct gs_ctx {
   int phi_per_chain = 0;  // GS_OPT_PHI_PER_CHAIN
   int sweep_sched = 0;    // GS_OPT_SWEEP_SCHED
   int dbg_handoff = 0;    // GS_OPT_DEBUG_HANDOFF
+  int last_shape = 0;     // GS_OPT_LAST_SWEEP_SHAPE (read only)
   const int64_t* sweep_dev = nullptr;  // gs_ctx_set_sweep_counter
   int32_t* fail_counts = nullptr;      // gs_ctx_set_fail_counts
   int32_t* grid_fallback = nullptr;    // gs_ctx_set_grid_fallback_counter
@@ -286,6 +287,8 @@ int gs_ctx_set_option(gs_ctx* ctx, int option, int value) {
       if (value != 0 && value != 1) return fail_arg(3, "GS_OPT_DEBUG_HANDOFF must be 0 or 1");
       ctx->dbg_handoff = value;
       return 0;
+    case GS_OPT_LAST_SWEEP_SHAPE:
+      return fail_arg(2, "GS_OPT_LAST_SWEEP_SHAPE is read only");
     default:
       return fail_arg(2, "unknown option");
   }
@@ -301,6 +304,7 @@ int gs_ctx_get_option(gs_ctx* ctx, int option) {
   if (option == GS_OPT_PHI_PER_CHAIN) return ctx->phi_per_chain;
   if (option == GS_OPT_SWEEP_SCHED) return ctx->sweep_sched;
   if (option == GS_OPT_DEBUG_HANDOFF) return ctx->dbg_handoff;
+  if (option == GS_OPT_LAST_SWEEP_SHAPE) return ctx->last_shape;
   return -1;
 }
 
@@ -586,7 +590,7 @@ int gs_sweep_freespec(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int 
   a.brec_nc = ctx->brec_nc < n_chain ? ctx->brec_nc : 0;
   a.sched = ctx->sweep_sched;
   a.dbg_handoff = ctx->dbg_handoff;
-  return launch_rc(launch_sweep_freespec(ctx->stream, a), "k_sweep_freespec");
+  return launch_rc(launch_sweep_freespec(ctx->stream, a, &ctx->last_shape), "k_sweep_freespec");
 }
 
 int gs_tau(gs_ctx* ctx, int n_psr, int n_chain, int NF, int ldb, const int32_t* fidx, const double* b,

@@ -1536,12 +1536,25 @@ static bool sweep_handoff_wins(const SweepArgs& a) {
   const double c12 = std::ceil(wg / ncu) * (4.0 / 3.0);
   return c12 < 0.97 * (k + g);
 }
-// GS_SWEEP_PAIR_AUTO: the cost model (GS_OPT_SWEEP_SCHED 0) picks the two-chains-per-wave kernel
-// wherever it applies
-#ifndef GS_SWEEP_PAIR_AUTO
-#define GS_SWEEP_PAIR_AUTO 0
-#endif
-int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
+// Two chains per wave (k_sweep_pair) against the one-chain shapes, in the same unit R.  Its waves run
+// 2 per SIMD: a full round (8 waves per CU, 16 chains) takes P = 1.27 R and a last round of at most one
+// wave per SIMD 0.70 P (r06l, 1 GPU: 4096 chains 1.965 ms = P, 8192 3.905 ms, 2048 and 1024 chains
+// 1.37-1.38 ms; R = 1.55 ms from the 4096-chain one-chain / hand-off times above).  4096 chains: 1.27 R
+// vs 1.33 R (hand-off); 8192: 2.54 R vs 2.67 R; 6144: 2.16 R vs 2 R; 2048: 0.89 R vs 0.74 R.
+static bool sweep_pair_wins(const SweepArgs& a) {
+  if (a.sched) return a.sched == 3;
+  const double ncu = device_cus();
+  const double q = (double)a.n_psr * a.n_chain / (4.0 * ncu);
+  const double k = std::floor(q / 3.0), r = q - 3.0 * k;
+  const double g = r <= 0.0 ? 0.0 : r <= 1.0 ? 0.46 * r : r <= 2.0 ? 0.46 + 0.28 * (r - 1.0) : 0.74 + 0.26 * (r - 2.0);
+  const double wg = (double)a.n_psr * ((a.n_chain + 15) / 16);
+  const double one = std::min(k + g, std::ceil(wg / ncu) * (4.0 / 3.0));
+  const double w = (double)a.n_psr * (a.n_chain / 2) / (4.0 * ncu);  // pair waves per SIMD
+  const double kp = std::floor(w / 2.0), rp = w - 2.0 * kp;
+  const double pair = 1.27 * (kp + (rp <= 0.0 ? 0.0 : rp <= 1.0 ? 0.70 : 1.0));
+  return pair < 0.97 * one;
+}
+int launch_sweep_freespec(hipStream_t s, const SweepArgs& a, int* shape) {
   const bool fixed = a.NF == 20 || a.NF == 40 || a.NF == 60;
   const bool tiled = GS_SWEEP_TILED && (!fixed || a.bcast == GS_BCAST_TILE);
   const size_t mlds = tiled ? (size_t)model_tiled_doubles(a.NF, a.NMX) : (size_t)a.mstride;
@@ -1549,13 +1562,14 @@ int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
   // Philox (no injected draws), an even chain count
   const bool pair_ok = a.NF == 60 && tiled && model_tiled_fix(a.NMX) && !a.z0_inj && !a.z_inj && !a.u_inj &&
                        (a.n_chain % 2) == 0 && !a.dbg_handoff;
-  if (pair_ok && (a.sched == 3 || (a.sched == 0 && GS_SWEEP_PAIR_AUTO))) {
+  if (pair_ok && sweep_pair_wins(a)) {
     constexpr int WPB = 4;
     const size_t lds = (mlds + (size_t)WPB * GS_PAIR_SCR) * sizeof(double);
     if (lds <= device_lds_optin()) {
       const int nb = (a.n_chain + 2 * WPB - 1) / (2 * WPB);
       if (lds > 65536 && set_lds(k_sweep_pair<WPB>, lds)) return 2;
       hipLaunchKernelGGL((k_sweep_pair<WPB>), dim3((unsigned)(a.n_psr * nb)), dim3(64 * WPB), lds, s, a);
+      *shape = 3;
       return 0;
     }
   }
@@ -1566,12 +1580,14 @@ int launch_sweep_freespec(hipStream_t s, const SweepArgs& a) {
   if (tiled && lds12 <= device_lds_optin() && sweep_handoff_wins(a)) {
     const int nb = (a.n_chain + 15) / 16;
     dim3 grid((unsigned)(a.n_psr * nb));
+    *shape = 1;
     return dispatch_nf_sweep<12>(a.NF, a.bcast, grid, lds12, s, a);
   }
   const int nb = (a.n_chain + GS_SWEEP_WPB - 1) / GS_SWEEP_WPB;
   dim3 grid((unsigned)(a.n_psr * nb));
   const size_t lds =
       (mlds + ((fixed ? GS_SCR_DOUBLES(a.bcast, a.NF) : gs_tile_scr(a.NF)) + 128) * GS_SWEEP_WPB) * sizeof(double);
+  *shape = 2;
   return dispatch_nf_sweep<GS_SWEEP_WPB>(a.NF, a.bcast, grid, lds, s, a);
 }
 

@@ -159,7 +159,8 @@ struct RhoArgs {
   gs_key key;
 };
 
-int launch_sweep_freespec(hipStream_t s, const SweepArgs& a);
+// *shape: the workgroup shape launched (GS_OPT_LAST_SWEEP_SHAPE: 1 hand-off, 2 one chain per wave, 3 two)
+int launch_sweep_freespec(hipStream_t s, const SweepArgs& a, int* shape);
 int launch_bdraw(hipStream_t s, const BdrawArgs& a);
 int launch_bdraw_tiled(hipStream_t s, const BdrawArgs& a);
 int launch_model_tile(hipStream_t s, const double* model, int n_psr, int NF, int NMX, const int32_t* nm,

@@ -174,16 +174,21 @@ def test_bdraw_flags_non_positive_definite(model):
     assert cnt.cpu().tolist() == [0, 1, 0]
 
 
-def test_fused_sweep_non_pd_mid_run_keeps_b(ctx, model, replay):
-    """k_sweep_freespec with Sigma made indefinite mid-run (the model block's S0[0][0] set to
-    -1e300 after 10 sweeps): the failing draws keep each chain's previous b (never NaN), the
-    rho|b step goes on, every failure is counted as it happens, and once the model is restored
-    the chains draw again."""
+@pytest.mark.parametrize("sched", [2, 3])
+def test_fused_sweep_non_pd_mid_run_keeps_b(ctx, model, replay, sched):
+    """k_sweep_freespec (sched 2) and k_sweep_pair (sched 3) with Sigma made indefinite mid-run (the
+    model block's S0[0][0] set to -1e300 after 10 sweeps): the failing draws keep each chain's
+    previous b (never NaN), the rho|b step goes on, every failure is counted as it happens, and once
+    the model is restored the chains draw again."""
+    from pulsar_timing_gibbsspec_amd import _lib
     from pulsar_timing_gibbsspec_amd.engine import FreeSpectrumChains
     g = golden("single_j1713.npz")
     C = 4
+    prev = ctx.get_option(_lib.OPT_SWEEP_SCHED)
+    ctx.set_option(_lib.OPT_SWEEP_SCHED, sched)
     run = FreeSpectrumChains(model, replay["rhomin"], replay["rhomax"], C, g["x0"])
     run.run(10)
+    assert ctx.get_option(_lib.OPT_LAST_SWEEP_SHAPE) == sched
     b10 = run.b.clone()
     saved = model.model.clone()
     try:
@@ -196,7 +201,10 @@ def test_fused_sweep_non_pd_mid_run_keeps_b(ctx, model, replay):
         assert run.fail_count.cpu().tolist() == [5] * C
     finally:
         model.model.copy_(saved)
+        ctx.set_option(_lib.OPT_SWEEP_SCHED, prev)
+    ctx.set_option(_lib.OPT_SWEEP_SCHED, sched)
     run.run(5)
+    ctx.set_option(_lib.OPT_SWEEP_SCHED, prev)
     assert run.fail_count.cpu().tolist() == [5] * C
     assert torch.isfinite(run.b).all() and not torch.equal(run.b, b10)
 
@@ -443,7 +451,7 @@ def test_sweep_two_chains_per_wave_equal_one_chain_per_wave(ctx, model, replay, 
     from pulsar_timing_gibbsspec_amd import _lib
     from pulsar_timing_gibbsspec_amd.engine import FreeSpectrumChains
     x0 = np.random.default_rng(6).uniform(-9, -5, (C, 30))
-    out = []
+    out, shapes = [], []
     prev = ctx.get_option(_lib.OPT_SWEEP_SCHED)
     try:
         for sched in (2, 3):
@@ -451,12 +459,34 @@ def test_sweep_two_chains_per_wave_equal_one_chain_per_wave(ctx, model, replay, 
             run = FreeSpectrumChains(model, replay["rhomin"], replay["rhomax"], C, x0)
             xr, br = run.run(S)
             xr2, br2 = run.run(S + 3)
+            shapes.append(ctx.get_option(_lib.OPT_LAST_SWEEP_SHAPE))
             out.append([t.cpu().numpy() for t in (xr, br, xr2, br2, run.x, run.b, run.info)])
     finally:
         ctx.set_option(_lib.OPT_SWEEP_SCHED, prev)
+    assert shapes == [2, 3]                      # the kernels that ran: one chain per wave, two
     for a, b in zip(*out):
         assert np.array_equal(a, b)
     assert not out[1][-1].any()
+
+
+def test_sweep_cost_model_shapes(ctx, model, replay):
+    """GS_OPT_SWEEP_SCHED = 0: the cost model runs two chains per wave where that kernel fills its
+    2 waves/SIMD (the headline's 4096 chains on a 256-CU MI355X) and the one-chain shapes where it
+    would leave SIMDs with one wave (2048 chains) or needs an even chain count (4095); setting the
+    read-only GS_OPT_LAST_SWEEP_SHAPE fails."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    from pulsar_timing_gibbsspec_amd.engine import FreeSpectrumChains
+    assert ctx.get_option(_lib.OPT_SWEEP_SCHED) == 0
+    got = {}
+    for C in (4096, 2048, 4095):
+        x0 = np.random.default_rng(C).uniform(-9, -5, (C, 30))
+        FreeSpectrumChains(model, replay["rhomin"], replay["rhomax"], C, x0).run(1)
+        got[C] = ctx.get_option(_lib.OPT_LAST_SWEEP_SHAPE)
+    if torch.cuda.get_device_properties(0).multi_processor_count == 256:
+        assert got[4096] == 3
+    assert got[2048] != 3 and got[4095] != 3
+    with pytest.raises(RuntimeError):
+        ctx.set_option(_lib.OPT_LAST_SWEEP_SHAPE, 1)
 
 
 def test_sweep_handoff_timeout_fails_loudly(ctx, model, replay):
