@@ -1139,6 +1139,10 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(BC, NFC, NTC)) void k_sweep_frees
 // exactly where the one-chain kernel skips it, and a failed factorisation keeps that chain's b.
 // 2 waves per SIMD (both chains' tiles: ~200 VGPRs): 4096 chains are 2048 waves, one round.
 constexpr int GS_PAIR_SCR = 2 * gs_tile_scr(60) + 256 + 128 + 128;
+// GS_PAIR_WPB: waves (chain pairs) per workgroup
+#ifndef GS_PAIR_WPB
+#define GS_PAIR_WPB 4
+#endif
 // GS_PAIR_RHO_MERGE: both chains' rho steps in one pass over the wave (30 frequencies each)
 #ifndef GS_PAIR_RHO_MERGE
 #define GS_PAIR_RHO_MERGE 1
@@ -1318,7 +1322,12 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_sweep_pair(SweepArgs A) {
       double zF[2], zM[2];
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch) {
+#ifdef GS_PROBE_NO_NORMALS  // cost attribution only (wrong draws): no Philox + Box-Muller pass
+        zF[ch] = __builtin_amdgcn_fract(x[ch] * 7.0) - 0.5;
+        zM[ch] = __builtin_amdgcn_fract(x[ch] * 3.0) - 0.5;
+#else
         gs_normal2(gs_counter(lane, ii, gchain[ch], p + A.psr_base, ev), A.key, zF[ch], zM[ch]);
+#endif
         if (pass == 0) phinv[ch] = act ? 1.0 / pow(10.0, 2.0 * x[ch]) : 0.0;  // first draw from xs
         // the previous b waits in the wave's save slot (a failed or shut draw keeps it)
         bsave[128 * ch + lane] = bF[ch];
@@ -1563,7 +1572,7 @@ int launch_sweep_freespec(hipStream_t s, const SweepArgs& a, int* shape) {
   const bool pair_ok = a.NF == 60 && tiled && model_tiled_fix(a.NMX) && !a.z0_inj && !a.z_inj && !a.u_inj &&
                        (a.n_chain % 2) == 0 && !a.dbg_handoff;
   if (pair_ok && sweep_pair_wins(a)) {
-    constexpr int WPB = 4;
+    constexpr int WPB = GS_PAIR_WPB;
     const size_t lds = (mlds + (size_t)WPB * GS_PAIR_SCR) * sizeof(double);
     if (lds <= device_lds_optin()) {
       const int nb = (a.n_chain + 2 * WPB - 1) / (2 * WPB);

@@ -33,6 +33,25 @@ __host__ __device__ constexpr int ptk(int k) { return 2 * (k >> 2) + ((k >> 1) &
 
 }  // namespace gpair
 
+// GS_PAIR_SOLVE_ILV: both chains' solves and fixed blocks interleaved (1) or one after the other (0)
+#ifndef GS_PAIR_SOLVE_ILV
+#define GS_PAIR_SOLVE_ILV 1
+#endif
+
+// gtile::to_row of two chains' column vectors through their own LDS rows, one round trip for both
+__device__ __forceinline__ void to_row2(const double (&v)[2], double* const (&vb)[2], gs_d4 (&o)[2], int q, int c) {
+  gtile::lds_fence();
+  vb[0][c] = v[0];
+  vb[1][c] = v[1];
+  gtile::lds_fence();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    o[0][s] = vb[0][4 * s + q];
+    o[1][s] = vb[1][4 * s + q];
+  }
+  gtile::lds_fence();
+}
+
 // tile_elim1's column elimination on two chains at once (paired layout): on return B * rsd is U^-1 of
 // each chain's tile and A its column-eliminated tile, both paired; rsd the lane's chain's pivot^-1/2
 // of column c.  Same operations per element as tile_elim1<KMAX, PR>.
@@ -214,6 +233,98 @@ __device__ __forceinline__ void bdraw_tile_pair60(const ModelTiled& M, int NMX, 
     if constexpr (PR && GS_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
   }
 
+#if GS_PAIR_SOLVE_ILV
+  // ---- the solves and the fixed block of both chains interleaved step by step (each chain's
+  // operations in the one-chain order); the LDS round trips of the row transposes and the fixed
+  // block's G / R loads are shared
+  {
+    double ycol[2][NT];
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+#pragma unroll
+      for (int K = 0; K + 1 < NT; ++K) ycol[ch][K] = bcast_group_bp(t[ch][tix(K, NT - 1, NT)][CP >> 2], CP & 3, c);
+      ycol[ch][NT - 1] = ylast[ch];
+    }
+    if constexpr (PR && GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_SOLVE_PRIO);
+    double xcol[2][NT];
+    gs_d4 xrow[2][NT];
+#pragma unroll
+    for (int K = NT - 1; K >= 0; --K) {
+      double v[2];
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch) {
+        double p = 0.0;
+#pragma unroll
+        for (int J = K + 1; J < NT; ++J) {
+          const gs_d4 ut = t[ch][tix(K, J, NT)];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) p = fma(ut[s], xrow[ch][J][s], p);
+        }
+        if (K + 1 < NT) p = qsum(p);
+        v[ch] = ycol[ch][K] + ob[ch][16 * K + c] - p;
+      }
+      gs_d4 sr[2];
+      to_row2(v, vb, sr, q, c);
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch) {
+        const gs_d4 W = t[ch][tix(K, K, NT)];
+        double p2 = 0.0;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) p2 = fma(W[s], sr[ch][s], p2);
+        xcol[ch][K] = qsum(p2);
+      }
+      const double xv[2] = {xcol[0][K], xcol[1][K]};
+      gs_d4 xr[2];
+      to_row2(xv, vb, xr, q, c);
+      xrow[0][K] = xr[0];
+      xrow[1][K] = xr[1];
+    }
+    lds_fence();
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int K = 0; K < NT; ++K) ob[ch][16 * K + c] = xcol[ch][K];
+    lds_fence();
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) bF[ch] = (lane < NF) ? ob[ch][lane] : 0.0;
+    lds_fence();
+    if constexpr (PR && GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+
+    if constexpr (PR && GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_FIX_PRIO);
+    // fixed-prior block x_M = h + R z_M - G x_F (tiled G' = -G and R', nM <= 16: one chunk); z_M was
+    // staged in the chains' zm slots before the factorisation
+    const int row = c;
+    const bool rok = row < nM;
+    double p[2] = {0.0, 0.0};
+    const double* Gl = M.G + lane + z0;
+#pragma unroll
+    for (int J = 0; J < NT; ++J)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const double g = Gl[(4 * J + s) * 64];
+        p[0] = fma(g, xrow[0][J][s], p[0]);
+        p[1] = fma(g, xrow[1][J][s], p[1]);
+      }
+    const double* Rl = M.R + lane + z0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const double r = Rl[s * 64];
+      p[0] = fma(r, zm[0][4 * s + q], p[0]);
+      p[1] = fma(r, zm[1][4 * s + q], p[1]);
+    }
+    const double hr = M.h[row + z0];
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      const double pp = qsum(p[ch]);
+      ob[ch][row] = rok ? hr + pp : 0.0;
+    }
+    lds_fence();
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) bM[ch] = (lane < nM) ? ob[ch][lane] : 0.0;
+    lds_fence();
+    if constexpr (PR && GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+  }
+#else
   // ---- the solves and the fixed block, one chain after the other: chain a's tiles and solution rows
   // are dead before chain b's solve needs its own (interleaving the two held ~250 VGPRs and spilled)
 #pragma unroll
@@ -278,4 +389,5 @@ __device__ __forceinline__ void bdraw_tile_pair60(const ModelTiled& M, int NMX, 
     lds_fence();
     if constexpr (PR && GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
   }
+#endif
 }
