@@ -33,10 +33,33 @@ __host__ __device__ constexpr int ptk(int k) { return 2 * (k >> 2) + ((k >> 1) &
 
 }  // namespace gpair
 
+// GS_PAIR_T2: both chains' tile transposes in one LDS round trip (1) or one after the other (0).
+// Measured (r06o, headline): 2.004-2.012 ms per launch against 1.953-1.962 -- the paired form holds
+// both chains' tiles live across the round trip (20 VGPRs spilled instead of 10)
+#ifndef GS_PAIR_T2
+#define GS_PAIR_T2 0
+#endif
 // GS_PAIR_SOLVE_ILV: both chains' solves and fixed blocks interleaved (1) or one after the other (0)
 #ifndef GS_PAIR_SOLVE_ILV
 #define GS_PAIR_SOLVE_ILV 1
 #endif
+
+// gtile::transpose of two chains' tiles through their own LDS staging tiles, one round trip for both
+__device__ __forceinline__ void transpose2(gs_d4& t0, gs_d4& t1, double* const (&tb)[2], int q, int c) {
+  gtile::lds_fence();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    tb[0][(4 * s + q) * 17 + c] = t0[s];
+    tb[1][(4 * s + q) * 17 + c] = t1[s];
+  }
+  gtile::lds_fence();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    t0[s] = tb[0][c * 17 + 4 * s + q];
+    t1[s] = tb[1][c * 17 + 4 * s + q];
+  }
+  gtile::lds_fence();
+}
 
 // gtile::to_row of two chains' column vectors through their own LDS rows, one round trip for both
 __device__ __forceinline__ void to_row2(const double (&v)[2], double* const (&vb)[2], gs_d4 (&o)[2], int q, int c) {
@@ -217,8 +240,14 @@ __device__ __forceinline__ void bdraw_tile_pair60(const ModelTiled& M, int NMX, 
         t[ch][tix(K, J, NT)] = mfma_tn(z, V[ch], t[ch][tix(K, J, NT)]);
       }
     }
+#if GS_PAIR_T2
+    t[0][kk] = V[0];
+    t[1][kk] = V[1];
+    transpose2(t[0][kk], t[1][kk], tb, q, c);
+#else
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) t[ch][kk] = transpose(V[ch], tb[ch], q, c);
+#endif
 #pragma unroll
     for (int I = K + 1; I < NT; ++I)
 #pragma unroll
@@ -226,10 +255,15 @@ __device__ __forceinline__ void bdraw_tile_pair60(const ModelTiled& M, int NMX, 
 #pragma unroll
         for (int ch = 0; ch < 2; ++ch)
           t[ch][tix(I, J, NT)] = mfma_tn_sub(t[ch][tix(I, J, NT)], t[ch][tix(K, I, NT)], t[ch][tix(K, J, NT)]);
+#if GS_PAIR_T2
+#pragma unroll
+    for (int J = K + 1; J < NT; ++J) transpose2(t[0][tix(K, J, NT)], t[1][tix(K, J, NT)], tb, q, c);
+#else
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
       for (int J = K + 1; J < NT; ++J) t[ch][tix(K, J, NT)] = transpose(t[ch][tix(K, J, NT)], tb[ch], q, c);
+#endif
     if constexpr (PR && GS_UPD_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
   }
 
