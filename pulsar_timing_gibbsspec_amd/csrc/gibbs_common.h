@@ -55,6 +55,12 @@ struct gs_u4 {
   uint32_t x, y, z, w;
 };
 
+// GS_PHILOX_MAD: each round's products as one v_mad_u64_u32 (both halves) instead of v_mul_lo_u32 +
+// v_mul_hi_u32.  Measured on the headline (r06q): 1.924-1.938 ms per launch against 1.919-1.930 with
+// the two multiplies -- not faster, off
+#ifndef GS_PHILOX_MAD
+#define GS_PHILOX_MAD 0
+#endif
 __device__ __forceinline__ gs_u4 philox4x32_10(gs_u4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -62,8 +68,15 @@ __device__ __forceinline__ gs_u4 philox4x32_10(gs_u4 c, uint32_t k0, uint32_t k1
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
     }
+#if GS_PHILOX_MAD
+    // one v_mad_u64_u32 per product (both halves) instead of v_mul_lo_u32 + v_mul_hi_u32
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
+#else
     const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
     const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+#endif
     gs_u4 n;
     n.x = hi1 ^ c.y ^ k0;
     n.y = lo1;

@@ -9,8 +9,8 @@
 // step and lane mask serve both chains (tile_elim_pair).  The layout is entered and left by
 // v_permlane32_swap (16 32-bit swaps each way per tile pair); the TRSM and trailing update run per
 // chain in the MFMA layout, their two instruction streams independent (ILP), and the solves and fixed
-// block one chain after the other (interleaved they spill).  Both chains' 2 x 10 tiles fit 2 waves per
-// SIMD (k_sweep_pair: 254 VGPRs, 44 B of scratch outside the draw); measured in
+// block of both chains interleaved step by step (shared LDS round trips and G / R loads).  Both chains'
+// 2 x 10 tiles fit 2 waves per SIMD (k_sweep_pair: 256 VGPRs, ~10 spilled outside the draw); measured in
 // tools/probe/pair_fact_probe.hip (r06j): the factorisation at 2 waves/SIMD 8,187 SIMD cycles per chain
 // against the one-chain kernel's 9,430 at its 3 waves/SIMD.
 #pragma once
@@ -33,6 +33,11 @@ __host__ __device__ constexpr int ptk(int k) { return 2 * (k >> 2) + ((k >> 1) &
 
 }  // namespace gpair
 
+// GS_PAIR_SKIP: the paired elimination updates only the registers holding rows it needs (one fmac
+// fewer per step than the row-group granularity of tile_elim1)
+#ifndef GS_PAIR_SKIP
+#define GS_PAIR_SKIP 1
+#endif
 // GS_PAIR_T2: both chains' tile transposes in one LDS round trip (1) or one after the other (0).
 // Measured (r06o, headline): 2.004-2.012 ms per launch against 1.953-1.962 -- the paired form holds
 // both chains' tiles live across the round trip (20 VGPRs spilled instead of 10)
@@ -108,10 +113,14 @@ __device__ __forceinline__ void tile_elim_pair(double (&A)[8], double (&B)[8], d
       const double ng = (akm * i0) * fma(akk, i0, -2.0);
 #endif
       akc = fmac_nb(rn, rn, ng, k);
+      // registers holding a row >= k of A and <= k of B: from / up to ptk(k).  tile_elim1 also
+      // updates the register's other rows of the row group (rows < k of A: eliminated rows nothing
+      // reads again; rows > k of B: still identity rows, whose update adds ng x 0 = +-0 and leaves
+      // them unchanged for a finite ng), so every value read afterwards is the same
 #pragma unroll
-      for (int t = 2 * k1; t < 8; ++t) A[t] = fmac_nb(A[t], A[t], ng, k);
+      for (int t = GS_PAIR_SKIP ? ptk(k) : 2 * k1; t < 8; ++t) A[t] = fmac_nb(A[t], A[t], ng, k);
 #pragma unroll
-      for (int t = 0; t <= 2 * k1 + 1; ++t) B[t] = fmac_nb(B[t], B[t], ng, k);
+      for (int t = 0; t <= (GS_PAIR_SKIP ? ptk(k) : 2 * k1 + 1); ++t) B[t] = fmac_nb(B[t], B[t], ng, k);
     }
   }
   // A[ptk(c)] as a select tree on the bits of ptk(c) (a select chain on a lane-varying index is turned
