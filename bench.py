@@ -326,6 +326,7 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess=True):
     lib, h, m = ctx.lib, ctx.handle, eng.model
     st = ctx.stream
     ms_b = event_ms(st, lambda: eng._bdraw(None, _lib.EV_B, None), 5)
+    b_shape = ctx.get_option(_lib.OPT_LAST_SWEEP_SHAPE)      # the tiled draw's kernel (cost model)
     mm = m.m.astype(float)
     bflop = C * float(np.sum(mm ** 3 / 3 + mm ** 2 / 2 + mm / 6 + 3 * mm ** 2))
     kernels = {"k_bdraw": dict(kernel_avg_ms=ms_b, bound="mfma", unit="TFLOP/s", peak=FP64_PEAK_TFLOPS,
@@ -334,7 +335,8 @@ def bench_pta(kind, C, K, W, rank, world, dev, ctx, shard="chain", ess=True):
                                                                 "curn_red": "pmc_traffic_red_bdraw.json",
                                                                 "curn_plred": "pmc_traffic_plred_bdraw.json"}[kind])
                                if kind in ("curn", "curn_red", "curn_plred") else None,
-                               name="k_bdraw_tiled" if m.model_tiled is not None else "k_bdraw",
+                               name=("k_bdraw_pair (two chains per wave)" if b_shape == 3 else "k_bdraw_tiled")
+                               if m.model_tiled is not None else "k_bdraw",
                                note="b|rho of every (pulsar, chain) system: sum_p m^3/3 + m^2/2 + m/6 + 3 m^2 "
                                     "flop per chain (SURVEY 8d)")}
     gp = grid_peak()

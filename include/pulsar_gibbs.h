@@ -91,8 +91,10 @@ enum {
                          3072 wave slots of 3 waves/SIMD in one round); 2 = 4-wave workgroups,
                          one chain per wave; 3 = two chains per wave (NF = 60 tile variant with
                          device Philox, even chain counts; else as 0), both chains' draws sharing
-                         the diagonal-tile eliminations at 2 waves/SIMD.  The 12-wave shape is
-                         used only when its LDS (model
+                         the diagonal-tile eliminations at 2 waves/SIMD.  gs_bdraw_tiled
+                         follows it too (3: two chains per wave where NF = 60, no lnL output is
+                         attached and the chain count is even; otherwise one chain per wave).
+                         The 12-wave shape is used only when its LDS (model
                          block + 12 waves' scratch, save, park and hand-off slots) fits the
                          device's per-workgroup limit; otherwise the 4-wave shape runs.  A
                          hand-off that does not arrive within the bounded wait (or arrives from a
@@ -102,8 +104,8 @@ enum {
                          hand-off (and the wait is shortened), so the 13th chain of workgroup 0
                          must end with info = -1 */
   GS_OPT_LAST_SWEEP_SHAPE = 9 /* read only (gs_ctx_get_option): the workgroup shape the context's
-                         last gs_sweep_freespec launch ran -- 1 = 12-wave hand-off, 2 = one chain
-                         per wave, 3 = two chains per wave, 0 = none yet */
+                         last gs_sweep_freespec or gs_bdraw_tiled launch ran -- 1 = 12-wave
+                         hand-off, 2 = one chain per wave, 3 = two chains per wave, 0 = none yet */
 };
 
 typedef struct gs_ctx gs_ctx;

@@ -513,7 +513,8 @@ int gs_bdraw_tiled(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb
   a.model_per_sys = 0;
   a.mask_per_sys = ctx->x_per_sys;
   a.phi_per_chain = ctx->phi_per_chain;
-  return launch_rc(launch_bdraw_tiled(ctx->stream, a), "k_bdraw_tiled");
+  a.sched = ctx->sweep_sched;
+  return launch_rc(launch_bdraw_tiled(ctx->stream, a, &ctx->last_shape), "k_bdraw_tiled");
 }
 
 int gs_bdraw_sys(gs_ctx* ctx, int n_psr, int n_chain, int NF, int NMX, int ldb, const double* model,

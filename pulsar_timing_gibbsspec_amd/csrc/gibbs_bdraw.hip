@@ -561,6 +561,93 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
   }
 }
 
+// ------------------------------------------------------------ b draws, two chains per wave
+// gs_bdraw_tiled at NF = 60 without the lnL output (GS_OPT_SWEEP_SCHED = 3, or the cost model where the
+// pairs fill 2 waves per SIMD): each wave draws chains c, c + 1 of one pulsar together
+// (gibbs_tile2.h bdraw_tile_pair60: both chains' diagonal eliminations in one paired register set),
+// bit-identical to bdraw_item's draws -- same normals (counters per chain), same tile core per chain; a
+// shut chain (chain_mask) has its draw discarded and nothing written, as bdraw_item skips it.  Pulsars
+// whose fixed block is row-major (nM > 16) run bdraw_item for each chain in turn.  Persistent ranges
+// of (pulsar, group of 2 WPB chains) items as k_bdraw_tiled; n_chain is even.
+constexpr int GS_BPAIR_SCR = 2 * gs_tile_scr(60) + 128;  // per wave: the chains' scratches + z_M slots
+
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_pair(BdrawArgs A) {
+  extern __shared__ double lds[];
+  constexpr int NF = 60, CPB = 2 * WPB;
+  const int wave = gs_wave_id(), lane = threadIdx.x & 63;
+  const int nb = (A.n_chain + CPB - 1) / CPB;
+  double* wl = lds + A.mstride + (int64_t)wave * GS_BPAIR_SCR;
+  double* const scr[2] = {wl, wl + gs_tile_scr(60)};
+  double* zmslot = wl + 2 * gs_tile_scr(60);
+  const int64_t n_items = (int64_t)A.n_psr * nb;
+  const int64_t G = A.persist ? A.persist : (int64_t)gridDim.x;
+  const int64_t lo = A.persist ? blockIdx.x * n_items / G : blockIdx.x;
+  const int64_t hi = A.persist ? (blockIdx.x + 1) * n_items / G : lo + 1;
+  int cur = -1, nM = 0, fi = 0, mi = 0, NMXe = A.NMX;
+  ModelTiled M;
+#pragma unroll 1
+  for (int64_t it = lo; it < hi; ++it) {
+    const int p = (int)(it / nb), grp = (int)(it % nb);
+    if (p != cur) {  // uniform over the workgroup
+      if (cur >= 0) __syncthreads();
+      stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
+      cur = p;
+      nM = __builtin_amdgcn_readfirstlane(A.nm[p]);
+      fi = lane < NF ? A.fidx[p * NF + lane] : 0;
+      mi = lane < nM ? A.midx[p * A.NMX + lane] : 0;
+      M = model_tiled_view_psr<false>(lds, NF, A.NMX, nM, NMXe);
+    }
+    const int c0 = grp * CPB + 2 * wave;
+    if (c0 >= A.n_chain) continue;
+    if (!M.fixt) {  // row-major fixed block (nM > 16): one chain at a time
+      bdraw_item<60, 0, GS_BCAST_TILE, false>(A, M, p, c0, NF, nM, fi, mi, scr[0], lane, NMXe);
+      bdraw_item<60, 0, GS_BCAST_TILE, false>(A, M, p, c0 + 1, NF, nM, fi, mi, scr[0], lane, NMXe);
+      continue;
+    }
+    const int64_t sys0 = (int64_t)p * A.n_chain + c0;
+    bool shut[2];
+    double phinv[2], zF[2], zM[2];
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      const int64_t sys = sys0 + ch;
+      const int c = c0 + ch;
+      shut[ch] = A.chain_mask && A.chain_mask[A.mask_per_sys ? sys : (int64_t)c] == 0;
+    }
+    if (shut[0] && shut[1]) continue;
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      const int64_t sys = sys0 + ch;
+      const int c = c0 + ch;
+      // a shut chain draws on a unit prior (its draw is discarded): no read of its phiinv row
+      phinv[ch] = shut[ch] ? (lane < NF ? 1.0 : 0.0)
+                           : (lane < NF ? A.phiinv_F[(A.phi_per_chain ? (int64_t)c : sys) * NF + lane] : 0.0);
+      if (A.z) {
+        zF[ch] = lane < NF ? A.z[sys * A.ldb + fi] : 0.0;
+        zM[ch] = lane < nM ? A.z[sys * A.ldb + mi] : 0.0;
+      } else {
+        gs_normal2(gs_counter(lane, gs_sweep(A.sweep, A.sweep_dev), A.chain_base + c, p + A.psr_base, A.event), A.key,
+                   zF[ch], zM[ch]);
+      }
+    }
+    double bF[2], bM[2];
+    int f[2];
+    bdraw_tile_pair60<GS_BDRAW_PR>(M, NMXe, nM, lane, phinv, zF, zM, bF, bM, scr, zmslot, f);
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      if (shut[ch]) continue;
+      const int64_t sys = sys0 + ch;
+      if (!f[ch]) {  // non-PD Sigma: the previous b stays (wave-uniform)
+        if (lane < NF) A.b[sys * A.ldb + fi] = bF[ch];
+        if (lane < nM) A.b[sys * A.ldb + mi] = bM[ch];
+      } else if (A.fail_count && lane == 0) {
+        A.fail_count[sys] += 1;
+      }
+      if (A.info && lane == 0) A.info[sys] = f[ch];
+    }
+  }
+}
+
 // ------------------------------------------------------------ marginalised likelihood
 //  get_lnlikelihood_fullmarg pulsar_gibbs.py:569-610, phiinv-dependent part:
 //   lnl = 1/2 (d^T Sigma^-1 d - log det Sigma) + 1/2 sum_F log phiinv_F
@@ -1634,9 +1721,43 @@ int launch_model_tile(hipStream_t s, const double* model, int n_psr, int NF, int
   return 0;
 }
 
-int launch_bdraw_tiled(hipStream_t s, const BdrawArgs& a0) {
+// k_bdraw_pair where it applies (NF = 60, no lnL output, an even chain count) and its waves fill 2 per
+// SIMD (n_psr x n_chain / 2 >= 8 waves per CU), or where GS_OPT_SWEEP_SCHED = 3 asks; 2 forces the
+// one-chain kernel
+// GS_BDRAW_PAIR (off): the cost model picks k_bdraw_pair where its pairs fill 2 waves per SIMD.
+// Measured (r06s, curn engine, every chain drawing): 0.430 vs 0.4375-0.468 ms per launch on 3 pulsars
+// x 30720 chains (all nM <= 16), but 0.554 vs 0.444-0.473 ms on the 45-pulsar array, whose two nM = 17
+// pulsars draw one chain at a time inside the pair kernel and leave the persistent ranges that cover
+// them ~1.3x longer than the rest.  GS_OPT_SWEEP_SCHED = 3 runs it (bit-identical).
+#ifndef GS_BDRAW_PAIR
+#define GS_BDRAW_PAIR 0
+#endif
+static bool bdraw_pair_wins(const BdrawArgs& a) {
+  if (a.NF != 60 || a.lnl || (a.n_chain & 1) || a.model_per_sys) return false;
+  if (a.sched == 3) return true;
+  if (a.sched || !GS_BDRAW_PAIR) return false;
+  return (double)a.n_psr * (a.n_chain / 2) >= 8.0 * device_cus();
+}
+int launch_bdraw_tiled(hipStream_t s, const BdrawArgs& a0, int* shape) {
   constexpr int WPB = GS_BDRAW_WPB;
   BdrawArgs a = a0;
+  if (bdraw_pair_wins(a)) {
+    constexpr int PW = GS_PAIR_WPB;
+    const size_t lds = ((size_t)a.mstride + (size_t)PW * GS_BPAIR_SCR) * sizeof(double);
+    if (lds <= device_lds_optin()) {
+      auto kern = k_bdraw_pair<PW>;
+      if (lds > 65536 && set_lds(kern, lds)) return 2;
+      const int64_t items = (int64_t)a.n_psr * ((a.n_chain + 2 * PW - 1) / (2 * PW));
+      int per_cu = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * PW, lds) == hipSuccess && per_cu > 0 &&
+          items > (int64_t)per_cu * device_cus())
+        a.persist = per_cu * device_cus();
+      hipLaunchKernelGGL(kern, dim3((unsigned)(a.persist ? a.persist : items)), dim3(64 * PW), lds, s, a);
+      *shape = 3;
+      return 0;
+    }
+  }
+  *shape = 2;
   const int nb = (a.n_chain + WPB - 1) / WPB;
   const int64_t nwg = (int64_t)a.n_psr * ((nb + GS_BDRAW_LOOP - 1) / GS_BDRAW_LOOP);
   const size_t lds = ((size_t)a.mstride + (size_t)gs_tile_scr(a.NF) * WPB) * sizeof(double);

@@ -129,6 +129,7 @@ struct BdrawArgs {
   const double* lnl_model;  // ... with the model constants from these row-major blocks
   int64_t lnl_mstride;
   int persist;  // k_bdraw_tiled: 0 = one workgroup per 16 chains of a pulsar, G = G persistent workgroups
+  int sched = 0;  // gs_bdraw_tiled: GS_OPT_SWEEP_SCHED (0 cost model, 2 one chain per wave, 3 two)
   gs_key key;
 };
 
@@ -162,7 +163,8 @@ struct RhoArgs {
 // *shape: the workgroup shape launched (GS_OPT_LAST_SWEEP_SHAPE: 1 hand-off, 2 one chain per wave, 3 two)
 int launch_sweep_freespec(hipStream_t s, const SweepArgs& a, int* shape);
 int launch_bdraw(hipStream_t s, const BdrawArgs& a);
-int launch_bdraw_tiled(hipStream_t s, const BdrawArgs& a);
+// *shape: 2 one chain per wave (k_bdraw_tiled), 3 two chains per wave (k_bdraw_pair)
+int launch_bdraw_tiled(hipStream_t s, const BdrawArgs& a, int* shape);
 int launch_model_tile(hipStream_t s, const double* model, int n_psr, int NF, int NMX, const int32_t* nm,
                       double* tiled);
 // large free-spectrum blocks (64 < NF <= 255), tiles in a context-owned workspace
