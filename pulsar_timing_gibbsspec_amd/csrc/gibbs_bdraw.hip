@@ -1230,6 +1230,12 @@ constexpr int GS_PAIR_SCR = 2 * gs_tile_scr(60) + 256 + 128 + 128;
 #ifndef GS_PAIR_WPB
 #define GS_PAIR_WPB 4
 #endif
+// GS_PAIR_RHO_PRIO: issue priority of the pair kernel's rho step (the one-chain kernels: GS_RHO_PRIO = 0).
+// Measured on the headline (r06x, 4 interleaved reps): 1.915-1.927 ms per launch at 1 against
+// 1.928-1.938 at 0 and 1.931-1.943 at 2
+#ifndef GS_PAIR_RHO_PRIO
+#define GS_PAIR_RHO_PRIO 1
+#endif
 // GS_PAIR_RHO_MERGE: both chains' rho steps in one pass over the wave (30 frequencies each)
 #ifndef GS_PAIR_RHO_MERGE
 #define GS_PAIR_RHO_MERGE 1
@@ -1301,7 +1307,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_sweep_pair(SweepArgs A) {
       double phinv[2] = {0.0, 0.0};
       bool draw[2] = {true, true};
       if (pass == 1) {
-        if constexpr (GS_RHO_PRIO > 0) __builtin_amdgcn_s_setprio(GS_RHO_PRIO);
+        if constexpr (GS_PAIR_RHO_PRIO > 0) __builtin_amdgcn_s_setprio(GS_PAIR_RHO_PRIO);
 #if GS_PAIR_RHO_MERGE
         {
           // rho|b analytic (pulsar_gibbs.py:208-216, 236), as sweep_freespec_body, for both chains in
@@ -1402,7 +1408,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_sweep_pair(SweepArgs A) {
           x[ch] = xnew;
         }
 #endif
-        if constexpr (GS_RHO_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+        if constexpr (GS_PAIR_RHO_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
         if (!draw[0] && !draw[1]) break;
         ev = GS_EV_B;
       }
