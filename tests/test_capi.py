@@ -74,3 +74,15 @@ def test_no_cpu_fallback():
     from pulsar_timing_gibbsspec_amd import _lib
     with pytest.raises(_lib.GibbsLibError):
         _lib.Context(0)
+
+
+def test_option_constants_match_header():
+    """_lib's OPT_* constants are the header's GS_OPT_* enum values (GS_OPT_SWEEP_SCHED's 0..3 and the
+    read-only GS_OPT_LAST_SWEEP_SHAPE included)."""
+    from pulsar_timing_gibbsspec_amd import _lib
+    src = open(os.path.join(ROOT, "include", "pulsar_gibbs.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    enum = {k: int(v) for k, v in re.findall(r"\bGS_OPT_(\w+)\s*=\s*(\d+)", src)}
+    assert {"SWEEP_SCHED", "LAST_SWEEP_SHAPE"} <= set(enum)
+    for name, val in enum.items():
+        assert getattr(_lib, "OPT_" + name) == val, name
