@@ -570,6 +570,12 @@ __global__ __launch_bounds__(64 * WPB, GS_MINW(GS_BCAST_TILE, NFC, NTC)) void k_
 // whose fixed block is row-major (nM > 16) run bdraw_item for each chain in turn.  Persistent ranges
 // of (pulsar, group of 2 WPB chains) items as k_bdraw_tiled; n_chain is even.
 constexpr int GS_BPAIR_SCR = 2 * gs_tile_scr(60) + 128;  // per wave: the chains' scratches + z_M slots
+// cost of a row-major pulsar's item (paired items = 10).  Measured on the 45-pulsar curn array (r06g2/3,
+// every chain drawing): 0.474 ms per launch at 13, 0.441-0.445 at 15, 0.461-0.464 at 18, against
+// 0.444-0.445 for k_bdraw_tiled and 0.554 unweighted (r06s)
+#ifndef GS_BPAIR_RM_COST
+#define GS_BPAIR_RM_COST 15
+#endif
 
 template <int WPB>
 __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_pair(BdrawArgs A) {
@@ -580,15 +586,32 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_pair(BdrawArgs A) {
   double* wl = lds + A.mstride + (int64_t)wave * GS_BPAIR_SCR;
   double* const scr[2] = {wl, wl + gs_tile_scr(60)};
   double* zmslot = wl + 2 * gs_tile_scr(60);
-  const int64_t n_items = (int64_t)A.n_psr * nb;
+  // persistent ranges weighted by cost: an item of a pulsar whose fixed block is row-major (drawn one
+  // chain at a time) costs GS_BPAIR_RM_COST / 10 of a paired one, so the workgroups covering such
+  // pulsars take fewer items (without the weights they ran ~1.3x longer than the rest, r06s)
   const int64_t G = A.persist ? A.persist : (int64_t)gridDim.x;
-  const int64_t lo = A.persist ? blockIdx.x * n_items / G : blockIdx.x;
-  const int64_t hi = A.persist ? (blockIdx.x + 1) * n_items / G : lo + 1;
+  auto cost = [&](int q) -> int {
+    if (!A.persist) return 1;  // one item per workgroup
+    const int nq = __builtin_amdgcn_readfirstlane(A.nm[q]);
+    return model_tiled_fix(model_tiled_layout(A.NMX, nq)) ? 10 : GS_BPAIR_RM_COST;
+  };
+  int64_t tot = 0;
+#pragma unroll 1
+  for (int q = 0; q < A.n_psr; ++q) tot += (int64_t)nb * cost(q);
+  const int64_t c_lo = blockIdx.x * tot / G, c_hi = (blockIdx.x + 1) * tot / G;
   int cur = -1, nM = 0, fi = 0, mi = 0, NMXe = A.NMX;
   ModelTiled M;
+  int64_t P0 = 0;
 #pragma unroll 1
-  for (int64_t it = lo; it < hi; ++it) {
-    const int p = (int)(it / nb), grp = (int)(it % nb);
+  for (int p = 0; p < A.n_psr && P0 < c_hi; ++p) {
+    const int cp = cost(p);
+    const int64_t P1 = P0 + (int64_t)nb * cp;
+    // items grp with start P0 + grp cp in [c_lo, c_hi)
+    const int g0 = c_lo > P0 ? (int)((c_lo - P0 + cp - 1) / cp) : 0;
+    const int g1 = P1 > c_lo ? (int)min((int64_t)nb, (c_hi - P0 + cp - 1) / cp) : 0;
+    P0 = P1;
+#pragma unroll 1
+  for (int grp = g0; grp < g1; ++grp) {
     if (p != cur) {  // uniform over the workgroup
       if (cur >= 0) __syncthreads();
       stage_model(lds, A.model + (int64_t)p * A.mstride, A.mstride);
@@ -645,6 +668,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void k_bdraw_pair(BdrawArgs A) {
       }
       if (A.info && lane == 0) A.info[sys] = f[ch];
     }
+  }
   }
 }
 
@@ -1733,8 +1757,10 @@ int launch_model_tile(hipStream_t s, const double* model, int n_psr, int NF, int
 // GS_BDRAW_PAIR (off): the cost model picks k_bdraw_pair where its pairs fill 2 waves per SIMD.
 // Measured (r06s, curn engine, every chain drawing): 0.430 vs 0.4375-0.468 ms per launch on 3 pulsars
 // x 30720 chains (all nM <= 16), but 0.554 vs 0.444-0.473 ms on the 45-pulsar array, whose two nM = 17
-// pulsars draw one chain at a time inside the pair kernel and leave the persistent ranges that cover
-// them ~1.3x longer than the rest.  GS_OPT_SWEEP_SCHED = 3 runs it (bit-identical).
+// pulsars draw one chain at a time inside the pair kernel and left the persistent ranges that cover
+// them longer than the rest; with the ranges weighted by item cost (GS_BPAIR_RM_COST) 0.441-0.445 vs
+// 0.444-0.445 ms (r06g3) -- within the noise, so it stays opt-in.  GS_OPT_SWEEP_SCHED = 3 runs it
+// (bit-identical).
 #ifndef GS_BDRAW_PAIR
 #define GS_BDRAW_PAIR 0
 #endif

@@ -1,8 +1,9 @@
 """gs_bdraw_tiled with two chains per wave (k_bdraw_pair, GS_OPT_SWEEP_SCHED = 3) against the one-chain
 kernel (GS_OPT_SWEEP_SCHED = 2): bit-identical b, info and failure counts, for Philox and injected
 normals, a mixed gate (shut chains keep b and get nothing written), phiinv per chain (curn) and per
-system (curn_red, grid-conditional red), and the 45-pulsar array whose two nM = 17 pulsars take the row-major fixed block
-(drawn one chain at a time inside the pair kernel).  Needs an MI355X."""
+system (curn_red, grid-conditional red), and the 45-pulsar array whose two nM = 17 pulsars take the
+row-major fixed block (drawn one chain at a time inside the pair kernel; at 128 chains the items outnumber
+one round of workgroups, so the cost-weighted persistent ranges run).  Needs an MI355X."""
 import numpy as np
 import pytest
 
@@ -41,7 +42,7 @@ def _draw(eng, sched, z, mask):
     return out
 
 
-@pytest.mark.parametrize("kind,n_psr,C", [("curn", 6, 64), ("curn_red", 6, 38), ("curn", 45, 32)])
+@pytest.mark.parametrize("kind,n_psr,C", [("curn", 6, 64), ("curn_red", 6, 38), ("curn", 45, 32), ("curn", 45, 128)])
 @pytest.mark.parametrize("inject", [False, True])
 def test_bdraw_pair_equals_one_chain(kind, n_psr, C, inject):
     eng = _engine(kind, n_psr, C)
