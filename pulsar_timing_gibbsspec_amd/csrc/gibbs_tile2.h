@@ -1,4 +1,5 @@
-// b|rho draws of TWO chains per wavefront (the fused sweep's GS_OPT_SWEEP_SCHED = 3 shape).
+// b|rho draws of TWO chains per wavefront: k_sweep_pair (the fused sweep's two-chains-per-wave shape, the
+// headline's kernel) and k_bdraw_pair (gs_bdraw_tiled, opt-in); GS_OPT_SWEEP_SCHED = 3, DESIGN.md §3.3.
 //
 // The draw is gibbs_tile.h's bdraw_tile_core (register tiles in the v_mfma_f64_16x16x4f64 C layout,
 // augmented Schur block, stored transposes, tiled fixed block) for two systems at once, with the same
