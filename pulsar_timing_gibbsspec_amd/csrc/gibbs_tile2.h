@@ -45,6 +45,12 @@ __host__ __device__ constexpr int ptk(int k) { return 2 * (k >> 2) + ((k >> 1) &
 #ifndef GS_PAIR_T2
 #define GS_PAIR_T2 0
 #endif
+// GS_PAIR_FIX_PRIO: issue priority of the pair draw's fixed block (the one-chain tile core: GS_FIX_PRIO
+// = 0).  Measured on the headline (r06p2, 3 interleaved reps): 1.901-1.907 ms per launch at 1 against
+// 1.910-1.922 at 0; the MFMA updates at 1 (1.908-1.913) and the elimination at 1 (1.936-1.943) not
+#ifndef GS_PAIR_FIX_PRIO
+#define GS_PAIR_FIX_PRIO 1
+#endif
 // GS_PAIR_SOLVE_ILV: both chains' solves and fixed blocks interleaved (1) or one after the other (0)
 #ifndef GS_PAIR_SOLVE_ILV
 #define GS_PAIR_SOLVE_ILV 1
@@ -334,7 +340,7 @@ __device__ __forceinline__ void bdraw_tile_pair60(const ModelTiled& M, int NMX, 
     lds_fence();
     if constexpr (PR && GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
 
-    if constexpr (PR && GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_FIX_PRIO);
+    if constexpr (PR && GS_PAIR_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_PAIR_FIX_PRIO);
     // fixed-prior block x_M = h + R z_M - G x_F (tiled G' = -G and R', nM <= 16: one chunk); z_M was
     // staged in the chains' zm slots before the factorisation
     const int row = c;
@@ -366,7 +372,7 @@ __device__ __forceinline__ void bdraw_tile_pair60(const ModelTiled& M, int NMX, 
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) bM[ch] = (lane < nM) ? ob[ch][lane] : 0.0;
     lds_fence();
-    if constexpr (PR && GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+    if constexpr (PR && GS_PAIR_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
   }
 #else
   // ---- the solves and the fixed block, one chain after the other: chain a's tiles and solution rows
@@ -409,7 +415,7 @@ __device__ __forceinline__ void bdraw_tile_pair60(const ModelTiled& M, int NMX, 
     lds_fence();
     if constexpr (PR && GS_SOLVE_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
 
-    if constexpr (PR && GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_FIX_PRIO);
+    if constexpr (PR && GS_PAIR_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_PAIR_FIX_PRIO);
     // fixed-prior block x_M = h + R z_M - G x_F (tiled G' = -G and R', nM <= 16: one chunk); z_M was
     // staged in the chain's zm slot before the factorisation
     {
@@ -431,7 +437,7 @@ __device__ __forceinline__ void bdraw_tile_pair60(const ModelTiled& M, int NMX, 
     lds_fence();
     bM[ch] = (lane < nM) ? ob[ch][lane] : 0.0;
     lds_fence();
-    if constexpr (PR && GS_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
+    if constexpr (PR && GS_PAIR_FIX_PRIO > 0) __builtin_amdgcn_s_setprio(GS_BASE_PRIO);
   }
 #endif
 }
