@@ -51,6 +51,13 @@ __host__ __device__ constexpr int ptk(int k) { return 2 * (k >> 2) + ((k >> 1) &
 #ifndef GS_PAIR_FIX_PRIO
 #define GS_PAIR_FIX_PRIO 1
 #endif
+// GS_PAIR_LOOKAHEAD: step K's trailing updates other than the next diagonal tile are issued inside the
+// next diagonal elimination, one tile-op per pivot step (each tile still sees its updates in K order, so
+// the draws are unchanged bit for bit; at NT = 4 at most 10 tile-ops wait, fewer than the 16 steps).
+// Measured on the headline (r06la, 3 interleaved reps): 1.912-1.920 ms per launch against 1.916-1.925
+#ifndef GS_PAIR_LOOKAHEAD
+#define GS_PAIR_LOOKAHEAD 1
+#endif
 // GS_PAIR_SOLVE_ILV: both chains' solves and fixed blocks interleaved (1) or one after the other (0)
 #ifndef GS_PAIR_SOLVE_ILV
 #define GS_PAIR_SOLVE_ILV 1
@@ -90,8 +97,12 @@ __device__ __forceinline__ void to_row2(const double (&v)[2], double* const (&vb
 // tile_elim1's column elimination on two chains at once (paired layout): on return B * rsd is U^-1 of
 // each chain's tile and A its column-eliminated tile, both paired; rsd the lane's chain's pivot^-1/2
 // of column c.  Same operations per element as tile_elim1<KMAX, PR>.
-template <int KMAX, bool PR>
-__device__ __forceinline__ void tile_elim_pair(double (&A)[8], double (&B)[8], double& rsd, int lane) {
+struct gpair_nofill {
+  __device__ void operator()(int) const {}
+};
+template <int KMAX, bool PR, typename F = gpair_nofill>
+__device__ __forceinline__ void tile_elim_pair(double (&A)[8], double (&B)[8], double& rsd, int lane,
+                                               F&& fill = F()) {
   using namespace gtile;
   using gpair::ptk;
   if constexpr (PR && GS_DIAG_PRIO > 0) __builtin_amdgcn_s_setprio(GS_DIAG_PRIO);
@@ -129,6 +140,7 @@ __device__ __forceinline__ void tile_elim_pair(double (&A)[8], double (&B)[8], d
 #pragma unroll
       for (int t = 0; t <= (GS_PAIR_SKIP ? ptk(k) : 2 * k1 + 1); ++t) B[t] = fmac_nb(B[t], B[t], ng, k);
     }
+    fill(k);  // GS_PAIR_LOOKAHEAD: independent work for this step's dependency waits
   }
   // A[ptk(c)] as a select tree on the bits of ptk(c) (a select chain on a lane-varying index is turned
   // into a private-array load, i.e. scratch)
@@ -220,10 +232,41 @@ __device__ __forceinline__ void bdraw_tile_pair60(const ModelTiled& M, int NMX, 
       gpair::swap32(PA[2 * s], PA[2 * s + 1]);
     }
     double rsd;
+#if GS_PAIR_LOOKAHEAD
+    // the trailing updates of step K - 1 other than tile (K, K), one tile-op per elimination step
+    auto fill = [&](int k) {
+      if (K == 0) return;
+      int n = 0;
+#pragma unroll
+      for (int I = K; I < NT; ++I)
+#pragma unroll
+        for (int J = I; J < NT; ++J) {
+          if (I == K && J == K) continue;
+#pragma unroll
+          for (int ch = 0; ch < 2; ++ch) {
+            if (n == k)
+              t[ch][tix(I, J, NT)] =
+                  mfma_tn_sub(t[ch][tix(I, J, NT)], t[ch][tix(K - 1, I, NT)], t[ch][tix(K - 1, J, NT)]);
+            ++n;
+          }
+        }
+    };
+    if (K == NT - 1)
+      tile_elim_pair<CP, PR>(PA, PB, rsd, lane, fill);
+    else
+      tile_elim_pair<16, PR>(PA, PB, rsd, lane, fill);
+    if (K > 0) {  // row K - 1's stored transposes, now that its last updates are issued
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+        for (int J = K; J < NT; ++J) t[ch][tix(K - 1, J, NT)] = transpose(t[ch][tix(K - 1, J, NT)], tb[ch], q, c);
+    }
+#else
     if (K == NT - 1)
       tile_elim_pair<CP, PR>(PA, PB, rsd, lane);
     else
       tile_elim_pair<16, PR>(PA, PB, rsd, lane);
+#endif
     if (K == NT - 1) {
       // y_last[k] = (row CP of the eliminated tile)[k] * pivot_k^-1/2, k < CP, of the lane's chain,
       // then to each chain's column layout (every row group)
@@ -264,6 +307,15 @@ __device__ __forceinline__ void bdraw_tile_pair60(const ModelTiled& M, int NMX, 
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) t[ch][kk] = transpose(V[ch], tb[ch], q, c);
 #endif
+#if GS_PAIR_LOOKAHEAD
+    // only tile (K + 1, K + 1) now: the next elimination needs it; the rest go into its steps
+    if (K + 1 < NT) {
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch)
+        t[ch][tix(K + 1, K + 1, NT)] =
+            mfma_tn_sub(t[ch][tix(K + 1, K + 1, NT)], t[ch][tix(K, K + 1, NT)], t[ch][tix(K, K + 1, NT)]);
+    }
+#else
 #pragma unroll
     for (int I = K + 1; I < NT; ++I)
 #pragma unroll
@@ -271,7 +323,10 @@ __device__ __forceinline__ void bdraw_tile_pair60(const ModelTiled& M, int NMX, 
 #pragma unroll
         for (int ch = 0; ch < 2; ++ch)
           t[ch][tix(I, J, NT)] = mfma_tn_sub(t[ch][tix(I, J, NT)], t[ch][tix(K, I, NT)], t[ch][tix(K, J, NT)]);
-#if GS_PAIR_T2
+#endif
+#if GS_PAIR_LOOKAHEAD
+    // (row K's transposes follow the next elimination, after its last use by the pending updates)
+#elif GS_PAIR_T2
 #pragma unroll
     for (int J = K + 1; J < NT; ++J) transpose2(t[0][tix(K, J, NT)], t[1][tix(K, J, NT)], tb, q, c);
 #else

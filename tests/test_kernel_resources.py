@@ -41,7 +41,8 @@ HOT = [
     ("k_sweep_freespecILi60ELi0ELi12ELi3E", 3, 40),    # 12-wave hand-off workgroups (the headline's
     ("k_sweep_freespec_rmILi60ELi0ELi12ELi3E", 3, 40),  # 4096 chains): 38 spills outside the body  # headline fused sweep (configs[1], [2]): 3 waves,
                                                     # 13 spills outside the inner body (round 3)
-    ("k_bdraw_pairILi4EE", 2, 0),                  # PTA b draw, two chains per wave (opt-in, round 6)
+    ("k_bdraw_pairILi4EE", 2, 2),                  # PTA b draw, two chains per wave (opt-in, round 6;
+                                                   # 1 spill with the look-ahead factorisation)
     ("k_sweep_pairILi4EE", 2, 12),                 # two chains per wave (the headline since round 6):
                                                    # both chains' tiles at 2 waves/SIMD, 10 spills
                                                    # outside the draw
