@@ -123,8 +123,28 @@ WARM_MS = 60.0
 
 def warm(fn, min_calls=1, min_ms=WARM_MS):
     """Call fn() (one untimed sweep / launch of the line) at least min_calls times and until min_ms of
-    wall time has passed, synchronising every few calls so the wall time follows the GPU."""
+    wall time has passed, synchronising every few calls so the wall time follows the GPU.  With more
+    than one rank every rank makes the SAME number of calls (fn may hold a collective: the pulsar-sharded
+    lines' per-sweep exchange): min_calls first, then the extra calls the slowest rank needs to reach
+    min_ms, agreed by an all-reduce while no rank is inside fn."""
     t0 = time.perf_counter()
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        for _ in range(min_calls):
+            fn()
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) * 1e3
+        per = el / max(1, min_calls)
+        extra = 0 if el >= min_ms else int(np.ceil((min_ms - el) / max(per, 1e-3)))
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([extra], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        extra = int(t.item())
+        for i in range(extra):
+            fn()
+            if i % 4 == 3:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        return min_calls + extra
     n = 0
     while n < min_calls or (time.perf_counter() - t0) * 1e3 < min_ms:
         fn()
